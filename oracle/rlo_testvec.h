@@ -1,0 +1,65 @@
+/*
+ * rlo_testvec.h -- TEST INFRASTRUCTURE ONLY (oracle side).
+ *
+ * Definition of the synthetic workloads shared by the reference harness
+ * (oracle/ref_harness.c, linked against the compiled reference), the CPU
+ * restatement (oracle/rlo_oracle.c) and the tests.  The product keeps its
+ * own device implementation of the same generator
+ * (rootless-coll-mpi-ops_amd/csrc/rlo_device.hpp) -- it never includes this.
+ *
+ *   storm payload  : word0 = (bid << 32) | origin ; word k>=1 =
+ *                    splitmix64(word0 ^ (k * GOLDEN)) ; little endian,
+ *                    truncated to len bytes.
+ *   storm origins  : origin(b) = splitmix64(seed + b) % N
+ *   data hash      : FNV-1a 64 over the 32,764-byte data region the reference
+ *                    delivers (payload followed by zero bytes).
+ */
+#ifndef RLO_TESTVEC_H
+#define RLO_TESTVEC_H
+#include <stdint.h>
+#include <string.h>
+
+#define RLO_TV_GOLDEN 0x9E3779B97F4A7C15ull
+#define RLO_TV_DATA_REGION 32764 /* RLO_MSG_SIZE_MAX - sizeof(int): rootless_ops.c:1588 */
+
+static inline uint64_t rlo_tv_splitmix64(uint64_t x) {
+    uint64_t z = x + RLO_TV_GOLDEN;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static inline uint64_t rlo_tv_word(uint32_t origin, uint32_t bid, uint32_t k) {
+    uint64_t w0 = ((uint64_t)bid << 32) | (uint64_t)origin;
+    if (k == 0) return w0;
+    return rlo_tv_splitmix64(w0 ^ ((uint64_t)k * RLO_TV_GOLDEN));
+}
+
+static inline void rlo_tv_payload(uint32_t origin, uint32_t bid, uint8_t* out, size_t len) {
+    for (size_t off = 0; off < len; off += 8) {
+        uint64_t w = rlo_tv_word(origin, bid, (uint32_t)(off / 8));
+        size_t n = len - off < 8 ? len - off : 8;
+        memcpy(out + off, &w, n); /* little endian host */
+    }
+}
+
+static inline uint32_t rlo_tv_origin(uint64_t seed, uint64_t b, uint32_t n) {
+    return (uint32_t)(rlo_tv_splitmix64(seed + b) % n);
+}
+
+static inline uint64_t rlo_tv_fnv1a(const uint8_t* p, size_t len, uint64_t h) {
+    for (size_t i = 0; i < len; i++) { h ^= p[i]; h *= 0x100000001b3ull; }
+    return h;
+}
+#define RLO_TV_FNV_INIT 0xcbf29ce484222325ull
+
+/* FNV-1a of (payload[0..len) ++ zeros) over the whole data region. */
+static inline uint64_t rlo_tv_region_hash(const uint8_t* payload, size_t len) {
+    static const uint8_t zeros[4096] = {0};
+    if (len > RLO_TV_DATA_REGION) len = RLO_TV_DATA_REGION;
+    uint64_t h = rlo_tv_fnv1a(payload, len, RLO_TV_FNV_INIT);
+    size_t rest = RLO_TV_DATA_REGION - len;
+    while (rest) { size_t n = rest < sizeof zeros ? rest : sizeof zeros; h = rlo_tv_fnv1a(zeros, n, h); rest -= n; }
+    return h;
+}
+#endif
