@@ -1,0 +1,142 @@
+/*
+ * rlo_hip.h -- C ABI of the MI355X rootless collective engine (librlo_hip.so).
+ *
+ * This is the device-engine layer underneath the drop-in rootless_ops.h API.
+ * Plain C types only (no HIP / torch types in signatures): a stream is passed
+ * as `void*` (a hipStream_t, NULL = default stream).
+ *
+ * A world is N virtual ranks hosted on one GPU, one 256-thread workgroup per
+ * rank of a persistent progress kernel.  Each rank's inboxes are SPSC rings in
+ * HBM, one per overlay in-edge and virtual channel (DESIGN.md "Data layout").
+ * A *program* is the workload the kernel runs until every rank is quiescent:
+ *   storm   : K bcasts from random originators          (replaces RLO_bcast_gen +
+ *             RLO_make_progress_all + RLO_user_pickup_next loops, rootless_ops.c:1581, :538, :938)
+ *   latency : one bcast at a time, completion latency per round
+ *   iar     : every rank runs its own proposal list, device judge, vote AND,
+ *             decision bcast (RLO_submit_proposal :876 ... _iar_decision_handler :814)
+ */
+#ifndef RLO_HIP_H
+#define RLO_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ errors */
+#define RLO_OK 0
+#define RLO_E_INVAL (-1)     /* bad argument / unsupported size                          */
+#define RLO_E_HIP (-2)       /* a HIP runtime call failed (rlo_last_hip_error)            */
+#define RLO_E_OCCUPANCY (-3) /* the ranks cannot all be co-resident on the device         */
+#define RLO_E_DEVICE (-4)    /* the kernel reported an error (see rlo_rank_stats_t.error) */
+#define RLO_E_NOPROGRAM (-5) /* rlo_launch without a program                              */
+#define RLO_E_NODEVICE (-6)  /* no HIP device                                              */
+
+/* device error codes (rlo_rank_stats_t.error) */
+#define RLO_DERR_TIMEOUT 1
+#define RLO_DERR_VOTE_RING 2
+#define RLO_DERR_PID_COLLISION 3 /* proposal carries the receiver's own pid (rootless_ops.c:690) */
+#define RLO_DERR_VOTE_ORPHAN 4
+#define RLO_DERR_LOG_FULL 5
+#define RLO_DERR_BAD_SLOT 6
+
+/* ------------------------------------------------------------------ topology (host only) */
+/* skip-ring overlay, restated from rootless_ops.c:1416-1579; usable without a GPU */
+int rlo_topology(int n, int rank, int* level, int* last_wall, int* send_channel_cnt, int* send_list_len,
+                 int* send_list /* >= 16 entries */);
+int rlo_children(int n, int rank, int origin, int from /* -1: originate */, int* out /* >= 16 */);
+
+/* ------------------------------------------------------------------ world */
+typedef struct rlo_world rlo_world_t;
+
+typedef struct {
+    int32_t n_ranks;      /* world size, 2 .. 4096                                        */
+    uint32_t max_payload; /* payload bytes per slot (rounded up to 16); default 4096       */
+    uint32_t ring_slots;  /* forward ring capacity (power of two); 0 = auto               */
+    int32_t device;       /* HIP device ordinal; -1 = current                              */
+} rlo_world_cfg_t;
+
+typedef struct {
+    int32_t n_ranks, max_in_degree, max_fanout, edges;
+    uint32_t ring_slots, slot_stride, vote_slots, pad;
+    uint64_t fwd_bytes, vote_bytes, ctrl_bytes;
+    int32_t cus, blocks_per_cu;
+} rlo_world_info_t;
+
+int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
+int rlo_world_destroy(rlo_world_t* w);
+int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
+
+/* ------------------------------------------------------------------ programs */
+#define RLO_FLAG_LOG 1u  /* record every delivery / judge / action / result (+ payload bytes) */
+#define RLO_FLAG_HIST 2u /* per-delivery latency histogram                                  */
+
+typedef struct {
+    uint64_t seed;       /* originator of bcast b = splitmix64(seed + b) % N              */
+    int64_t k;           /* bcasts in the storm                                            */
+    uint32_t len;        /* payload bytes (<= max_payload)                                 */
+    uint32_t window;     /* max originations per rank per progress iteration (0 = 32)      */
+    uint32_t flags;      /* RLO_FLAG_*                                                      */
+    uint32_t log_cap;    /* log records per rank when RLO_FLAG_LOG                          */
+} rlo_storm_cfg_t;
+int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg);
+
+/* one bcast per round, round i from splitmix64(seed + i) % N; round i+1 starts when every
+ * rank has picked up round i.  rlo_latencies() returns per-round completion ticks (10 ns). */
+int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags);
+
+#define RLO_JUDGE_APPROVE 0u /* approve everything                                           */
+#define RLO_JUDGE_MASK 1u    /* decline iff mask[rank] != 0 (arg != NULL)                     */
+#define RLO_JUDGE_ISP 2u     /* testcases.c:18-37 is_proposal_approved_cb, per-rank string    */
+#define RLO_JUDGE_HASH 3u    /* decline iff splitmix64(seed^rank<<32^pid) % 1e6 < ppm         */
+
+typedef struct {
+    uint32_t judge_kind, judge_ppm;
+    uint64_t judge_seed;
+    const uint8_t* judge_mask; /* [N] for RLO_JUDGE_MASK                                   */
+    const char* judge_isp;     /* N NUL-terminated strings, concatenated (RLO_JUDGE_ISP)    */
+    uint32_t flags, log_cap;
+} rlo_iar_cfg_t;
+/* proposals in per-origin submission order: origin[i] submits pid[i] with
+ * data[data_off[i] .. +data_len[i]); a rank submits its next proposal when its
+ * previous decision has been broadcast (one own proposal per engine, rootless_ops.c:241). */
+int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, const int32_t* origin, const int32_t* pid,
+                    const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len);
+
+/* ------------------------------------------------------------------ run */
+int rlo_launch(rlo_world_t* w, void* stream);          /* async: reset rings, launch   */
+int rlo_wait(rlo_world_t* w);                          /* sync; RLO_E_DEVICE on error  */
+int rlo_run(rlo_world_t* w, void* stream, float* kernel_ms); /* launch + wait, HIP-event time */
+int rlo_last_kernel_ms(rlo_world_t* w, float* ms);
+
+/* ------------------------------------------------------------------ results */
+typedef struct {
+    uint64_t bcast_delivered, bcast_sum, originated;
+    uint64_t dec_delivered, dec_approved, actions, judge_calls;
+    uint64_t own_decided, own_approved, proposals_recv;
+    uint64_t iterations, busy_iterations, stalls, log_count;
+    uint64_t t_start, t_end;
+    uint32_t error, error_aux;
+    uint32_t hist[128];
+} rlo_rank_stats_t;
+
+typedef struct {
+    uint32_t kind; /* 1 deliver | 2 judge | 3 action | 4 result | 5 error, | tag << 8 */
+    int32_t origin, from;
+    uint32_t id, len;
+    int32_t vote;
+    uint32_t aux, payload_idx;
+} rlo_log_rec_t;
+
+int rlo_stats(rlo_world_t* w, rlo_rank_stats_t* out, int n);
+int rlo_log(rlo_world_t* w, int rank, rlo_log_rec_t* out, uint32_t cap, uint8_t* payload, uint32_t payload_stride);
+int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap);
+
+const char* rlo_strerror(int code);
+int rlo_last_hip_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,138 @@
+// rlo_device.hpp -- plain-old-data shared by the host world builder (rlo_world.cpp)
+// and the persistent progress kernel (rlo_kernel.hip).
+//
+// One "world" = N virtual ranks.  Every rank is one 256-thread workgroup of the
+// persistent kernel.  Every directed overlay edge (r -> send_list(r)[j]) owns
+//   * two forward rings (virtual channels vc = 0/1, vc = child < origin; the
+//     "dateline" split that makes the ring channel-dependency graph acyclic),
+//   * one reverse vote ring (child -> parent).
+// Ring bytes live in the consumer's HBM; the producer count (tail) sits in the
+// consumer's packed inbox control block, the consumer count (head, = credits)
+// in the producer's packed outbox control block.
+#pragma once
+#include <stdint.h>
+
+namespace rlo {
+
+constexpr int kBlock = 256;       // threads per rank-workgroup (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxFanout = 16;    // send_list_len <= ceil(log2 N) <= 16  (N <= 65536)
+constexpr int kMaxIn = 32;        // forward in-edges per rank
+constexpr int kMaxOut = 2 * kMaxFanout;
+constexpr int kHdr = 16;          // slot header bytes
+constexpr int kVoteSlot = 16;     // vote ring slot bytes
+constexpr int kMaxCand = kBlock;  // messages handled per rank per progress iteration
+constexpr int kHistBins = 128;    // latency histogram: 8 sub-bins per octave of 10 ns ticks
+
+// message classes == enum RLO_COMM_TAGS (rootless_ops.h:50-61)
+enum Tag : uint32_t { TAG_BCAST = 0, TAG_PROPOSAL = 2, TAG_VOTE = 3, TAG_DECISION = 4 };
+
+enum Mode : uint32_t {
+    MODE_STORM = 1u,   // every rank originates its share of K bcasts (random originators)
+    MODE_LAT = 2u,     // one bcast at a time, completion latency per round
+    MODE_IAR = 4u,     // every rank runs its proposal list (proposal / vote / decision)
+    MODE_LOG = 16u,    // record every event (+ delivered payload bytes) for parity tests
+    MODE_HIST = 32u,   // per-delivery latency histogram
+};
+
+enum Judge : uint32_t { JUDGE_APPROVE = 0, JUDGE_MASK = 1, JUDGE_ISP = 2, JUDGE_HASH = 3 };
+
+enum LogKind : uint32_t { LOG_DELIVER = 1, LOG_JUDGE = 2, LOG_ACTION = 3, LOG_RESULT = 4, LOG_ERROR = 5 };
+
+enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_COLLISION = 3, ERR_VOTE_ORPHAN = 4,
+                      ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6 };
+
+// Slot header, 16 bytes:
+//   w0 = origin (16 b) | tag (8 b) << 16 | vote (8 b) << 24
+//   w1 = id   (bcast id / proposal pid)
+//   w2 = len  (24 b, payload bytes) | pseq (8 b) << 24   (pseq: per-origin proposal sequence)
+//   w3 = t0   (low 32 bits of s_memrealtime at origination, 100 MHz)
+// Vote slot, 16 bytes: w0 = origin | vote << 24, w1 = pid, w2 = pseq, w3 = voter
+
+struct RankTopo {
+    int32_t level, last_wall, scc, sll;   // rootless_ops.c:86-112 fields, restated
+    int32_t send_list[kMaxFanout];
+    int32_t n_in;                          // forward in-edges
+    int32_t in_src[kMaxIn];                // sender rank of in-edge k
+    // forward rings I produce into: (j, vc)
+    uint32_t out_data[kMaxFanout][2];      // byte offset of ring data in the forward region
+    uint32_t out_tail[kMaxFanout][2];      // index of its tail word in ctrl[]
+    uint32_t out_head[kMaxFanout][2];      // index of its head word in ctrl[]
+    // forward rings I consume: (k, vc)
+    uint32_t in_data[kMaxIn][2];
+    uint32_t in_tail[kMaxIn][2];
+    uint32_t in_head[kMaxIn][2];
+    // vote rings: I produce towards parent over in-edge k, I consume from child j
+    uint32_t vout_data[kMaxIn], vout_tail[kMaxIn], vout_head[kMaxIn];
+    uint32_t vin_data[kMaxFanout], vin_tail[kMaxFanout], vin_head[kMaxFanout];
+    uint32_t inbox_ctrl, n_inbox;          // my packed tails (fwd in 2*n_in, then votes-in sll)
+    uint32_t outbox_ctrl, n_outbox;        // my packed heads (fwd out 2*sll, then votes-out n_in)
+};
+
+struct RankStats {
+    uint64_t bcast_delivered, bcast_sum, originated;
+    uint64_t dec_delivered, dec_approved, actions, judge_calls;
+    uint64_t own_decided, own_approved, proposals_recv;
+    uint64_t iterations, busy_iterations, stalls, log_count;
+    uint64_t t_start, t_end;              // s_memrealtime
+    uint32_t error, error_aux;
+    uint32_t hist[kHistBins];
+};
+
+struct LogRec {            // 32 bytes
+    uint32_t kind;         // LogKind | tag << 8
+    int32_t origin;
+    int32_t from;          // parent rank (deliveries) / -1
+    uint32_t id;           // bid / pid
+    uint32_t len;
+    int32_t vote;          // decision / judge return / -1
+    uint32_t aux;          // judge: arg==NULL ; action: data_len
+    uint32_t payload_idx;  // index into log payload area, 0xffffffff if none
+};
+
+struct Params {
+    int32_t n, rank_begin, rank_end;
+    uint32_t mode;
+    const RankTopo* topo;         // [rank_end - rank_begin]
+    uint8_t* fwd_region;          // all forward ring bytes of this GPU (<= 4 GiB, one buffer rsrc)
+    uint32_t fwd_region_bytes;
+    uint32_t fwd_cap, fwd_stride; // slots per forward ring (pow2), slot stride bytes
+    uint8_t* vote_region;
+    uint32_t vote_region_bytes;
+    uint32_t vote_cap;            // slots per vote ring (pow2), >= 2 * N
+    uint64_t* ctrl;               // tails / heads
+    // storm / latency workload
+    uint64_t seed;
+    uint32_t len, window;         // payload bytes; max originations per iteration
+    const int64_t* sched_off;     // [n_local + 1] CSR of bcast ids originated by each local rank
+    const uint32_t* sched_ids;
+    const int64_t* expect_bcast;  // [n_local]
+    uint32_t lat_rounds;
+    const int32_t* lat_origin;    // [lat_rounds]
+    uint32_t* lat_count;          // [lat_rounds] deliveries so far
+    uint64_t* lat_out;            // [lat_rounds] completion ticks
+    uint32_t* lat_round;          // current round (global)
+    // IAR workload
+    uint32_t judge_kind, judge_ppm;
+    uint64_t judge_seed;
+    const uint8_t* judge_mask;    // [n]
+    const char* judge_isp;        // concatenated NUL-terminated strings
+    const uint32_t* judge_isp_off;// [n]
+    const int64_t* prop_off;      // [n_local + 1] CSR of own proposals per local rank
+    const int32_t* prop_pid;
+    const uint32_t* prop_data_off;
+    const uint32_t* prop_data_len;
+    const uint8_t* prop_data;
+    const int64_t* expect_dec;    // [n_local] decisions each rank picks up
+    // outputs
+    RankStats* stats;             // [n_local]
+    LogRec* log;                  // [n_local * log_cap]
+    uint8_t* log_payload;         // [n_local * log_cap * log_stride] or null
+    uint32_t log_cap, log_stride;
+    // control
+    uint64_t timeout_ticks;       // no progress for this long -> ERR_TIMEOUT (100 MHz ticks)
+    uint64_t deadline_ticks;      // hard cap on one launch (every spin is bounded)
+    uint32_t* error_flag;         // any rank's first error
+};
+
+}  // namespace rlo

@@ -1,0 +1,105 @@
+"""ctypes binding of librlo_hip.so (include/rlo_hip.h).
+
+The shared library is built in-tree (rootless-coll-mpi-ops_amd/lib/librlo_hip.so) by
+`make -C rootless-coll-mpi-ops_amd` (or __graft_entry__.build()).  There is no CPU
+fallback: if the library is missing the import fails loudly.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
+
+RLO_OK = 0
+RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6
+RLO_FLAG_LOG, RLO_FLAG_HIST = 1, 2
+RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
+DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot"}
+
+
+class WorldCfg(ctypes.Structure):
+    _fields_ = [("n_ranks", ctypes.c_int32), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
+                ("device", ctypes.c_int32)]
+
+
+class WorldInfo(ctypes.Structure):
+    _fields_ = [("n_ranks", ctypes.c_int32), ("max_in_degree", ctypes.c_int32), ("max_fanout", ctypes.c_int32),
+                ("edges", ctypes.c_int32), ("ring_slots", ctypes.c_uint32), ("slot_stride", ctypes.c_uint32),
+                ("vote_slots", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("fwd_bytes", ctypes.c_uint64),
+                ("vote_bytes", ctypes.c_uint64), ("ctrl_bytes", ctypes.c_uint64), ("cus", ctypes.c_int32),
+                ("blocks_per_cu", ctypes.c_int32)]
+
+
+class StormCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("k", ctypes.c_int64), ("len", ctypes.c_uint32), ("window", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("log_cap", ctypes.c_uint32)]
+
+
+class IarCfg(ctypes.Structure):
+    _fields_ = [("judge_kind", ctypes.c_uint32), ("judge_ppm", ctypes.c_uint32), ("judge_seed", ctypes.c_uint64),
+                ("judge_mask", ctypes.c_void_p), ("judge_isp", ctypes.c_char_p), ("flags", ctypes.c_uint32),
+                ("log_cap", ctypes.c_uint32)]
+
+
+class RankStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "bcast_delivered", "bcast_sum", "originated", "dec_delivered", "dec_approved", "actions", "judge_calls",
+        "own_decided", "own_approved", "proposals_recv", "iterations", "busy_iterations", "stalls", "log_count",
+        "t_start", "t_end")] + [("error", ctypes.c_uint32), ("error_aux", ctypes.c_uint32), ("hist", ctypes.c_uint32 * 128)]
+
+
+class LogRec(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("origin", ctypes.c_int32), ("from_", ctypes.c_int32), ("id", ctypes.c_uint32),
+                ("len", ctypes.c_uint32), ("vote", ctypes.c_int32), ("aux", ctypes.c_uint32), ("payload_idx", ctypes.c_uint32)]
+
+
+# every symbol include/rlo_hip.h declares (checked by tests/test_abi.py)
+EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destroy", "rlo_world_query",
+           "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
+           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_strerror", "rlo_last_hip_error"]
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("librlo_hip.so not built (%s): run `make -C rootless-coll-mpi-ops_amd`" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    ip = ctypes.POINTER(ctypes.c_int)
+    vp = ctypes.c_void_p
+    L.rlo_topology.argtypes = [ctypes.c_int, ctypes.c_int, ip, ip, ip, ip, ip]
+    L.rlo_children.argtypes = [ctypes.c_int] * 4 + [ip]
+    L.rlo_world_create.argtypes = [ctypes.POINTER(WorldCfg), ctypes.POINTER(vp)]
+    L.rlo_world_destroy.argtypes = [vp]
+    L.rlo_world_query.argtypes = [vp, ctypes.POINTER(WorldInfo)]
+    L.rlo_program_storm.argtypes = [vp, ctypes.POINTER(StormCfg)]
+    L.rlo_program_latency.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]
+    L.rlo_program_iar.argtypes = [vp, ctypes.POINTER(IarCfg), ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.rlo_launch.argtypes = [vp, vp]
+    L.rlo_wait.argtypes = [vp]
+    L.rlo_run.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
+    L.rlo_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.rlo_stats.argtypes = [vp, ctypes.POINTER(RankStats), ctypes.c_int]
+    L.rlo_log.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), ctypes.c_uint32, vp, ctypes.c_uint32]
+    L.rlo_latencies.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    L.rlo_strerror.argtypes = [ctypes.c_int]
+    L.rlo_strerror.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+class RloError(RuntimeError):
+    pass
+
+
+def check(rc, what=""):
+    if rc < 0:
+        L = load()
+        msg = L.rlo_strerror(rc).decode()
+        if rc == RLO_E_HIP:
+            msg += " (hipError %d)" % L.rlo_last_hip_error()
+        raise RloError("%s failed: %s [%d]" % (what, msg, rc))
+    return rc

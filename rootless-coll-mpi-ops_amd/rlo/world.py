@@ -1,0 +1,176 @@
+"""Python host mirror of the device engine (librlo_hip.so).
+
+World(n) hosts n virtual ranks on one MI355X (one persistent workgroup each).
+Programs map the reference's application loops onto the device:
+
+  storm()    -- K bcasts from random originators: RLO_msg_new_bc + RLO_bcast_gen at the
+                originator, RLO_make_progress_all + RLO_user_pickup_next everywhere
+                (rootless_ops.c:311, :1581, :538, :938; testcases.c:638-697)
+  latency()  -- one bcast at a time (test_gen_bcast style, testcases.c:59-108)
+  iar()      -- RLO_submit_proposal / vote / decision (rootless_ops.c:668-917)
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import check
+
+
+class World:
+    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1):
+        self.lib = L.load()
+        cfg = L.WorldCfg(n, max_payload, ring_slots, device)
+        h = ctypes.c_void_p()
+        check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
+        self.h = h
+        self.n = n
+        info = L.WorldInfo()
+        check(self.lib.rlo_world_query(self.h, ctypes.byref(info)), "rlo_world_query")
+        self.info = {f: getattr(info, f) for f, _ in L.WorldInfo._fields_}
+        self._lat_rounds = 0
+
+    def close(self):
+        if self.h:
+            self.lib.rlo_world_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ programs
+    def program_storm(self, k, length, seed=0x5EED, window=32, log=False, hist=False, log_cap=0):
+        flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0)
+        cfg = L.StormCfg(seed, k, length, window, flags, log_cap)
+        check(self.lib.rlo_program_storm(self.h, ctypes.byref(cfg)), "rlo_program_storm")
+
+    def program_latency(self, rounds, length, seed=0x5EED, hist=False, log=False):
+        flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0)
+        check(self.lib.rlo_program_latency(self.h, rounds, length, seed, flags), "rlo_program_latency")
+        self._lat_rounds = rounds
+
+    def program_iar(self, proposals, judge=L.RLO_JUDGE_APPROVE, mask=None, isp=None, seed=0, ppm=0, log=False,
+                    log_cap=0):
+        """proposals: list of (origin, pid, data bytes) in per-origin submission order."""
+        origin = np.array([p[0] for p in proposals], dtype=np.int32)
+        pid = np.array([p[1] for p in proposals], dtype=np.int32)
+        blob = np.frombuffer(b"".join(p[2] for p in proposals) or b"\0", dtype=np.uint8).copy()
+        dlen = np.array([len(p[2]) for p in proposals], dtype=np.uint32)
+        doff = (np.cumsum(dlen) - dlen).astype(np.uint32)
+        self._keep = [origin, pid, blob, dlen, doff]
+        cfg = L.IarCfg()
+        cfg.judge_kind = judge
+        cfg.judge_ppm = ppm
+        cfg.judge_seed = seed
+        if mask is not None:
+            m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8))
+            self._keep.append(m)
+            cfg.judge_mask = m.ctypes.data
+        if isp is not None:
+            cfg.judge_isp = b"".join(s.encode() + b"\0" for s in isp)
+            self._keep.append(cfg.judge_isp)
+        cfg.flags = L.RLO_FLAG_LOG if log else 0
+        cfg.log_cap = log_cap
+        self._keep.append(cfg)
+        d = lambda a: a.ctypes.data
+        check(self.lib.rlo_program_iar(self.h, ctypes.byref(cfg), len(proposals), d(origin), d(pid), d(blob), d(doff),
+                                       d(dlen)), "rlo_program_iar")
+
+    # ------------------------------------------------------------ run
+    def launch(self, stream=None):
+        check(self.lib.rlo_launch(self.h, stream), "rlo_launch")
+
+    def wait(self, raise_on_device_error=True):
+        rc = self.lib.rlo_wait(self.h)
+        if rc == L.RLO_E_DEVICE and not raise_on_device_error:
+            return rc
+        if rc == L.RLO_E_DEVICE:
+            errs = {(r, L.DERR.get(s.error, s.error), s.error_aux) for r, s in enumerate(self.stats_raw()) if s.error}
+            raise L.RloError("device engine error: %s" % sorted(errs)[:8])
+        return check(rc, "rlo_wait")
+
+    def run(self, stream=None):
+        """launch + wait; returns the kernel time in ms (HIP events on the launch stream)."""
+        ms = ctypes.c_float()
+        rc = self.lib.rlo_run(self.h, stream, ctypes.byref(ms))
+        if rc == L.RLO_E_DEVICE:
+            self.wait()
+        check(rc, "rlo_run")
+        return ms.value
+
+    def kernel_ms(self):
+        ms = ctypes.c_float()
+        check(self.lib.rlo_last_kernel_ms(self.h, ctypes.byref(ms)), "rlo_last_kernel_ms")
+        return ms.value
+
+    # ------------------------------------------------------------ results
+    def stats_raw(self):
+        arr = (L.RankStats * self.n)()
+        check(self.lib.rlo_stats(self.h, arr, self.n), "rlo_stats")
+        return list(arr)
+
+    def stats(self):
+        raw = self.stats_raw()
+        out = {}
+        for f, _ in L.RankStats._fields_:
+            if f == "hist":
+                out[f] = np.array([list(s.hist) for s in raw], dtype=np.uint64)
+            else:
+                out[f] = np.array([getattr(s, f) for s in raw], dtype=np.uint64)
+        return out
+
+    def log(self, rank, cap=1 << 16, payload=False):
+        recs = (L.LogRec * cap)()
+        stride = self.info["slot_stride"] - 16
+        buf = np.zeros(cap * stride, dtype=np.uint8) if payload else None
+        n = check(self.lib.rlo_log(self.h, rank, recs, cap, buf.ctypes.data if payload else None, stride), "rlo_log")
+        rows = [(r.kind & 0xff, (r.kind >> 8) & 0xff, r.origin, r.from_, r.id, r.len, r.vote, r.aux, r.payload_idx)
+                for r in recs[:n]]
+        if payload:
+            return rows, buf.reshape(cap, stride)
+        return rows
+
+    def latencies_ticks(self):
+        arr = (ctypes.c_uint64 * self._lat_rounds)()
+        n = check(self.lib.rlo_latencies(self.h, arr, self._lat_rounds), "rlo_latencies")
+        return np.array(arr[:n], dtype=np.uint64)
+
+
+def hist_percentile(hist, p):
+    """Percentile (in 10 ns ticks) from the device log-bucket histogram (8 sub-bins per octave)."""
+    hist = np.asarray(hist, dtype=np.float64)
+    tot = hist.sum()
+    if tot == 0:
+        return 0.0
+    c = np.cumsum(hist)
+    b = int(np.searchsorted(c, p / 100.0 * tot))
+    if b < 8:
+        return float(b)
+    o, sub = b // 8 + 2, b % 8
+    lo = (8 + sub) << (o - 3)
+    hi = (9 + sub) << (o - 3)
+    return 0.5 * (lo + hi)
+
+
+def topology(n, rank):
+    lib = L.load()
+    v = [ctypes.c_int() for _ in range(4)]
+    sl = (ctypes.c_int * 16)()
+    check(lib.rlo_topology(n, rank, *[ctypes.byref(x) for x in v], sl), "rlo_topology")
+    level, lw, scc, sll = (x.value for x in v)
+    return {"level": level, "last_wall": lw, "send_channel_cnt": scc, "send_list_len": sll, "send_list": list(sl[:sll])}
+
+
+def children(n, rank, origin, frm):
+    out = (ctypes.c_int * 16)()
+    k = check(L.load().rlo_children(n, rank, origin, frm, out), "rlo_children")
+    return list(out[:k])

@@ -1,0 +1,222 @@
+"""GPU parity: the HIP engine (librlo_hip.so) against the pinned oracle and the reference fixtures.
+
+Bit-exact checks: per-rank delivery sets, tree parents, delivered payload bytes (the
+32,764-byte data region hash of the reference), judge-call sets, decisions, actions.
+At full sizes: size-independent properties (delivery counts, checksum of checksums,
+decision counts) against the oracle's analytic model.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as orc
+
+pytestmark = pytest.mark.gpu
+
+LOG_DELIVER, LOG_JUDGE, LOG_ACTION, LOG_RESULT = 1, 2, 3, 4
+
+
+@pytest.fixture(scope="module")
+def rlo():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rlo as _rlo
+
+    return _rlo
+
+
+def _storm_logged(rlo, n, k, ln, seed, max_payload=4096):
+    with rlo.World(n, max_payload=max_payload) as w:
+        w.program_storm(k, ln, seed=seed, log=True, log_cap=k + 8)
+        w.run()
+        st = w.stats()
+        logs = [w.log(r, cap=k + 8, payload=True) for r in range(n)]
+    return st, logs
+
+
+@pytest.mark.parametrize("n,k,ln,seed", [(4, 64, 64, 7), (5, 40, 8, 3), (8, 64, 1000, 11), (13, 52, 200, 5),
+                                          (16, 100, 4096, 1), (64, 64, 64, 9), (256, 32, 100, 2)])
+def test_storm_logged_matches_oracle(rlo, n, k, ln, seed):
+    st, logs = _storm_logged(rlo, n, k, ln, seed)
+    ref = orc.storm(n, seed, k, ln, want_parent=True)
+    assert (st["error"] == 0).all()
+    assert np.array_equal(st["bcast_delivered"].astype(np.int64), ref["count"])
+    assert np.array_equal(st["bcast_sum"], ref["sum"])
+    par = ref["parent"]
+    for r in range(n):
+        rows, payload = logs[r]
+        got = sorted((row[4], row[2], row[3]) for row in rows if row[0] == LOG_DELIVER)
+        want = sorted((b, orc.origin_of(seed, b, n), int(par[b, r])) for b in range(k) if orc.origin_of(seed, b, n) != r)
+        assert got == want, (n, r)
+        for row in rows:  # delivered bytes, exactly
+            bid, origin, idx = row[4], row[2], row[8]
+            assert row[5] == ln
+            assert bytes(payload[idx][:ln]) == orc.payload(origin, bid, ln)
+
+
+def test_storm_matches_reference_fixture(rlo, golden):
+    """Same streams the compiled reference delivered: (bid, origin, parent, data-region hash) per rank."""
+    for case in golden("stream.json")["cases"]:
+        n, seed, k, ln = case["n"], case["seed"], case["k"], case["len"]
+        st, logs = _storm_logged(rlo, n, k, ln, seed)
+        for r in range(n):
+            rows, payload = logs[r]
+            got = sorted([row[4], row[2], row[3], "%016x" % orc.region_hash(bytes(payload[row[8]][:ln]))]
+                         for row in rows if row[0] == LOG_DELIVER)
+            assert got == case["deliveries"][r], (n, r)
+
+
+def test_parent_trees_match_reference(rlo, golden):
+    """One bcast per origin (bid == origin, as the reference harness did): parent == MPI_SOURCE."""
+    fx = golden("parents.json")
+    for ns in ("4", "8", "13", "17", "33", "64", "128", "255", "256", "257"):
+        if ns not in fx["by_n"]:
+            continue
+        n = int(ns)
+        case = fx["by_n"][ns]
+        # storm whose bid b is originated by rank b: pick seeds per bid is not possible, so check
+        # the tree of every origin from a storm that covers every origin at least once
+        seed = 1234
+        k = 0
+        seen = set()
+        while len(seen) < n:
+            seen.add(orc.origin_of(seed, k, n))
+            k += 1
+        st, logs = _storm_logged(rlo, n, k, 64, seed, max_payload=64)
+        parent = {}
+        for r in range(n):
+            for row in logs[r][0]:
+                parent[(row[4], r)] = row[3]
+        for b in range(k):
+            o = orc.origin_of(seed, b, n)
+            for r in range(n):
+                if r != o:
+                    assert parent[(b, r)] == case["parent"][o][r], (n, o, r)
+
+
+@pytest.mark.parametrize("n,k,ln", [(256, 1 << 16, 64), (256, 1 << 14, 4096), (100, 20000, 200), (500, 4000, 64)])
+def test_storm_full_size_checksums(rlo, n, k, ln):
+    with rlo.World(n) as w:
+        w.program_storm(k, ln, seed=0x5EED)
+        w.run()
+        st = w.stats()
+    exp = orc.storm_expected(n, 0x5EED, k, ln)
+    assert (st["error"] == 0).all()
+    assert np.array_equal(st["bcast_delivered"].astype(np.int64), exp["count"])
+    assert np.array_equal(st["bcast_sum"], exp["sum"])
+    assert int(st["originated"].sum()) == k
+
+
+def test_storm_repeatable_across_launches(rlo):
+    with rlo.World(64) as w:
+        w.program_storm(5000, 64, seed=3)
+        sums = []
+        for _ in range(3):
+            w.run()
+            sums.append(w.stats()["bcast_sum"].copy())
+        assert all(np.array_equal(sums[0], s) for s in sums)
+
+
+def test_storm_small_rings_backpressure(rlo):
+    """16-slot rings force constant back-pressure: dateline VCs must keep it deadlock-free."""
+    with rlo.World(64, max_payload=64, ring_slots=16) as w:
+        w.program_storm(20000, 64, seed=11, window=64)
+        w.run()
+        st = w.stats()
+    exp = orc.storm_expected(64, 11, 20000, 64)
+    assert np.array_equal(st["bcast_sum"], exp["sum"])
+    assert int(st["stalls"].sum()) > 0
+
+
+def _iar_device(rlo, n, proposals, judge, mask=None, isp=None):
+    with rlo.World(n) as w:
+        w.program_iar(proposals, judge=judge, mask=mask, isp=isp, log=True, log_cap=4096)
+        w.run()
+        st = w.stats()
+        logs = [w.log(r, cap=4096) for r in range(n)]
+    assert (st["error"] == 0).all(), st["error"]
+    return st, logs
+
+
+def test_iar_single_proposal_matches_reference(rlo, golden):
+    for case in golden("iar.json")["cases"]:
+        n, o, mask = case["n"], case["origin"], case["mask"]
+        prop = ("proposal-from-%d" % o).encode()
+        m = [(mask >> r) & 1 for r in range(n)]
+        st, logs = _iar_device(rlo, n, [(o, 100 + o, prop)], rlo.abi.RLO_JUDGE_MASK, mask=m)
+        judge, actions, pickups, result = [], [], [], []
+        for r in range(n):
+            for kind, tag, origin, frm, pid, ln, vote, aux, _ in logs[r]:
+                if kind == LOG_JUDGE:
+                    judge.append([r, aux, "" if aux else prop.decode()])
+                elif kind == LOG_ACTION:
+                    actions.append([r, pid, vote, aux, prop.decode()])
+                elif kind == LOG_DELIVER and tag == 4:
+                    pickups.append([r, 4, pid, vote, 7, "IAR_DEC", origin])
+                elif kind == LOG_RESULT:
+                    result.append(vote)
+        assert sorted(judge) == case["judge"], case
+        assert sorted(actions) == case["actions"], case
+        assert sorted(pickups) == case["pickups"], case
+        assert result == [case["decision"]]
+
+
+def test_iar_multi_proposal_matches_reference(rlo, golden):
+    for case in golden("multi.json")["cases"]:
+        n, a1, mod, agree = case["n"], case["active_1"], case["mod"], case["agree"]
+        isp, props = [], []
+        for r in range(n):  # testcases.c:417-469
+            if r == a1:
+                isp.append("555"); props.append((r, r, b"555"))
+            elif r % mod == 0:
+                s = "555" if agree else "333"
+                isp.append(s); props.append((r, r, s.encode()))
+            else:
+                isp.append("555" if agree else "111")
+        st, logs = _iar_device(rlo, n, props, rlo.abi.RLO_JUDGE_ISP, isp=isp)
+        pdata = {pid: d.decode() for (_, pid, d) in props}
+        judge, dec, res = [], [], []
+        for r in range(n):
+            for kind, tag, origin, frm, pid, ln, vote, aux, _ in logs[r]:
+                if kind == LOG_JUDGE:
+                    judge.append([r, aux, "" if aux else pdata[pid], vote])
+                elif kind == LOG_DELIVER and tag == 4:
+                    dec.append([r, pid, vote, origin])
+                elif kind == LOG_RESULT:
+                    res.append([r, pid, vote])
+        assert sorted(judge) == case["judge"], case
+        assert sorted(dec) == case["decisions"], case
+        assert sorted(res) == case["results"], case
+
+
+@pytest.mark.parametrize("n,p,ppm", [(8, 20, 0), (64, 8, 50000), (256, 4, 50000), (256, 6, 0)])
+def test_iar_concurrent_all_ranks(rlo, n, p, ppm):
+    """C4 shape: every rank keeps one outstanding proposal; seeded 5% declines."""
+    kind = rlo.abi.RLO_JUDGE_HASH if ppm else rlo.abi.RLO_JUDGE_APPROVE
+    props = [(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)]
+    with rlo.World(n) as w:
+        w.program_iar(props, judge=kind, seed=99, ppm=ppm)
+        w.run()
+        st = w.stats()
+    cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_HASH if ppm else orc.ORC_JUDGE_APPROVE, seed=99, ppm=ppm)
+    ref = orc.iar_bench(n, p, cfg)
+    assert (st["error"] == 0).all()
+    assert int(st["own_decided"].sum()) == ref["decisions"] == n * p
+    assert int(st["own_approved"].sum()) == ref["approved"]
+    assert int(st["actions"].sum()) == ref["actions"]
+    assert int(st["judge_calls"].sum()) == ref["judge_calls"]
+    assert (st["dec_delivered"] == (n - 1) * p).all()
+
+
+def test_latency_program(rlo):
+    n, rounds = 32, 64
+    with rlo.World(n) as w:
+        w.program_latency(rounds, 64, seed=5)
+        w.run()
+        lat = w.latencies_ticks()
+        st = w.stats()
+    assert (st["error"] == 0).all()
+    assert len(lat) == rounds and (lat > 0).all()
+    org = [orc.origin_of(5, i, n) for i in range(rounds)]
+    assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]
