@@ -1,0 +1,88 @@
+"""CPU tests of the C-ABI boundary: the library loads without a GPU, exports every function
+the public headers in include/ declare, and its host-side topology equals the pinned oracle."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(REPO, "include")
+
+
+def declared_functions(header):
+    src = open(os.path.join(INCLUDE, header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r"#[^\n]*", "", src)
+    names = []
+    for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_]*)\s*\(([^;{}()]*(\([^()]*\)[^;{}()]*)*)\)\s*;", src):
+        name = m.group(1)
+        head = src[max(0, m.start() - 80):m.start()]
+        if "typedef" in head.split(";")[-1] or name in ("if", "while", "return", "sizeof"):
+            continue
+        names.append(name)
+    return sorted(set(names))
+
+
+def test_library_loads_without_gpu():
+    import rlo
+
+    assert os.path.exists(rlo.LIB_PATH)
+
+
+@pytest.mark.parametrize("header", sorted(h for h in os.listdir(INCLUDE) if h.endswith(".h")))
+def test_every_declared_symbol_is_exported(header):
+    import rlo
+
+    lib = ctypes.CDLL(rlo.LIB_PATH)
+    names = declared_functions(header)
+    assert names, header
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, (header, missing)
+
+
+def test_python_export_list_matches_header():
+    from rlo import _lib
+
+    assert sorted(_lib.EXPORTS) == declared_functions("rlo_hip.h")
+
+
+def test_world_create_without_gpu_fails_cleanly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import rlo
+
+    with pytest.raises(rlo.RloError):
+        rlo.World(8)
+
+
+def test_topology_matches_oracle():
+    import pyoracle as orc
+    import rlo
+
+    for n in list(range(2, 70)) + [127, 128, 129, 255, 256, 257, 1000, 1024, 4096]:
+        ranks = range(n) if n <= 70 else range(0, n, max(1, n // 40))
+        for r in ranks:
+            assert rlo.topology(n, r) == orc.topology(n, r), (n, r)
+            for o in range(0, n, max(1, n // 9)):
+                for f in [-1] + list(range(0, n, max(1, n // 6))):
+                    assert rlo.children(n, r, o, f) == orc.children(n, r, o, f), (n, r, o, f)
+
+
+def test_children_cover_exact_spanning_tree():
+    """Product topology alone (no GPU): BFS over rlo.children yields each rank exactly once."""
+    import rlo
+
+    for n in (2, 3, 7, 13, 64, 100, 256, 257):
+        for o in range(0, n, max(1, n // 8)):
+            seen = {o}
+            frontier = [(c, o) for c in rlo.children(n, o, o, -1)]
+            while frontier:
+                r, frm = frontier.pop()
+                assert r not in seen, (n, o, r)
+                seen.add(r)
+                frontier += [(c, r) for c in rlo.children(n, r, o, frm)]
+            assert len(seen) == n
