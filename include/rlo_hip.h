@@ -71,6 +71,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 /* ------------------------------------------------------------------ programs */
 #define RLO_FLAG_LOG 1u  /* record every delivery / judge / action / result (+ payload bytes) */
 #define RLO_FLAG_HIST 2u /* per-delivery latency histogram                                  */
+#define RLO_FLAG_PROF 4u /* per-phase cycle accounting (diagnostic)                         */
 
 typedef struct {
     uint64_t seed;       /* originator of bcast b = splitmix64(seed + b) % N              */
@@ -118,6 +119,9 @@ typedef struct {
     uint64_t iterations, busy_iterations, stalls, log_count;
     uint64_t t_start, t_end;
     uint32_t error, error_aux;
+    uint64_t prof[8];  /* RLO_FLAG_PROF: shader cycles per phase (poll, votes+select, classify,
+                          admit, effects, copy, publish) */
+    uint64_t dbg[8];   /* RLO_FLAG_PROF: engine counters (DESIGN.md "Diagnostics") */
     uint32_t hist[128];
 } rlo_rank_stats_t;
 

@@ -1,8 +1,8 @@
 // rlo_device.hpp -- plain-old-data shared by the host world builder (rlo_world.cpp)
 // and the persistent progress kernel (rlo_kernel.hip).
 //
-// One "world" = N virtual ranks.  Every rank is one 256-thread workgroup of the
-// persistent kernel.  Every directed overlay edge (r -> send_list(r)[j]) owns
+// One "world" = N virtual ranks.  Every rank is one 4-wave (256-thread) workgroup
+// of the persistent kernel.  Every directed overlay edge (r -> send_list(r)[j]) owns
 //   * two forward rings (virtual channels vc = 0/1, vc = child < origin; the
 //     "dateline" split that makes the ring channel-dependency graph acyclic),
 //   * one reverse vote ring (child -> parent).
@@ -14,14 +14,15 @@
 
 namespace rlo {
 
-constexpr int kBlock = 256;       // threads per rank-workgroup (4 waves)
+constexpr int kBlock = 256;       // threads per rank-workgroup: 4 waves, one 64-message pass each
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxFanout = 16;    // send_list_len <= ceil(log2 N) <= 16  (N <= 65536)
 constexpr int kMaxIn = 32;        // forward in-edges per rank
 constexpr int kMaxOut = 2 * kMaxFanout;
 constexpr int kHdr = 16;          // slot header bytes
 constexpr int kVoteSlot = 16;     // vote ring slot bytes
-constexpr int kMaxCand = kBlock;  // messages handled per rank per progress iteration
+constexpr int kMaxCand = 256;     // messages handled per rank per progress iteration (4 passes of 64)
+constexpr int kStagePasses = 4;  // 4 x 64 messages per progress iteration
 constexpr int kHistBins = 128;    // latency histogram: 8 sub-bins per octave of 10 ns ticks
 
 // message classes == enum RLO_COMM_TAGS (rootless_ops.h:50-61)
@@ -33,6 +34,7 @@ enum Mode : uint32_t {
     MODE_IAR = 4u,     // every rank runs its proposal list (proposal / vote / decision)
     MODE_LOG = 16u,    // record every event (+ delivered payload bytes) for parity tests
     MODE_HIST = 32u,   // per-delivery latency histogram
+    MODE_PROF = 64u,   // per-phase shader-clock accounting (diagnostic build of the same kernel)
 };
 
 enum Judge : uint32_t { JUDGE_APPROVE = 0, JUDGE_MASK = 1, JUDGE_ISP = 2, JUDGE_HASH = 3 };
@@ -76,6 +78,9 @@ struct RankStats {
     uint64_t iterations, busy_iterations, stalls, log_count;
     uint64_t t_start, t_end;              // s_memrealtime
     uint32_t error, error_aux;
+    uint64_t prof[8];                     // MODE_PROF: s_memtime cycles per phase A..H
+    uint64_t dbg[8];                      // MODE_PROF: ring cands, admitted, storm-allowed iters, storm offered,
+                                          //   shallow-blocked, backlog-blocked, child copies, max out-ring fill
     uint32_t hist[kHistBins];
 };
 
@@ -133,6 +138,11 @@ struct Params {
     uint64_t timeout_ticks;       // no progress for this long -> ERR_TIMEOUT (100 MHz ticks)
     uint64_t deadline_ticks;      // hard cap on one launch (every spin is bounded)
     uint32_t* error_flag;         // any rank's first error
+    // dynamic LDS carve-out: [pend: 2N x 16 B][olist: nout_max x 256 x 2 B]
+    //                        [stage: 256 x nsmall x 16 B][stage2: stage2_bytes]
+    uint32_t nsmall;              // slot chunks staged per message on the small path (<= 8)
+    uint32_t stage2_bytes;        // LDS staging for large messages (multiple of 1 KiB, >= 1 KiB)
+    uint32_t nout_max;            // 2 x max send_list_len over the ranks of this launch
 };
 
 }  // namespace rlo

@@ -1,23 +1,33 @@
 // rlo_kernel.hip -- the persistent progress kernel (gfx950 / CDNA4).
 //
-// One 256-thread workgroup = one virtual rank.  Each progress iteration is the
-// device restatement of make_progress_gen (rootless_ops.c:551-641), batched:
+// One 4-wave (256-thread) workgroup = one virtual rank.  A progress iteration is the
+// device restatement of make_progress_gen (rootless_ops.c:551-641), batched: up to 256
+// messages, wave w owning messages [64w, 64w + 64):
 //
-//   A  poll     : one relaxed agent-scope load per in-ring tail / out-ring head
-//                 (replaces MPI_Test of the single ANY_SOURCE irecv, :643-650)
-//   B  votes    : drain every vote ring; LDS-atomic AND-merge (_iar_vote_handler :743-812)
-//   C  select   : up to 256 messages: the in-ring backlog (FIFO per ring), then
-//                 local originations (RLO_bcast_gen :1581, own proposal / decision)
-//   D  classify : header load, skip-ring child set relative to the dynamic origin
-//                 (_bc_forward :1104-1225), device judge for proposals (:698)
-//   E  admit    : per out-ring positions by wave ballots; credit check; FIFO prefix
-//   F  effects  : deliveries (pickup), proposal state, decisions + actions (:814-859), votes up (:728)
-//   G  copy     : wave-wide 16-byte chunks: one write-through (sc1) load, one sc1 store per child
-//   H  publish  : every wave drains vmcnt, barrier, relaxed agent-scope tail/head stores
+//   A  poll     : wave 0 loads the packed inbox tails / outbox heads (replaces MPI_Test of the
+//                 single ANY_SOURCE irecv, :643-650); every wave drains its own stores
+//   C  select   : wave 0 publishes the previous iteration's counters, then takes fair per-ring
+//                 quotas of the in-ring backlog (FIFO per ring) and the local originations
+//                 (RLO_bcast_gen :1581, own proposal :876, decision :908)
+//   B  votes    : wave 1 loads every vote slot that arrived and AND-merges them with LDS
+//                 atomics (_iar_vote_handler :743-812); completed merges vote up (:728-741)
+//   D  stage    : each wave pulls its messages' slots into LDS with LDS-DMA, coalesced
+//                 (consecutive messages of an in-ring are consecutive slots), ONE round trip;
+//                 skip-ring children relative to the dynamic origin (_bc_forward :1104-1225),
+//                 device judge for proposals (:698)
+//   E  admit    : per out-ring positions from wave ballots + cross-wave prefixes in LDS; credit
+//                 check; FIFO prefix per source (head-of-line order of a ring); every admitted
+//                 message gets its slot index in each out-ring it goes to (olist)
+//   F  effects  : deliveries (pickup), proposal state, decisions + actions (:814-859)
+//   G  copy     : per out-ring, the admitted messages occupy consecutive slots: lanes take
+//                 (message, chunk) items so every store writes contiguous slot bytes; large
+//                 messages are staged first (loads before stores: vmcnt is in-order on CDNA)
 //
-// Memory ordering (MI355X_MICROARCH.md "Valid forms", row 1): payload stores and
-// loads are all sc1 (L1-bypassing, written through), each storing wave drains
-// vmcnt(0) before the workgroup barrier, then one lane stores the counter.
+// Inside the workgroup synchronisation is s_barrier + LDS waits (BAR), never a vmcnt drain:
+// payload stores stay in flight until the next iteration's poll has been issued.
+// Memory ordering across ranks (MI355X_MICROARCH.md "Valid forms", row 1): every handed-off
+// byte is stored sc1 and loaded sc1; each storing wave drains vmcnt(0) before the barrier
+// that precedes the counter store.
 #include <hip/hip_runtime.h>
 
 #include "rlo_device.hpp"
@@ -29,73 +39,81 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 static constexpr int kAuxSc1 = 16;  // cache policy: sc1 (agent scope, write-through / L1 bypass)
 static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
+static constexpr int kPass = 64;  // messages per wave per iteration
 
-enum CandKind : uint8_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_BAD = 7 };
-static constexpr int kGroupLocal = 2 * kMaxIn;   // groups [0, 64) = in-rings (k*2+vc); 64.. local kinds
+enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_BAD = 7 };
+static constexpr int kGroupLocal = 2 * kMaxIn;  // groups [0, 64) = in-rings (k*2+vc); 64.. local kinds
 static constexpr int kGroups = kGroupLocal + 8;
-static constexpr int kMaxVoteEmit = 2 * kMaxCand;
-
-struct Cand {
-    uint32_t src;     // K_RING: byte offset of the slot in the forward region; K_PROP: proposal index
-    uint32_t w0;      // origin | tag << 16 | vote << 24
-    uint32_t id;      // bcast id / pid
-    uint32_t w2;      // len | pseq << 24
-    uint32_t t0;
-    uint32_t need;    // out-ring bits oi = j*2 + vc
-    uint32_t kids;    // child bits j
-    uint32_t logidx;  // log record of this delivery (payload capture) or ~0u
-    int16_t from;     // sender rank (-1: originated here)
-    uint8_t group;
-    uint8_t kind;
-    int32_t judge;    // proposals: judge result
-};
+static constexpr uint16_t kBigFlag = 0x8000u;
 
 struct PendState {      // a proposal held at a non-originator (queue_iar_pending, :1138)
     int32_t pid;
     uint32_t word;      // votes received (low 16 b) | zero votes (high 16 b)
-    uint16_t parent_k;  // in-edge the proposal came from (vote goes back on it)
+    uint16_t parent_k;  // in-edge the proposal came from (the vote goes back on it)
     uint8_t needed;     // fwd_send_cnt (:694)
     uint8_t valid;
-    uint32_t pseq;
+    uint32_t pseq;      // proposal sequence (low 8 b) | proposal data_len << 8
 };
 
-struct VoteEmit {
-    uint32_t k, w0, pid, pseq;
+struct CandL {          // one message of this iteration, kept for the copy phase
+    uint32_t w0, id, w2, t0;  // slot header (forwarded unchanged)
+    uint32_t src;       // K_RING: slot byte offset in the forward region; K_PROP: proposal index
+    uint32_t need;      // admitted out-ring bits (2j + vc); 0 when not admitted
+    uint32_t logidx;    // log record of this delivery (payload capture) or ~0u
+    uint32_t kind, group;
 };
 
 struct Shared {
     RankTopo t;
-    uint64_t in_head[2 * kMaxIn], in_tail[2 * kMaxIn];
-    uint64_t out_tail[kMaxOut], out_head[kMaxOut], out_tail0[kMaxOut];
-    uint64_t vin_head[kMaxFanout], vin_tail[kMaxFanout];
-    uint64_t vout_tail[kMaxIn], vout_head[kMaxIn];
-    Cand cand[kMaxCand];
-    uint16_t pos[kMaxCand][kMaxFanout];
-    uint32_t ring_base[2 * kMaxIn + 1], ring_take[2 * kMaxIn];
-    uint32_t vbase[kMaxFanout + 1];
-    uint32_t wave_cnt[kWaves][kMaxOut];
+    // selection of this iteration (wave 0)
+    uint64_t ring_head[2 * kMaxIn];  // consumer count of in-ring g at iteration start
+    uint32_t ring_base[2 * kMaxIn], ring_take[2 * kMaxIn];
+    uint64_t ract;                   // in-rings with candidates
+    uint64_t out_tail0[kMaxOut];     // producer count of out-ring oi at iteration start
+    uint32_t ofree[kMaxOut];         // free slots of out-ring oi at iteration start
+    uint32_t n_oi[kMaxOut];          // slots admitted into out-ring oi this iteration
+    uint32_t R, C, nstorm, storm_base, loc_kind, lat_id, exit_now;
+    int64_t prop_idx;
+    uint32_t storm_ids[kPass];
+    uint64_t vhead[kMaxFanout];
+    uint32_t vbase[kMaxFanout], va[kMaxFanout], vtot;
+    // admission
+    uint32_t wcnt[kWaves][kMaxOut];
     uint32_t first_bad[kGroups];
-    uint32_t cum[kMaxCand + 1];
-    uint32_t wave_sum[kWaves];
-    VoteEmit vemit[kMaxVoteEmit];
-    uint32_t nvemit;
-    uint32_t ncand, nring, nvote, nlocal_storm;
+    CandL cand[kMaxCand];
+    uint16_t pos[kMaxCand][kMaxFanout];  // large messages: slot in out-ring (j, vc) relative to tail0
+    uint16_t big[kMaxCand];              // admitted messages too large for the stage path
+    uint32_t nbig, bm, bq0, nblk;
+    uint32_t blk_c[64], blk_q0[64];      // large-message blocks staged in stage2
+    // vote rings towards my parents (LDS atomics from every wave)
+    uint64_t vout_tail[kMaxIn], vout_head[kMaxIn];
     // own proposal (my_own_proposal, :241)
     int32_t own_pid;
     uint32_t own_word, own_needed, own_state, own_decision, own_pseq;
     int64_t own_iter, own_n;
     // origination progress
     int64_t sched_next, sched_n;
-    uint32_t lat_next;
+    uint32_t lat_next, done, error, error_aux, progressed;
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, iterations, busy, stalls;
-    uint32_t error, error_aux, done, progressed;
-    uint64_t last_progress;
+    uint64_t prof[8], prof_t, dbg[8];
+    int64_t expect_bcast, expect_dec;
     uint32_t hist[kHistBins];
 };
 
 // ------------------------------------------------------------------ helpers
+
+// Workgroup barrier without the global-memory fence of __syncthreads() (which would wait for
+// every in-flight payload store): only this wave's LDS results must have landed.  The "memory"
+// clobbers keep the compiler from moving memory accesses across it.
+#define BAR()                                              \
+    do {                                                   \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        __builtin_amdgcn_s_barrier();                      \
+        asm volatile("" ::: "memory");                     \
+    } while (0)
+#define VM_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
@@ -109,6 +127,13 @@ __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, u
 __device__ __forceinline__ uint8_t ld8_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, kAuxSc1);
 }
+__device__ __forceinline__ __attribute__((address_space(3))) void* lds_ptr(uint8_t* p) {
+    return (__attribute__((address_space(3))) void*)(p);
+}
+// LDS-DMA: 64 lanes x 16 B of the forward region -> LDS (lane i lands at dst + 16 i; dst uniform)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t* dst, uint32_t off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_ptr(dst), 16, off, 0, 0, kAuxSc1);
+}
 __device__ __forceinline__ uint64_t poll64(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -120,6 +145,23 @@ __device__ __forceinline__ uint32_t poll32(uint32_t* p) {
 }
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
+// per-ring state lives lane-distributed in registers; a wave-uniform index reads it with v_readlane
+__device__ __forceinline__ uint32_t rdl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// i / d for the small d = nsmall (<= 8) and i < 2^16: multiply-high by ceil(2^32 / d)
+__device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { return magic ? __umulhi(i, magic) : i; }
+
+// MODE_PROF: thread 0 charges the shader cycles since the last stamp to phase `ph`
+#define PROF_STAMP(ph)                                  \
+    do {                                                \
+        if ((P.mode & MODE_PROF) && tid == 0) {         \
+            uint64_t c_ = __builtin_amdgcn_s_memtime(); \
+            S.prof[ph] += c_ - S.prof_t;                \
+            S.prof_t = c_;                              \
+        }                                               \
+    } while (0)
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + kGolden64;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -127,7 +169,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-// storm payload word k (DESIGN.md "storm workload"; the oracle's rlo_testvec.h states the same)
+// storm payload word k (DESIGN.md "Storm workload"; the oracle's rlo_testvec.h states the same)
 __device__ __forceinline__ uint64_t storm_word(uint32_t origin, uint32_t bid, uint32_t k) {
     uint64_t w0 = ((uint64_t)bid << 32) | origin;
     return k == 0 ? w0 : splitmix64(w0 ^ ((uint64_t)k * kGolden64));
@@ -145,7 +187,7 @@ __device__ __forceinline__ uint32_t chunk_mix(uint32_t q, u32x4 w) {
     return fmix32(w.x ^ fmix32(w.y ^ fmix32(w.z ^ fmix32(w.w ^ (q * kGolden32 + 0x7F4A7C15u)))));
 }
 
-__device__ __forceinline__ uint32_t mask_bytes(uint32_t w, int keep) {  // keep low `keep` bytes
+__device__ __forceinline__ uint32_t mask_bytes(uint32_t w, int keep) {  // keep the low `keep` bytes
     return keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
 }
 
@@ -160,31 +202,33 @@ __device__ __forceinline__ bool passed_origin(int me, int origin, int to) {
     return !(to > me && to < origin);
 }
 
-// child index set j of send_list: originate (:1587) or _bc_forward (:1116-1223)
-__device__ __forceinline__ uint32_t children(const RankTopo& t, int me, int origin, int from) {
-    if (from < 0) return (1u << t.sll) - 1u;
-    if (t.level <= 0) return 0u;
-    if (from > t.last_wall) return (1u << (t.scc + 1)) - 1u;
+// child index set j of send_list: originate (:1587) or _bc_forward (:1116-1223); sl_r = send_list
+// distributed over lanes
+__device__ __forceinline__ uint32_t kids_of(int me, int origin, int from, int level, int last_wall, int scc, int sll,
+                                            uint32_t sl_r) {
+    if (from < 0) return (1u << sll) - 1u;
+    if (level <= 0) return 0u;
+    if (from > last_wall) return (1u << (scc + 1)) - 1u;
     uint32_t m = 0;
-    for (int j = t.scc - 1; j >= 0; j--)
-        if (!passed_origin(me, origin, t.send_list[j])) m |= 1u << j;
+    for (int j = 0; j < scc; j++)
+        if (!passed_origin(me, origin, (int)rdl32(sl_r, j))) m |= 1u << j;
     return m;
 }
 
-__device__ __forceinline__ uint32_t need_bits(const RankTopo& t, uint32_t kids, int origin) {
+// out-ring bits oi = 2j + vc; vc = 1 once the message has wrapped past rank N-1 (child < origin):
+// the "dateline" virtual channel that keeps the ring dependency graph acyclic
+__device__ __forceinline__ uint32_t need_of(uint32_t kids, int origin, int sll, uint32_t sl_r) {
     uint32_t need = 0;
-    while (kids) {
-        int j = __builtin_ctz(kids);
-        kids &= kids - 1;
-        need |= 1u << (2 * j + (t.send_list[j] < origin ? 1 : 0));
-    }
+    for (int j = 0; j < sll; j++)
+        if ((kids >> j) & 1u) need |= 1u << (2 * j + ((int)rdl32(sl_r, j) < origin ? 1 : 0));
     return need;
 }
 
+// latency histogram of 10 ns ticks: values < 4 exact, then 4 sub-bins per octave (to ~2^33 ticks)
 __device__ __forceinline__ uint32_t hist_bin(uint64_t d) {
-    if (d < 8) return (uint32_t)d;
+    if (d < 4) return (uint32_t)d;
     int o = 63 - __builtin_clzll(d);
-    uint32_t b = (uint32_t)(o - 2) * 8u + (uint32_t)((d >> (o - 3)) & 7u);
+    uint32_t b = (uint32_t)(o - 1) * 4u + (uint32_t)((d >> (o - 2)) & 3u);
     return b < kHistBins ? b : kHistBins - 1;
 }
 
@@ -199,15 +243,14 @@ __device__ __forceinline__ uint32_t judge_hash(uint64_t seed, uint32_t rank, int
     return (uint32_t)(splitmix64(seed ^ ((uint64_t)rank << 32) ^ (uint32_t)pid) % 1000000u);
 }
 
-// device judge registry; arg_off = byte offset of the proposal data in the forward region
-// (data_len bytes, zero-extended: the reference's calloc'd receive buffer).  testcases.c:18-37
-// for ISP.  The originator's final call passes NULL (rootless_ops.c:773): every device judge
-// approves NULL.
-__device__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, int32_t pid, uint32_t arg_off,
-                          uint32_t data_len) {
+// device judge registry.  arg = proposal data at byte offset arg_off of the forward region,
+// data_len bytes, zero-extended (the reference's calloc'd receive buffer).  ISP restates
+// testcases.c:18-37.  The originator's final call passes NULL (:773): device judges approve it.
+__device__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, uint32_t my_mask, int32_t pid,
+                          uint32_t arg_off, uint32_t data_len) {
     switch (P.judge_kind) {
         case JUDGE_MASK:
-            return P.judge_mask[me] ? 0 : 1;
+            return my_mask ? 0 : 1;
         case JUDGE_HASH:
             return judge_hash(P.judge_seed, me, pid) < P.judge_ppm ? 0 : 1;
         case JUDGE_ISP: {
@@ -247,53 +290,99 @@ __device__ __forceinline__ uint32_t log_put(Shared& S, const Params& P, int lr, 
     return r.payload_idx;
 }
 
-__device__ __forceinline__ void emit_vote(Shared& S, const Params& P, uint32_t k, int origin, int32_t pid, uint32_t pseq,
-                                          int vote) {
-    uint32_t i = atomicAdd(&S.nvemit, 1u);
-    if (i >= kMaxVoteEmit) {
-        set_error(S, P, ERR_VOTE_RING, 0xffffffffu);
+// vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741)
+__device__ __forceinline__ void emit_vote(Shared& S, const Params& P, __amdgpu_buffer_rsrc_t rv, int me, uint32_t k,
+                                          int origin, int32_t pid, uint32_t pseq, int vote) {
+    unsigned long long p = atomicAdd((unsigned long long*)&S.vout_tail[k], 1ull);
+    if (p - S.vout_head[k] >= P.vote_cap) {
+        set_error(S, P, ERR_VOTE_RING, k);
         return;
     }
-    S.vemit[i].k = k;
-    S.vemit[i].w0 = (uint32_t)origin | ((uint32_t)(vote & 0xff) << 24);
-    S.vemit[i].pid = (uint32_t)pid;
-    S.vemit[i].pseq = pseq;
+    u32x4 v;
+    v.x = (uint32_t)origin | ((uint32_t)(vote & 0xff) << 24);
+    v.y = (uint32_t)pid;
+    v.z = pseq & 0xffu;
+    v.w = (uint32_t)me;
+    st_sc1(rv, S.t.vout_data[k] + (uint32_t)(p & (P.vote_cap - 1)) * kVoteSlot, v);
 }
 
-__device__ __forceinline__ uint32_t block_excl_scan(Shared& S, uint32_t v, uint32_t* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// exclusive wave-wide prefix sum with DPP row shifts + row broadcasts (no LDS traffic)
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
     uint32_t x = v;
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    return x - v;
+}
+
+// payload chunk q >= 1 of a locally originated message (payload bytes [16(q-1), 16q))
+__device__ __forceinline__ u32x4 gen_chunk(const Params& P, uint32_t kind, int me, uint32_t id, uint32_t len,
+                                           uint32_t src, int vote, uint32_t q) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (kind == K_STORM || kind == K_LAT) {
+        const uint32_t k0 = 2u * (q - 1u);
+        const int b0 = (int)len - (int)(8u * k0);
+        uint64_t a = b0 > 0 ? storm_word((uint32_t)me, id, k0) : 0ull;
+        uint64_t b = b0 > 8 ? storm_word((uint32_t)me, id, k0 + 1u) : 0ull;
+        v.x = mask_bytes((uint32_t)a, b0);
+        v.y = mask_bytes((uint32_t)(a >> 32), b0 - 4);
+        v.z = mask_bytes((uint32_t)b, b0 - 8);
+        v.w = mask_bytes((uint32_t)(b >> 32), b0 - 12);
+    } else if (kind == K_PROP) {  // PBuf [pid][vote=1][data_len u64][data] (:1369-1396)
+        const uint32_t dl = P.prop_data_len[src];
+        if (q == 1) {
+            v.x = id; v.y = 1u; v.z = dl; v.w = 0u;
+        } else {
+            const uint8_t* d = P.prop_data + P.prop_data_off[src];
+            uint32_t w[4];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
+            for (int e = 0; e < 4; e++) {
+                uint32_t x = 0;
+                for (int bb = 0; bb < 4; bb++) {
+                    uint32_t idx = 16u * (q - 2u) + 4u * e + bb;
+                    if (idx < dl) x |= (uint32_t)d[idx] << (8 * bb);
+                }
+                w[e] = x;
+            }
+            v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
+        }
+    } else if (kind == K_DEC) {  // PBuf(pid, decision, 7, "IAR_DEC") (:908-917)
+        if (q == 1) {
+            v.x = id; v.y = (uint32_t)vote; v.z = 7u; v.w = 0u;
+        } else if (q == 2) {
+            v.x = 0x5F524149u; v.y = 0x00434544u;
+        }
     }
-    if (lane == 63) S.wave_sum[wave] = x;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; w++) {
-        if (w < wave) off += S.wave_sum[w];
-        tot += S.wave_sum[w];
-    }
-    *total = tot;
-    return off + x - v;
+    return v;
 }
 
 // ------------------------------------------------------------------ the kernel
 
-__global__ __launch_bounds__(kBlock, 1) void rlo_progress_kernel(Params P) {
+__global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     __shared__ Shared S;
-    PendState* pend = reinterpret_cast<PendState*>(dyn_lds);  // [2 * n]
+    const uint32_t nsmall = P.nsmall;  // chunks per staged message
+    const uint32_t nmagic = nsmall > 1 ? 0xFFFFFFFFu / nsmall + 1u : 0u;
+    PendState* pend = reinterpret_cast<PendState*>(dyn_lds);                        // [2 * n]
+    uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + 32u * (uint32_t)P.n);  // [oi][256]
+    uint8_t* stage = dyn_lds + 32u * (uint32_t)P.n + P.nout_max * 512u;             // [message][q] x 16 B
+    uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
+    const uint32_t s2_blocks = P.stage2_bytes / 1024u;
+#define STG(c, q) (stage + (((uint32_t)(c) * nsmall + (uint32_t)(q)) << 4))
+#define OL(oi, r) olist[((uint32_t)(oi) << 8) + (uint32_t)(r)]
 
     const int lr = blockIdx.x;
     const int me = P.rank_begin + lr;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1;
+    const uint32_t my_mask = ((P.mode & MODE_IAR) && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
 
     // ---------------- init
     {
@@ -302,12 +391,10 @@ __global__ __launch_bounds__(kBlock, 1) void rlo_progress_kernel(Params P) {
         for (int i = tid; i < (int)(sizeof(RankTopo) / 4); i += kBlock) dst[i] = src[i];
         for (int i = tid; i < 2 * P.n; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
         for (int i = tid; i < kHistBins; i += kBlock) S.hist[i] = 0;
-        if (tid < 2 * kMaxIn) { S.in_head[tid] = 0; S.in_tail[tid] = 0; }
-        if (tid < kMaxOut) { S.out_tail[tid] = 0; S.out_head[tid] = 0; }
-        if (tid < kMaxFanout) { S.vin_head[tid] = 0; S.vin_tail[tid] = 0; }
         if (tid < kMaxIn) { S.vout_tail[tid] = 0; S.vout_head[tid] = 0; }
+        if (tid < 8) { S.prof[tid] = 0; S.dbg[tid] = 0; }
         if (tid == 0) {
-            S.nvemit = 0;
+            S.prof_t = __builtin_amdgcn_s_memtime();
             S.own_pid = -1;  // proposal_state_init, :1238
             S.own_word = 0; S.own_needed = 0; S.own_state = 0; S.own_decision = 0; S.own_pseq = 0;
             S.own_iter = 0;
@@ -315,516 +402,621 @@ __global__ __launch_bounds__(kBlock, 1) void rlo_progress_kernel(Params P) {
             S.sched_next = 0;
             S.sched_n = (P.mode & MODE_STORM) ? (P.sched_off[lr + 1] - P.sched_off[lr]) : 0;
             S.lat_next = 0;
+            S.expect_bcast = (P.mode & (MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
+            S.expect_dec = (P.mode & MODE_IAR) ? P.expect_dec[lr] : 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.iterations = S.busy = S.stalls = 0;
-            S.error = 0; S.error_aux = 0; S.done = 0;
-            S.last_progress = now_ticks();
+            S.error = 0; S.error_aux = 0; S.done = 0; S.exit_now = 0; S.progressed = 0;
         }
     }
-    __syncthreads();
+    BAR();
     const uint64_t t_start = now_ticks();
     unsigned long long acc_sum = 0;  // checksum of delivered bcast chunks (this thread's share)
 
+    // topology: wave-uniform scalars + lane-distributed tables (constant for the launch)
+    const RankTopo& t = S.t;
+    const int level = uni(t.level), last_wall = uni(t.last_wall), scc = uni(t.scc), sll = uni(t.sll);
+    const int n_in = uni(t.n_in), n_in2 = 2 * n_in, nout = 2 * sll;
+    const uint32_t inbox = (uint32_t)uni((int)t.inbox_ctrl), outbox = (uint32_t)uni((int)t.outbox_ctrl);
+    const uint32_t sl_r = lane < sll ? (uint32_t)t.send_list[lane] : 0u;
+    const uint32_t od_r = lane < nout ? t.out_data[lane >> 1][lane & 1] : 0u;  // out-ring data offset
+    // wave 0 owns the ring counters: lane g = in-ring g, lane oi = out-ring oi, lane j = vote ring j
+    const uint32_t otix_r = lane < nout ? t.out_tail[lane >> 1][lane & 1] : 0u;  // where its tail is published
+    const uint32_t ihix_r = lane < n_in2 ? t.in_head[lane >> 1][lane & 1] : 0u;  // where its head is published
+    const uint32_t vhix_r = lane < sll ? t.vin_head[lane] : 0u;
+    const uint32_t vtix_r = lane < n_in ? t.vout_tail[lane] : 0u;
+    uint64_t in_head_r = 0, pub_in_r = 0, out_tail_r = 0, pub_out_r = 0, vin_head_r = 0, pub_vin_r = 0, pub_vout_r = 0;
+    // per in-ring window: messages worth staging next iteration.  A ring whose prefix was cut by
+    // out-ring credits is re-staged only a little past what fitted, so a hot rank does not pull
+    // (and classify) hundreds of messages per iteration that cannot leave anyway
+    uint32_t win_r = kMaxCand;
+    bool peer_failed = false;
+    uint64_t idle_since = 0;
+    uint32_t idle_n = 0;
+
     for (;;) {
-        const RankTopo& t = S.t;
-        const int n_in2 = 2 * t.n_in;
-        // ---------------- A: poll
-        if (tid < (int)t.n_inbox) {
-            uint64_t v = poll64(&P.ctrl[t.inbox_ctrl + tid]);
-            if (tid < n_in2) S.in_tail[tid] = v;
-            else S.vin_tail[tid - n_in2] = v;
-        } else if (tid >= 128 && tid - 128 < (int)t.n_outbox) {
-            int i = tid - 128;
-            uint64_t v = poll64(&P.ctrl[t.outbox_ctrl + i]);
-            if (i < 2 * t.sll) S.out_head[i] = v;
-            else S.vout_head[i - 2 * t.sll] = v;
+        // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
+        uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
+        uint32_t errf = 0, sid = 0;
+        if (w == 0) {
+            if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
+            if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
+            if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
+            if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
+            if (lane == 0) errf = poll32(P.error_flag);
+            const int64_t sn = S.sched_next;
+            if ((P.mode & MODE_STORM) && sn + lane < S.sched_n && (uint32_t)lane < P.window)
+                sid = P.sched_ids[P.sched_off[lr] + sn + lane];
         }
-        if (tid == 0) { S.nvemit = 0; S.progressed = 0; }
-        __syncthreads();
+        VM_DRAIN();
+        BAR();  // every payload / vote store of the previous iteration has left its wave
+        PROF_STAMP(0);
 
-        // ---------------- B: votes (children -> me)
-        if (tid == 0) {
-            uint32_t v = 0;
-            for (int j = 0; j < t.sll; j++) {
-                S.vbase[j] = v;
-                uint64_t a = S.vin_tail[j] - S.vin_head[j];
-                uint32_t room = kMaxCand - v;
-                v += a < room ? (uint32_t)a : room;  // at most 256 votes per iteration
+        // ---------------- C (wave 0): publish the previous iteration, select this one
+        if (w == 0) {
+            if (lane < nout && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(&P.ctrl[otix_r], out_tail_r); }
+            if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(&P.ctrl[ihix_r], in_head_r); }
+            if (lane < sll && vin_head_r != pub_vin_r) { pub_vin_r = vin_head_r; pub64(&P.ctrl[vhix_r], vin_head_r); }
+            if (lane < n_in) {
+                const uint64_t vt = S.vout_tail[lane];
+                if (vt != pub_vout_r) { pub_vout_r = vt; pub64(&P.ctrl[vtix_r], vt); }
+                S.vout_head[lane] = vout_head_r;
             }
-            S.vbase[t.sll] = v;
-            S.nvote = v;
-        }
-        __syncthreads();
-        const uint32_t nvote = S.nvote;
-        if (nvote) {
-            for (uint32_t i = tid; i < nvote; i += kBlock) {
-                int j = 0;
-                while (i >= S.vbase[j + 1]) j++;
-                uint64_t slot = S.vin_head[j] + (i - S.vbase[j]);
-                u32x4 v = ld_sc1(rv, t.vin_data[j] + (uint32_t)(slot & vcap_m) * kVoteSlot);
-                int origin = (int)(v.x & 0xffffu);
-                int vote = (int)(int8_t)(v.x >> 24);
-                int32_t pid = (int32_t)v.y;
-                uint32_t pseq = v.z;
-                if (origin >= P.n) {
-                    set_error(S, P, ERR_BAD_SLOT, v.x);
-                    continue;
-                }
-                uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
-                if (origin == me) {  // a vote for my own proposal (:756-783)
-                    if (S.own_state != 1 || pid != S.own_pid) {
-                        set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
-                        continue;
-                    }
-                    uint32_t old = atomicAdd(&S.own_word, inc);
-                    uint32_t nw = old + inc;
-                    if ((nw & 0xffffu) == S.own_needed) {
-                        int d = (nw >> 16) == 0 ? 1 : 0;
-                        if (d) {  // final judge(NULL) (:770-775)
-                            d = 1;
-                            atomicAdd(&S.judge_calls, 1ull);
-                            log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, d, 1);
-                        }
-                        S.own_decision = (uint32_t)d;
-                        S.own_state = 2;
-                    }
-                } else {  // _vote_merge (:1056-1070)
-                    PendState* ps = &pend[2 * origin + (pseq & 1u)];
-                    if (!ps->valid || ps->pid != pid) {
-                        set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
-                        continue;
-                    }
-                    uint32_t old = atomicAdd(&ps->word, inc);
-                    uint32_t nw = old + inc;
-                    if ((nw & 0xffffu) == ps->needed) emit_vote(S, P, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
-                }
+            peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
+            // votes to merge (wave 1), at most 256 per iteration: trim the ring prefixes
+            const uint32_t va = lane < sll ? (uint32_t)min(vin_tail_r - vin_head_r, (uint64_t)256) : 0u;
+            uint32_t vtot = 0, vex = 0;
+            if (__ballot(va > 0)) vex = wave_excl_scan(va, &vtot);
+            uint32_t vtake = va;
+            if (vtot > 256u) {
+                vtake = vex >= 256u ? 0u : (vex + va > 256u ? 256u - vex : va);
+                vtot = 256u;
             }
-        }
-
-        __syncthreads();
-
-        // ---------------- C: select candidates (thread 0)
-        if (tid == 0) {
-            uint32_t n = 0;
+            if (lane < sll) { S.vbase[lane] = vex; S.va[lane] = vtake; S.vhead[lane] = vin_head_r; }
+            vin_head_r += vtake;  // merged by wave 1 before the next publish
+            // in-rings: fair per-ring quotas
+            const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)256) : 0u;
             const uint32_t reserve = (P.mode & MODE_IAR) ? 2u : 0u;
-            // fair share: rotate which in-ring may fill the batch first (no ring starves)
-            uint32_t* take_g = S.ring_take;
-            const int g0 = n_in2 ? (int)(S.iterations % (uint64_t)n_in2) : 0;
-            for (int i = 0; i < n_in2; i++) {
-                const int g = (g0 + i) % n_in2;
-                uint64_t a = S.in_tail[g] - S.in_head[g];
-                uint32_t room = kMaxCand - reserve - n;
-                uint32_t take = a < room ? (uint32_t)a : room;
-                take_g[g] = take;
-                n += take;
+            const uint64_t ract = __ballot(ra > 0);
+            const int nact = __popcll(ract);
+            const uint32_t quota = nact ? (kMaxCand - reserve) / (uint32_t)nact : 0u;
+            const uint32_t take = min(min(ra, quota), win_r);
+            const bool backlog = __ballot(ra > take) != 0;
+            uint32_t R;
+            const uint32_t base = wave_excl_scan(take, &R);
+            if (lane < n_in2) { S.ring_base[lane] = base; S.ring_take[lane] = take; S.ring_head[lane] = in_head_r; }
+            if (lane < nout) {
+                S.out_tail0[lane] = out_tail_r;
+                S.ofree[lane] = P.fwd_cap - (uint32_t)(out_tail_r - out_head_r);
+                S.n_oi[lane] = 0;
             }
-            n = 0;
-            for (int g = 0; g < n_in2; g++) {  // candidates stay grouped by ring, in ring order
-                S.ring_base[g] = n;
-                n += take_g[g];
-            }
-            S.ring_base[n_in2] = n;
-            S.nring = n;
-            // own proposal / decision (RLO_submit_proposal :876, _iar_decision_bcast :908)
+            if (lane < kGroups) S.first_bad[lane] = 0xffffffffu;
+            if (lane + 64 < kGroups) S.first_bad[lane + 64] = 0xffffffffu;
+            // local originations
+            uint32_t C = R, loc_kind = 0, nstorm = 0, storm_base = 0, lat_id = 0xffffffffu;
+            int64_t prop_idx = -1;
             if (P.mode & MODE_IAR) {
-                if (S.own_state == 2) {
-                    Cand& c = S.cand[n++];
-                    c.kind = K_DEC;
-                    c.group = kGroupLocal + K_DEC;
-                    c.id = (uint32_t)S.own_pid;
-                    c.w0 = (uint32_t)me | (TAG_DECISION << 16) | ((S.own_decision & 0xffu) << 24);
-                    c.w2 = 23u | (S.own_pseq << 24);
-                } else if (S.own_state == 0 && S.own_iter < S.own_n) {
-                    int64_t pi = P.prop_off[lr] + S.own_iter;
-                    Cand& c = S.cand[n++];
-                    c.kind = K_PROP;
-                    c.group = kGroupLocal + K_PROP;
-                    c.src = (uint32_t)pi;
-                    c.id = (uint32_t)P.prop_pid[pi];
-                    c.w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
-                    c.w2 = (16u + P.prop_data_len[pi]) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                if (S.own_state == 2) { loc_kind = K_DEC; C++; }
+                else if (S.own_state == 0 && S.own_iter < S.own_n) { loc_kind = K_PROP; prop_idx = P.prop_off[lr] + S.own_iter; C++; }
+            }
+            if ((P.mode & MODE_STORM) && S.sched_next < S.sched_n) {
+                // throttle: originate only into shallow out-rings so forwarding never waits behind originations
+                const bool deep = lane < nout && (out_tail_r - out_head_r) * 2 >= P.fwd_cap;
+                const bool allow = !backlog && R < 2 * kPass && __ballot(deep) == 0;
+                if ((P.mode & MODE_PROF) && lane == 0) { if (!allow) S.dbg[5]++; else S.dbg[2]++; }
+                if (allow) {
+                    const int64_t rem = S.sched_n - S.sched_next;
+                    uint32_t ww = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
+                    if (ww > kMaxCand - C) ww = kMaxCand - C;
+                    storm_base = C;
+                    nstorm = ww;
+                    C += ww;
+                    if ((uint32_t)lane < ww) S.storm_ids[lane] = sid;
                 }
             }
-            // storm originations (RLO_msg_new_bc + RLO_bcast_gen)
-            S.nlocal_storm = 0;
-            if (P.mode & MODE_STORM) {
-                int64_t rem = S.sched_n - S.sched_next;
-                uint32_t w = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
-                if (w > kMaxCand - n) w = kMaxCand - n;
-                const uint32_t* ids = P.sched_ids + P.sched_off[lr] + S.sched_next;
-                for (uint32_t i = 0; i < w; i++) {
-                    Cand& c = S.cand[n++];
-                    c.kind = K_STORM;
-                    c.group = kGroupLocal + K_STORM;
-                    c.id = ids[i];
-                }
-                S.nlocal_storm = w;
-            }
-            if ((P.mode & MODE_LAT) && S.lat_next < P.lat_rounds && n < kMaxCand) {
-                uint32_t r = poll32(P.lat_round);
+            if ((P.mode & MODE_LAT) && C < kMaxCand) {
                 while (S.lat_next < P.lat_rounds && P.lat_origin[S.lat_next] != me) S.lat_next++;
-                if (S.lat_next < P.lat_rounds && r == S.lat_next) {
-                    Cand& c = S.cand[n++];
-                    c.kind = K_LAT;
-                    c.group = kGroupLocal + K_LAT;
-                    c.id = S.lat_next;
-                }
+                if (S.lat_next < P.lat_rounds && poll32(P.lat_round) == S.lat_next) { lat_id = S.lat_next; C++; }
             }
-            S.ncand = n;
+            if (lane == 0) {
+                S.ract = ract;
+                S.vtot = vtot;
+                S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
+                S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = 0;
+                S.exit_now = S.done;
+                if (P.mode & MODE_PROF) S.dbg[0] += R;
+            }
         }
-        __syncthreads();
-        const uint32_t ncand = S.ncand, nring = S.nring;
+        BAR();  // selection visible
+        if (S.exit_now) break;  // the final counters are published
+        const uint32_t R = S.R, C = S.C;
+        const uint32_t nstorm = S.nstorm, storm_base = S.storm_base, loc_kind = S.loc_kind;
 
-        // ---------------- D: classify
-        uint32_t my_need = 0;
-        uint8_t my_group = 0;
-        if ((uint32_t)tid < ncand) {
-            Cand& c = S.cand[tid];
-            if ((uint32_t)tid < nring) {
-                int g = 0;
-                while ((uint32_t)tid >= S.ring_base[g + 1]) g++;
-                const int k = g >> 1, vc = g & 1;
-                uint64_t slot = S.in_head[g] + (tid - S.ring_base[g]);
-                uint32_t off = t.in_data[k][vc] + (uint32_t)(slot & fcap_m) * P.fwd_stride;
-                u32x4 h = ld_sc1(rf, off);
-                c.src = off;
-                c.w0 = h.x;
-                c.id = h.y;
-                c.w2 = h.z;
-                c.t0 = h.w;
-                c.from = (int16_t)t.in_src[k];
-                c.group = (uint8_t)g;
-                c.kind = K_RING;
-                const int origin = (int)(h.x & 0xffffu);
-                const uint32_t tag = (h.x >> 16) & 0xffu;
-                uint32_t kids = 0;
-                c.judge = 1;
-                if (origin >= P.n || (tag == TAG_BCAST && (P.mode & MODE_LAT) && h.y >= P.lat_rounds)) {
-                    set_error(S, P, ERR_BAD_SLOT, h.x);
-                    c.kind = K_BAD;  // consumed, never forwarded, no side effects
-                } else if (tag == TAG_BCAST || tag == TAG_DECISION) {
-                    kids = children(t, me, origin, t.in_src[k]);
-                } else if (tag == TAG_PROPOSAL) {
-                    // PBuf [pid][vote][data_len u64][data] starts at slot + 16 (rootless_ops.c:1402-1410)
-                    u32x4 pb = ld_sc1(rf, off + kHdr);
-                    uint32_t dl = pb.z;
-                    uint32_t plen = (h.z & 0xffffffu);
-                    if (dl > plen - 16u) dl = plen > 16u ? plen - 16u : 0u;
-                    c.judge = judge_eval(P, rf, me, (int32_t)h.y, off + kHdr + 16u, dl);
-                    kids = c.judge ? children(t, me, origin, t.in_src[k]) : 0u;
-                } else {
-                    set_error(S, P, ERR_BAD_SLOT, h.x);
-                    c.kind = K_BAD;
-                }
-                c.kids = kids;
-                my_need = need_bits(t, kids, origin);
-            } else {
-                c.from = -1;
-                c.t0 = (uint32_t)now_ticks();
-                if (c.kind == K_STORM || c.kind == K_LAT) {
-                    c.w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
-                    c.w2 = P.len;
-                }
-                c.kids = (1u << t.sll) - 1u;
-                my_need = need_bits(t, c.kids, me);
-            }
-            c.need = my_need;
-            c.logidx = ~0u;
-            my_group = c.group;
-        }
-        if (tid < kGroups) S.first_bad[tid] = 0xffffffffu;
-        __syncthreads();
-
-        // ---------------- E: admission
-        const int nout = 2 * t.sll;
-        for (int oi = 0; oi < nout; oi++) {
-            uint64_t b = __ballot((my_need >> oi) & 1u);
-            if (lane == 0) S.wave_cnt[wave][oi] = (uint32_t)__popcll(b);
-        }
-        __syncthreads();
-        bool fits = (uint32_t)tid < ncand;
-        for (int oi = 0; oi < nout; oi++) {
-            uint64_t b = __ballot((my_need >> oi) & 1u);
-            if ((my_need >> oi) & 1u) {
-                uint32_t pre = (uint32_t)__popcll(b & lt_mask);
-                for (int w = 0; w < wave; w++) pre += S.wave_cnt[w][oi];
-                uint64_t used = S.out_tail[oi] - S.out_head[oi];
-                if ((uint64_t)pre + used >= P.fwd_cap) fits = false;
-            }
-        }
-        __syncthreads();  // wave_cnt reuse below
-        if ((uint32_t)tid < ncand && !fits) atomicMin(&S.first_bad[my_group], (uint32_t)tid);
-        __syncthreads();
-        const bool admitted = (uint32_t)tid < ncand && fits && (uint32_t)tid < S.first_bad[my_group];
-        const uint32_t adm_need = admitted ? my_need : 0u;
-        for (int oi = 0; oi < nout; oi++) {
-            uint64_t b = __ballot((adm_need >> oi) & 1u);
-            if (lane == 0) S.wave_cnt[wave][oi] = (uint32_t)__popcll(b);
-        }
-        __syncthreads();
-        // per-oi positions: every lane takes part in each ballot
-        for (int oi = 0; oi < nout; oi++) {
-            const bool bit = (adm_need >> oi) & 1u;
-            uint64_t b = __ballot(bit);
-            if (bit) {
-                uint32_t pre = (uint32_t)__popcll(b & lt_mask);
-                for (int w = 0; w < wave; w++) pre += S.wave_cnt[w][oi];
-                const int j = oi >> 1;
-                S.pos[tid][j] = (uint16_t)pre;
-            }
-        }
-        __syncthreads();
-        if (tid < nout) {
-            uint32_t tot = 0;
-            for (int w = 0; w < kWaves; w++) tot += S.wave_cnt[w][tid];
-            S.out_tail0[tid] = S.out_tail[tid];
-            S.out_tail[tid] += tot;
-        }
-        if (tid < n_in2) {  // consume the admitted prefix of every in-ring
-            uint32_t base = S.ring_base[tid], take = S.ring_take[tid];
-            uint32_t fb = S.first_bad[tid];
-            uint32_t adm = fb == 0xffffffffu ? take : (fb > base ? fb - base : 0u);
-            if (adm > take) adm = take;
-            S.in_head[tid] += adm;
-            if (adm < take) atomicAdd(&S.stalls, 1ull);
-        }
-
-        // ---------------- F: side effects of admitted messages
-        if (admitted) {
-            S.progressed = 1;
-            Cand& c = S.cand[tid];
-            const int origin = (int)(c.w0 & 0xffffu);
-            const uint32_t tag = (c.w0 >> 16) & 0xffu;
-            const int vote = (int)(int8_t)(c.w0 >> 24);
-            const uint32_t len = c.w2 & 0xffffffu, pseq = c.w2 >> 24;
-            if (c.kind == K_RING) {
-                if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
-                    atomicAdd(&S.bcast_delivered, 1ull);
-                    const uint64_t tn = now_ticks();
-                    if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)tn - c.t0)], 1u);
-                    c.logidx = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, c.from, c.id, len, -1, 0);
-                    if (P.mode & MODE_LAT) {
-                        uint32_t old = atomicAdd(&P.lat_count[c.id], 1u);
-                        if (old + 1u == (uint32_t)(P.n - 1)) {
-                            P.lat_out[c.id] = (uint64_t)((uint32_t)tn - c.t0);
-                            __hip_atomic_store(P.lat_round, c.id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
+        // an iteration with nothing to do goes straight to the bookkeeping (uniform: read after the barrier)
+        if (C != 0 || S.vtot != 0) {
+            // ---------------- B (wave 1): vote slots (children -> me): loads now, merge after the wait
+            const uint32_t vtot = S.vtot;
+            u32x4 vreg[4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+            if (w == 1 && vtot) {
+    #pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t i = (uint32_t)u * 64u + lane;
+                    if (i < vtot) {
+                        int j = 0;
+                        while (i >= S.vbase[j] + S.va[j]) j++;
+                        const uint64_t slot = S.vhead[j] + (i - S.vbase[j]);
+                        vreg[u] = ld_sc1(rv, t.vin_data[j] + (uint32_t)(slot & vcap_m) * kVoteSlot);
                     }
-                } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler (:668-726)
-                    const int32_t pid = (int32_t)c.id;
-                    const int k = c.group >> 1;
-                    atomicAdd(&S.proposals_recv, 1ull);
-                    if (S.own_state != 0 && pid == S.own_pid) {
-                        set_error(S, P, ERR_PID_COLLISION, (uint32_t)pid);  // :690-692 (reference never votes)
-                    } else {
-                        atomicAdd(&S.judge_calls, 1ull);
-                        log_put(S, P, lr, LOG_JUDGE, origin, c.from, (uint32_t)pid, len, c.judge, 0);
-                        if (!c.judge) {
-                            emit_vote(S, P, (uint32_t)k, origin, pid, pseq, 0);
-                        } else {
-                            PendState* ps = &pend[2 * origin + (pseq & 1u)];
-                            uint32_t nk = (uint32_t)__builtin_popcount(c.kids);
-                            ps->pid = pid;
-                            ps->word = 0;
-                            ps->parent_k = (uint16_t)k;
-                            ps->needed = (uint8_t)nk;
-                            ps->pseq = pseq | ((len - 16u) << 8);  // + proposal data_len (action argument)
-                            ps->valid = 1;
-                            if (nk == 0) emit_vote(S, P, (uint32_t)k, origin, pid, pseq, 1);
-                        }
-                    }
-                } else if (tag == TAG_DECISION) {  // :603-615, _iar_decision_handler :814-859
-                    PendState* ps = &pend[2 * origin + (pseq & 1u)];
-                    if (ps->valid && ps->pid == (int32_t)c.id) {
-                        if (vote != 0) {
-                            atomicAdd(&S.actions, 1ull);
-                            log_put(S, P, lr, LOG_ACTION, origin, c.from, c.id, 0, 1, ps->pseq >> 8);
-                        }
-                        ps->valid = 0;
-                    }
-                    atomicAdd(&S.dec_delivered, 1ull);
-                    if (vote != 0) atomicAdd(&S.dec_approved, 1ull);
-                    log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, c.from, c.id, 7, vote, 0);
                 }
-            } else if (c.kind == K_PROP) {
-                S.own_pid = (int32_t)c.id;
-                S.own_word = 0;
-                S.own_needed = (uint32_t)t.sll;  // votes_needed = send_list_len (:881)
-                S.own_pseq = pseq;
-                S.own_state = 1;
-            } else if (c.kind == K_DEC) {
-                atomicAdd(&S.own_decided, 1ull);
-                if (vote) atomicAdd(&S.own_approved, 1ull);
-                log_put(S, P, lr, LOG_RESULT, me, -1, c.id, 0, vote, 0);
-                S.own_state = 0;
-                S.own_pid = -1;  // RLO_proposal_reset via RLO_get_vote_my_proposal (:1649-1673)
-                S.own_iter++;
-            } else if (c.kind == K_STORM || c.kind == K_LAT) {
-                atomicAdd(&S.originated, 1ull);
-                if (c.kind == K_LAT) S.lat_next = c.id + 1;
             }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t fb = S.first_bad[kGroupLocal + K_STORM];
-            uint32_t nst = S.nlocal_storm;
-            if (nst) {
-                uint32_t base = ncand - nst;  // storm candidates are last
-                uint32_t adm = fb == 0xffffffffu ? nst : (fb > base ? fb - base : 0u);
-                if (adm > nst) adm = nst;
-                S.sched_next += adm;
-            }
-            if (S.nvote) S.progressed = 1;
-        }
-        // vote placement: one 16-byte write-through slot per vote, towards the parent
-        {
-            const uint32_t nv = S.nvemit < kMaxVoteEmit ? S.nvemit : kMaxVoteEmit;
-            for (uint32_t i = tid; i < nv; i += kBlock) {
-                const VoteEmit e = S.vemit[i];
-                unsigned long long p = atomicAdd((unsigned long long*)&S.vout_tail[e.k], 1ull);
-                if (p - S.vout_head[e.k] >= P.vote_cap) {
-                    set_error(S, P, ERR_VOTE_RING, e.k);
-                    continue;
-                }
-                u32x4 v;
-                v.x = e.w0;
-                v.y = e.pid;
-                v.z = e.pseq;
-                v.w = (uint32_t)me;
-                st_sc1(rv, t.vout_data[e.k] + (uint32_t)(p & vcap_m) * kVoteSlot, v);
-            }
-        }
 
-        // ---------------- G: copy admitted messages to their children
-        {
-            uint32_t nch = 0;
-            if (admitted) nch = (kHdr + (S.cand[tid].w2 & 0xffffffu) + 15u) >> 4;
-            uint32_t total;
-            uint32_t ex = block_excl_scan(S, nch, &total);
-            S.cum[tid] = ex;
-            if (tid == kBlock - 1) S.cum[kBlock] = total;
-            __syncthreads();
-            for (uint32_t i = tid; i < total; i += kBlock) {
-                // candidate owning chunk i: largest c with cum[c] <= i
-                int lo = 0, hi = kBlock;
-                while (hi - lo > 1) {
-                    int mid = (lo + hi) >> 1;
-                    if (S.cum[mid] <= i) lo = mid;
-                    else hi = mid;
-                }
-                const Cand& c = S.cand[lo];
-                const uint32_t q = i - S.cum[lo];
-                const uint32_t len = c.w2 & 0xffffffu;
-                const int origin = (int)(c.w0 & 0xffffu);
-                u32x4 v;
-                if (q == 0) {
-                    v.x = c.w0; v.y = c.id; v.z = c.w2; v.w = c.t0;
-                } else if (c.kind == K_RING) {
-                    v = ld_sc1(rf, c.src + 16u * q);
-                } else if (c.kind == K_STORM || c.kind == K_LAT) {
-                    const uint32_t k0 = 2u * (q - 1u);
-                    const int b0 = (int)len - (int)(8u * k0);
-                    uint64_t a = b0 > 0 ? storm_word((uint32_t)me, c.id, k0) : 0ull;
-                    uint64_t b = b0 > 8 ? storm_word((uint32_t)me, c.id, k0 + 1u) : 0ull;
-                    v.x = mask_bytes((uint32_t)a, b0);
-                    v.y = mask_bytes((uint32_t)(a >> 32), b0 - 4);
-                    v.z = mask_bytes((uint32_t)b, b0 - 8);
-                    v.w = mask_bytes((uint32_t)(b >> 32), b0 - 12);
-                } else if (c.kind == K_PROP) {
-                    const int64_t pi = (int64_t)c.src;
-                    const uint32_t dl = P.prop_data_len[pi];
-                    if (q == 1) {
-                        v.x = c.id; v.y = 1u; v.z = dl; v.w = 0u;  // PBuf header (:1381-1383)
-                    } else {
-                        const uint8_t* d = P.prop_data + P.prop_data_off[pi];
-                        uint32_t w[4];
-                        for (int e = 0; e < 4; e++) {
-                            uint32_t x = 0;
-                            for (int bb = 0; bb < 4; bb++) {
-                                uint32_t idx = 16u * (q - 2u) + 4u * e + bb;
-                                if (idx < dl) x |= (uint32_t)d[idx] << (8 * bb);
+            // ---------------- D0: this wave's ring slots -> LDS (LDS-DMA), coalesced per in-ring run
+            const uint32_t c_lo = (uint32_t)w * kPass, c_hi = min(c_lo + kPass, R);
+            if (c_lo < c_hi) {
+                for (uint64_t m = S.ract; m; m &= m - 1) {  // active in-rings (uniform loop)
+                    const int g = __builtin_ctzll(m);
+                    const uint32_t gb = S.ring_base[g], ge = gb + S.ring_take[g];
+                    const uint32_t lo = max(gb, c_lo), hi = min(ge, c_hi);
+                    if (lo >= hi) continue;
+                    const uint64_t head = S.ring_head[g] + (lo - gb);
+                    const uint32_t gdat = t.in_data[g >> 1][g & 1];
+                    const uint32_t nit = (hi - lo) * nsmall;
+                    for (uint32_t i0 = 0; i0 < nit; i0 += 64) {
+                        const uint32_t i = i0 + lane;
+                        if (i < nit) {
+                            const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
+                            const uint32_t off = gdat + (uint32_t)((head + mi) & fcap_m) * P.fwd_stride;
+                            if (q == 0) {
+                                S.cand[lo + mi].src = off;
+                                S.cand[lo + mi].group = (uint32_t)g;
                             }
-                            w[e] = x;
+                            dma16(rf, STG(lo, 0) + (i0 << 4), off + 16u * q);
                         }
-                        v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
-                    }
-                } else {  // K_DEC: PBuf(pid, decision, 7, "IAR_DEC") (:908-917)
-                    if (q == 1) {
-                        v.x = c.id; v.y = (uint32_t)(int32_t)(int8_t)(c.w0 >> 24); v.z = 7u; v.w = 0u;
-                    } else {
-                        v.x = 0x5F524149u; v.y = 0x00434544u; v.z = 0u; v.w = 0u;
-                    }
-                }
-                uint32_t kids = c.kids;
-                while (kids) {
-                    const int j = __builtin_ctz(kids);
-                    kids &= kids - 1;
-                    const int vc = t.send_list[j] < origin ? 1 : 0;
-                    const int oi = 2 * j + vc;
-                    const uint64_t slot = S.out_tail0[oi] + S.pos[lo][j];
-                    st_sc1(rf, t.out_data[j][vc] + (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v);
-                }
-                if (c.kind == K_RING && ((c.w0 >> 16) & 0xffu) == TAG_BCAST) {
-                    acc_sum += (q == 0) ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, c.id, TAG_BCAST, len})
-                                        : chunk_mix(q - 1u, v);
-                    if (q > 0 && c.logidx != ~0u && 16u * q <= P.log_stride) {
-                        uint8_t* dst = P.log_payload + ((size_t)lr * P.log_cap + c.logidx) * P.log_stride + 16u * (q - 1u);
-                        *reinterpret_cast<u32x4*>(dst) = v;
                     }
                 }
             }
+            VM_DRAIN();  // this wave's stage loads (wave 1: and its vote loads)
+            PROF_STAMP(1);
+
+            // ---------------- B1 (wave 1): merge the votes (_iar_vote_handler :743-812)
+            if (w == 1 && vtot) {
+    #pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t i = (uint32_t)u * 64u + lane;
+                    if (i >= vtot) continue;
+                    const u32x4 v = vreg[u];
+                    const int origin = (int)(v.x & 0xffffu);
+                    const int vote = (int)(int8_t)(v.x >> 24);
+                    const int32_t pid = (int32_t)v.y;
+                    const uint32_t pseq = v.z;
+                    const uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
+                    if (origin >= P.n) {
+                        set_error(S, P, ERR_BAD_SLOT, v.x);
+                    } else if (origin == me) {  // a vote for my own proposal (:756-783)
+                        if (S.own_state != 1 || pid != S.own_pid) {
+                            set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+                        } else {
+                            const uint32_t nw = atomicAdd(&S.own_word, inc) + inc;
+                            if ((nw & 0xffffu) == S.own_needed) {
+                                const int d = (nw >> 16) == 0 ? 1 : 0;
+                                if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
+                                    atomicAdd(&S.judge_calls, 1ull);
+                                    log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                                }
+                                S.own_decision = (uint32_t)d;
+                                S.own_state = 2;
+                            }
+                        }
+                    } else {  // _vote_merge (:1056-1070)
+                        PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                        if (!ps->valid || ps->pid != pid) {
+                            set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+                        } else {
+                            const uint32_t nw = atomicAdd(&ps->word, inc) + inc;
+                            if ((nw & 0xffffu) == ps->needed)
+                                emit_vote(S, P, rv, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+                        }
+                    }
+                }
+                if (lane == 0) S.progressed = 1;
+            }
+
+            // ---------------- D: classify this wave's messages
+            const uint32_t c = (uint32_t)w * kPass + lane;
+            const bool active = c < C;
+            uint32_t kind = K_BAD, w0 = 0, id = 0, w2 = 0, t0 = 0, src = 0, kids = 0, group = 0;
+            int from = -1, judge = 1;
+            if (active && c < R) {
+                const u32x4 h = *reinterpret_cast<const u32x4*>(STG(c, 0));
+                group = S.cand[c].group;
+                src = S.cand[c].src;
+                w0 = h.x; id = h.y; w2 = h.z; t0 = h.w;
+                from = t.in_src[group >> 1];
+                kind = K_RING;
+                const int origin = (int)(w0 & 0xffffu);
+                const uint32_t tag = (w0 >> 16) & 0xffu;
+                if (origin >= P.n || (tag == TAG_BCAST && (P.mode & MODE_LAT) && id >= P.lat_rounds)) {
+                    set_error(S, P, ERR_BAD_SLOT, w0);
+                    kind = K_BAD;  // consumed, never forwarded, no side effects
+                } else if (tag == TAG_BCAST || tag == TAG_DECISION) {
+                    kids = kids_of(me, origin, from, level, last_wall, scc, sll, sl_r);
+                } else if (tag == TAG_PROPOSAL) {
+                    // PBuf [pid][vote][data_len u64][data] at slot + 16 (rootless_ops.c:1402-1410)
+                    const uint32_t plen = w2 & 0xffffffu;
+                    uint32_t dl = nsmall > 1 ? reinterpret_cast<const u32x4*>(STG(c, 1))->z : 0u;
+                    if (dl > plen - 16u) dl = plen > 16u ? plen - 16u : 0u;
+                    judge = judge_eval(P, rf, me, my_mask, (int32_t)id, src + kHdr + 16u, dl);
+                    kids = judge ? kids_of(me, origin, from, level, last_wall, scc, sll, sl_r) : 0u;
+                } else {
+                    set_error(S, P, ERR_BAD_SLOT, w0);
+                    kind = K_BAD;
+                }
+            } else if (active) {
+                t0 = (uint32_t)now_ticks();
+                kids = (1u << sll) - 1u;
+                if (c >= storm_base && c < storm_base + nstorm) {
+                    kind = K_STORM;
+                    group = kGroupLocal + K_STORM;
+                    id = S.storm_ids[c - storm_base];
+                    w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
+                    w2 = P.len;
+                } else if (loc_kind == K_DEC && c == R) {
+                    kind = K_DEC;
+                    group = kGroupLocal + K_DEC;
+                    id = (uint32_t)S.own_pid;
+                    w0 = (uint32_t)me | (TAG_DECISION << 16) | ((S.own_decision & 0xffu) << 24);
+                    w2 = 23u | (S.own_pseq << 24);
+                } else if (loc_kind == K_PROP && c == R) {
+                    const int64_t pi = S.prop_idx;
+                    kind = K_PROP;
+                    group = kGroupLocal + K_PROP;
+                    src = (uint32_t)pi;
+                    id = (uint32_t)P.prop_pid[pi];
+                    w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
+                    w2 = (16u + P.prop_data_len[pi]) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                } else {
+                    kind = K_LAT;
+                    group = kGroupLocal + K_LAT;
+                    id = S.lat_id;
+                    w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
+                    w2 = P.len;
+                }
+                // stage the header (+ the payload of a small message) like a received slot
+                const uint32_t nch = (kHdr + (w2 & 0xffffffu) + 15u) >> 4;
+                *reinterpret_cast<u32x4*>(STG(c, 0)) = u32x4{w0, id, w2, t0};
+                if (nch <= nsmall)
+                    for (uint32_t q = 1; q < nch; q++)
+                        *reinterpret_cast<u32x4*>(STG(c, q)) =
+                            gen_chunk(P, kind, me, id, w2 & 0xffffffu, src, (int)(int8_t)(w0 >> 24), q);
+            }
+            const int origin = (int)(w0 & 0xffffu);
+            const uint32_t need = active ? need_of(kids, origin, sll, sl_r) : 0u;
+            PROF_STAMP(2);
+
+            // ---------------- E: admission: credits per out-ring, FIFO prefix per source
+            for (int oi = 0; oi < nout; oi++) {
+                const uint64_t b = __ballot((need >> oi) & 1u);
+                if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
+            }
+            BAR();
+            uint32_t room_r = 0;  // lane oi: free slots of out-ring oi left for this wave
+            if (lane < nout) {
+                uint32_t pre = 0;
+                for (int v = 0; v < w; v++) pre += S.wcnt[v][lane];
+                const uint32_t f = S.ofree[lane];
+                room_r = f > pre ? f - pre : 0u;
+            }
+            bool fits = active;
+            for (int oi = 0; oi < nout; oi++) {
+                const bool bit = (need >> oi) & 1u;
+                const uint64_t b = __ballot(bit);
+                if (b && bit && (uint32_t)__popcll(b & lt_mask) >= rdl32(room_r, oi)) {
+                    fits = false;
+                    if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) atomicAdd(&S.hist[oi], 1u);  // misfits per out-ring
+                }
+            }
+            if (active && !fits) atomicMin(&S.first_bad[group], c);
+            BAR();  // every wave has read wcnt and posted its first misfit per source
+            const bool admitted = active && fits && c < S.first_bad[group];
+            const uint32_t an = admitted ? need : 0u;
+            const uint32_t len = w2 & 0xffffffu;
+            const bool isbig = admitted && ((kHdr + len + 15u) >> 4) > nsmall;
+            for (int oi = 0; oi < nout; oi++) {
+                const uint64_t b = __ballot((an >> oi) & 1u);
+                if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
+            }
+            BAR();
+            uint32_t pre_r = 0;  // lane oi: slots of out-ring oi taken by lower waves
+            if (lane < nout) {
+                uint32_t tot = 0;
+                for (int v = 0; v < kWaves; v++) {
+                    const uint32_t x = S.wcnt[v][lane];
+                    if (v < w) pre_r += x;
+                    tot += x;
+                }
+                if (w == 0) S.n_oi[lane] = tot;
+            }
+            for (int oi = 0; oi < nout; oi++) {
+                const bool bit = (an >> oi) & 1u;
+                const uint64_t b = __ballot(bit);
+                if (b && bit) {
+                    const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
+                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : 0u));
+                    if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
+                }
+            }
+            const uint64_t amask = __ballot(admitted);
+            PROF_STAMP(3);
+
+            // ---------------- F: side effects of admitted messages
+            const uint32_t tag = (w0 >> 16) & 0xffu;
+            const int vote = (int)(int8_t)(w0 >> 24);
+            const uint32_t pseq = w2 >> 24;
+            uint32_t logidx = ~0u;
+            if (admitted) {
+                if (kind == K_RING) {
+                    if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
+                        if (P.mode & (MODE_HIST | MODE_LAT)) {
+                            const uint64_t tn = now_ticks();
+                            if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)tn - t0)], 1u);
+                            if (P.mode & MODE_LAT) {
+                                uint32_t old = atomicAdd(&P.lat_count[id], 1u);
+                                if (old + 1u == (uint32_t)(P.n - 1)) {
+                                    P.lat_out[id] = (uint64_t)((uint32_t)tn - t0);
+                                    __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                }
+                            }
+                        }
+                        logidx = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, 0);
+                    } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler (:668-726)
+                        const int32_t pid = (int32_t)id;
+                        const int k = (int)(group >> 1);
+                        atomicAdd(&S.proposals_recv, 1ull);
+                        if (S.own_state != 0 && pid == S.own_pid) {
+                            set_error(S, P, ERR_PID_COLLISION, (uint32_t)pid);  // :690-692 (the reference never votes)
+                        } else {
+                            atomicAdd(&S.judge_calls, 1ull);
+                            log_put(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
+                            if (!judge) {
+                                emit_vote(S, P, rv, me, (uint32_t)k, origin, pid, pseq, 0);
+                            } else {
+                                PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                                const uint32_t nk = (uint32_t)__builtin_popcount(kids);
+                                ps->pid = pid;
+                                ps->word = 0;
+                                ps->parent_k = (uint16_t)k;
+                                ps->needed = (uint8_t)nk;
+                                ps->pseq = pseq | ((len - 16u) << 8);
+                                ps->valid = 1;
+                                if (nk == 0) emit_vote(S, P, rv, me, (uint32_t)k, origin, pid, pseq, 1);
+                            }
+                        }
+                    } else if (tag == TAG_DECISION) {  // :603-615, _iar_decision_handler :814-859
+                        PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                        if (ps->valid && ps->pid == (int32_t)id) {
+                            if (vote != 0) {
+                                atomicAdd(&S.actions, 1ull);
+                                log_put(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, ps->pseq >> 8);
+                            }
+                            ps->valid = 0;
+                        }
+                        atomicAdd(&S.dec_delivered, 1ull);
+                        if (vote != 0) atomicAdd(&S.dec_approved, 1ull);
+                        log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+                    }
+                } else if (kind == K_PROP) {
+                    S.own_pid = (int32_t)id;
+                    S.own_word = 0;
+                    S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
+                    S.own_pseq = pseq;
+                    S.own_state = 1;
+                } else if (kind == K_DEC) {
+                    atomicAdd(&S.own_decided, 1ull);
+                    if (vote) atomicAdd(&S.own_approved, 1ull);
+                    log_put(S, P, lr, LOG_RESULT, me, -1, id, 0, vote, 0);
+                    S.own_state = 0;
+                    S.own_pid = -1;  // RLO_proposal_reset via RLO_get_vote_my_proposal (:1649-1673)
+                    S.own_iter++;
+                } else if (kind == K_LAT) {
+                    S.lat_next = id + 1;
+                }
+            }
+            if (active) {
+                CandL& cl = S.cand[c];
+                cl.w0 = w0; cl.id = id; cl.w2 = w2; cl.t0 = t0;
+                cl.src = src; cl.need = an; cl.logidx = logidx; cl.kind = kind;
+            }
+            {  // wave-aggregated counters (one LDS op per wave instead of 64 same-address atomics)
+                const uint64_t bdel = __ballot(admitted && kind == K_RING && tag == TAG_BCAST);
+                const uint64_t borg = __ballot(admitted && (kind == K_STORM || kind == K_LAT));
+                const uint64_t bbig = __ballot(isbig);
+                if (lane == 0) {
+                    if (bdel) atomicAdd(&S.bcast_delivered, (unsigned long long)__popcll(bdel));
+                    if (borg) atomicAdd(&S.originated, (unsigned long long)__popcll(borg));
+                    if (amask) S.progressed = 1;
+                }
+                if (bbig) {
+                    uint32_t bb = 0;
+                    if (lane == 0) bb = atomicAdd(&S.nbig, (uint32_t)__popcll(bbig));
+                    bb = rdl32(bb, 0);
+                    if (isbig) S.big[bb + (uint32_t)__popcll(bbig & lt_mask)] = (uint16_t)c;
+                }
+                if (P.mode & MODE_PROF) {
+                    uint32_t tot;
+                    wave_excl_scan(admitted ? (uint32_t)__builtin_popcount(kids) : 0u, &tot);
+                    if (lane == 0) atomicAdd((unsigned long long*)&S.dbg[6], (unsigned long long)tot);
+                }
+            }
+            BAR();  // olist / cand / n_oi / big complete
+            PROF_STAMP(4);
+
+            // ---------------- G1: stage the first group of large messages (before any store)
+            const uint32_t nbig = S.nbig;
+            auto plan_big = [&]() {  // thread 0: next (message, 64-chunk block) pairs for stage2
+                if (tid == 0) {
+                    uint32_t bm = S.bm, bq0 = S.bq0, nblk = 0;
+                    while (bm < nbig && nblk < s2_blocks && nblk < 64) {
+                        const uint32_t cc = S.big[bm];
+                        const uint32_t nch = (kHdr + (S.cand[cc].w2 & 0xffffffu) + 15u) >> 4;
+                        S.blk_c[nblk] = cc;
+                        S.blk_q0[nblk] = bq0;
+                        nblk++;
+                        bq0 += 64;
+                        if (bq0 >= nch) { bm++; bq0 = 0; }
+                    }
+                    S.bm = bm; S.bq0 = bq0; S.nblk = nblk;
+                }
+            };
+            auto stage_big = [&]() {  // wave w stages (and later stores) blocks b = w, w + 4, ...
+                const uint32_t nblk = S.nblk;
+                for (uint32_t b = (uint32_t)w; b < nblk; b += kWaves) {
+                    const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
+                    const CandL& cl = S.cand[cc];
+                    const uint32_t nch = (kHdr + (cl.w2 & 0xffffffu) + 15u) >> 4;
+                    uint8_t* dst = stage2 + (b << 10);
+                    if (cl.kind == K_RING) {
+                        if (q < nch) dma16(rf, dst, cl.src + 16u * q);
+                    } else if (q < nch) {
+                        *reinterpret_cast<u32x4*>(dst + 16u * lane) =
+                            q == 0 ? u32x4{cl.w0, cl.id, cl.w2, cl.t0}
+                                   : gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), q);
+                    }
+                }
+                VM_DRAIN();
+            };
+            if (nbig) {
+                if (tid == 0) { S.bm = 0; S.bq0 = 0; }
+                plan_big();
+                BAR();
+                stage_big();
+            }
+
+            // ---------------- G2: small messages.  Out-ring oi (oi = w, w + 4, ...) receives its
+            // admitted messages' staged slots as contiguous (message, chunk) items
+            for (int oi = w; oi < nout; oi += kWaves) {
+                const uint32_t n = S.n_oi[oi];
+                if (!n) continue;
+                const uint64_t slot0 = S.out_tail0[oi];
+                const uint32_t odat = rdl32(od_r, oi);
+                const uint32_t nit = n * nsmall;
+                for (uint32_t i = lane; i < nit; i += 64) {
+                    const uint32_t r = div_small(i, nmagic), q = i - r * nsmall;
+                    const uint16_t e = OL(oi, r);
+                    if (e & kBigFlag) continue;
+                    const uint32_t nch = (kHdr + (S.cand[e].w2 & 0xffffffu) + 15u) >> 4;
+                    if (q < nch)
+                        st_sc1(rf, odat + (uint32_t)((slot0 + r) & fcap_m) * P.fwd_stride + 16u * q,
+                               *reinterpret_cast<const u32x4*>(STG(e, q)));
+                }
+            }
+            if (admitted && !isbig && kind == K_RING && tag == TAG_BCAST) {  // pickup: checksum (+ log payload)
+                const uint32_t nch = (kHdr + len + 15u) >> 4;
+                acc_sum += chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, id, TAG_BCAST, len});
+                for (uint32_t q = 1; q < nch; q++) {
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(STG(c, q));
+                    acc_sum += chunk_mix(q - 1u, v);
+                    if (logidx != ~0u)
+                        *reinterpret_cast<u32x4*>(P.log_payload + ((size_t)lr * P.log_cap + logidx) * P.log_stride + 16u * (q - 1)) = v;
+                }
+            }
+
+            // ---------------- G3: large messages, 64 x 16 B per wave store instruction
+            if (nbig) {
+                for (;;) {
+                    const uint32_t nblk = S.nblk;
+                    for (uint32_t b = (uint32_t)w; b < nblk; b += kWaves) {
+                        const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
+                        const CandL& cl = S.cand[cc];
+                        const uint32_t blen = cl.w2 & 0xffffffu, nch = (kHdr + blen + 15u) >> 4;
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(stage2 + (b << 10) + 16u * lane);
+                        for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
+                            const int oi = __builtin_ctz(a2);
+                            const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
+                            if (q < nch) st_sc1(rf, rdl32(od_r, oi) + (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v);
+                        }
+                        if (q < nch && cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
+                            acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})
+                                              : chunk_mix(q - 1u, v);
+                            if (q > 0 && cl.logidx != ~0u && 16u * q <= P.log_stride)
+                                *reinterpret_cast<u32x4*>(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride +
+                                                          16u * (q - 1)) = v;
+                        }
+                    }
+                    if (S.bm >= nbig) break;  // S.bm is rewritten only after the next barrier
+                    BAR();                    // every wave is done with stage2 and blk_*
+                    plan_big();
+                    BAR();
+                    stage_big();  // loads behind this iteration's stores drain in order (only when > stage2)
+                }
+            }
+            PROF_STAMP(5);
         }
 
-        // ---------------- H: drain, publish counters, bookkeeping
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid < nout) {
-            if (S.out_tail[tid] != S.out_tail0[tid]) pub64(&P.ctrl[t.out_tail[tid >> 1][tid & 1]], S.out_tail[tid]);
-        } else if (tid >= 64 && tid - 64 < n_in2) {
-            const int g = tid - 64;
-            pub64(&P.ctrl[t.in_head[g >> 1][g & 1]], S.in_head[g]);
-        } else if (tid >= 128 && tid - 128 < t.sll) {
-            const int j = tid - 128;
-            const uint64_t nh = S.vin_head[j] + (S.vbase[j + 1] - S.vbase[j]);
-            if (nh != S.vin_head[j]) {
-                S.vin_head[j] = nh;
-                pub64(&P.ctrl[t.vin_head[j]], nh);
+        // ---------------- consume (wave 0): in-ring prefixes, producer counts, bookkeeping
+        if (w == 0) {
+            if (lane < n_in2) {
+                const uint32_t bse = S.ring_base[lane], tk = S.ring_take[lane], fb = S.first_bad[lane];
+                uint32_t adm = fb == 0xffffffffu ? tk : (fb > bse ? fb - bse : 0u);
+                if (adm > tk) adm = tk;
+                in_head_r += adm;
+                if (adm < tk) win_r = max(adm + adm / 2u, 16u);
+                else if (adm == tk && tk == win_r) win_r = min(2u * win_r, (uint32_t)kMaxCand);
+                if (P.mode & MODE_PROF) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
             }
-        } else if (tid >= 192 && tid - 192 < t.n_in) {
-            const int k = tid - 192;
-            pub64(&P.ctrl[t.vout_tail[k]], S.vout_tail[k]);
+            {
+                const uint64_t bst = __ballot(lane < n_in2 && S.first_bad[lane] < S.ring_base[lane] + S.ring_take[lane]);
+                if (lane == 0 && bst) S.stalls += (unsigned long long)__popcll(bst);
+            }
+            if (lane < nout) {
+                out_tail_r += S.n_oi[lane];
+                if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
+                    S.hist[32 + lane] += S.n_oi[lane];
+                    S.hist[64 + lane] += S.ofree[lane] >> 4;
+                }
+                if (P.mode & MODE_PROF)
+                    atomicMax((unsigned long long*)&S.dbg[7], (unsigned long long)(out_tail_r - S.out_tail0[lane] +
+                                                                                   (P.fwd_cap - S.ofree[lane])));
+            }
+            if (lane == 0) {
+                if (nstorm) {
+                    const uint32_t fb = S.first_bad[kGroupLocal + K_STORM];
+                    uint32_t adm = fb == 0xffffffffu ? nstorm : (fb > storm_base ? fb - storm_base : 0u);
+                    if (adm > nstorm) adm = nstorm;
+                    S.sched_next += adm;
+                }
+                S.iterations++;
+                if (S.progressed) {  // the clock is read on the 1st and every 64th idle iteration only
+                    S.busy++;
+                    idle_n = 0;
+                } else if ((++idle_n & 63u) == 1u) {
+                    const uint64_t tn = now_ticks();
+                    if (idle_n == 1) idle_since = tn;
+                    else if (tn - idle_since > P.timeout_ticks) set_error(S, P, ERR_TIMEOUT, 0);
+                }
+                if ((S.iterations & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
+                bool done = true;
+                if (P.mode & MODE_STORM) done &= S.sched_next == S.sched_n;
+                if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == S.expect_bcast;
+                if (P.mode & MODE_LAT) {
+                    while (S.lat_next < P.lat_rounds && P.lat_origin[S.lat_next] != me) S.lat_next++;
+                    done &= S.lat_next >= P.lat_rounds;
+                }
+                if (P.mode & MODE_IAR)
+                    done &= S.own_iter == S.own_n && S.own_state == 0 && (int64_t)S.dec_delivered == S.expect_dec;
+                if (S.error == ERR_TIMEOUT) done = true;
+                if (peer_failed) done = true;  // another rank failed: stop everyone
+                S.done = done;
+            }
         }
-        if (tid == 0) {
-            S.iterations++;
-            const uint64_t tn = now_ticks();
-            if (S.progressed || S.nvote) {
-                S.busy++;
-                S.last_progress = tn;
-            } else if (tn - S.last_progress > P.timeout_ticks) {
-                set_error(S, P, ERR_TIMEOUT, 0);
-            }
-            if (tn - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
-            bool done = true;
-            if (P.mode & MODE_STORM) done &= S.sched_next == S.sched_n;
-            if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == P.expect_bcast[lr];
-            if (P.mode & MODE_LAT) {
-                while (S.lat_next < P.lat_rounds && P.lat_origin[S.lat_next] != me) S.lat_next++;
-                done &= S.lat_next >= P.lat_rounds;
-            }
-            if (P.mode & MODE_IAR)
-                done &= S.own_iter == S.own_n && S.own_state == 0 && (int64_t)S.dec_delivered == P.expect_dec[lr];
-            if (S.error == ERR_TIMEOUT) done = true;
-            if (poll32(P.error_flag) != 0) done = true;  // another rank failed: stop everyone
-            S.done = done;
-        }
-        __syncthreads();
-        if (S.done) break;
+        PROF_STAMP(6);
     }
+#undef STG
+#undef OL
 
     // ---------------- flush statistics
     atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
-    __syncthreads();
-    if (tid < kHistBins) P.stats[lr].hist[tid] = S.hist[tid];
+    for (int i = tid; i < kHistBins; i += kBlock) P.stats[lr].hist[i] = S.hist[i];
+    if (tid < 8) { P.stats[lr].prof[tid] = S.prof[tid]; P.stats[lr].dbg[tid] = S.dbg[tid]; }
     if (tid == 0) {
         RankStats& st = P.stats[lr];
         st.bcast_delivered = S.bcast_delivered;
@@ -850,7 +1042,20 @@ __global__ __launch_bounds__(kBlock, 1) void rlo_progress_kernel(Params P) {
 }  // namespace rlo
 
 // C-ABI launch shim used by rlo_world.cpp
+static hipError_t grant_dyn_lds(size_t dyn_lds) {
+    static size_t granted = 0;
+    if (dyn_lds > granted) {  // > 64 KiB of dynamic LDS must be requested explicitly
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
+        if (e != hipSuccess) return e;
+        granted = dyn_lds;
+    }
+    return hipSuccess;
+}
+
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
+    hipError_t e = grant_dyn_lds(dyn_lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rlo::rlo_progress_kernel, dim3(blocks), dim3(rlo::kBlock), dyn_lds, stream, *p);
     return hipGetLastError();
 }
@@ -858,5 +1063,7 @@ extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size
 extern "C" size_t rlo_kernel_static_lds(void) { return sizeof(rlo::Shared); }
 
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds) {
+    hipError_t e = grant_dyn_lds(dyn_lds);
+    if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel, rlo::kBlock, dyn_lds);
 }

@@ -150,6 +150,7 @@ struct rlo_world {
     hipStream_t last_stream = nullptr;
     float last_ms = 0.f;
     size_t dyn_lds = 0;
+    uint32_t nsmall = 8, stage2 = 1024;
 };
 
 // ====================================================================== C ABI
@@ -296,24 +297,39 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
         P.vin_data[ed.j] = vdata; P.vin_tail[ed.j] = vtail; P.vin_head[ed.j] = vhead;
     }
 
-    // ---- residency: every rank-workgroup must be resident at once (persistent kernel)
-    w->dyn_lds = (size_t)2 * n * 16;
+    // ---- residency: every rank-workgroup must be resident at once (persistent kernel).
+    // Dynamic LDS = [pend 2N x 16 B][olist 2 max_fan x 256 x 2 B][stage 256 x nsmall x 16 B][stage2].
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, w->device) != hipSuccess) { delete w; return RLO_E_HIP; }
     w->cus = prop.multiProcessorCount;
-    int bpc = 0;
-    if (rlo_kernel_static_lds() + w->dyn_lds > (size_t)prop.sharedMemPerBlock) { delete w; return RLO_E_INVAL; }
     {
-        // LDS bound (160 KiB per CU) and the occupancy API (registers); the persistent kernel
-        // needs every rank resident, so never trust more than 3 blocks of 4 waves per CU
-        size_t per = rlo_kernel_static_lds() + w->dyn_lds;
-        int by_lds = (int)(163840 / per);
+        // Largest small-path stage (nsmall chunks per message, <= 8) and then the largest stage2
+        // (<= 64 KiB) at which the occupancy calculator (LDS allocation granularity, registers,
+        // waves) still co-schedules need_bpc rank-workgroups per CU.
+        const size_t lds_cu = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
+        const int need_bpc = (n + w->cus - 1) / w->cus;
+        const size_t per_block = lds_cu / need_bpc;
         int api = 0;
-        if (rlo_occupancy(&api, w->dyn_lds) != hipSuccess) api = 1;
-        bpc = std::max(1, std::min(std::min(by_lds, api), 3));
+        bool ok = false;
+        for (uint32_t ns = std::min<uint32_t>(8u, w->stride / 16u); ns >= 1 && !ok; ns--) {
+            const size_t fixed = rlo_kernel_static_lds() + (size_t)32 * n + (size_t)2 * w->max_fan * 256 * 2 +
+                                 (size_t)rlo::kMaxCand * ns * 16;
+            if (per_block < fixed + 1024 + 512) continue;
+            size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
+            for (;;) {
+                w->dyn_lds = fixed - rlo_kernel_static_lds() + s2;
+                if (rlo_occupancy(&api, w->dyn_lds) != hipSuccess) api = 0;
+                if (api >= need_bpc) { ok = true; break; }
+                if (s2 <= 1024) break;
+                s2 -= 1024;
+            }
+            w->nsmall = ns;
+            w->stage2 = (uint32_t)s2;
+        }
+        if (!ok) { delete w; return RLO_E_OCCUPANCY; }
+        w->blocks_per_cu = std::max(1, api);
+        if (n > w->blocks_per_cu * w->cus) { delete w; return RLO_E_OCCUPANCY; }
     }
-    w->blocks_per_cu = bpc;
-    if (n > bpc * w->cus) { delete w; return RLO_E_OCCUPANCY; }
 
     // ---- allocate
     if (hipMalloc(&w->fwd, w->fwd_bytes) != hipSuccess ||
@@ -387,6 +403,9 @@ static void base_params(rlo_world* w) {
     P.ctrl = w->ctrl;
     P.stats = w->d_stats.p;
     P.error_flag = w->d_err.p;
+    P.nsmall = w->nsmall;
+    P.nout_max = 2u * (uint32_t)w->max_fan;
+    P.stage2_bytes = w->stage2;
     P.timeout_ticks = 100000000ull * 10;   // 10 s without progress on a rank
     P.deadline_ticks = 100000000ull * 120; // 120 s per launch
     P.window = 32;
@@ -427,10 +446,11 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
     for (int64_t b = 0; b < cfg->k; b++) ids[fill[org[b]]++] = (uint32_t)b;
     for (int r = 0; r < n; r++) expect[r] = cfg->k - (off[r + 1] - off[r]);
     if (w->d_sched_off.upload(off) || w->d_sched_ids.upload(ids) || w->d_expect_bcast.upload(expect)) return RLO_E_HIP;
-    P.mode = rlo::MODE_STORM | ((cfg->flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u);
+    P.mode = rlo::MODE_STORM | ((cfg->flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u) |
+             ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
     P.seed = cfg->seed;
     P.len = cfg->len;
-    P.window = cfg->window ? cfg->window : 32;
+    P.window = std::min<uint32_t>(cfg->window ? cfg->window : 32, 64u);  // one wave prefetches the ids
     P.sched_off = w->d_sched_off.p;
     P.sched_ids = w->d_sched_ids.p;
     P.expect_bcast = w->d_expect_bcast.p;
@@ -498,7 +518,7 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
     if (w->d_prop_off.upload(off) || w->d_prop_pid.upload(ppid) || w->d_prop_data_off.upload(pdo) ||
         w->d_prop_data_len.upload(pdl) || w->d_prop_data.upload(blob) || w->d_expect_dec.upload(expect))
         return RLO_E_HIP;
-    P.mode = rlo::MODE_IAR;
+    P.mode = rlo::MODE_IAR | ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
     P.judge_kind = cfg->judge_kind;
     P.judge_ppm = cfg->judge_ppm;
     P.judge_seed = cfg->judge_seed;

@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
 
 RLO_OK = 0
 RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6
-RLO_FLAG_LOG, RLO_FLAG_HIST = 1, 2
+RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
 DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot"}
 
@@ -45,7 +45,9 @@ class RankStats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint64) for f in (
         "bcast_delivered", "bcast_sum", "originated", "dec_delivered", "dec_approved", "actions", "judge_calls",
         "own_decided", "own_approved", "proposals_recv", "iterations", "busy_iterations", "stalls", "log_count",
-        "t_start", "t_end")] + [("error", ctypes.c_uint32), ("error_aux", ctypes.c_uint32), ("hist", ctypes.c_uint32 * 128)]
+        "t_start", "t_end")] + [("error", ctypes.c_uint32), ("error_aux", ctypes.c_uint32), ("prof", ctypes.c_uint64 * 8),
+                           ("dbg", ctypes.c_uint64 * 8),
+                           ("hist", ctypes.c_uint32 * 128)]
 
 
 class LogRec(ctypes.Structure):

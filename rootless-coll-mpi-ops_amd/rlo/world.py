@@ -48,8 +48,8 @@ class World:
             pass
 
     # ------------------------------------------------------------ programs
-    def program_storm(self, k, length, seed=0x5EED, window=32, log=False, hist=False, log_cap=0):
-        flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0)
+    def program_storm(self, k, length, seed=0x5EED, window=32, log=False, hist=False, log_cap=0, prof=False):
+        flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0) | (L.RLO_FLAG_PROF if prof else 0)
         cfg = L.StormCfg(seed, k, length, window, flags, log_cap)
         check(self.lib.rlo_program_storm(self.h, ctypes.byref(cfg)), "rlo_program_storm")
 
@@ -59,7 +59,7 @@ class World:
         self._lat_rounds = rounds
 
     def program_iar(self, proposals, judge=L.RLO_JUDGE_APPROVE, mask=None, isp=None, seed=0, ppm=0, log=False,
-                    log_cap=0):
+                    log_cap=0, prof=False):
         """proposals: list of (origin, pid, data bytes) in per-origin submission order."""
         origin = np.array([p[0] for p in proposals], dtype=np.int32)
         pid = np.array([p[1] for p in proposals], dtype=np.int32)
@@ -78,7 +78,7 @@ class World:
         if isp is not None:
             cfg.judge_isp = b"".join(s.encode() + b"\0" for s in isp)
             self._keep.append(cfg.judge_isp)
-        cfg.flags = L.RLO_FLAG_LOG if log else 0
+        cfg.flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_PROF if prof else 0)
         cfg.log_cap = log_cap
         self._keep.append(cfg)
         d = lambda a: a.ctypes.data
@@ -122,8 +122,8 @@ class World:
         raw = self.stats_raw()
         out = {}
         for f, _ in L.RankStats._fields_:
-            if f == "hist":
-                out[f] = np.array([list(s.hist) for s in raw], dtype=np.uint64)
+            if f in ("hist", "prof", "dbg"):
+                out[f] = np.array([list(getattr(s, f)) for s in raw], dtype=np.uint64)
             else:
                 out[f] = np.array([getattr(s, f) for s in raw], dtype=np.uint64)
         return out
@@ -146,18 +146,18 @@ class World:
 
 
 def hist_percentile(hist, p):
-    """Percentile (in 10 ns ticks) from the device log-bucket histogram (8 sub-bins per octave)."""
+    """Percentile (in 10 ns ticks) from the device log-bucket histogram (4 sub-bins per octave)."""
     hist = np.asarray(hist, dtype=np.float64)
     tot = hist.sum()
     if tot == 0:
         return 0.0
     c = np.cumsum(hist)
     b = int(np.searchsorted(c, p / 100.0 * tot))
-    if b < 8:
+    if b < 4:
         return float(b)
-    o, sub = b // 8 + 2, b % 8
-    lo = (8 + sub) << (o - 3)
-    hi = (9 + sub) << (o - 3)
+    o, sub = b // 4 + 1, b % 4
+    lo = (4 + sub) << (o - 2)
+    hi = (5 + sub) << (o - 2)
     return 0.5 * (lo + hi)
 
 
