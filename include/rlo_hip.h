@@ -5,9 +5,12 @@
  * Plain C types only (no HIP / torch types in signatures): a stream is passed
  * as `void*` (a hipStream_t, NULL = default stream).
  *
- * A world is N virtual ranks hosted on one GPU, one 256-thread workgroup per
- * rank of a persistent progress kernel.  Each rank's inboxes are SPSC rings in
- * HBM, one per overlay in-edge and virtual channel (DESIGN.md "Data layout").
+ * A world is N ranks.  It is hosted by one or more PARTS (contiguous rank ranges,
+ * one per process / GPU); every rank of a part is one 256-thread workgroup of that
+ * part's persistent progress kernel.  Each rank's inboxes are SPSC rings in its
+ * part's HBM, one per overlay in-edge and virtual channel; producers in other
+ * parts store into them through hipIpc mappings (xGMI across GPUs)
+ * (DESIGN.md "Data layout").
  * A *program* is the workload the kernel runs until every rank is quiescent:
  *   storm   : K bcasts from random originators          (replaces RLO_bcast_gen +
  *             RLO_make_progress_all + RLO_user_pickup_next loops, rootless_ops.c:1581, :538, :938)
@@ -32,6 +35,7 @@ extern "C" {
 #define RLO_E_DEVICE (-4)    /* the kernel reported an error (see rlo_rank_stats_t.error) */
 #define RLO_E_NOPROGRAM (-5) /* rlo_launch without a program                              */
 #define RLO_E_NODEVICE (-6)  /* no HIP device                                              */
+#define RLO_E_NOTCONNECTED (-7) /* part created but rlo_part_connect not called yet          */
 
 /* device error codes (rlo_rank_stats_t.error) */
 #define RLO_DERR_TIMEOUT 1
@@ -60,11 +64,34 @@ typedef struct {
 typedef struct {
     int32_t n_ranks, max_in_degree, max_fanout, edges;
     uint32_t ring_slots, slot_stride, vote_slots, pad;
-    uint64_t fwd_bytes, vote_bytes, ctrl_bytes;
+    uint64_t fwd_bytes, vote_bytes, ctrl_bytes; /* this part's regions                    */
     int32_t cus, blocks_per_cu;
+    int32_t part, n_parts, rank_begin, rank_end; /* ranks [rank_begin, rank_end) are local */
+    int32_t sys_scope, pad2;                     /* 1: parts span GPUs (system-scope stores) */
 } rlo_world_info_t;
 
+/* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522
+ * + bcomm_init :1454-1522 for every rank of the communicator at once) */
 int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
+
+/* ---- sharded world: one part per process / GPU.
+ * create (allocates the rings this part consumes) -> export a fixed-size blob -> exchange
+ * blobs out of band (MPI_Allgather, torch.distributed, a file) -> connect (maps every peer
+ * part: same process = direct pointer, other process = hipIpc / dmabuf, xGMI across GPUs).
+ * Every part must rlo_reset before ANY part launches (host barrier in between). */
+#define RLO_PART_BLOB_BYTES 512u
+#define RLO_PART_UNCACHED 1u /* allocate the part's rings uncached (for peer GPUs writing over xGMI) */
+typedef struct {
+    int32_t n_ranks;           /* world size                                               */
+    int32_t n_parts, part;     /* number of parts, this part                                */
+    const int32_t* part_begin; /* [n_parts + 1] rank boundaries, NULL = even contiguous split */
+    uint32_t max_payload, ring_slots;
+    int32_t device;            /* -1 = current                                              */
+    uint32_t flags;            /* RLO_PART_*                                                */
+} rlo_part_cfg_t;
+int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out);
+int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap); /* returns RLO_PART_BLOB_BYTES */
+int rlo_part_connect(rlo_world_t* w, const void* blobs /* n_parts x RLO_PART_BLOB_BYTES, by part */, int n_parts);
 int rlo_world_destroy(rlo_world_t* w);
 int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 
@@ -106,7 +133,13 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len);
 
 /* ------------------------------------------------------------------ run */
-int rlo_launch(rlo_world_t* w, void* stream);          /* async: reset rings, launch   */
+int rlo_reset(rlo_world_t* w, void* stream);           /* zero this part's counters (sync) */
+#define RLO_LAUNCH_NO_RESET 1u
+int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags); /* async launch of this part */
+int rlo_launch(rlo_world_t* w, void* stream);          /* rlo_reset + rlo_launch_ex        */
+/* a non-blocking HIP stream for one part's launch (parts of one process need one each) */
+int rlo_stream_create(int device, void** stream);
+int rlo_stream_destroy(void* stream);
 int rlo_wait(rlo_world_t* w);                          /* sync; RLO_E_DEVICE on error  */
 int rlo_run(rlo_world_t* w, void* stream, float* kernel_ms); /* launch + wait, HIP-event time */
 int rlo_last_kernel_ms(rlo_world_t* w, float* ms);
@@ -133,6 +166,7 @@ typedef struct {
     uint32_t aux, payload_idx;
 } rlo_log_rec_t;
 
+/* results of this part's ranks: stats index = rank - rank_begin; rlo_log takes the world rank */
 int rlo_stats(rlo_world_t* w, rlo_rank_stats_t* out, int n);
 int rlo_log(rlo_world_t* w, int rank, rlo_log_rec_t* out, uint32_t cap, uint8_t* payload, uint32_t payload_stride);
 int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap);

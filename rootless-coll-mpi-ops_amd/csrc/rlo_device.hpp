@@ -1,14 +1,17 @@
 // rlo_device.hpp -- plain-old-data shared by the host world builder (rlo_world.cpp)
 // and the persistent progress kernel (rlo_kernel.hip).
 //
-// One "world" = N virtual ranks.  Every rank is one 4-wave (256-thread) workgroup
-// of the persistent kernel.  Every directed overlay edge (r -> send_list(r)[j]) owns
+// One "world" = N ranks, partitioned into parts (contiguous rank ranges).  A part is
+// hosted by one process on one GPU; every rank of a part is one 4-wave (256-thread)
+// workgroup of that part's persistent kernel.  Every directed overlay edge
+// (r -> send_list(r)[j]) owns
 //   * two forward rings (virtual channels vc = 0/1, vc = child < origin; the
 //     "dateline" split that makes the ring channel-dependency graph acyclic),
 //   * one reverse vote ring (child -> parent).
-// Ring bytes live in the consumer's HBM; the producer count (tail) sits in the
-// consumer's packed inbox control block, the consumer count (head, = credits)
-// in the producer's packed outbox control block.
+// A ring's bytes and its producer count (tail) live in the CONSUMER's part; the
+// consumer count (head, = credits) lives in the PRODUCER's part.  So every poll is
+// local, and every remote access is a store (payload, tail, head) into a peer part's
+// HBM -- through a hipIpc mapping when the peer is another process / GPU (xGMI).
 #pragma once
 #include <stdint.h>
 
@@ -23,7 +26,9 @@ constexpr int kHdr = 16;          // slot header bytes
 constexpr int kVoteSlot = 16;     // vote ring slot bytes
 constexpr int kMaxCand = 256;     // messages handled per rank per progress iteration (4 passes of 64)
 constexpr int kStagePasses = 4;  // 4 x 64 messages per progress iteration
-constexpr int kHistBins = 128;    // latency histogram: 8 sub-bins per octave of 10 ns ticks
+constexpr int kHistBins = 128;    // latency histogram: 4 sub-bins per octave of 10 ns ticks
+constexpr int kMaxParts = 64;     // parts (processes x GPUs) of one world
+constexpr int kCtrlHdrWords = 16; // per-part control words before the rank blocks: [0] error flag
 
 // message classes == enum RLO_COMM_TAGS (rootless_ops.h:50-61)
 enum Tag : uint32_t { TAG_BCAST = 0, TAG_PROPOSAL = 2, TAG_VOTE = 3, TAG_DECISION = 4 };
@@ -56,19 +61,18 @@ struct RankTopo {
     int32_t send_list[kMaxFanout];
     int32_t n_in;                          // forward in-edges
     int32_t in_src[kMaxIn];                // sender rank of in-edge k
-    // forward rings I produce into: (j, vc)
-    uint32_t out_data[kMaxFanout][2];      // byte offset of ring data in the forward region
-    uint32_t out_tail[kMaxFanout][2];      // index of its tail word in ctrl[]
-    uint32_t out_head[kMaxFanout][2];      // index of its head word in ctrl[]
-    // forward rings I consume: (k, vc)
-    uint32_t in_data[kMaxIn][2];
-    uint32_t in_tail[kMaxIn][2];
-    uint32_t in_head[kMaxIn][2];
-    // vote rings: I produce towards parent over in-edge k, I consume from child j
-    uint32_t vout_data[kMaxIn], vout_tail[kMaxIn], vout_head[kMaxIn];
-    uint32_t vin_data[kMaxFanout], vin_tail[kMaxFanout], vin_head[kMaxFanout];
-    uint32_t inbox_ctrl, n_inbox;          // my packed tails (fwd in 2*n_in, then votes-in sll)
-    uint32_t outbox_ctrl, n_outbox;        // my packed heads (fwd out 2*sll, then votes-out n_in)
+    // rings I consume (local part): byte offsets in my part's forward / vote regions
+    uint32_t in_data[kMaxIn][2];           // forward in-ring (k, vc)
+    uint32_t vin_data[kMaxFanout];         // vote ring from child j
+    uint32_t inbox_ctrl, n_inbox;          // my tails in my part's ctrl: fwd in 2*n_in, then votes-in sll
+    uint32_t outbox_ctrl, n_outbox;        // my heads in my part's ctrl: fwd out 2*sll, then votes-out n_in
+    // remote ends, as addresses valid in the hosting process (peer HBM via hipIpc / P2P)
+    uint64_t out_ring[kMaxFanout][2];      // forward ring (j, vc) data, in the child's part
+    uint64_t out_tail[kMaxFanout][2];      // its tail word, in the child's ctrl
+    uint64_t in_head[kMaxIn][2];           // head word of in-ring (k, vc), in the parent's ctrl
+    uint64_t vout_ring[kMaxIn];            // vote ring to the parent of in-edge k, in the parent's part
+    uint64_t vout_tail[kMaxIn];            // its tail word, in the parent's ctrl
+    uint64_t vin_head[kMaxFanout];         // head word of the vote ring from child j, in the child's ctrl
 };
 
 struct RankStats {
@@ -99,13 +103,16 @@ struct Params {
     int32_t n, rank_begin, rank_end;
     uint32_t mode;
     const RankTopo* topo;         // [rank_end - rank_begin]
-    uint8_t* fwd_region;          // all forward ring bytes of this GPU (<= 4 GiB, one buffer rsrc)
+    uint8_t* fwd_region;          // this part's forward in-rings (<= 4 GiB, one buffer rsrc)
     uint32_t fwd_region_bytes;
     uint32_t fwd_cap, fwd_stride; // slots per forward ring (pow2), slot stride bytes
-    uint8_t* vote_region;
+    uint8_t* vote_region;         // this part's vote in-rings
     uint32_t vote_region_bytes;
     uint32_t vote_cap;            // slots per vote ring (pow2), >= 2 * N
-    uint64_t* ctrl;               // tails / heads
+    uint64_t* ctrl;               // this part's control words (tails / heads of its ranks)
+    uint32_t sys_scope;           // 1: some peer part is on another GPU -> system-scope remote stores
+    uint32_t n_parts;
+    uint32_t* err_flag[kMaxParts];// every part's error word (ctrl word 0 of each part)
     // storm / latency workload
     uint64_t seed;
     uint32_t len, window;         // payload bytes; max originations per iteration
@@ -137,7 +144,7 @@ struct Params {
     // control
     uint64_t timeout_ticks;       // no progress for this long -> ERR_TIMEOUT (100 MHz ticks)
     uint64_t deadline_ticks;      // hard cap on one launch (every spin is bounded)
-    uint32_t* error_flag;         // any rank's first error
+    uint32_t* error_flag;         // this part's error word (polled every iteration)
     // dynamic LDS carve-out: [pend: 2N x 16 B][olist: nout_max x 256 x 2 B]
     //                        [stage: 256 x nsmall x 16 B][stage2: stage2_bytes]
     uint32_t nsmall;              // slot chunks staged per message on the small path (<= 8)

@@ -137,8 +137,17 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t* dst, ui
 __device__ __forceinline__ uint64_t poll64(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void pub64(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// a counter store into a (possibly peer) part: agent scope inside one GPU, system scope when
+// the world spans GPUs (the store then crosses xGMI into the peer's HBM)
+__device__ __forceinline__ void pub64(uint64_t addr, uint64_t v, bool sys) {
+    uint64_t* p = reinterpret_cast<uint64_t*>(addr);
+    if (sys) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-B slot store into a remote ring through a wave-uniform ring base (buffer rsrc built on the fly)
+__device__ __forceinline__ void st_ring(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, bool sys) {
+    if (sys) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1 | 1);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1);
 }
 __device__ __forceinline__ uint32_t poll32(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -147,6 +156,9 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 
 // per-ring state lives lane-distributed in registers; a wave-uniform index reads it with v_readlane
 __device__ __forceinline__ uint32_t rdl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
+    return ((uint64_t)rdl32((uint32_t)(v >> 32), l) << 32) | rdl32((uint32_t)v, l);
+}
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // i / d for the small d = nsmall (<= 8) and i < 2^16: multiply-high by ceil(2^32 / d)
@@ -236,6 +248,8 @@ __device__ __forceinline__ void set_error(Shared& S, const Params& P, uint32_t c
     if (atomicCAS(&S.error, 0u, code) == 0u) {
         S.error_aux = aux;
         atomicCAS(P.error_flag, 0u, code);
+        for (uint32_t q = 0; q < P.n_parts; q++)  // every other part stops too (they poll their own word)
+            if (P.err_flag[q] != P.error_flag) __hip_atomic_store(P.err_flag[q], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -291,19 +305,23 @@ __device__ __forceinline__ uint32_t log_put(Shared& S, const Params& P, int lr, 
 }
 
 // vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741)
-__device__ __forceinline__ void emit_vote(Shared& S, const Params& P, __amdgpu_buffer_rsrc_t rv, int me, uint32_t k,
+__device__ __forceinline__ void emit_vote(Shared& S, const Params& P, int me, uint32_t k,
                                           int origin, int32_t pid, uint32_t pseq, int vote) {
     unsigned long long p = atomicAdd((unsigned long long*)&S.vout_tail[k], 1ull);
     if (p - S.vout_head[k] >= P.vote_cap) {
         set_error(S, P, ERR_VOTE_RING, k);
         return;
     }
-    u32x4 v;
-    v.x = (uint32_t)origin | ((uint32_t)(vote & 0xff) << 24);
-    v.y = (uint32_t)pid;
-    v.z = pseq & 0xffu;
-    v.w = (uint32_t)me;
-    st_sc1(rv, S.t.vout_data[k] + (uint32_t)(p & (P.vote_cap - 1)) * kVoteSlot, v);
+    const uint64_t lo = (uint64_t)((uint32_t)origin | ((uint32_t)(vote & 0xff) << 24)) | ((uint64_t)(uint32_t)pid << 32);
+    const uint64_t hi = (uint64_t)(pseq & 0xffu) | ((uint64_t)(uint32_t)me << 32);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(S.t.vout_ring[k] + (uint64_t)(p & (P.vote_cap - 1)) * kVoteSlot);
+    if (P.sys_scope) {
+        __hip_atomic_store(dst, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dst + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        __hip_atomic_store(dst, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // exclusive wave-wide prefix sum with DPP row shifts + row broadcasts (no LDS traffic)
@@ -419,12 +437,15 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     const int n_in = uni(t.n_in), n_in2 = 2 * n_in, nout = 2 * sll;
     const uint32_t inbox = (uint32_t)uni((int)t.inbox_ctrl), outbox = (uint32_t)uni((int)t.outbox_ctrl);
     const uint32_t sl_r = lane < sll ? (uint32_t)t.send_list[lane] : 0u;
-    const uint32_t od_r = lane < nout ? t.out_data[lane >> 1][lane & 1] : 0u;  // out-ring data offset
-    // wave 0 owns the ring counters: lane g = in-ring g, lane oi = out-ring oi, lane j = vote ring j
-    const uint32_t otix_r = lane < nout ? t.out_tail[lane >> 1][lane & 1] : 0u;  // where its tail is published
-    const uint32_t ihix_r = lane < n_in2 ? t.in_head[lane >> 1][lane & 1] : 0u;  // where its head is published
-    const uint32_t vhix_r = lane < sll ? t.vin_head[lane] : 0u;
-    const uint32_t vtix_r = lane < n_in ? t.vout_tail[lane] : 0u;
+    const bool sys = P.sys_scope != 0;
+    const uint64_t oring_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;  // out-ring data (child's part)
+    const uint32_t oring_bytes = P.fwd_cap * P.fwd_stride;
+    // wave 0 owns the ring counters: lane g = in-ring g, lane oi = out-ring oi, lane j = vote ring j;
+    // each counter is published by a store into the part that polls it
+    const uint64_t otptr_r = lane < nout ? t.out_tail[lane >> 1][lane & 1] : 0ull;
+    const uint64_t ihptr_r = lane < n_in2 ? t.in_head[lane >> 1][lane & 1] : 0ull;
+    const uint64_t vhptr_r = lane < sll ? t.vin_head[lane] : 0ull;
+    const uint64_t vtptr_r = lane < n_in ? t.vout_tail[lane] : 0ull;
     uint64_t in_head_r = 0, pub_in_r = 0, out_tail_r = 0, pub_out_r = 0, vin_head_r = 0, pub_vin_r = 0, pub_vout_r = 0;
     // per in-ring window: messages worth staging next iteration.  A ring whose prefix was cut by
     // out-ring credits is re-staged only a little past what fitted, so a hot rank does not pull
@@ -454,12 +475,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
         // ---------------- C (wave 0): publish the previous iteration, select this one
         if (w == 0) {
-            if (lane < nout && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(&P.ctrl[otix_r], out_tail_r); }
-            if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(&P.ctrl[ihix_r], in_head_r); }
-            if (lane < sll && vin_head_r != pub_vin_r) { pub_vin_r = vin_head_r; pub64(&P.ctrl[vhix_r], vin_head_r); }
+            if (lane < nout && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(otptr_r, out_tail_r, sys); }
+            if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(ihptr_r, in_head_r, sys); }
+            if (lane < sll && vin_head_r != pub_vin_r) { pub_vin_r = vin_head_r; pub64(vhptr_r, vin_head_r, sys); }
             if (lane < n_in) {
                 const uint64_t vt = S.vout_tail[lane];
-                if (vt != pub_vout_r) { pub_vout_r = vt; pub64(&P.ctrl[vtix_r], vt); }
+                if (vt != pub_vout_r) { pub_vout_r = vt; pub64(vtptr_r, vt, sys); }
                 S.vout_head[lane] = vout_head_r;
             }
             peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
@@ -614,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                         } else {
                             const uint32_t nw = atomicAdd(&ps->word, inc) + inc;
                             if ((nw & 0xffffu) == ps->needed)
-                                emit_vote(S, P, rv, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+                                emit_vote(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
                         }
                     }
                 }
@@ -778,7 +799,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                             atomicAdd(&S.judge_calls, 1ull);
                             log_put(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
                             if (!judge) {
-                                emit_vote(S, P, rv, me, (uint32_t)k, origin, pid, pseq, 0);
+                                emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 0);
                             } else {
                                 PendState* ps = &pend[2 * origin + (pseq & 1u)];
                                 const uint32_t nk = (uint32_t)__builtin_popcount(kids);
@@ -788,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                                 ps->needed = (uint8_t)nk;
                                 ps->pseq = pseq | ((len - 16u) << 8);
                                 ps->valid = 1;
-                                if (nk == 0) emit_vote(S, P, rv, me, (uint32_t)k, origin, pid, pseq, 1);
+                                if (nk == 0) emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 1);
                             }
                         }
                     } else if (tag == TAG_DECISION) {  // :603-615, _iar_decision_handler :814-859
@@ -897,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 const uint32_t n = S.n_oi[oi];
                 if (!n) continue;
                 const uint64_t slot0 = S.out_tail0[oi];
-                const uint32_t odat = rdl32(od_r, oi);
+                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(oring_r, oi)), oring_bytes);
                 const uint32_t nit = n * nsmall;
                 for (uint32_t i = lane; i < nit; i += 64) {
                     const uint32_t r = div_small(i, nmagic), q = i - r * nsmall;
@@ -905,8 +926,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (e & kBigFlag) continue;
                     const uint32_t nch = (kHdr + (S.cand[e].w2 & 0xffffffu) + 15u) >> 4;
                     if (q < nch)
-                        st_sc1(rf, odat + (uint32_t)((slot0 + r) & fcap_m) * P.fwd_stride + 16u * q,
-                               *reinterpret_cast<const u32x4*>(STG(e, q)));
+                        st_ring(ro, (uint32_t)((slot0 + r) & fcap_m) * P.fwd_stride + 16u * q,
+                                *reinterpret_cast<const u32x4*>(STG(e, q)), sys);
                 }
             }
             if (admitted && !isbig && kind == K_RING && tag == TAG_BCAST) {  // pickup: checksum (+ log payload)
@@ -932,7 +953,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                         for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
                             const int oi = __builtin_ctz(a2);
                             const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
-                            if (q < nch) st_sc1(rf, rdl32(od_r, oi) + (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v);
+                            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(oring_r, oi)), oring_bytes);
+                            if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
                         }
                         if (q < nch && cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
                             acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})

@@ -1,11 +1,14 @@
-// rlo_world.cpp -- host side of the engine: overlay topology, HBM layout of the
-// mailbox rings, programs (storm / latency / iar), launch and result readout.
-// Exposes the C ABI of include/rlo_hip.h.
+// rlo_world.cpp -- host side of the engine: overlay topology, the global HBM layout of
+// the mailbox rings, parts (one per process / GPU) and their connection through hipIpc,
+// programs (storm / latency / iar), launch and result readout.  Exposes the C ABI of
+// include/rlo_hip.h.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -119,23 +122,151 @@ struct DevBuf {
     }
 };
 
+// ------------------------------------------------------------------ global layout
+// Computed identically by every part from (n, part boundaries, payload, ring slots), so
+// parts agree on every offset without exchanging tables.
+struct Edge { int src, dst, j, k; };
+
+struct Layout {
+    int n = 0, nparts = 0;
+    std::vector<int> pb;          // part boundaries [nparts + 1]
+    std::vector<int> part_of;     // [n]
+    std::vector<Topo> T;          // [n]
+    std::vector<Edge> E;
+    std::vector<std::vector<int>> in_edges;
+    int max_in = 0, max_fan = 0;
+    uint32_t cap = 0, stride = 0, vote_cap = 0;
+    std::vector<uint64_t> fwd_bytes, vote_bytes, ctrl_words;  // per part
+    std::vector<uint64_t> fwd_off, vote_off;                  // per edge (vc 0 ring; vc 1 follows)
+    std::vector<uint32_t> inbox, outbox;                      // per rank: word index in its part's ctrl
+};
+
+int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uint32_t ring_slots, Layout& L) {
+    if (n < 2 || n > 65535 || nparts < 1 || nparts > rlo::kMaxParts) return RLO_E_INVAL;
+    L.n = n;
+    L.nparts = nparts;
+    L.pb.assign(nparts + 1, 0);
+    if (pb) {
+        for (int p = 0; p <= nparts; p++) L.pb[p] = pb[p];
+    } else {  // contiguous, as even as possible
+        for (int p = 0; p <= nparts; p++) L.pb[p] = (int)((int64_t)n * p / nparts);
+    }
+    if (L.pb[0] != 0 || L.pb[nparts] != n) return RLO_E_INVAL;
+    for (int p = 0; p < nparts; p++)
+        if (L.pb[p + 1] <= L.pb[p]) return RLO_E_INVAL;
+    L.part_of.assign(n, 0);
+    for (int p = 0; p < nparts; p++)
+        for (int r = L.pb[p]; r < L.pb[p + 1]; r++) L.part_of[r] = p;
+    L.stride = rlo::kHdr + max_payload;
+
+    L.T.assign(n, Topo{});
+    for (int r = 0; r < n; r++)
+        if (topo_of(n, r, &L.T[r])) return RLO_E_INVAL;
+    L.in_edges.assign(n, {});
+    for (int r = 0; r < n; r++)
+        for (int j = 0; j < L.T[r].sll; j++) {
+            L.in_edges[L.T[r].send_list[j]].push_back((int)L.E.size());
+            L.E.push_back({r, L.T[r].send_list[j], j, 0});
+        }
+    for (int c = 0; c < n; c++) {
+        if ((int)L.in_edges[c].size() > rlo::kMaxIn) return RLO_E_INVAL;
+        L.max_in = std::max(L.max_in, (int)L.in_edges[c].size());
+        for (int k = 0; k < (int)L.in_edges[c].size(); k++) L.E[L.in_edges[c][k]].k = k;
+    }
+    for (int r = 0; r < n; r++) L.max_fan = std::max(L.max_fan, L.T[r].sll);
+
+    // ring capacity: every part's forward region must fit one 32-bit buffer resource
+    std::vector<uint64_t> rings(nparts, 0), vrings(nparts, 0);
+    for (const Edge& e : L.E) {
+        rings[L.part_of[e.dst]] += 2;
+        vrings[L.part_of[e.src]] += 1;
+    }
+    const uint64_t max_rings = *std::max_element(rings.begin(), rings.end());
+    uint32_t cap = ring_slots ? pow2_ceil(ring_slots) : 512u;
+    const uint64_t limit = 0xFFFF0000ull;
+    if (max_rings * cap * L.stride > limit) cap = pow2_floor(limit / (max_rings * L.stride));
+    if (cap < 16) return RLO_E_INVAL;
+    L.cap = cap;
+    L.vote_cap = std::max<uint32_t>(64u, pow2_ceil(2u * (uint32_t)n));
+
+    const uint64_t ring_bytes = (uint64_t)cap * L.stride;
+    L.fwd_bytes.assign(nparts, 0);
+    L.vote_bytes.assign(nparts, 0);
+    L.fwd_off.assign(L.E.size(), 0);
+    L.vote_off.assign(L.E.size(), 0);
+    for (size_t e = 0; e < L.E.size(); e++) {
+        const int pd = L.part_of[L.E[e].dst], ps = L.part_of[L.E[e].src];
+        L.fwd_off[e] = L.fwd_bytes[pd];
+        L.fwd_bytes[pd] += 2 * ring_bytes;
+        L.vote_off[e] = L.vote_bytes[ps];
+        L.vote_bytes[ps] += (uint64_t)L.vote_cap * rlo::kVoteSlot;
+    }
+    if (*std::max_element(L.vote_bytes.begin(), L.vote_bytes.end()) > limit) return RLO_E_INVAL;
+
+    // control words: per part a header (word 0 = error flag), then per rank an inbox block
+    // (tails of its in-rings + vote in-rings) and an outbox block (heads), 128-B aligned
+    L.ctrl_words.assign(nparts, 0);
+    L.inbox.assign(n, 0);
+    L.outbox.assign(n, 0);
+    for (int p = 0; p < nparts; p++) {
+        uint64_t words = rlo::kCtrlHdrWords;
+        for (int r = L.pb[p]; r < L.pb[p + 1]; r++) {
+            L.inbox[r] = (uint32_t)words;
+            words += (2 * L.in_edges[r].size() + L.T[r].sll + 15) & ~15ull;
+            L.outbox[r] = (uint32_t)words;
+            words += (2 * L.T[r].sll + L.in_edges[r].size() + 15) & ~15ull;
+        }
+        L.ctrl_words[p] = words;
+    }
+    return RLO_OK;
+}
+
+// one part's connection record: what a peer needs to map this part's regions
+struct PartBlob {
+    uint32_t magic, version;
+    int32_t part, nparts, n, device;
+    uint32_t cap, stride, vote_cap, pad;
+    uint64_t token;  // identifies the hosting process
+    uint64_t fwd_ptr, vote_ptr, ctrl_ptr;
+    uint64_t fwd_bytes, vote_bytes, ctrl_bytes;
+    char bus[32];
+    hipIpcMemHandle_t hf, hv, hc;
+};
+static_assert(sizeof(PartBlob) <= RLO_PART_BLOB_BYTES, "blob");
+constexpr uint32_t kBlobMagic = 0x524C4F50u;  // "RLOP"
+
+uint64_t process_token() {
+    static uint64_t tok = 0;
+    if (!tok) {
+        std::random_device rd;
+        tok = ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 17) ^ (uint64_t)(uintptr_t)&tok;
+        if (!tok) tok = 1;
+    }
+    return tok;
+}
+
 }  // namespace
 
 struct rlo_world {
-    int n = 0, device = 0;
-    uint32_t max_payload = 0, stride = 0, fwd_cap = 0, vote_cap = 0;
-    int edges = 0, max_in = 0, max_fan = 0;
+    Layout L;
+    int part = 0, nl = 0, rb = 0;  // my part, local rank count, first local rank
+    int device = 0;
+    uint32_t max_payload = 0, flags = 0;
     int cus = 0, blocks_per_cu = 0;
-    std::vector<rlo::RankTopo> topo;
+    bool connected = false;
+    int sys_scope = 0;
+    // local regions (the rings / counters this part consumes)
     uint8_t* fwd = nullptr;
     uint8_t* vote = nullptr;
     uint64_t* ctrl = nullptr;
-    uint64_t fwd_bytes = 0, vote_bytes = 0, ctrl_words = 0;
+    // every part's regions as addresses in this process
+    std::vector<uint8_t*> pf, pv;
+    std::vector<uint64_t*> pc;
+    std::vector<void*> opened;  // hipIpc mappings to close
+    std::vector<rlo::RankTopo> topo;
     DevBuf<rlo::RankTopo> d_topo;
     DevBuf<rlo::RankStats> d_stats;
-    DevBuf<uint32_t> d_err;
     // program
-    uint32_t mode = 0;
     bool have_program = false;
     rlo::Params P{};
     DevBuf<int64_t> d_sched_off, d_expect_bcast, d_prop_off, d_expect_dec;
@@ -147,11 +278,97 @@ struct rlo_world {
     DevBuf<rlo::LogRec> d_log;
     uint32_t lat_rounds = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipStream_t last_stream = nullptr;
     float last_ms = 0.f;
     size_t dyn_lds = 0;
     uint32_t nsmall = 8, stage2 = 1024;
 };
+
+namespace {
+
+int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
+    if (bytes == 0) bytes = 256;
+    hipError_t e;
+    if (w->flags & RLO_PART_UNCACHED) e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    else e = hipMalloc(p, bytes);
+    if (e != hipSuccess) { g_last_hip = (int)e; *p = nullptr; return RLO_E_HIP; }
+    return RLO_OK;
+}
+
+// co-residency of the part's rank-workgroups: largest small-path stage (nsmall chunks per
+// message, <= 8) and then the largest stage2 (<= 64 KiB) at which the occupancy calculator
+// (LDS allocation granularity, registers, waves) still co-schedules them
+int size_lds(rlo_world* w) {
+    const Layout& L = w->L;
+    const size_t lds_cu = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
+    const int need_bpc = (w->nl + w->cus - 1) / w->cus;
+    const size_t per_block = lds_cu / need_bpc;
+    int api = 0;
+    bool ok = false;
+    for (uint32_t ns = std::min<uint32_t>(8u, L.stride / 16u); ns >= 1 && !ok; ns--) {
+        const size_t fixed = rlo_kernel_static_lds() + (size_t)32 * L.n + (size_t)2 * L.max_fan * 256 * 2 +
+                             (size_t)rlo::kMaxCand * ns * 16;
+        if (per_block < fixed + 1024 + 512) continue;
+        size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
+        for (;;) {
+            w->dyn_lds = fixed - rlo_kernel_static_lds() + s2;
+            if (rlo_occupancy(&api, w->dyn_lds) != hipSuccess) api = 0;
+            if (api >= need_bpc) { ok = true; break; }
+            if (s2 <= 1024) break;
+            s2 -= 1024;
+        }
+        w->nsmall = ns;
+        w->stage2 = (uint32_t)s2;
+    }
+    if (!ok) return RLO_E_OCCUPANCY;
+    w->blocks_per_cu = std::max(1, api);
+    if (w->nl > w->blocks_per_cu * w->cus) return RLO_E_OCCUPANCY;
+    return RLO_OK;
+}
+
+// RankTopo of every local rank, with remote ends resolved to addresses in this process
+void build_topo(rlo_world* w) {
+    const Layout& L = w->L;
+    const uint64_t ring_bytes = (uint64_t)L.cap * L.stride;
+    w->topo.assign(w->nl, rlo::RankTopo{});
+    for (int r = w->rb; r < w->rb + w->nl; r++) {
+        rlo::RankTopo& t = w->topo[r - w->rb];
+        t.level = L.T[r].level;
+        t.last_wall = L.T[r].last_wall;
+        t.scc = L.T[r].scc;
+        t.sll = L.T[r].sll;
+        for (int j = 0; j < L.T[r].sll; j++) t.send_list[j] = L.T[r].send_list[j];
+        t.n_in = (int)L.in_edges[r].size();
+        t.inbox_ctrl = L.inbox[r];
+        t.n_inbox = 2 * t.n_in + t.sll;
+        t.outbox_ctrl = L.outbox[r];
+        t.n_outbox = 2 * t.sll + t.n_in;
+    }
+    for (size_t e = 0; e < L.E.size(); e++) {
+        const Edge& ed = L.E[e];
+        const int ps = L.part_of[ed.src], pd = L.part_of[ed.dst];
+        if (ps == w->part) {  // I produce its forward rings, consume its votes
+            rlo::RankTopo& t = w->topo[ed.src - w->rb];
+            for (int vc = 0; vc < 2; vc++) {
+                t.out_ring[ed.j][vc] = (uint64_t)(uintptr_t)(w->pf[pd] + L.fwd_off[e] + vc * ring_bytes);
+                t.out_tail[ed.j][vc] = (uint64_t)(uintptr_t)(w->pc[pd] + L.inbox[ed.dst] + 2 * ed.k + vc);
+            }
+            t.vin_data[ed.j] = (uint32_t)L.vote_off[e];
+            t.vin_head[ed.j] = (uint64_t)(uintptr_t)(w->pc[pd] + L.outbox[ed.dst] + 2 * L.T[ed.dst].sll + ed.k);
+        }
+        if (pd == w->part) {  // I consume its forward rings, produce its votes
+            rlo::RankTopo& t = w->topo[ed.dst - w->rb];
+            for (int vc = 0; vc < 2; vc++) {
+                t.in_data[ed.k][vc] = (uint32_t)(L.fwd_off[e] + vc * ring_bytes);
+                t.in_head[ed.k][vc] = (uint64_t)(uintptr_t)(w->pc[ps] + L.outbox[ed.src] + 2 * ed.j + vc);
+            }
+            t.in_src[ed.k] = ed.src;
+            t.vout_ring[ed.k] = (uint64_t)(uintptr_t)(w->pv[ps] + L.vote_off[e]);
+            t.vout_tail[ed.k] = (uint64_t)(uintptr_t)(w->pc[ps] + L.inbox[ed.src] + 2 * L.in_edges[ed.src].size() + ed.j);
+        }
+    }
+}
+
+}  // namespace
 
 // ====================================================================== C ABI
 
@@ -168,6 +385,7 @@ const char* rlo_strerror(int code) {
         case RLO_E_DEVICE: return "device-side engine error";
         case RLO_E_NOPROGRAM: return "no program loaded";
         case RLO_E_NODEVICE: return "no HIP device";
+        case RLO_E_NOTCONNECTED: return "part not connected";
         default: return "unknown";
     }
 }
@@ -202,161 +420,149 @@ int rlo_children(int n, int rank, int origin, int from, int* out) {
     return c;
 }
 
-int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
-    if (!cfg || !out || cfg->n_ranks < 2 || cfg->n_ranks > 4096) return RLO_E_INVAL;
+int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
+    if (!cfg || !out || cfg->n_parts < 1 || cfg->part < 0 || cfg->part >= cfg->n_parts) return RLO_E_INVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return RLO_E_NODEVICE;
     rlo_world* w = new rlo_world();
-    const int n = cfg->n_ranks;
-    w->n = n;
-    if (cfg->device >= 0) {
-        if (hipSetDevice(cfg->device) != hipSuccess) { delete w; return RLO_E_HIP; }
-    }
-    (void)hipGetDevice(&w->device);
     w->max_payload = (std::max<uint32_t>(cfg->max_payload ? cfg->max_payload : 4096u, 16u) + 15u) & ~15u;
-    w->stride = rlo::kHdr + w->max_payload;
-
-    // ---- overlay: nodes, directed edges, in-edge lists
-    std::vector<Topo> T(n);
-    for (int r = 0; r < n; r++)
-        if (topo_of(n, r, &T[r])) { delete w; return RLO_E_INVAL; }
-    struct Edge { int src, dst, j, k; };
-    std::vector<Edge> E;
-    std::vector<std::vector<int>> in_edges(n);
-    std::vector<std::vector<int>> out_edge(n);
-    for (int r = 0; r < n; r++) {
-        out_edge[r].resize(T[r].sll);
-        for (int j = 0; j < T[r].sll; j++) {
-            int e = (int)E.size();
-            E.push_back({r, T[r].send_list[j], j, 0});
-            out_edge[r][j] = e;
-            in_edges[T[r].send_list[j]].push_back(e);
-        }
-    }
-    for (int c = 0; c < n; c++) {
-        if ((int)in_edges[c].size() > rlo::kMaxIn) { delete w; return RLO_E_INVAL; }
-        w->max_in = std::max(w->max_in, (int)in_edges[c].size());
-        for (int k = 0; k < (int)in_edges[c].size(); k++) E[in_edges[c][k]].k = k;
-    }
-    for (int r = 0; r < n; r++) w->max_fan = std::max(w->max_fan, T[r].sll);
-    w->edges = (int)E.size();
-
-    // ---- ring sizing: the whole forward region must fit one 32-bit buffer resource
-    const uint64_t nrings = 2ull * E.size();
-    uint32_t cap = cfg->ring_slots ? pow2_ceil(cfg->ring_slots) : 512u;
-    const uint64_t limit = 0xFFFF0000ull;
-    if (nrings * cap * w->stride > limit) cap = pow2_floor(limit / (nrings * w->stride));
-    if (cap < 16) { delete w; return RLO_E_INVAL; }
-    w->fwd_cap = cap;
-    w->vote_cap = std::max<uint32_t>(64u, pow2_ceil(2u * (uint32_t)n));
-    w->fwd_bytes = nrings * cap * w->stride;
-    w->vote_bytes = (uint64_t)E.size() * w->vote_cap * rlo::kVoteSlot;
-
-    // ---- control words: per rank an inbox block (tails) and an outbox block (heads)
-    std::vector<uint32_t> inbox(n), outbox(n);
-    uint64_t words = 0;
-    for (int r = 0; r < n; r++) {
-        inbox[r] = (uint32_t)words;
-        words += (2 * in_edges[r].size() + T[r].sll + 15) & ~15ull;  // 128-byte blocks
-        outbox[r] = (uint32_t)words;
-        words += (2 * T[r].sll + in_edges[r].size() + 15) & ~15ull;
-    }
-    w->ctrl_words = words;
-
-    w->topo.assign(n, rlo::RankTopo{});
-    for (int r = 0; r < n; r++) {
-        rlo::RankTopo& t = w->topo[r];
-        t.level = T[r].level;
-        t.last_wall = T[r].last_wall;
-        t.scc = T[r].scc;
-        t.sll = T[r].sll;
-        for (int j = 0; j < T[r].sll; j++) t.send_list[j] = T[r].send_list[j];
-        t.n_in = (int)in_edges[r].size();
-        t.inbox_ctrl = inbox[r];
-        t.n_inbox = 2 * t.n_in + t.sll;
-        t.outbox_ctrl = outbox[r];
-        t.n_outbox = 2 * t.sll + t.n_in;
-    }
-    const uint64_t ring_bytes = (uint64_t)cap * w->stride;
-    for (int e = 0; e < (int)E.size(); e++) {
-        const Edge& ed = E[e];
-        rlo::RankTopo& P = w->topo[ed.src];  // producer of forward rings, consumer of votes
-        rlo::RankTopo& C = w->topo[ed.dst];  // consumer of forward rings, producer of votes
-        for (int vc = 0; vc < 2; vc++) {
-            uint32_t data = (uint32_t)((2ull * e + vc) * ring_bytes);
-            uint32_t tail = inbox[ed.dst] + 2 * ed.k + vc;
-            uint32_t head = outbox[ed.src] + 2 * ed.j + vc;
-            P.out_data[ed.j][vc] = data; P.out_tail[ed.j][vc] = tail; P.out_head[ed.j][vc] = head;
-            C.in_data[ed.k][vc] = data; C.in_tail[ed.k][vc] = tail; C.in_head[ed.k][vc] = head;
-        }
-        C.in_src[ed.k] = ed.src;
-        uint32_t vdata = (uint32_t)((uint64_t)e * w->vote_cap * rlo::kVoteSlot);
-        uint32_t vtail = inbox[ed.src] + 2 * P.n_in + ed.j;
-        uint32_t vhead = outbox[ed.dst] + 2 * C.sll + ed.k;
-        C.vout_data[ed.k] = vdata; C.vout_tail[ed.k] = vtail; C.vout_head[ed.k] = vhead;
-        P.vin_data[ed.j] = vdata; P.vin_tail[ed.j] = vtail; P.vin_head[ed.j] = vhead;
-    }
-
-    // ---- residency: every rank-workgroup must be resident at once (persistent kernel).
-    // Dynamic LDS = [pend 2N x 16 B][olist 2 max_fan x 256 x 2 B][stage 256 x nsmall x 16 B][stage2].
+    w->flags = cfg->flags;
+    int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, w->L);
+    if (rc) { delete w; return rc; }
+    w->part = cfg->part;
+    w->rb = w->L.pb[w->part];
+    w->nl = w->L.pb[w->part + 1] - w->rb;
+    if (cfg->device >= 0 && hipSetDevice(cfg->device) != hipSuccess) { delete w; return RLO_E_HIP; }
+    (void)hipGetDevice(&w->device);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, w->device) != hipSuccess) { delete w; return RLO_E_HIP; }
     w->cus = prop.multiProcessorCount;
-    {
-        // Largest small-path stage (nsmall chunks per message, <= 8) and then the largest stage2
-        // (<= 64 KiB) at which the occupancy calculator (LDS allocation granularity, registers,
-        // waves) still co-schedules need_bpc rank-workgroups per CU.
-        const size_t lds_cu = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
-        const int need_bpc = (n + w->cus - 1) / w->cus;
-        const size_t per_block = lds_cu / need_bpc;
-        int api = 0;
-        bool ok = false;
-        for (uint32_t ns = std::min<uint32_t>(8u, w->stride / 16u); ns >= 1 && !ok; ns--) {
-            const size_t fixed = rlo_kernel_static_lds() + (size_t)32 * n + (size_t)2 * w->max_fan * 256 * 2 +
-                                 (size_t)rlo::kMaxCand * ns * 16;
-            if (per_block < fixed + 1024 + 512) continue;
-            size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
-            for (;;) {
-                w->dyn_lds = fixed - rlo_kernel_static_lds() + s2;
-                if (rlo_occupancy(&api, w->dyn_lds) != hipSuccess) api = 0;
-                if (api >= need_bpc) { ok = true; break; }
-                if (s2 <= 1024) break;
-                s2 -= 1024;
-            }
-            w->nsmall = ns;
-            w->stage2 = (uint32_t)s2;
-        }
-        if (!ok) { delete w; return RLO_E_OCCUPANCY; }
-        w->blocks_per_cu = std::max(1, api);
-        if (n > w->blocks_per_cu * w->cus) { delete w; return RLO_E_OCCUPANCY; }
-    }
-
-    // ---- allocate
-    if (hipMalloc(&w->fwd, w->fwd_bytes) != hipSuccess ||
-        hipMalloc(&w->vote, w->vote_bytes) != hipSuccess ||
-        hipMalloc(&w->ctrl, w->ctrl_words * 8) != hipSuccess) {
-        g_last_hip = (int)hipGetLastError();
+    rc = size_lds(w);
+    if (rc) { delete w; return rc; }
+    const int me = w->part;
+    if (alloc_region(w, (void**)&w->fwd, w->L.fwd_bytes[me]) || alloc_region(w, (void**)&w->vote, w->L.vote_bytes[me]) ||
+        alloc_region(w, (void**)&w->ctrl, w->L.ctrl_words[me] * 8)) {
         rlo_world_destroy(w);
         return RLO_E_HIP;
     }
-    if (w->d_topo.upload(w->topo) || w->d_stats.alloc(n) || w->d_err.alloc(4)) {
-        rlo_world_destroy(w);
-        return RLO_E_HIP;
-    }
-    (void)hipMemset(w->fwd, 0, w->fwd_bytes);
-    (void)hipMemset(w->vote, 0, w->vote_bytes);
+    (void)hipMemset(w->fwd, 0, std::max<uint64_t>(w->L.fwd_bytes[me], 1));
+    (void)hipMemset(w->vote, 0, std::max<uint64_t>(w->L.vote_bytes[me], 1));
+    (void)hipMemset(w->ctrl, 0, w->L.ctrl_words[me] * 8);
+    if (w->d_stats.alloc(w->nl)) { rlo_world_destroy(w); return RLO_E_HIP; }
+    (void)hipDeviceSynchronize();
     (void)hipEventCreate(&w->ev0);
     (void)hipEventCreate(&w->ev1);
     *out = w;
     return RLO_OK;
 }
 
+int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap) {
+    if (!w || !blob || cap < RLO_PART_BLOB_BYTES) return RLO_E_INVAL;
+    PartBlob b;
+    std::memset(&b, 0, sizeof b);
+    b.magic = kBlobMagic;
+    b.version = 1;
+    b.part = w->part;
+    b.nparts = w->L.nparts;
+    b.n = w->L.n;
+    b.device = w->device;
+    b.cap = w->L.cap;
+    b.stride = w->L.stride;
+    b.vote_cap = w->L.vote_cap;
+    b.token = process_token();
+    b.fwd_ptr = (uint64_t)(uintptr_t)w->fwd;
+    b.vote_ptr = (uint64_t)(uintptr_t)w->vote;
+    b.ctrl_ptr = (uint64_t)(uintptr_t)w->ctrl;
+    b.fwd_bytes = w->L.fwd_bytes[w->part];
+    b.vote_bytes = w->L.vote_bytes[w->part];
+    b.ctrl_bytes = w->L.ctrl_words[w->part] * 8;
+    HIPCHK(hipDeviceGetPCIBusId(b.bus, sizeof b.bus, w->device));
+    HIPCHK(hipIpcGetMemHandle(&b.hf, w->fwd));
+    HIPCHK(hipIpcGetMemHandle(&b.hv, w->vote));
+    HIPCHK(hipIpcGetMemHandle(&b.hc, w->ctrl));
+    std::memset(blob, 0, RLO_PART_BLOB_BYTES);
+    std::memcpy(blob, &b, sizeof b);
+    return (int)RLO_PART_BLOB_BYTES;
+}
+
+int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
+    if (!w || !blobs || n_parts != w->L.nparts || w->connected) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
+    const Layout& L = w->L;
+    w->pf.assign(n_parts, nullptr);
+    w->pv.assign(n_parts, nullptr);
+    w->pc.assign(n_parts, nullptr);
+    char mybus[32] = {0};
+    HIPCHK(hipDeviceGetPCIBusId(mybus, sizeof mybus, w->device));
+    const uint64_t tok = process_token();
+    w->sys_scope = 0;
+    for (int q = 0; q < n_parts; q++) {
+        PartBlob b;
+        std::memcpy(&b, (const uint8_t*)blobs + (size_t)q * RLO_PART_BLOB_BYTES, sizeof b);
+        if (b.magic != kBlobMagic || b.part != q || b.nparts != n_parts || b.n != L.n || b.cap != L.cap ||
+            b.stride != L.stride || b.vote_cap != L.vote_cap || b.fwd_bytes != L.fwd_bytes[q] ||
+            b.vote_bytes != L.vote_bytes[q] || b.ctrl_bytes != L.ctrl_words[q] * 8)
+            return RLO_E_INVAL;
+        if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->sys_scope = 1;
+        if (q == w->part) {
+            w->pf[q] = w->fwd; w->pv[q] = w->vote; w->pc[q] = w->ctrl;
+        } else if (b.token == tok) {  // same process: the addresses are usable as they are
+            if (b.device != w->device) {
+                hipError_t e = hipDeviceEnablePeerAccess(b.device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { g_last_hip = (int)e; return RLO_E_HIP; }
+                (void)hipGetLastError();
+            }
+            w->pf[q] = (uint8_t*)(uintptr_t)b.fwd_ptr;
+            w->pv[q] = (uint8_t*)(uintptr_t)b.vote_ptr;
+            w->pc[q] = (uint64_t*)(uintptr_t)b.ctrl_ptr;
+        } else {  // another process: map its regions (dmabuf IPC; xGMI when on another GPU)
+            void* p = nullptr;
+            HIPCHK(hipIpcOpenMemHandle(&p, b.hf, hipIpcMemLazyEnablePeerAccess));
+            w->opened.push_back(p);
+            w->pf[q] = (uint8_t*)p;
+            HIPCHK(hipIpcOpenMemHandle(&p, b.hv, hipIpcMemLazyEnablePeerAccess));
+            w->opened.push_back(p);
+            w->pv[q] = (uint8_t*)p;
+            HIPCHK(hipIpcOpenMemHandle(&p, b.hc, hipIpcMemLazyEnablePeerAccess));
+            w->opened.push_back(p);
+            w->pc[q] = (uint64_t*)p;
+        }
+    }
+    build_topo(w);
+    if (w->d_topo.upload(w->topo)) return RLO_E_HIP;
+    w->connected = true;
+    return RLO_OK;
+}
+
+int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
+    if (!cfg || !out || cfg->n_ranks < 2 || cfg->n_ranks > 4096) return RLO_E_INVAL;
+    rlo_part_cfg_t pc;
+    std::memset(&pc, 0, sizeof pc);
+    pc.n_ranks = cfg->n_ranks;
+    pc.n_parts = 1;
+    pc.part = 0;
+    pc.max_payload = cfg->max_payload;
+    pc.ring_slots = cfg->ring_slots;
+    pc.device = cfg->device;
+    rlo_world* w = nullptr;
+    int rc = rlo_part_create(&pc, &w);
+    if (rc) return rc;
+    uint8_t blob[RLO_PART_BLOB_BYTES];
+    rc = rlo_part_export(w, blob, sizeof blob);
+    if (rc >= 0) rc = rlo_part_connect(w, blob, 1);
+    if (rc) { rlo_world_destroy(w); return rc; }
+    *out = w;
+    return RLO_OK;
+}
+
 int rlo_world_destroy(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
+    (void)hipSetDevice(w->device);
+    for (void* p : w->opened) (void)hipIpcCloseMemHandle(p);
     if (w->fwd) (void)hipFree(w->fwd);
     if (w->vote) (void)hipFree(w->vote);
     if (w->ctrl) (void)hipFree(w->ctrl);
-    w->d_topo.release(); w->d_stats.release(); w->d_err.release();
+    w->d_topo.release(); w->d_stats.release();
     w->d_sched_off.release(); w->d_expect_bcast.release(); w->d_prop_off.release(); w->d_expect_dec.release();
     w->d_sched_ids.release(); w->d_prop_data_off.release(); w->d_prop_data_len.release(); w->d_isp_off.release();
     w->d_lat_count.release(); w->d_lat_round.release(); w->d_lat_origin.release(); w->d_prop_pid.release();
@@ -371,59 +577,65 @@ int rlo_world_destroy(rlo_world_t* w) {
 int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     if (!w || !o) return RLO_E_INVAL;
     std::memset(o, 0, sizeof *o);
-    o->n_ranks = w->n;
-    o->max_in_degree = w->max_in;
-    o->max_fanout = w->max_fan;
-    o->edges = w->edges;
-    o->ring_slots = w->fwd_cap;
-    o->slot_stride = w->stride;
-    o->vote_slots = w->vote_cap;
-    o->fwd_bytes = w->fwd_bytes;
-    o->vote_bytes = w->vote_bytes;
-    o->ctrl_bytes = w->ctrl_words * 8;
+    o->n_ranks = w->L.n;
+    o->max_in_degree = w->L.max_in;
+    o->max_fanout = w->L.max_fan;
+    o->edges = (int)w->L.E.size();
+    o->ring_slots = w->L.cap;
+    o->slot_stride = w->L.stride;
+    o->vote_slots = w->L.vote_cap;
+    o->fwd_bytes = w->L.fwd_bytes[w->part];
+    o->vote_bytes = w->L.vote_bytes[w->part];
+    o->ctrl_bytes = w->L.ctrl_words[w->part] * 8;
     o->cus = w->cus;
     o->blocks_per_cu = w->blocks_per_cu;
+    o->part = w->part;
+    o->n_parts = w->L.nparts;
+    o->rank_begin = w->rb;
+    o->rank_end = w->rb + w->nl;
+    o->sys_scope = w->sys_scope;
     return RLO_OK;
 }
 
 static void base_params(rlo_world* w) {
     rlo::Params& P = w->P;
     std::memset(&P, 0, sizeof P);
-    P.n = w->n;
-    P.rank_begin = 0;
-    P.rank_end = w->n;
+    P.n = w->L.n;
+    P.rank_begin = w->rb;
+    P.rank_end = w->rb + w->nl;
     P.topo = w->d_topo.p;
     P.fwd_region = w->fwd;
-    P.fwd_region_bytes = (uint32_t)w->fwd_bytes;
-    P.fwd_cap = w->fwd_cap;
-    P.fwd_stride = w->stride;
+    P.fwd_region_bytes = (uint32_t)std::max<uint64_t>(w->L.fwd_bytes[w->part], 1);
+    P.fwd_cap = w->L.cap;
+    P.fwd_stride = w->L.stride;
     P.vote_region = w->vote;
-    P.vote_region_bytes = (uint32_t)w->vote_bytes;
-    P.vote_cap = w->vote_cap;
+    P.vote_region_bytes = (uint32_t)std::max<uint64_t>(w->L.vote_bytes[w->part], 1);
+    P.vote_cap = w->L.vote_cap;
     P.ctrl = w->ctrl;
+    P.sys_scope = (uint32_t)w->sys_scope;
+    P.n_parts = (uint32_t)w->L.nparts;
+    for (int q = 0; q < w->L.nparts; q++) P.err_flag[q] = reinterpret_cast<uint32_t*>(w->pc[q]);
+    P.error_flag = reinterpret_cast<uint32_t*>(w->ctrl);
     P.stats = w->d_stats.p;
-    P.error_flag = w->d_err.p;
     P.nsmall = w->nsmall;
-    P.nout_max = 2u * (uint32_t)w->max_fan;
+    P.nout_max = 2u * (uint32_t)w->L.max_fan;
     P.stage2_bytes = w->stage2;
     P.timeout_ticks = 100000000ull * 10;   // 10 s without progress on a rank
     P.deadline_ticks = 100000000ull * 120; // 120 s per launch
     P.window = 32;
-    // harmless non-null defaults for unused arrays
-    static_assert(sizeof(int64_t) == 8, "");
 }
 
 static int setup_log(rlo_world* w, uint32_t flags, uint32_t log_cap, bool payload) {
     rlo::Params& P = w->P;
     if (!(flags & RLO_FLAG_LOG)) return RLO_OK;
     if (log_cap == 0) log_cap = 1024;
-    if (w->d_log.alloc((size_t)w->n * log_cap)) return RLO_E_HIP;
+    if (w->d_log.alloc((size_t)w->nl * log_cap)) return RLO_E_HIP;
     P.log = w->d_log.p;
     P.log_cap = log_cap;
     P.mode |= rlo::MODE_LOG;
     if (payload) {
         P.log_stride = w->max_payload;
-        if (w->d_log_payload.alloc((size_t)w->n * log_cap * P.log_stride)) return RLO_E_HIP;
+        if (w->d_log_payload.alloc((size_t)w->nl * log_cap * P.log_stride)) return RLO_E_HIP;
         P.log_payload = w->d_log_payload.p;
     }
     return RLO_OK;
@@ -431,20 +643,24 @@ static int setup_log(rlo_world* w, uint32_t flags, uint32_t log_cap, bool payloa
 
 int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
     if (!w || !cfg || cfg->k < 0 || cfg->len > w->max_payload || cfg->k > 0xFFFFFFFFll) return RLO_E_INVAL;
+    if (!w->connected) return RLO_E_NOTCONNECTED;
     base_params(w);
     rlo::Params& P = w->P;
-    const int n = w->n;
-    std::vector<int64_t> off(n + 1, 0), expect(n, 0);
-    std::vector<uint32_t> ids((size_t)std::max<int64_t>(cfg->k, 1));
+    const int n = w->L.n, nl = w->nl, rb = w->rb;
+    // the whole world's schedule is a pure function of (seed, k): each part keeps its own ranks'
+    std::vector<int64_t> off(nl + 1, 0), expect(nl, 0), per(n, 0);
     std::vector<uint32_t> org((size_t)std::max<int64_t>(cfg->k, 1));
     for (int64_t b = 0; b < cfg->k; b++) {
         org[b] = (uint32_t)(splitmix64(cfg->seed + (uint64_t)b) % (uint64_t)n);
-        off[org[b] + 1]++;
+        per[org[b]]++;
+        if ((int)org[b] >= rb && (int)org[b] < rb + nl) off[org[b] - rb + 1]++;
     }
-    for (int r = 0; r < n; r++) off[r + 1] += off[r];
+    for (int r = 0; r < nl; r++) off[r + 1] += off[r];
+    std::vector<uint32_t> ids((size_t)std::max<int64_t>(off[nl], 1));
     std::vector<int64_t> fill(off.begin(), off.end() - 1);
-    for (int64_t b = 0; b < cfg->k; b++) ids[fill[org[b]]++] = (uint32_t)b;
-    for (int r = 0; r < n; r++) expect[r] = cfg->k - (off[r + 1] - off[r]);
+    for (int64_t b = 0; b < cfg->k; b++)
+        if ((int)org[b] >= rb && (int)org[b] < rb + nl) ids[fill[org[b] - rb]++] = (uint32_t)b;
+    for (int r = 0; r < nl; r++) expect[r] = cfg->k - per[rb + r];
     if (w->d_sched_off.upload(off) || w->d_sched_ids.upload(ids) || w->d_expect_bcast.upload(expect)) return RLO_E_HIP;
     P.mode = rlo::MODE_STORM | ((cfg->flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u) |
              ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
@@ -462,9 +678,11 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
 
 int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags) {
     if (!w || rounds == 0 || len > w->max_payload) return RLO_E_INVAL;
+    if (!w->connected) return RLO_E_NOTCONNECTED;
+    if (w->L.nparts != 1) return RLO_E_INVAL;  // the round counter is one device word
     base_params(w);
     rlo::Params& P = w->P;
-    const int n = w->n;
+    const int n = w->L.n;
     std::vector<int32_t> org(rounds);
     std::vector<int64_t> expect(n, 0);
     for (uint32_t i = 0; i < rounds; i++) org[i] = (int32_t)(splitmix64(seed + i) % (uint64_t)n);
@@ -492,29 +710,33 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
 int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, const int32_t* origin, const int32_t* pid,
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len) {
     if (!w || !cfg || nprop < 0 || (nprop && (!origin || !pid || !data_off || !data_len))) return RLO_E_INVAL;
+    if (!w->connected) return RLO_E_NOTCONNECTED;
     base_params(w);
     rlo::Params& P = w->P;
-    const int n = w->n;
-    std::vector<int64_t> off(n + 1, 0), expect(n, 0);
+    const int n = w->L.n, nl = w->nl, rb = w->rb;
+    std::vector<int64_t> off(nl + 1, 0), expect(nl, 0), per(n, 0);
     for (int64_t i = 0; i < nprop; i++) {
         if (origin[i] < 0 || origin[i] >= n) return RLO_E_INVAL;
         if (16ull + data_len[i] > w->max_payload) return RLO_E_INVAL;
-        off[origin[i] + 1]++;
+        per[origin[i]]++;
+        if (origin[i] >= rb && origin[i] < rb + nl) off[origin[i] - rb + 1]++;
     }
-    for (int r = 0; r < n; r++) off[r + 1] += off[r];
+    for (int r = 0; r < nl; r++) off[r + 1] += off[r];
     std::vector<int64_t> fill(off.begin(), off.end() - 1);
-    std::vector<int32_t> ppid((size_t)std::max<int64_t>(nprop, 1));
-    std::vector<uint32_t> pdo((size_t)std::max<int64_t>(nprop, 1)), pdl((size_t)std::max<int64_t>(nprop, 1));
+    const size_t nown = (size_t)std::max<int64_t>(off[nl], 1);
+    std::vector<int32_t> ppid(nown);
+    std::vector<uint32_t> pdo(nown), pdl(nown);
     std::vector<uint8_t> blob;
     for (int64_t i = 0; i < nprop; i++) {
-        int64_t at = fill[origin[i]]++;
+        if (origin[i] < rb || origin[i] >= rb + nl) continue;
+        int64_t at = fill[origin[i] - rb]++;
         ppid[at] = pid[i];
         pdo[at] = (uint32_t)blob.size();
         pdl[at] = data_len[i];
         blob.insert(blob.end(), data + data_off[i], data + data_off[i] + data_len[i]);
     }
     if (blob.empty()) blob.push_back(0);
-    for (int r = 0; r < n; r++) expect[r] = nprop - (off[r + 1] - off[r]);
+    for (int r = 0; r < nl; r++) expect[r] = nprop - per[rb + r];
     if (w->d_prop_off.upload(off) || w->d_prop_pid.upload(ppid) || w->d_prop_data_off.upload(pdo) ||
         w->d_prop_data_len.upload(pdl) || w->d_prop_data.upload(blob) || w->d_expect_dec.upload(expect))
         return RLO_E_HIP;
@@ -558,33 +780,62 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
     return RLO_OK;
 }
 
-int rlo_launch(rlo_world_t* w, void* stream) {
+int rlo_reset(rlo_world_t* w, void* stream) {
     if (!w) return RLO_E_INVAL;
-    if (!w->have_program) return RLO_E_NOPROGRAM;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(w->device));
-    HIPCHK(hipMemsetAsync(w->ctrl, 0, w->ctrl_words * 8, s));
-    HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->n, s));
-    HIPCHK(hipMemsetAsync(w->d_err.p, 0, sizeof(uint32_t) * 4, s));
-    if (w->P.mode & rlo::MODE_LAT) {
+    HIPCHK(hipMemsetAsync(w->ctrl, 0, w->L.ctrl_words[w->part] * 8, s));
+    HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->nl, s));
+    if (w->have_program && (w->P.mode & rlo::MODE_LAT)) {
         HIPCHK(hipMemsetAsync(w->d_lat_count.p, 0, sizeof(uint32_t) * w->lat_rounds, s));
         HIPCHK(hipMemsetAsync(w->d_lat_out.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
         HIPCHK(hipMemsetAsync(w->d_lat_round.p, 0, sizeof(uint32_t), s));
     }
+    HIPCHK(hipStreamSynchronize(s));
+    return RLO_OK;
+}
+
+int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
+    if (!w) return RLO_E_INVAL;
+    if (!w->connected) return RLO_E_NOTCONNECTED;
+    if (!w->have_program) return RLO_E_NOPROGRAM;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(w->device));
+    if (!(flags & RLO_LAUNCH_NO_RESET)) {
+        int rc = rlo_reset(w, stream);
+        if (rc) return rc;
+    }
     HIPCHK(hipEventRecord(w->ev0, s));
-    hipError_t e = rlo_launch_progress(&w->P, w->n, w->dyn_lds, s);
+    hipError_t e = rlo_launch_progress(&w->P, w->nl, w->dyn_lds, s);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));
-    w->last_stream = s;
+    return RLO_OK;
+}
+
+int rlo_launch(rlo_world_t* w, void* stream) { return rlo_launch_ex(w, stream, 0); }
+
+int rlo_stream_create(int device, void** stream) {
+    if (!stream) return RLO_E_INVAL;
+    if (device >= 0) HIPCHK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void*)s;
+    return RLO_OK;
+}
+
+int rlo_stream_destroy(void* stream) {
+    if (!stream) return RLO_E_INVAL;
+    HIPCHK(hipStreamDestroy((hipStream_t)stream));
     return RLO_OK;
 }
 
 int rlo_wait(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipEventSynchronize(w->ev1));
     HIPCHK(hipEventElapsedTime(&w->last_ms, w->ev0, w->ev1));
     uint32_t err = 0;
-    HIPCHK(hipMemcpy(&err, w->d_err.p, sizeof err, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&err, w->ctrl, sizeof err, hipMemcpyDeviceToHost));
     return err ? RLO_E_DEVICE : RLO_OK;
 }
 
@@ -603,23 +854,26 @@ int rlo_last_kernel_ms(rlo_world_t* w, float* ms) {
 }
 
 int rlo_stats(rlo_world_t* w, rlo_rank_stats_t* out, int n) {
-    if (!w || !out || n < 0 || n > w->n) return RLO_E_INVAL;
+    if (!w || !out || n < 0 || n > w->nl) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipMemcpy(out, w->d_stats.p, sizeof(rlo::RankStats) * n, hipMemcpyDeviceToHost));
     return RLO_OK;
 }
 
 int rlo_log(rlo_world_t* w, int rank, rlo_log_rec_t* out, uint32_t cap, uint8_t* payload, uint32_t payload_stride) {
-    if (!w || rank < 0 || rank >= w->n || !out) return RLO_E_INVAL;
+    if (!w || rank < w->rb || rank >= w->rb + w->nl || !out) return RLO_E_INVAL;
     if (!w->d_log.p) return RLO_E_NOPROGRAM;
+    HIPCHK(hipSetDevice(w->device));
+    const int lr = rank - w->rb;
     rlo::RankStats st;
-    HIPCHK(hipMemcpy(&st, w->d_stats.p + rank, sizeof st, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&st, w->d_stats.p + lr, sizeof st, hipMemcpyDeviceToHost));
     uint32_t cnt = (uint32_t)std::min<uint64_t>(st.log_count, w->P.log_cap);
     cnt = std::min(cnt, cap);
-    if (cnt) HIPCHK(hipMemcpy(out, w->d_log.p + (size_t)rank * w->P.log_cap, sizeof(rlo::LogRec) * cnt, hipMemcpyDeviceToHost));
+    if (cnt) HIPCHK(hipMemcpy(out, w->d_log.p + (size_t)lr * w->P.log_cap, sizeof(rlo::LogRec) * cnt, hipMemcpyDeviceToHost));
     if (payload && w->d_log_payload.p && cnt) {
         const uint32_t ls = w->P.log_stride;
         std::vector<uint8_t> tmp((size_t)cnt * ls);
-        HIPCHK(hipMemcpy(tmp.data(), w->d_log_payload.p + (size_t)rank * w->P.log_cap * ls, tmp.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(tmp.data(), w->d_log_payload.p + (size_t)lr * w->P.log_cap * ls, tmp.size(), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < cnt; i++)
             std::memcpy(payload + (size_t)i * payload_stride, tmp.data() + (size_t)i * ls, std::min(ls, payload_stride));
     }
@@ -629,6 +883,7 @@ int rlo_log(rlo_world_t* w, int rank, rlo_log_rec_t* out, uint32_t cap, uint8_t*
 int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
     if (!w || !ticks || !w->d_lat_out.p) return RLO_E_INVAL;
     uint32_t n = std::min(cap, w->lat_rounds);
+    HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipMemcpy(ticks, w->d_lat_out.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return (int)n;
 }

@@ -12,6 +12,10 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
 
 RLO_OK = 0
 RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6
+RLO_E_NOTCONNECTED = -7
+RLO_PART_BLOB_BYTES = 512
+RLO_PART_UNCACHED = 1
+RLO_LAUNCH_NO_RESET = 1
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
 DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot"}
@@ -27,7 +31,15 @@ class WorldInfo(ctypes.Structure):
                 ("edges", ctypes.c_int32), ("ring_slots", ctypes.c_uint32), ("slot_stride", ctypes.c_uint32),
                 ("vote_slots", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("fwd_bytes", ctypes.c_uint64),
                 ("vote_bytes", ctypes.c_uint64), ("ctrl_bytes", ctypes.c_uint64), ("cus", ctypes.c_int32),
-                ("blocks_per_cu", ctypes.c_int32)]
+                ("blocks_per_cu", ctypes.c_int32), ("part", ctypes.c_int32), ("n_parts", ctypes.c_int32),
+                ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),
+                ("pad2", ctypes.c_int32)]
+
+
+class PartCfg(ctypes.Structure):
+    _fields_ = [("n_ranks", ctypes.c_int32), ("n_parts", ctypes.c_int32), ("part", ctypes.c_int32),
+                ("part_begin", ctypes.c_void_p), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
 
 
 class StormCfg(ctypes.Structure):
@@ -57,6 +69,8 @@ class LogRec(ctypes.Structure):
 
 # every symbol include/rlo_hip.h declares (checked by tests/test_abi.py)
 EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destroy", "rlo_world_query",
+           "rlo_part_create", "rlo_part_export", "rlo_part_connect", "rlo_reset", "rlo_launch_ex",
+           "rlo_stream_create", "rlo_stream_destroy",
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_strerror", "rlo_last_hip_error"]
 
@@ -80,7 +94,14 @@ def load():
     L.rlo_program_storm.argtypes = [vp, ctypes.POINTER(StormCfg)]
     L.rlo_program_latency.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]
     L.rlo_program_iar.argtypes = [vp, ctypes.POINTER(IarCfg), ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.rlo_part_create.argtypes = [ctypes.POINTER(PartCfg), ctypes.POINTER(vp)]
+    L.rlo_part_export.argtypes = [vp, vp, ctypes.c_uint32]
+    L.rlo_part_connect.argtypes = [vp, vp, ctypes.c_int]
+    L.rlo_reset.argtypes = [vp, vp]
+    L.rlo_launch_ex.argtypes = [vp, vp, ctypes.c_uint32]
     L.rlo_launch.argtypes = [vp, vp]
+    L.rlo_stream_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.rlo_stream_destroy.argtypes = [vp]
     L.rlo_wait.argtypes = [vp]
     L.rlo_run.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
     L.rlo_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]

@@ -1,0 +1,136 @@
+"""Sharded worlds: the ranks of one world split into parts, each part its own kernel and
+its own rings, producers storing into peer parts' rings.
+
+run_inprocess(): every part in this process, one HIP stream each (same GPU or several).
+run_processes(): one spawned process per part; blobs are exchanged through a queue, the
+                 regions are mapped with hipIpc (dmabuf), launches start after a barrier
+                 that follows every part's reset.
+A program spec is a dict: {"kind": "storm", "k", "len", "seed", "window", "log"} or
+{"kind": "iar", "props": [(origin, pid, bytes)], "judge", "mask", "isp", "seed", "ppm", "log"}.
+"""
+import ctypes
+import multiprocessing as mp
+
+import numpy as np
+
+
+def even_bounds(n, parts):
+    return [n * p // parts for p in range(parts + 1)]
+
+
+def _program(w, spec):
+    if spec["kind"] == "storm":
+        w.program_storm(spec["k"], spec["len"], seed=spec.get("seed", 0x5EED), window=spec.get("window", 32),
+                        log=spec.get("log", False), log_cap=spec.get("log_cap", 0), hist=spec.get("hist", False))
+    elif spec["kind"] == "iar":
+        from . import _lib as L
+        w.program_iar(spec["props"], judge=spec.get("judge", L.RLO_JUDGE_APPROVE), mask=spec.get("mask"),
+                      isp=spec.get("isp"), seed=spec.get("seed", 0), ppm=spec.get("ppm", 0),
+                      log=spec.get("log", False), log_cap=spec.get("log_cap", 0))
+    else:
+        raise ValueError(spec["kind"])
+
+
+def _collect(w, spec):
+    st = w.stats()
+    out = {"rank_begin": w.rank_begin, "stats": st, "ms": w.kernel_ms(), "info": dict(w.info)}
+    if spec.get("log"):
+        cap = spec.get("log_cap", 0) or 1024
+        out["logs"] = {r: w.log(r, cap=cap, payload=spec["kind"] == "storm") for r in range(w.rank_begin, w.rank_end)}
+    return out
+
+
+def merge(results):
+    """Concatenate per-part stats (ordered by rank) into world-wide arrays."""
+    results = sorted(results, key=lambda r: r["rank_begin"])
+    st = {}
+    for key in results[0]["stats"]:
+        st[key] = np.concatenate([r["stats"][key] for r in results])
+    logs = {}
+    for r in results:
+        logs.update(r.get("logs", {}))
+    return st, logs, [r["ms"] for r in results]
+
+
+def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False):
+    from . import _lib as L
+    from .world import World
+
+    parts = len(bounds) - 1
+    devices = devices or [0] * parts
+    streams = []
+    ws = [World.part(n, parts, p, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
+                     device=devices[p], uncached=uncached) for p in range(parts)]
+    try:
+        blobs = [w.export() for w in ws]
+        for w in ws:
+            w.connect(blobs)
+        for w in ws:
+            _program(w, spec)
+        for w in ws:
+            w.reset()
+        lib = L.load()
+        for d in devices:
+            s = ctypes.c_void_p()
+            L.check(lib.rlo_stream_create(d, ctypes.byref(s)), "rlo_stream_create")
+            streams.append(s)
+        for w, s in zip(ws, streams):
+            w.launch(stream=s, no_reset=True)
+        rcs = [w.wait(raise_on_device_error=False) for w in ws]
+        res = [_collect(w, spec) for w in ws]
+        return merge(res), rcs
+    finally:
+        for w in ws:
+            w.close()
+        for s in streams:
+            L.load().rlo_stream_destroy(s)
+
+
+def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, blob_q, blobs_q, barrier, out_q):
+    try:
+        from .world import World
+
+        w = World.part(n, len(bounds) - 1, part, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
+                       device=device, uncached=uncached)
+        blob_q.put((part, w.export()))
+        blobs = blobs_q.get(timeout=120)
+        w.connect(blobs)
+        _program(w, spec)
+        w.reset()
+        barrier.wait(timeout=120)  # every part is reset before any part launches
+        w.launch(no_reset=True)
+        rc = w.wait(raise_on_device_error=False)
+        res = _collect(w, spec)
+        barrier.wait(timeout=120)  # no peer still stores into this part's rings
+        w.close()
+        out_q.put((part, rc, res, None))
+    except Exception as e:  # report instead of hanging the parent
+        out_q.put((part, -99, None, repr(e)))
+
+
+def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, timeout=300):
+    parts = len(bounds) - 1
+    devices = devices or [0] * parts
+    ctx = mp.get_context("spawn")
+    blob_q, out_q = ctx.Queue(), ctx.Queue()
+    blobs_qs = [ctx.Queue() for _ in range(parts)]
+    barrier = ctx.Barrier(parts)
+    procs = [ctx.Process(target=_worker, args=(n, bounds, p, devices[p], spec, max_payload, ring_slots, uncached,
+                                               blob_q, blobs_qs[p], barrier, out_q)) for p in range(parts)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(blob_q.get(timeout=timeout) for _ in range(parts))
+        blobs = [got[p] for p in range(parts)]
+        for q in blobs_qs:
+            q.put(blobs)
+        outs = [out_q.get(timeout=timeout) for _ in range(parts)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = [(p, e) for p, rc, r, e in outs if e]
+    if errs:
+        raise RuntimeError("part failed: %s" % errs)
+    return merge([r for _, _, r, _ in outs]), [rc for _, rc, _, _ in sorted(outs, key=lambda x: x[0])]

@@ -18,17 +18,53 @@ from ._lib import check
 
 
 class World:
-    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1):
+    """A world of n ranks.  World(n) hosts all of them on one GPU; World.part(...) creates one
+    part of a sharded world (export() -> exchange blobs -> connect(blobs))."""
+
+    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None):
         self.lib = L.load()
-        cfg = L.WorldCfg(n, max_payload, ring_slots, device)
         h = ctypes.c_void_p()
-        check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
+        if _part is None:
+            cfg = L.WorldCfg(n, max_payload, ring_slots, device)
+            check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
+        else:
+            n_parts, part, begin, flags = _part
+            self._pb = None
+            pb = None
+            if begin is not None:
+                self._pb = (ctypes.c_int32 * (n_parts + 1))(*begin)
+                pb = ctypes.cast(self._pb, ctypes.c_void_p)
+            cfg = L.PartCfg(n, n_parts, part, pb, max_payload, ring_slots, device, flags)
+            check(self.lib.rlo_part_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_part_create")
         self.h = h
         self.n = n
+        self._query()
+        self._lat_rounds = 0
+
+    @classmethod
+    def part(cls, n, n_parts, part, part_begin=None, max_payload=4096, ring_slots=0, device=-1, uncached=False):
+        return cls(n, max_payload, ring_slots, device,
+                   _part=(n_parts, part, part_begin, L.RLO_PART_UNCACHED if uncached else 0))
+
+    def _query(self):
         info = L.WorldInfo()
         check(self.lib.rlo_world_query(self.h, ctypes.byref(info)), "rlo_world_query")
         self.info = {f: getattr(info, f) for f, _ in L.WorldInfo._fields_}
-        self._lat_rounds = 0
+        self.rank_begin, self.rank_end = self.info["rank_begin"], self.info["rank_end"]
+        self.n_local = self.rank_end - self.rank_begin
+
+    def export(self):
+        buf = ctypes.create_string_buffer(L.RLO_PART_BLOB_BYTES)
+        check(self.lib.rlo_part_export(self.h, buf, L.RLO_PART_BLOB_BYTES), "rlo_part_export")
+        return buf.raw
+
+    def connect(self, blobs):
+        joined = b"".join(blobs)
+        check(self.lib.rlo_part_connect(self.h, joined, len(blobs)), "rlo_part_connect")
+        self._query()
+
+    def reset(self, stream=None):
+        check(self.lib.rlo_reset(self.h, stream), "rlo_reset")
 
     def close(self):
         if self.h:
@@ -86,15 +122,16 @@ class World:
                                        d(dlen)), "rlo_program_iar")
 
     # ------------------------------------------------------------ run
-    def launch(self, stream=None):
-        check(self.lib.rlo_launch(self.h, stream), "rlo_launch")
+    def launch(self, stream=None, no_reset=False):
+        check(self.lib.rlo_launch_ex(self.h, stream, L.RLO_LAUNCH_NO_RESET if no_reset else 0), "rlo_launch")
 
     def wait(self, raise_on_device_error=True):
         rc = self.lib.rlo_wait(self.h)
         if rc == L.RLO_E_DEVICE and not raise_on_device_error:
             return rc
         if rc == L.RLO_E_DEVICE:
-            errs = {(r, L.DERR.get(s.error, s.error), s.error_aux) for r, s in enumerate(self.stats_raw()) if s.error}
+            errs = {(self.rank_begin + r, L.DERR.get(s.error, s.error), s.error_aux)
+                    for r, s in enumerate(self.stats_raw()) if s.error}
             raise L.RloError("device engine error: %s" % sorted(errs)[:8])
         return check(rc, "rlo_wait")
 
@@ -114,8 +151,8 @@ class World:
 
     # ------------------------------------------------------------ results
     def stats_raw(self):
-        arr = (L.RankStats * self.n)()
-        check(self.lib.rlo_stats(self.h, arr, self.n), "rlo_stats")
+        arr = (L.RankStats * self.n_local)()
+        check(self.lib.rlo_stats(self.h, arr, self.n_local), "rlo_stats")
         return list(arr)
 
     def stats(self):

@@ -1,0 +1,126 @@
+"""GPU parity of sharded worlds: the ranks of ONE world split into parts, each
+part a separate kernel over its own rings, producers storing into the peer part's rings.
+
+In one process (parts on separate HIP streams) and across processes (regions mapped with
+hipIpc / dmabuf), against the pinned oracle: per-rank delivery sets and parents, delivered
+bytes, checksums, and IAR outcomes are identical to the single-part engine's.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as orc
+
+pytestmark = pytest.mark.gpu
+LOG_DELIVER = 1
+
+
+@pytest.fixture(scope="module")
+def rlo():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rlo as _rlo
+
+    return _rlo
+
+
+def _check_storm(st, logs, n, k, ln, seed, logged):
+    ref = orc.storm(n, seed, k, ln, want_parent=logged)
+    assert (st["error"] == 0).all(), st["error"]
+    assert np.array_equal(st["bcast_delivered"].astype(np.int64), ref["count"])
+    assert np.array_equal(st["bcast_sum"], ref["sum"])
+    if not logged:
+        return
+    par = ref["parent"]
+    for r in range(n):
+        rows, payload = logs[r]
+        got = sorted((row[4], row[2], row[3]) for row in rows if row[0] == LOG_DELIVER)
+        want = sorted((b, orc.origin_of(seed, b, n), int(par[b, r])) for b in range(k) if orc.origin_of(seed, b, n) != r)
+        assert got == want, r
+        for row in rows:
+            assert bytes(payload[row[8]][:ln]) == orc.payload(row[2], row[4], ln)
+
+
+# In one process the parts' persistent kernels run on separate HIP streams; the process has
+# GPU_MAX_HW_QUEUES = 4 hardware queues, so in-process worlds keep to 2 parts (more parts
+# run one process each, below).
+@pytest.mark.parametrize("n,bounds,k,ln,seed", [
+    (8, [0, 4, 8], 64, 64, 3),
+    (13, [0, 5, 13], 52, 200, 5),
+    (64, [0, 1, 64], 96, 64, 9),
+    (100, [0, 37, 100], 120, 1000, 2),
+])
+def test_storm_sharded_inprocess_logged(rlo, n, bounds, k, ln, seed):
+    from rlo import sharded
+
+    spec = {"kind": "storm", "k": k, "len": ln, "seed": seed, "log": True, "log_cap": k + 8}
+    (st, logs, _), rcs = sharded.run_inprocess(n, bounds, spec, max_payload=max(64, ln))
+    assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
+    _check_storm(st, logs, n, k, ln, seed, True)
+
+
+def test_storm_sharded_inprocess_full_size(rlo):
+    from rlo import sharded
+
+    n, k, ln, seed = 256, 1 << 15, 64, 11
+    spec = {"kind": "storm", "k": k, "len": ln, "seed": seed}
+    (st, logs, _), rcs = sharded.run_inprocess(n, sharded.even_bounds(n, 2), spec, max_payload=64)
+    assert rcs == [0, 0], (st["error"], st["error_aux"])
+    _check_storm(st, logs, n, k, ln, seed, False)
+
+
+def test_storm_sharded_uncached_rings(rlo):
+    """The allocation used when parts sit on different GPUs (uncached), exercised on one GPU."""
+    from rlo import sharded
+
+    n, k, ln, seed = 32, 256, 64, 4
+    spec = {"kind": "storm", "k": k, "len": ln, "seed": seed, "log": True, "log_cap": k + 8}
+    (st, logs, _), rcs = sharded.run_inprocess(n, [0, 16, 32], spec, max_payload=64, uncached=True)
+    assert rcs == [0, 0]
+    _check_storm(st, logs, n, k, ln, seed, True)
+
+
+def test_iar_sharded_inprocess(rlo):
+    from rlo import sharded
+
+    n, p = 24, 4
+    props = [(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)]
+    spec = {"kind": "iar", "props": props, "judge": rlo.abi.RLO_JUDGE_HASH, "seed": 99, "ppm": 50000}
+    (st, _, _), rcs = sharded.run_inprocess(n, [0, 7, 24], spec)
+    assert rcs == [0, 0], (st["error"], st["error_aux"])
+    cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_HASH, seed=99, ppm=50000)
+    ref = orc.iar_bench(n, p, cfg)
+    assert (st["error"] == 0).all()
+    assert int(st["own_decided"].sum()) == ref["decisions"] == n * p
+    assert int(st["own_approved"].sum()) == ref["approved"]
+    assert int(st["actions"].sum()) == ref["actions"]
+    assert int(st["judge_calls"].sum()) == ref["judge_calls"]
+    assert (st["dec_delivered"] == (n - 1) * p).all()
+
+
+@pytest.mark.parametrize("n,bounds,ln", [(16, [0, 8, 16], 64), (13, [0, 5, 9, 13], 200), (64, [0, 1, 32, 63, 64], 64),
+                                         (256, [0, 64, 128, 192, 256], 64)])
+def test_storm_sharded_processes(rlo, n, bounds, ln):
+    """One process per part; rings mapped across processes with hipIpc."""
+    from rlo import sharded
+
+    k, seed = 8 * n, 21
+    spec = {"kind": "storm", "k": k, "len": ln, "seed": seed, "log": True, "log_cap": k + 8}
+    (st, logs, _), rcs = sharded.run_processes(n, bounds, spec, max_payload=max(64, ln))
+    assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
+    _check_storm(st, logs, n, k, ln, seed, True)
+
+
+def test_iar_sharded_processes(rlo):
+    from rlo import sharded
+
+    n, p = 16, 3
+    props = [(r, it * n + r, b"abc") for it in range(p) for r in range(n)]
+    spec = {"kind": "iar", "props": props}
+    (st, _, _), rcs = sharded.run_processes(n, [0, 8, 16], spec)
+    assert rcs == [0, 0]
+    assert (st["error"] == 0).all()
+    assert int(st["own_approved"].sum()) == n * p
+    assert (st["dec_delivered"] == (n - 1) * p).all()
+    assert (st["actions"] == (n - 1) * p).all()
