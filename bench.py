@@ -1,16 +1,21 @@
 #!/usr/bin/env python3
-"""bench.py -- rootless bcast storm on MI355X (BASELINE.json configs[1]).
+"""bench.py -- rootless bcast storm on MI355X (BASELINE.json configs[1], [4]).
 
 One step = one launch of the persistent progress kernel that carries a storm of
-K rootless bcasts (random originators, 64-byte payloads by default) across 256
-workgroup-ranks until every rank has picked up every bcast it is owed.  Inputs
+K rootless bcasts (random originators, 64-byte payloads by default) across the
+world's ranks until every rank has picked up every bcast it is owed.  Inputs
 (schedule, rings) are resident in HBM before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W]
 
-Multi-GPU (torch.distributed.run, one process per GPU): every GPU hosts its own
-256-rank world (weak scaling, no data-path collective); the barrier + max over
-ranks timing contract is kept.  One JSON line is printed by rank 0.
+N = 1: one GPU hosts a 256-rank world (256 workgroup-ranks).
+N > 1 (torch.distributed.run, one process per GPU): ONE world of 256 x N ranks,
+sharded contiguously (256 ranks per GPU); every bcast's tree crosses the GPUs over
+xGMI through peer-HBM ring stores (no collective on the data path; gloo only
+exchanges the ring-mapping blobs and runs the barriers).  K bcasts per step at every
+N, so each GPU delivers ~K x 256 messages per step: weak scaling.  `value` is
+delivered bcast messages per second over all ranks (K x (R - 1) per step);
+`bcast_per_s` is reported beside it.  One JSON line is printed by rank 0.
 """
 import argparse
 import json
@@ -45,7 +50,7 @@ def cpu_baseline(n, length, seed, target_s):
     t = time.perf_counter()
     res = orc.storm(n, seed, k, length)
     dt = time.perf_counter() - t
-    out = {"value": k / dt, "unit": "bcast/s", "cores": 1, "kind": "port",
+    out = {"value": res["deliveries"] / dt, "unit": "msgs/s", "bcast_per_s": k / dt, "cores": 1, "kind": "port",
            "sample": "oracle/rlo_oracle.c storm, %d virtual ranks, %d B, %d bcasts (%d deliveries), %.1f s, 1 thread"
                      % (n, length, k, res["deliveries"], dt)}
     ref = reference_datapoint(length)
@@ -80,7 +85,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--ranks", type=int, default=256, help="workgroup-ranks per GPU")
     ap.add_argument("--len", type=int, default=64, help="payload bytes")
-    ap.add_argument("--k", type=int, default=1 << 18, help="bcasts per step (per GPU)")
+    ap.add_argument("--k", type=int, default=1 << 18, help="bcasts per step")
     ap.add_argument("--lat-rounds", type=int, default=1000)
     ap.add_argument("--iar-p", type=int, default=32, help="proposals per rank for the decisions/s leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -91,6 +96,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RLO_BENCH_DEVICE"):  # rehearsal of the N-part path on one GPU
+        local = int(os.environ["RLO_BENCH_DEVICE"])
+
+    import ctypes
 
     import numpy as np
     import torch
@@ -100,83 +109,148 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")  # control plane only: blob exchange, barriers, max-reduce
 
     import rlo
 
     def barrier():
+        torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
 
     def max_over_ranks(x):
         if dist is None:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    n, length, k = args.ranks, args.len, args.k
-    stream = torch.cuda.current_stream().cuda_stream
-    w = rlo.World(n, max_payload=max(64, length), device=local)
-    w.program_storm(k, length, seed=0x5EED + rank)
+    def sum_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
 
+    per, length, k = args.ranks, args.len, args.k
+    R = per * world  # world size in ranks
+    mode = "sharded"
+    if world == 1:
+        w = rlo.World(R, max_payload=max(64, length), device=local)
+    else:
+        w, err = None, ""
+        try:
+            w = rlo.World.part(R, world, rank, max_payload=max(64, length), device=local, uncached=True)
+            blobs = [None] * world
+            dist.all_gather_object(blobs, w.export())
+            w.connect(blobs)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line, never silent
+            err = repr(e)[:300]
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        if any(errs):
+            # the sharded world could not be mapped on this node: fall back to one independent
+            # 256-rank world per GPU and SAY so in the line (mode / sharded_error)
+            if w is not None:
+                w.close()
+            mode = "replicas"
+            R = per
+            w = rlo.World(R, max_payload=max(64, length), device=local)
+            sharded_error = [e for e in errs if e][0]
+    lib = rlo.abi.load()
+    stream = ctypes.c_void_p()
+    rlo.abi.check(lib.rlo_stream_create(local, ctypes.byref(stream)), "rlo_stream_create")
+
+    def step():
+        """one launch of the loaded program; every part reset before any part launches"""
+        w.reset(stream)
+        if dist is not None:
+            dist.barrier()
+        w.launch(stream, no_reset=True)
+        rc = w.wait(raise_on_device_error=False)
+        if dist is not None:
+            dist.barrier()  # no peer still stores into this part's rings
+        return rc, w.kernel_ms()
+
+    seed = 0x5EED
+    w.program_storm(k, length, seed=seed)
+    ok = True
     for _ in range(args.warmup):
-        w.run(stream)
+        rc, _ = step()
+        ok &= rc == 0
     ref_sum = w.stats()["bcast_sum"].copy() if args.warmup else None
 
     barrier()
     t0 = time.perf_counter()
     kms = []
     for _ in range(args.steps):
-        kms.append(w.run(stream))
+        rc, ms = step()
+        ok &= rc == 0
+        kms.append(ms)
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     st = w.stats()
-    ok = bool((st["error"] == 0).all()) and int(st["originated"].sum()) == k
+    ok &= bool((st["error"] == 0).all())
+    copies = world if mode == "replicas" else 1  # independent worlds each run the whole storm
+    ok &= int(sum_over_ranks(float(st["originated"].sum()))) == k * copies
     if ref_sum is not None:
         ok &= bool(np.array_equal(ref_sum, st["bcast_sum"]))  # every step delivers the same bytes
 
-    total = world * k * args.steps
-    value = total / elapsed
-    kernel_ms = float(np.mean(kms))
-    alg_bytes = k * 2.0 * (n - 1) * (length + 16)  # 2(N-1)(S+16) per bcast
+    deliveries = k * (R - 1) * args.steps * copies
+    value = deliveries / elapsed
+    bcast_per_s = k * copies * args.steps / elapsed
+    kernel_ms = max_over_ranks(float(np.mean(kms)))
+    # SURVEY.md 8(d): 2(N-1)(S+16) HBM bytes per bcast; this GPU's share is its ranks' receipts
+    alg_bytes = k * 2.0 * (R - 1) * (length + 16) * copies / world
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
-    extras = {}
+    extras = {"bcast_per_s": round(bcast_per_s, 1), "world_ranks": R, "mode": mode}
+    if mode == "replicas":
+        extras["sharded_error"] = sharded_error
+    if world > 1 and mode == "sharded":
+        # cross-GPU tree edges per bcast: G-1 .. G (SURVEY 8(e)); each moves header + payload over xGMI
+        extras["xgmi_alg_GBps_per_gpu"] = round(k * (world - 1) * (length + 16) / world / (kernel_ms * 1e-3) / 1e9, 3)
     if not args.no_extras:
-        # unloaded latency: one random originator per round (bcast completion = last pickup)
-        w.program_latency(args.lat_rounds, length, seed=17 + rank)
-        w.run(stream)
-        lat_us = w.latencies_ticks().astype(np.float64) * 0.01
-        extras["p50_us"] = round(percentile(lat_us, 50), 2)
-        extras["p99_us"] = round(percentile(lat_us, 99), 2)
+        if world == 1 or mode == "replicas":
+            # unloaded latency: one random originator per round (bcast completion = last pickup)
+            w.program_latency(args.lat_rounds, length, seed=17)
+            step()
+            lat_us = w.latencies_ticks().astype(np.float64) * 0.01
+            extras["p50_us"] = round(percentile(lat_us, 50), 2)
+            extras["p99_us"] = round(percentile(lat_us, 99), 2)
         # loaded per-delivery latency inside the storm
-        w.program_storm(k, length, seed=0x5EED + rank, hist=True)
-        w.run(stream)
-        hist = w.stats()["hist"].sum(axis=0)
+        w.program_storm(k, length, seed=seed, hist=True)
+        step()
+        hist = w.stats()["hist"].sum(axis=0).astype(np.float64)
+        if dist is not None:
+            t = torch.tensor(hist)
+            dist.all_reduce(t)
+            hist = t.numpy()
         extras["storm_delivery_p50_us"] = round(rlo.hist_percentile(hist, 50) * 0.01, 2)
         extras["storm_delivery_p99_us"] = round(rlo.hist_percentile(hist, 99) * 0.01, 2)
         # consensus: every rank keeps one outstanding proposal (approve-all)
         p = args.iar_p
-        props = [(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)]
+        props = [(r, it * R + r, b"0123456789abcdef") for it in range(p) for r in range(R)]
         w.program_iar(props)
-        w.run(stream)  # warm
+        step()  # warm
         barrier()
         t1 = time.perf_counter()
-        ims = w.run(stream)
+        rc, ims = step()
         barrier()
         idt = max_over_ranks(time.perf_counter() - t1)
         ist = w.stats()
-        extras["decisions_per_s"] = round(world * n * p / idt, 1)
-        extras["decisions_kernel_ms"] = round(ims, 3)
-        ok &= int(ist["own_decided"].sum()) == n * p and bool((ist["error"] == 0).all())
+        extras["decisions_per_s"] = round(R * p * copies / idt, 1)
+        extras["decisions_kernel_ms"] = round(max_over_ranks(ims), 3)
+        ok &= rc == 0 and int(sum_over_ranks(float(ist["own_decided"].sum()))) == R * p * copies
+        ok &= bool((ist["error"] == 0).all())
+    lib.rlo_stream_destroy(stream)
     w.close()
+    ok = bool(sum_over_ranks(0.0 if ok else 1.0) == 0.0)
 
     line = {
         "metric": "rootless bcast msgs/s",
         "value": round(value, 1),
-        "unit": "bcast/s",
+        "unit": "msgs/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -186,10 +260,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": "rootless bcast storm, %d workgroup-ranks per GPU, %d B payload, random originators, "
-                               "%d bcasts per step per GPU" % (n, length, k),
-                   "ranks_per_gpu": n, "payload_bytes": length, "bcasts_per_step": k,
-                   "parallelism": "one %d-rank world per GPU" % n},
+        "config": {"workload": "rootless bcast storm over one world of %d workgroup-ranks (%d per GPU), %d B payload, "
+                               "random originators, %d bcasts per step; value = delivered bcast messages/s "
+                               "(each bcast reaches %d ranks)" % (R, per, length, k, R - 1),
+                   "ranks_per_gpu": per, "world_ranks": R, "payload_bytes": length, "bcasts_per_step": k,
+                   "parallelism": ("one world sharded over %d GPU(s), contiguous rank ranges" % world) if mode == "sharded"
+                   else "%d independent %d-rank worlds, one per GPU" % (world, R)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                      "kernel": "rlo_progress_kernel", "kernel_ms": round(kernel_ms, 4),
@@ -198,7 +274,7 @@ def main():
     }
     line.update(extras)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(n, length, 0x5EED, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
