@@ -59,6 +59,40 @@ def cpu_baseline(n, length, seed, target_s):
     return out
 
 
+def pmc_traffic(ranks, length, k, device, timeout_s=120):
+    """HBM bytes per launch of the storm kernel from rocprofv3 PMC counters, collected live in
+    two separate passes (FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2: they cannot share a pass).
+    gfx950 corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reports half the bytes of wide
+    (16 B/lane) streaming reads -> x2; WRITE_SIZE is exact for 16-B stores.  Both are in KiB."""
+    import shutil
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import rocpd_summary
+
+    vals = {}
+    with tempfile.TemporaryDirectory() as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(td, ctr)
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", ctr, "-d", d, "-o", "run", "--",
+                   sys.executable, os.path.join(REPO, "tools", "pmc_probe.py"), "--ranks", str(ranks), "--len",
+                   str(length), "--k", str(k), "--launches", "2", "--device", str(device)]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            if r.returncode != 0:
+                return None, "rocprofv3 %s pass rc=%d" % (ctr, r.returncode)
+            dbs = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs if f.endswith(".db")]
+            rows = rocpd_summary.pmc(dbs[0]) if dbs else []
+            if not rows:
+                return None, "no %s rows" % ctr
+            vals[ctr] = rows[-1][3] * 1024.0  # last launch, KiB -> bytes
+    fetch = 2.0 * vals["FETCH_SIZE"]
+    write = vals["WRITE_SIZE"]
+    return {"bytes": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, last of 2 launches; FETCH x2 (gfx950)"}, None
+
+
 def reference_datapoint(length):
     """The compiled reference itself under host MPI (8 ranks), if it was built and MPI exists."""
     exe = os.path.join(REPO, "oracle", "_ref", "ref_harness")
@@ -91,6 +125,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / decisions legs")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -273,6 +308,15 @@ def main():
         "verified": ok,
     }
     line.update(extras)
+    if rank == 0 and world == 1 and not args.no_pmc:
+        tr, why = pmc_traffic(per, length, k, local)
+        if tr is not None:
+            line["roofline"]["traffic"] = round(tr["bytes"] / 1e9, 4)
+            line["roofline"]["traffic_unit"] = "GB per launch (HBM, PMC)"
+            line["roofline"]["alg_GB_per_launch"] = round(alg_bytes / 1e9, 4)
+            line["roofline"]["traffic_detail"] = tr
+        else:
+            line["roofline"]["traffic_error"] = why
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds)
     if rank == 0:
