@@ -36,6 +36,7 @@ extern "C" {
 #define RLO_E_NOPROGRAM (-5) /* rlo_launch without a program                              */
 #define RLO_E_NODEVICE (-6)  /* no HIP device                                              */
 #define RLO_E_NOTCONNECTED (-7) /* part created but rlo_part_connect not called yet          */
+#define RLO_E_AGAIN (-8)     /* host-service ring full / nothing to do, retry after progress  */
 
 /* device error codes (rlo_rank_stats_t.error) */
 #define RLO_DERR_TIMEOUT 1
@@ -44,6 +45,7 @@ extern "C" {
 #define RLO_DERR_VOTE_ORPHAN 4
 #define RLO_DERR_LOG_FULL 5
 #define RLO_DERR_BAD_SLOT 6
+#define RLO_DERR_HOST_CMD 7      /* malformed / unexpected host-service command                */
 
 /* ------------------------------------------------------------------ topology (host only) */
 /* skip-ring overlay, restated from rootless_ops.c:1416-1579; usable without a GPU */
@@ -132,6 +134,65 @@ typedef struct {
 int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, const int32_t* origin, const int32_t* pid,
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len);
 
+/* one event record (parity log / host pickup ring) */
+typedef struct {
+    uint32_t kind; /* 1 deliver | 2 judge | 3 action | 4 result | 5 error | 6 judge req | 7 own judge req; | tag << 8 */
+    int32_t origin, from;
+    uint32_t id, len;
+    int32_t vote;
+    uint32_t aux, payload_idx;
+} rlo_log_rec_t;
+
+/* ---- host-service program: the kernel serves the rootless_ops.h API of this part's ranks.
+ * The host posts originations and judge verdicts into a per-rank command ring and drains a
+ * per-rank pickup ring of events; both rings live in pinned host memory.  The kernel runs
+ * (persistent) from rlo_launch_ex until every local rank has received RLO_CMD_QUIT.
+ * Replaces the MPI transport under RLO_bcast_gen :1581, RLO_make_progress_all :538,
+ * RLO_user_pickup_next :938, RLO_submit_proposal :876 and the judge / action callbacks
+ * (:698, :773, :842), which the host layer (librootless_ops.so) invokes on pickup events. */
+typedef struct {
+    uint32_t cmd_slots;      /* command ring capacity per rank (power of two), 0 = 256       */
+    uint32_t pickup_slots;   /* pickup ring capacity per rank (power of two, >= 64), 0 = 1024 */
+    uint32_t idle_timeout_s; /* kernel stops (RLO_DERR_TIMEOUT) after this long without any
+                                progress; 0 = never                                          */
+    uint32_t flags;
+} rlo_host_cfg_t;
+int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg);
+
+/* command kinds: originations use the reference tags (enum RLO_COMM_TAGS) */
+#define RLO_CMD_BCAST 0u      /* payload = user bytes; id = caller's sequence number           */
+#define RLO_CMD_PROPOSAL 2u   /* payload = serialized PBuf (pid, vote, data_len, data) :1369   */
+#define RLO_CMD_JUDGE 16u     /* verdict for an RLO_EV_JUDGE event: origin, pid, pseq, vote     */
+#define RLO_CMD_OWN_JUDGE 17u /* verdict of the originator's final judge(NULL) (:773): vote      */
+#define RLO_CMD_QUIT 18u      /* stop this rank's progress (after everything before it)          */
+typedef struct {
+    uint32_t kind;
+    int32_t origin; /* RLO_CMD_JUDGE: origin of the proposal                                  */
+    int32_t id;     /* BCAST: sequence number; PROPOSAL / JUDGE: pid                          */
+    uint32_t pseq;  /* RLO_CMD_JUDGE: the event's aux (proposal sequence)                     */
+    int32_t vote;   /* JUDGE / OWN_JUDGE: 0 or 1                                              */
+    uint32_t pad;
+} rlo_cmd_t;
+/* world rank `rank` must be local; RLO_E_AGAIN when the command ring is full */
+int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* cmd, const void* payload, uint32_t len);
+
+/* pickup events (rlo_log_rec_t.kind) */
+#define RLO_EV_DELIVER_BCAST (1u | (0u << 8))    /* origin, from (tree parent), id, len + payload */
+#define RLO_EV_DELIVER_DECISION (1u | (4u << 8)) /* origin, id = pid, vote = decision             */
+#define RLO_EV_ACTION 3u    /* decision 1 for a proposal this rank approved: run action (:842)   */
+#define RLO_EV_RESULT 4u    /* my own proposal decided: id = pid, vote = decision                */
+#define RLO_EV_JUDGE 6u     /* call judge(data): origin, from, id = pid, aux = pseq,
+                               payload = the proposal's PBuf (len bytes)                        */
+#define RLO_EV_OWN_JUDGE 7u /* call judge(NULL) for my proposal id (all votes were 1)          */
+/* next event of local rank `rank`: 1 = got one (payload copied, up to cap bytes), 0 = none */
+int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, uint32_t cap);
+/* 1 while this part's kernel runs, 0 once it has ended (rlo_wait then reports its status) */
+int rlo_host_running(rlo_world_t* w);
+/* commands of local rank `rank` taken by the device so far / posted so far */
+int rlo_host_cmd_count(rlo_world_t* w, int rank, uint64_t* consumed, uint64_t* posted);
+/* number of HIP devices visible to this process (0 without a GPU) */
+int rlo_device_count(void);
+
 /* ------------------------------------------------------------------ run */
 int rlo_reset(rlo_world_t* w, void* stream);           /* zero this part's counters (sync) */
 #define RLO_LAUNCH_NO_RESET 1u
@@ -158,13 +219,6 @@ typedef struct {
     uint32_t hist[128];
 } rlo_rank_stats_t;
 
-typedef struct {
-    uint32_t kind; /* 1 deliver | 2 judge | 3 action | 4 result | 5 error, | tag << 8 */
-    int32_t origin, from;
-    uint32_t id, len;
-    int32_t vote;
-    uint32_t aux, payload_idx;
-} rlo_log_rec_t;
 
 /* results of this part's ranks: stats index = rank - rank_begin; rlo_log takes the world rank */
 int rlo_stats(rlo_world_t* w, rlo_rank_stats_t* out, int n);

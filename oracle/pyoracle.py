@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 ORC_JUDGE_APPROVE, ORC_JUDGE_MASK, ORC_JUDGE_ISP, ORC_JUDGE_HASH = 0, 1, 2, 3
+ORC_EV_JUDGE, ORC_EV_ACTION, ORC_EV_PICKUP, ORC_EV_RESULT, ORC_EV_ERROR = 1, 2, 3, 4, 5  # rlo_oracle.h
 EV_JUDGE, EV_ACTION, EV_PICKUP, EV_RESULT, EV_ERROR = 1, 2, 3, 4, 5
 
 

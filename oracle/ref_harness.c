@@ -3,7 +3,9 @@
  *
  * Driver that links the *compiled reference* (oracle/_ref/rootless_ops.o, built
  * from /root/reference/rootless_ops.c in place by oracle/Makefile) and runs it
- * under host MPI to capture golden vectors.  It only uses the public API of
+ * under host MPI to capture golden vectors.  Built a second time with -DRLO_DROPIN
+ * against include/rootless_ops.h + librootless_ops.so (oracle/_ref/dropin_harness):
+ * the same capture modes then drive the MI355X drop-in, and tests/ compare the two.  It only uses the public API of
  * rootless_ops.h, plus the reference's own test callbacks from testcases.c
  * (is_proposal_approved_cb / proposal_action_cb, testcases.c:18-42) and the
  * two exported topology helpers get_level / last_wall (rootless_ops.c:1427,1444).
@@ -16,6 +18,7 @@
  *   iar    ORIGIN MASK           single proposal, decline iff rank in MASK (arg != NULL)
  *   multi  ACTIVE1 MOD AGREE     test_iar_multi_proposal roles (testcases.c:401-486), logging decisions
  *   tests                        the reference's own test wrappers' return values
+ *   tests2                       its two-engine IAR tests
  *   bench  K LEN                 storm throughput: every rank originates K bcasts
  *   lat    ROUNDS LEN SEED       unloaded latency: one random originator per round
  *   iarbench P                   every rank keeps one outstanding proposal, approve-all
@@ -25,8 +28,10 @@
 #include <stdarg.h>
 #include <stdint.h>
 
+#ifndef RLO_DROPIN
 int get_level(int world_size, int rank); /* rootless_ops.c:1427 */
 int last_wall(int rank);                 /* rootless_ops.c:1444 */
+#endif
 int is_proposal_approved_cb(const void* buf, void* app_data); /* testcases.c:18 */
 int proposal_action_cb(const void* buf, void* app_data);      /* testcases.c:39 */
 int test_wrapper_bcast(int bc_cnt);                            /* testcases.c:699 */
@@ -89,9 +94,18 @@ static void json_str(char* dst, size_t cap, const char* s, size_t maxlen) {
 }
 
 /* parent rank of a received message = MPI_SOURCE of its irecv (rootless_ops.h:115) */
+#ifdef RLO_DROPIN
+/* built against the MI355X drop-in (include/rootless_ops.h): the engine reports the tree
+ * parent through its RLO_user_msg_source extension */
+static int msg_parent(RLO_user_msg* u) { return RLO_user_msg_source(u); }
+#else
 static int msg_parent(RLO_user_msg* u) { return ((RLO_msg_t*)u)->irecv_stat.MPI_SOURCE; }
+#endif
 
 /* ---------------------------------------------------------------- topo */
+#ifdef RLO_DROPIN
+static void mode_topo(int nmax) { (void)nmax; } /* reference internals only */
+#else
 static void mode_topo(int nmax) {
     /* get_level(N, r) depends on N only for r == 0; last_wall(r) never depends on N */
     if (g_rank != 0) return;
@@ -99,6 +113,8 @@ static void mode_topo(int nmax) {
     for (int r = 1; r < nmax; r++)
         emit("{\"rank\":%d,\"level\":%d,\"last_wall_fn\":%d}", r, get_level(nmax, r), last_wall(r));
 }
+
+#endif
 
 /* ---------------------------------------------------------------- parents */
 static void mode_parents(int len) {
@@ -284,6 +300,22 @@ static void mode_tests(void) {
     if (g_rank == 0) emit("{\"test\":\"test_iar_multi_proposal(1,3,1)\",\"ret\":%d}", r);
 }
 
+/* the reference's two-engine tests (testcases.c:110-241, :488-595) */
+int test_concurrent_iar_single_proposal(MPI_Comm comm, int starter, int no_rank, int agree);
+int test_concurrent_iar_multi_proposal(MPI_Comm comm, int active_1, int active_2_mod, int agree);
+
+static void mode_tests2(void) {
+    int r;
+    r = test_concurrent_iar_single_proposal(MPI_COMM_WORLD, 1, 2, 0);
+    if (g_rank == 0) emit("{\"test\":\"test_concurrent_iar_single_proposal(1,2,0)\",\"ret\":%d}", r);
+    r = test_concurrent_iar_single_proposal(MPI_COMM_WORLD, 1, 2, 1);
+    if (g_rank == 0) emit("{\"test\":\"test_concurrent_iar_single_proposal(1,2,1)\",\"ret\":%d}", r);
+    r = test_concurrent_iar_multi_proposal(MPI_COMM_WORLD, 1, 3, 1);
+    if (g_rank == 0) emit("{\"test\":\"test_concurrent_iar_multi_proposal(1,3,1)\",\"ret\":%d}", r);
+    r = test_concurrent_iar_multi_proposal(MPI_COMM_WORLD, 1, 3, 0);
+    if (g_rank == 0) emit("{\"test\":\"test_concurrent_iar_multi_proposal(1,3,0)\",\"ret\":%d}", r);
+}
+
 /* ---------------------------------------------------------------- bench */
 static double now_s(void) { struct timeval tv; gettimeofday(&tv, NULL); return tv.tv_sec + tv.tv_usec * 1e-6; }
 
@@ -399,6 +431,7 @@ static void mode_iarbench(int P) {
 }
 
 int main(int argc, char** argv) {
+    setvbuf(stdout, NULL, _IOLBF, 0); /* progress lines survive a kill */
     MPI_Init(&argc, &argv);
     MPI_Comm_rank(MPI_COMM_WORLD, &g_rank);
     MPI_Comm_size(MPI_COMM_WORLD, &g_size);
@@ -416,6 +449,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(mode, "iar")) mode_iar(atoi(argv[3]), (unsigned)strtoul(argv[4], 0, 0));
     else if (!strcmp(mode, "multi")) mode_multi(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
     else if (!strcmp(mode, "tests")) mode_tests();
+    else if (!strcmp(mode, "tests2")) mode_tests2();
     else if (!strcmp(mode, "bench")) mode_bench(atoi(argv[3]), atoi(argv[4]));
     else if (!strcmp(mode, "lat")) mode_lat(atoi(argv[3]), atoi(argv[4]), strtoull(argv[5], 0, 0));
     else if (!strcmp(mode, "iarbench")) mode_iarbench(atoi(argv[3]));

@@ -40,14 +40,25 @@ enum Mode : uint32_t {
     MODE_LOG = 16u,    // record every event (+ delivered payload bytes) for parity tests
     MODE_HIST = 32u,   // per-delivery latency histogram
     MODE_PROF = 64u,   // per-phase shader-clock accounting (diagnostic build of the same kernel)
+    MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
+                       //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };
+
+// host-service command kinds (tag field of a command slot); tags < 16 are originations
+// (TAG_BCAST: RLO_bcast_gen :1581, TAG_PROPOSAL: RLO_submit_proposal :876)
+enum HostCmd : uint32_t { CMD_JUDGE = 16, CMD_OWN_JUDGE = 17, CMD_QUIT = 18 };
+// per local rank, 64 host words (one 128-B line per counter)
+constexpr int kHctlWords = 64;
+constexpr int kHctlInjTail = 0, kHctlInjHead = 16, kHctlPkTail = 32, kHctlPkHead = 48;
 
 enum Judge : uint32_t { JUDGE_APPROVE = 0, JUDGE_MASK = 1, JUDGE_ISP = 2, JUDGE_HASH = 3 };
 
-enum LogKind : uint32_t { LOG_DELIVER = 1, LOG_JUDGE = 2, LOG_ACTION = 3, LOG_RESULT = 4, LOG_ERROR = 5 };
+enum LogKind : uint32_t { LOG_DELIVER = 1, LOG_JUDGE = 2, LOG_ACTION = 3, LOG_RESULT = 4, LOG_ERROR = 5,
+                          LOG_JREQ = 6,      // host mode: judge(data) request for a received proposal (:698)
+                          LOG_OWN_JREQ = 7 };// host mode: the originator's final judge(NULL) request (:773)
 
 enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_COLLISION = 3, ERR_VOTE_ORPHAN = 4,
-                      ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6 };
+                      ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6, ERR_HOST_CMD = 7 };
 
 // Slot header, 16 bytes:
 //   w0 = origin (16 b) | tag (8 b) << 16 | vote (8 b) << 24
@@ -150,6 +161,11 @@ struct Params {
     uint32_t nsmall;              // slot chunks staged per message on the small path (<= 8)
     uint32_t stage2_bytes;        // LDS staging for large messages (multiple of 1 KiB, >= 1 KiB)
     uint32_t nout_max;            // 2 x max send_list_len over the ranks of this launch
+    // host-service mode (MODE_HOST): all in pinned host memory.  Pickup records / payloads use
+    // log / log_payload above as per-rank rings of log_cap slots.
+    uint8_t* hin;                 // command slots [n_local][hin_cap] x fwd_stride (forward-slot layout)
+    uint32_t hin_cap;
+    uint64_t* hctl;               // [n_local][kHctlWords] ring counters
 };
 
 }  // namespace rlo

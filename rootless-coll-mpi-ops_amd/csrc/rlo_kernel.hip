@@ -41,7 +41,9 @@ static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
 
-enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_BAD = 7 };
+enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
+// PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
+enum PendValid : uint8_t { PS_NONE = 0, PS_ACTIVE = 1, PS_JREQ = 2, PS_JYES = 3, PS_JNO = 4 };
 static constexpr int kGroupLocal = 2 * kMaxIn;  // groups [0, 64) = in-rings (k*2+vc); 64.. local kinds
 static constexpr int kGroups = kGroupLocal + 8;
 static constexpr uint16_t kBigFlag = 0x8000u;
@@ -73,6 +75,9 @@ struct Shared {
     uint32_t ofree[kMaxOut];         // free slots of out-ring oi at iteration start
     uint32_t n_oi[kMaxOut];          // slots admitted into out-ring oi this iteration
     uint32_t R, C, nstorm, storm_base, loc_kind, lat_id, exit_now;
+    // host-service mode: command run selected this iteration, pickup ring position
+    uint32_t hbase, nh, ev_n, quit;
+    uint64_t hhead, hin_head, pk_tail;
     int64_t prop_idx;
     uint32_t storm_ids[kPass];
     uint64_t vhead[kMaxFanout];
@@ -148,6 +153,20 @@ __device__ __forceinline__ void pub64(uint64_t addr, uint64_t v, bool sys) {
 __device__ __forceinline__ void st_ring(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, bool sys) {
     if (sys) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1 | 1);
     else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1);
+}
+// 16-B write-through store that reaches host memory (pinned pickup rings) or HBM for the log
+__device__ __forceinline__ void st_sys16(void* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+// 16-B command-slot load from pinned host memory (written by the host CPU)
+__device__ __forceinline__ u32x4 ld_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1 | 1);
+}
+__device__ __forceinline__ uint64_t poll64_sys(uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void pub64_sys(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint32_t poll32(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -283,13 +302,20 @@ __device__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, ui
     }
 }
 
+// one event record: the parity log (MODE_LOG, linear) or the host pickup ring (MODE_HOST, the
+// slot after this iteration's earlier events; the selection phase guaranteed the room)
 __device__ __forceinline__ uint32_t log_put(Shared& S, const Params& P, int lr, uint32_t kind, int origin, int from,
                                             uint32_t id, uint32_t len, int vote, uint32_t aux) {
-    if (!(P.mode & MODE_LOG)) return ~0u;
-    uint32_t i = (uint32_t)atomicAdd(&S.log_count, 1ull);
-    if (i >= P.log_cap) {
-        set_error(S, P, ERR_LOG_FULL, i);
-        return ~0u;
+    if (!(P.mode & (MODE_LOG | MODE_HOST))) return ~0u;
+    uint32_t i;
+    if (P.mode & MODE_HOST) {
+        i = (uint32_t)((S.pk_tail + atomicAdd(&S.ev_n, 1u)) & (uint64_t)(P.log_cap - 1u));
+    } else {
+        i = (uint32_t)atomicAdd(&S.log_count, 1ull);
+        if (i >= P.log_cap) {
+            set_error(S, P, ERR_LOG_FULL, i);
+            return ~0u;
+        }
     }
     LogRec r;
     r.kind = kind;
@@ -299,8 +325,10 @@ __device__ __forceinline__ uint32_t log_put(Shared& S, const Params& P, int lr, 
     r.len = len;
     r.vote = vote;
     r.aux = aux;
-    r.payload_idx = (P.log_payload && kind == (LOG_DELIVER | (TAG_BCAST << 8))) ? i : ~0u;
-    P.log[(size_t)lr * P.log_cap + i] = r;
+    r.payload_idx = (P.log_payload && (kind == (LOG_DELIVER | (TAG_BCAST << 8)) || kind == LOG_JREQ)) ? i : ~0u;
+    u32x4* dst = reinterpret_cast<u32x4*>(&P.log[(size_t)lr * P.log_cap + i]);
+    st_sys16(dst, u32x4{r.kind, (uint32_t)r.origin, (uint32_t)r.from, r.id});
+    st_sys16(dst + 1, u32x4{r.len, (uint32_t)r.vote, r.aux, r.payload_idx});
     return r.payload_idx;
 }
 
@@ -400,7 +428,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1;
-    const uint32_t my_mask = ((P.mode & MODE_IAR) && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
+    const bool host = (P.mode & MODE_HOST) != 0;
+    const uint32_t my_mask = ((P.mode & MODE_IAR) && !host && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
+    // host-service mode: this rank's command ring (pinned host memory) and its counters
+    const __amdgpu_buffer_rsrc_t rh =
+        mk_rsrc(host ? P.hin + (size_t)lr * P.hin_cap * P.fwd_stride : P.fwd_region, host ? P.hin_cap * P.fwd_stride : 16u);
+    uint64_t* const hctl = host ? P.hctl + (size_t)lr * kHctlWords : nullptr;
+    const uint32_t hcap_m = host ? P.hin_cap - 1u : 0u;
 
     // ---------------- init
     {
@@ -416,12 +450,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             S.own_pid = -1;  // proposal_state_init, :1238
             S.own_word = 0; S.own_needed = 0; S.own_state = 0; S.own_decision = 0; S.own_pseq = 0;
             S.own_iter = 0;
-            S.own_n = (P.mode & MODE_IAR) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
+            S.own_n = ((P.mode & MODE_IAR) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
             S.sched_next = 0;
             S.sched_n = (P.mode & MODE_STORM) ? (P.sched_off[lr + 1] - P.sched_off[lr]) : 0;
             S.lat_next = 0;
             S.expect_bcast = (P.mode & (MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
-            S.expect_dec = (P.mode & MODE_IAR) ? P.expect_dec[lr] : 0;
+            S.expect_dec = ((P.mode & MODE_IAR) && !host) ? P.expect_dec[lr] : 0;
+            S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.iterations = S.busy = S.stalls = 0;
             S.error = 0; S.error_aux = 0; S.done = 0; S.exit_now = 0; S.progressed = 0;
@@ -459,7 +494,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
         // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
         uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
         uint32_t errf = 0, sid = 0;
+        uint64_t hpoll = 0;  // host mode: lane 0 = command-ring tail, lane 1 = pickup-ring head
         if (w == 0) {
+            if (host && lane < 2) hpoll = poll64_sys(&hctl[lane == 0 ? kHctlInjTail : kHctlPkHead]);
             if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
             if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
             if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
@@ -484,8 +521,21 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 S.vout_head[lane] = vout_head_r;
             }
             peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
+            // host mode: publish the command head / pickup tail of the previous iteration; the pickup
+            // ring bounds this iteration's events: a ring message makes <= 2 (action + decision), plus
+            // <= 2 of the own proposal (final-judge request, result)
+            bool hblock = false;
+            uint32_t hlim = kMaxCand;
+            if (host) {
+                if (lane == 0) pub64_sys(&hctl[kHctlInjHead], S.hin_head);
+                if (lane == 1) pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
+                const uint64_t pk_head = rdl64(hpoll, 1);
+                const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - pk_head);
+                hblock = pk_free < 8u;
+                hlim = hblock ? 0u : (pk_free - 4u) / 2u;
+            }
             // votes to merge (wave 1), at most 256 per iteration: trim the ring prefixes
-            const uint32_t va = lane < sll ? (uint32_t)min(vin_tail_r - vin_head_r, (uint64_t)256) : 0u;
+            const uint32_t va = (lane < sll && !hblock) ? (uint32_t)min(vin_tail_r - vin_head_r, (uint64_t)256) : 0u;
             uint32_t vtot = 0, vex = 0;
             if (__ballot(va > 0)) vex = wave_excl_scan(va, &vtot);
             uint32_t vtake = va;
@@ -497,11 +547,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             vin_head_r += vtake;  // merged by wave 1 before the next publish
             // in-rings: fair per-ring quotas
             const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)256) : 0u;
-            const uint32_t reserve = (P.mode & MODE_IAR) ? 2u : 0u;
-            const uint64_t ract = __ballot(ra > 0);
+            const uint32_t reserve = host ? 64u : ((P.mode & MODE_IAR) ? 2u : 0u);
+            const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
-            const uint32_t quota = nact ? (kMaxCand - reserve) / (uint32_t)nact : 0u;
-            const uint32_t take = min(min(ra, quota), win_r);
+            const uint32_t quota = nact ? min(kMaxCand - reserve, hlim) / (uint32_t)nact : 0u;
+            const uint32_t take = hblock ? 0u : min(min(ra, quota), win_r);
             const bool backlog = __ballot(ra > take) != 0;
             uint32_t R;
             const uint32_t base = wave_excl_scan(take, &R);
@@ -516,9 +566,52 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             // local originations
             uint32_t C = R, loc_kind = 0, nstorm = 0, storm_base = 0, lat_id = 0xffffffffu;
             int64_t prop_idx = -1;
-            if (P.mode & MODE_IAR) {
+            if ((P.mode & MODE_IAR) && !hblock) {
                 if (S.own_state == 2) { loc_kind = K_DEC; C++; }
                 else if (S.own_state == 0 && S.own_iter < S.own_n) { loc_kind = K_PROP; prop_idx = P.prop_off[lr] + S.own_iter; C++; }
+            }
+            uint32_t hbase = C, nh = 0;
+            if (host && !hblock) {
+                // commands in FIFO order: a leading run of control commands (judge verdicts, quit) is
+                // applied now; the run of originations behind it becomes candidates (a proposal only
+                // when no own proposal is active, and it ends the run)
+                const uint64_t pend_n = rdl64(hpoll, 0) - S.hin_head;
+                const uint32_t np = (uint32_t)min(pend_n, (uint64_t)64);
+                if (np) {
+                    u32x4 hd = {0u, 0u, 0u, 0u};
+                    if ((uint32_t)lane < np) hd = ld_sys(rh, (uint32_t)((S.hin_head + lane) & hcap_m) * P.fwd_stride);
+                    const uint32_t htag = (hd.x >> 16) & 0xffu;
+                    const bool inq = (uint32_t)lane < np;
+                    const uint64_t cm = __ballot(inq && htag >= 16u);
+                    const uint32_t ncp = ~cm == 0ull ? 64u : (uint32_t)__builtin_ctzll(~cm);
+                    if ((uint32_t)lane < ncp) {
+                        const int vo = (int)(int8_t)(hd.x >> 24);
+                        if (htag == CMD_JUDGE) {  // verdict of judge(data) for a held proposal (:698)
+                            const int og = (int)(hd.x & 0xffffu);
+                            PendState* ps = &pend[2 * (og < P.n ? og : 0) + ((hd.z >> 24) & 1u)];
+                            if (og < P.n && ps->valid == PS_JREQ && ps->pid == (int32_t)hd.y) ps->valid = vo ? PS_JYES : PS_JNO;
+                            else set_error(S, P, ERR_HOST_CMD, hd.x);
+                        } else if (htag == CMD_OWN_JUDGE) {  // final judge(NULL) of my proposal (:770-775)
+                            if (S.own_state == 3) { S.own_decision = vo ? 1u : 0u; S.own_state = 2; }
+                            else set_error(S, P, ERR_HOST_CMD, hd.x);
+                        } else if (htag == CMD_QUIT) {
+                            S.quit = 1;
+                        } else {
+                            set_error(S, P, ERR_HOST_CMD, hd.x);
+                        }
+                    }
+                    const bool org = inq && (uint32_t)lane >= ncp && (htag == TAG_BCAST || htag == TAG_PROPOSAL);
+                    const uint64_t om = __ballot(org) >> ncp;
+                    uint32_t run = ~om == 0ull ? 64u - ncp : (uint32_t)__builtin_ctzll(~om);
+                    const uint64_t pm = (__ballot(org && htag == TAG_PROPOSAL) >> ncp) & (run >= 64 ? ~0ull : ((1ull << run) - 1ull));
+                    if (pm) {
+                        const uint32_t fp = (uint32_t)__builtin_ctzll(pm);
+                        run = (S.own_state == 0 && loc_kind != K_DEC) ? fp + 1u : fp;
+                    }
+                    nh = min(run, kMaxCand - C);
+                    if (lane == 0) { S.hhead = S.hin_head + ncp; S.hin_head += ncp; }
+                    C += nh;
+                }
             }
             if ((P.mode & MODE_STORM) && S.sched_next < S.sched_n) {
                 // throttle: originate only into shallow out-rings so forwarding never waits behind originations
@@ -544,6 +637,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 S.vtot = vtot;
                 S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
                 S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = 0;
+                S.hbase = hbase; S.nh = nh;
                 S.exit_now = S.done;
                 if (P.mode & MODE_PROF) S.dbg[0] += R;
             }
@@ -596,6 +690,27 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     }
                 }
             }
+            if (host && S.nh) {  // the host command run: slots in pinned memory, same layout as a ring slot
+                const uint32_t hb = S.hbase, he = hb + S.nh;
+                const uint32_t lo = max(hb, c_lo), hi = min(he, c_lo + kPass);
+                if (lo < hi) {
+                    const uint64_t head = S.hhead + (lo - hb);
+                    const uint32_t nit = (hi - lo) * nsmall;
+                    for (uint32_t i0 = 0; i0 < nit; i0 += 64) {
+                        const uint32_t i = i0 + lane;
+                        if (i < nit) {
+                            const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
+                            const uint32_t off = (uint32_t)((head + mi) & hcap_m) * P.fwd_stride;
+                            if (q == 0) {
+                                S.cand[lo + mi].src = off;
+                                S.cand[lo + mi].group = kGroupLocal + K_HOST;
+                            }
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(STG(lo, 0) + (i0 << 4)), 16, off + 16u * q, 0, 0,
+                                                                     kAuxSc1 | 1);
+                        }
+                    }
+                }
+            }
             VM_DRAIN();  // this wave's stage loads (wave 1: and its vote loads)
             PROF_STAMP(1);
 
@@ -620,17 +735,22 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                             const uint32_t nw = atomicAdd(&S.own_word, inc) + inc;
                             if ((nw & 0xffffu) == S.own_needed) {
                                 const int d = (nw >> 16) == 0 ? 1 : 0;
-                                if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
-                                    atomicAdd(&S.judge_calls, 1ull);
-                                    log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                                if (d && host) {  // final judge(NULL) (:770-775) is the host's callback
+                                    log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, 1);
+                                    S.own_state = 3;
+                                } else {
+                                    if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
+                                        atomicAdd(&S.judge_calls, 1ull);
+                                        log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                                    }
+                                    S.own_decision = (uint32_t)d;
+                                    S.own_state = 2;
                                 }
-                                S.own_decision = (uint32_t)d;
-                                S.own_state = 2;
                             }
                         }
                     } else {  // _vote_merge (:1056-1070)
                         PendState* ps = &pend[2 * origin + (pseq & 1u)];
-                        if (!ps->valid || ps->pid != pid) {
+                        if (ps->valid != PS_ACTIVE || ps->pid != pid) {
                             set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
                         } else {
                             const uint32_t nw = atomicAdd(&ps->word, inc) + inc;
@@ -647,6 +767,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             const bool active = c < C;
             uint32_t kind = K_BAD, w0 = 0, id = 0, w2 = 0, t0 = 0, src = 0, kids = 0, group = 0;
             int from = -1, judge = 1;
+            bool want_jreq = false;  // host mode: a proposal whose verdict has not been asked for yet
             if (active && c < R) {
                 const u32x4 h = *reinterpret_cast<const u32x4*>(STG(c, 0));
                 group = S.cand[c].group;
@@ -664,10 +785,22 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 } else if (tag == TAG_PROPOSAL) {
                     // PBuf [pid][vote][data_len u64][data] at slot + 16 (rootless_ops.c:1402-1410)
                     const uint32_t plen = w2 & 0xffffffu;
-                    uint32_t dl = nsmall > 1 ? reinterpret_cast<const u32x4*>(STG(c, 1))->z : 0u;
-                    if (dl > plen - 16u) dl = plen > 16u ? plen - 16u : 0u;
-                    judge = judge_eval(P, rf, me, my_mask, (int32_t)id, src + kHdr + 16u, dl);
-                    kids = judge ? kids_of(me, origin, from, level, last_wall, scc, sll, sl_r) : 0u;
+                    if (host) {  // the host judges: hold the proposal at the head of its ring until the verdict
+                        PendState* ps = &pend[2 * origin + ((w2 >> 24) & 1u)];
+                        const uint8_t pv = ps->valid;
+                        if ((pv == PS_JYES || pv == PS_JNO) && ps->pid == (int32_t)id) {
+                            judge = pv == PS_JYES ? 1 : 0;
+                        } else {
+                            judge = -1;
+                            if (S.own_state != 0 && (int32_t)id == S.own_pid) set_error(S, P, ERR_PID_COLLISION, id);  // :690-692
+                            else want_jreq = !(pv == PS_JREQ && ps->pid == (int32_t)id);
+                        }
+                    } else {
+                        uint32_t dl = nsmall > 1 ? reinterpret_cast<const u32x4*>(STG(c, 1))->z : 0u;
+                        if (dl > plen - 16u) dl = plen > 16u ? plen - 16u : 0u;
+                        judge = judge_eval(P, rf, me, my_mask, (int32_t)id, src + kHdr + 16u, dl);
+                    }
+                    kids = judge == 1 ? kids_of(me, origin, from, level, last_wall, scc, sll, sl_r) : 0u;
                 } else {
                     set_error(S, P, ERR_BAD_SLOT, w0);
                     kind = K_BAD;
@@ -681,6 +814,24 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     id = S.storm_ids[c - storm_base];
                     w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
                     w2 = P.len;
+                } else if (host && c >= S.hbase && c < S.hbase + S.nh) {  // host origination (RLO_bcast_gen :1581)
+                    const u32x4 h = *reinterpret_cast<const u32x4*>(STG(c, 0));
+                    kind = K_HOST;
+                    group = kGroupLocal + K_HOST;
+                    src = S.cand[c].src;
+                    id = h.y;
+                    if (((h.x >> 16) & 0xffu) == TAG_PROPOSAL) {  // RLO_submit_proposal :876-906 (payload = PBuf)
+                        w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
+                        w2 = (h.z & 0xffffffu) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                    } else {
+                        w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
+                        w2 = h.z & 0xffffffu;
+                    }
+                    if ((w2 & 0xffffffu) + kHdr > P.fwd_stride) {
+                        set_error(S, P, ERR_HOST_CMD, h.x);
+                        kind = K_BAD;
+                        kids = 0;
+                    }
                 } else if (loc_kind == K_DEC && c == R) {
                     kind = K_DEC;
                     group = kGroupLocal + K_DEC;
@@ -705,13 +856,30 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 // stage the header (+ the payload of a small message) like a received slot
                 const uint32_t nch = (kHdr + (w2 & 0xffffffu) + 15u) >> 4;
                 *reinterpret_cast<u32x4*>(STG(c, 0)) = u32x4{w0, id, w2, t0};
-                if (nch <= nsmall)
+                if (nch <= nsmall && kind != K_HOST && kind != K_BAD)
                     for (uint32_t q = 1; q < nch; q++)
                         *reinterpret_cast<u32x4*>(STG(c, q)) =
                             gen_chunk(P, kind, me, id, w2 & 0xffffffu, src, (int)(int8_t)(w0 >> 24), q);
             }
             const int origin = (int)(w0 & 0xffffu);
             const uint32_t need = active ? need_of(kids, origin, sll, sl_r) : 0u;
+            for (uint64_t jb = __ballot(want_jreq); jb; jb &= jb - 1) {  // host judge requests (uniform loop)
+                const int l = __builtin_ctzll(jb);
+                const uint32_t lsrc = rdl32(src, l), lw2 = rdl32(w2, l), lid = rdl32(id, l);
+                const int lorg = (int)(rdl32(w0, l) & 0xffffu), lfrom = (int)rdl32((uint32_t)from, l);
+                const uint32_t plen = lw2 & 0xffffffu;
+                uint32_t slot = 0;
+                if (lane == 0) {
+                    PendState* ps = &pend[2 * lorg + ((lw2 >> 24) & 1u)];
+                    ps->pid = (int32_t)lid;
+                    ps->valid = PS_JREQ;
+                    slot = log_put(S, P, lr, LOG_JREQ, lorg, lfrom, lid, plen, -1, lw2 >> 24);
+                }
+                slot = rdl32(slot, 0);
+                uint8_t* dst = P.log_payload + ((size_t)lr * P.log_cap + slot) * P.log_stride;
+                for (uint32_t q = (uint32_t)lane; 16u * q < plen && 16u * q < P.log_stride; q += 64u)
+                    st_sys16(dst + 16u * q, ld_sc1(rf, lsrc + kHdr + 16u * q));
+            }
             PROF_STAMP(2);
 
             // ---------------- E: admission: credits per out-ring, FIFO prefix per source
@@ -727,7 +895,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 const uint32_t f = S.ofree[lane];
                 room_r = f > pre ? f - pre : 0u;
             }
-            bool fits = active;
+            bool fits = active && judge >= 0;
             for (int oi = 0; oi < nout; oi++) {
                 const bool bit = (need >> oi) & 1u;
                 const uint64_t b = __ballot(bit);
@@ -797,35 +965,36 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                             set_error(S, P, ERR_PID_COLLISION, (uint32_t)pid);  // :690-692 (the reference never votes)
                         } else {
                             atomicAdd(&S.judge_calls, 1ull);
-                            log_put(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
-                            if (!judge) {
+                            if (!host) log_put(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
+                            PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                            if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
+                                ps->valid = PS_NONE;
                                 emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 0);
                             } else {
-                                PendState* ps = &pend[2 * origin + (pseq & 1u)];
                                 const uint32_t nk = (uint32_t)__builtin_popcount(kids);
                                 ps->pid = pid;
                                 ps->word = 0;
                                 ps->parent_k = (uint16_t)k;
                                 ps->needed = (uint8_t)nk;
                                 ps->pseq = pseq | ((len - 16u) << 8);
-                                ps->valid = 1;
+                                ps->valid = PS_ACTIVE;
                                 if (nk == 0) emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 1);
                             }
                         }
                     } else if (tag == TAG_DECISION) {  // :603-615, _iar_decision_handler :814-859
                         PendState* ps = &pend[2 * origin + (pseq & 1u)];
-                        if (ps->valid && ps->pid == (int32_t)id) {
+                        if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)id) {
                             if (vote != 0) {
                                 atomicAdd(&S.actions, 1ull);
                                 log_put(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, ps->pseq >> 8);
                             }
-                            ps->valid = 0;
+                            ps->valid = PS_NONE;
                         }
                         atomicAdd(&S.dec_delivered, 1ull);
                         if (vote != 0) atomicAdd(&S.dec_approved, 1ull);
                         log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
                     }
-                } else if (kind == K_PROP) {
+                } else if (kind == K_PROP || (kind == K_HOST && tag == TAG_PROPOSAL)) {
                     S.own_pid = (int32_t)id;
                     S.own_word = 0;
                     S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
@@ -849,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             }
             {  // wave-aggregated counters (one LDS op per wave instead of 64 same-address atomics)
                 const uint64_t bdel = __ballot(admitted && kind == K_RING && tag == TAG_BCAST);
-                const uint64_t borg = __ballot(admitted && (kind == K_STORM || kind == K_LAT));
+                const uint64_t borg = __ballot(admitted && (kind == K_STORM || kind == K_LAT || (kind == K_HOST && tag == TAG_BCAST)));
                 const uint64_t bbig = __ballot(isbig);
                 if (lane == 0) {
                     if (bdel) atomicAdd(&S.bcast_delivered, (unsigned long long)__popcll(bdel));
@@ -897,6 +1066,10 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     uint8_t* dst = stage2 + (b << 10);
                     if (cl.kind == K_RING) {
                         if (q < nch) dma16(rf, dst, cl.src + 16u * q);
+                    } else if (cl.kind == K_HOST) {  // payload from the command slot, header as classified
+                        if (q < nch && q != 0)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(dst), 16, cl.src + 16u * q, 0, 0, kAuxSc1 | 1);
+                        if (q == 0) *reinterpret_cast<u32x4*>(dst) = u32x4{cl.w0, cl.id, cl.w2, cl.t0};
                     } else if (q < nch) {
                         *reinterpret_cast<u32x4*>(dst + 16u * lane) =
                             q == 0 ? u32x4{cl.w0, cl.id, cl.w2, cl.t0}
@@ -937,7 +1110,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     const u32x4 v = *reinterpret_cast<const u32x4*>(STG(c, q));
                     acc_sum += chunk_mix(q - 1u, v);
                     if (logidx != ~0u)
-                        *reinterpret_cast<u32x4*>(P.log_payload + ((size_t)lr * P.log_cap + logidx) * P.log_stride + 16u * (q - 1)) = v;
+                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + logidx) * P.log_stride + 16u * (q - 1), v);
                 }
             }
 
@@ -960,8 +1133,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                             acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})
                                               : chunk_mix(q - 1u, v);
                             if (q > 0 && cl.logidx != ~0u && 16u * q <= P.log_stride)
-                                *reinterpret_cast<u32x4*>(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride +
-                                                          16u * (q - 1)) = v;
+                                st_sys16(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride + 16u * (q - 1), v);
                         }
                     }
                     if (S.bm >= nbig) break;  // S.bm is rewritten only after the next barrier
@@ -1006,6 +1178,17 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (adm > nstorm) adm = nstorm;
                     S.sched_next += adm;
                 }
+                if (host) {
+                    if (S.nh) {
+                        const uint32_t fb = S.first_bad[kGroupLocal + K_HOST];
+                        uint32_t adm = fb == 0xffffffffu ? S.nh : (fb > S.hbase ? fb - S.hbase : 0u);
+                        if (adm > S.nh) adm = S.nh;
+                        S.hin_head = S.hhead + adm;
+                    }
+                    S.pk_tail += S.ev_n;
+                    S.log_count += S.ev_n;
+                    S.ev_n = 0;
+                }
                 S.iterations++;
                 if (S.progressed) {  // the clock is read on the 1st and every 64th idle iteration only
                     S.busy++;
@@ -1023,8 +1206,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     while (S.lat_next < P.lat_rounds && P.lat_origin[S.lat_next] != me) S.lat_next++;
                     done &= S.lat_next >= P.lat_rounds;
                 }
-                if (P.mode & MODE_IAR)
+                if ((P.mode & MODE_IAR) && !host)
                     done &= S.own_iter == S.own_n && S.own_state == 0 && (int64_t)S.dec_delivered == S.expect_dec;
+                if (host) done = S.quit != 0;
                 if (S.error == ERR_TIMEOUT) done = true;
                 if (peer_failed) done = true;  // another rank failed: stop everyone
                 S.done = done;

@@ -277,6 +277,13 @@ struct rlo_world {
     DevBuf<char> d_isp;
     DevBuf<rlo::LogRec> d_log;
     uint32_t lat_rounds = 0;
+    // host-service program (pinned host memory)
+    uint8_t* h_cmd = nullptr;       // [nl][cmd_cap][stride]
+    uint64_t* h_ctl = nullptr;      // [nl][kHctlWords]
+    rlo::LogRec* h_ev = nullptr;    // [nl][pk_cap]
+    uint8_t* h_evp = nullptr;       // [nl][pk_cap][max_payload]
+    uint32_t cmd_cap = 0, pk_cap = 0;
+    std::vector<uint64_t> cmd_tail, pk_head;  // host-side copies of the counters it owns
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
     size_t dyn_lds = 0;
@@ -386,6 +393,7 @@ const char* rlo_strerror(int code) {
         case RLO_E_NOPROGRAM: return "no program loaded";
         case RLO_E_NODEVICE: return "no HIP device";
         case RLO_E_NOTCONNECTED: return "part not connected";
+        case RLO_E_AGAIN: return "ring full, retry";
         default: return "unknown";
     }
 }
@@ -449,7 +457,9 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     (void)hipMemset(w->vote, 0, std::max<uint64_t>(w->L.vote_bytes[me], 1));
     (void)hipMemset(w->ctrl, 0, w->L.ctrl_words[me] * 8);
     if (w->d_stats.alloc(w->nl)) { rlo_world_destroy(w); return RLO_E_HIP; }
-    (void)hipDeviceSynchronize();
+    // the null stream only: another part's persistent kernel may already run on this device
+    // (a second engine in the process), and a device-wide sync would wait for it forever
+    (void)hipStreamSynchronize(nullptr);
     (void)hipEventCreate(&w->ev0);
     (void)hipEventCreate(&w->ev1);
     *out = w;
@@ -568,6 +578,10 @@ int rlo_world_destroy(rlo_world_t* w) {
     w->d_lat_count.release(); w->d_lat_round.release(); w->d_lat_origin.release(); w->d_prop_pid.release();
     w->d_lat_out.release(); w->d_mask.release(); w->d_prop_data.release(); w->d_log_payload.release();
     w->d_isp.release(); w->d_log.release();
+    if (w->h_cmd) (void)hipHostFree(w->h_cmd);
+    if (w->h_ctl) (void)hipHostFree(w->h_ctl);
+    if (w->h_ev) (void)hipHostFree(w->h_ev);
+    if (w->h_evp) (void)hipHostFree(w->h_evp);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
     delete w;
@@ -780,10 +794,127 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
     return RLO_OK;
 }
 
+static void host_free(rlo_world* w) {
+    if (w->h_cmd) (void)hipHostFree(w->h_cmd);
+    if (w->h_ctl) (void)hipHostFree(w->h_ctl);
+    if (w->h_ev) (void)hipHostFree(w->h_ev);
+    if (w->h_evp) (void)hipHostFree(w->h_evp);
+    w->h_cmd = nullptr; w->h_ctl = nullptr; w->h_ev = nullptr; w->h_evp = nullptr;
+}
+
+static int host_alloc(void** p, size_t bytes) {
+    // coherent (fine-grained) pinned memory: the kernel polls words the CPU writes and vice versa
+    hipError_t e = hipHostMalloc(p, std::max<size_t>(bytes, 256), hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) { g_last_hip = (int)e; *p = nullptr; return RLO_E_HIP; }
+    std::memset(*p, 0, std::max<size_t>(bytes, 256));
+    return RLO_OK;
+}
+
+int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
+    if (!w) return RLO_E_INVAL;
+    if (!w->connected) return RLO_E_NOTCONNECTED;
+    const uint32_t cc = cfg && cfg->cmd_slots ? pow2_ceil(cfg->cmd_slots) : 256u;
+    const uint32_t pc = cfg && cfg->pickup_slots ? pow2_ceil(cfg->pickup_slots) : 1024u;
+    if (pc < 64 || cc < 4 || (uint64_t)cc * w->L.stride > 0xFFFF0000ull) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
+    host_free(w);
+    w->cmd_cap = cc;
+    w->pk_cap = pc;
+    const size_t nl = (size_t)w->nl;
+    if (host_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) || host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
+        host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) || host_alloc((void**)&w->h_evp, nl * pc * w->max_payload)) {
+        host_free(w);
+        return RLO_E_HIP;
+    }
+    w->cmd_tail.assign(nl, 0);
+    w->pk_head.assign(nl, 0);
+    base_params(w);
+    rlo::Params& P = w->P;
+    P.mode = rlo::MODE_HOST | rlo::MODE_IAR;
+    P.log = w->h_ev;
+    P.log_cap = pc;
+    P.log_payload = w->h_evp;
+    P.log_stride = w->max_payload;
+    P.hin = w->h_cmd;
+    P.hin_cap = cc;
+    P.hctl = w->h_ctl;
+    const uint64_t idle = cfg ? cfg->idle_timeout_s : 0;
+    P.timeout_ticks = idle ? 100000000ull * idle : ~0ull >> 2;
+    P.deadline_ticks = ~0ull >> 2;  // serves until RLO_CMD_QUIT
+    w->have_program = true;
+    return RLO_OK;
+}
+
+int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payload, uint32_t len) {
+    if (!w || !c || !w->h_cmd || rank < w->rb || rank >= w->rb + w->nl) return RLO_E_INVAL;
+    if (len + rlo::kHdr > w->L.stride || len > 0xffffffu || (len && !payload)) return RLO_E_INVAL;
+    const int lr = rank - w->rb;
+    uint64_t* ctl = w->h_ctl + (size_t)lr * rlo::kHctlWords;
+    const uint64_t tail = w->cmd_tail[lr];
+    const uint64_t head = __atomic_load_n(&ctl[rlo::kHctlInjHead], __ATOMIC_ACQUIRE);
+    if (tail - head >= w->cmd_cap) return RLO_E_AGAIN;
+    uint8_t* slot = w->h_cmd + ((size_t)lr * w->cmd_cap + (tail & (w->cmd_cap - 1))) * w->L.stride;
+    uint32_t hdr[4];
+    hdr[0] = (uint32_t)(c->origin & 0xffff) | ((c->kind & 0xffu) << 16) | ((uint32_t)(c->vote & 0xff) << 24);
+    hdr[1] = (uint32_t)c->id;
+    hdr[2] = (len & 0xffffffu) | ((c->pseq & 0xffu) << 24);
+    hdr[3] = 0;
+    std::memcpy(slot, hdr, sizeof hdr);
+    if (len) std::memcpy(slot + rlo::kHdr, payload, len);
+    w->cmd_tail[lr] = tail + 1;
+    __atomic_store_n(&ctl[rlo::kHctlInjTail], tail + 1, __ATOMIC_RELEASE);
+    return RLO_OK;
+}
+
+int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, uint32_t cap) {
+    if (!w || !ev || !w->h_ev || rank < w->rb || rank >= w->rb + w->nl) return RLO_E_INVAL;
+    const int lr = rank - w->rb;
+    uint64_t* ctl = w->h_ctl + (size_t)lr * rlo::kHctlWords;
+    const uint64_t head = w->pk_head[lr];
+    const uint64_t tail = __atomic_load_n(&ctl[rlo::kHctlPkTail], __ATOMIC_ACQUIRE);
+    if (head == tail) return 0;
+    const uint32_t i = (uint32_t)(head & (w->pk_cap - 1));
+    std::memcpy(ev, &w->h_ev[(size_t)lr * w->pk_cap + i], sizeof *ev);
+    if (payload && cap && ev->payload_idx != 0xffffffffu) {
+        const uint32_t n = std::min(std::min(ev->len, cap), w->max_payload);
+        std::memcpy(payload, w->h_evp + ((size_t)lr * w->pk_cap + i) * w->max_payload, n);
+    }
+    w->pk_head[lr] = head + 1;
+    __atomic_store_n(&ctl[rlo::kHctlPkHead], head + 1, __ATOMIC_RELEASE);
+    return 1;
+}
+
+int rlo_host_cmd_count(rlo_world_t* w, int rank, uint64_t* consumed, uint64_t* posted) {
+    if (!w || !w->h_ctl || rank < w->rb || rank >= w->rb + w->nl) return RLO_E_INVAL;
+    const int lr = rank - w->rb;
+    if (consumed) *consumed = __atomic_load_n(&w->h_ctl[(size_t)lr * rlo::kHctlWords + rlo::kHctlInjHead], __ATOMIC_ACQUIRE);
+    if (posted) *posted = w->cmd_tail[lr];
+    return RLO_OK;
+}
+
+int rlo_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rlo_host_running(rlo_world_t* w) {
+    if (!w) return RLO_E_INVAL;
+    hipError_t e = hipEventQuery(w->ev1);
+    if (e == hipErrorNotReady) return 1;
+    if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
+    return 0;
+}
+
 int rlo_reset(rlo_world_t* w, void* stream) {
     if (!w) return RLO_E_INVAL;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(w->device));
+    if (w->have_program && (w->P.mode & rlo::MODE_HOST)) {  // the kernel is not running: rings restart at 0
+        std::memset(w->h_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
+        std::fill(w->cmd_tail.begin(), w->cmd_tail.end(), 0);
+        std::fill(w->pk_head.begin(), w->pk_head.end(), 0);
+    }
     HIPCHK(hipMemsetAsync(w->ctrl, 0, w->L.ctrl_words[w->part] * 8, s));
     HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->nl, s));
     if (w->have_program && (w->P.mode & rlo::MODE_LAT)) {

@@ -1,0 +1,704 @@
+// rootless_ops.cpp -- the drop-in rootless_ops.h API (librootless_ops.so) over the device
+// engine's host-service program (rlo_hip.h).
+//
+// One engine = one rank of a device world whose parts are the ranks of the engine's
+// communicator (one part per process).  RLO_progress_engine_new builds the part on this
+// process' GPU, exchanges the ring mappings with MPI_Allgather and launches the rank's
+// persistent progress kernel.  From then on the kernel forwards, merges votes and
+// broadcasts decisions by itself; this library only
+//   * posts originations (RLO_bcast_gen, RLO_submit_proposal) and judge verdicts into the
+//     rank's command ring, and
+//   * drains the rank's pickup ring in RLO_make_progress_all: deliveries become
+//     RLO_user_msg pickups, judge / action callbacks run on this thread
+//     (rootless_ops.c:698, :773, :842), own results update my_own_proposal.
+// Everything here is the reference's host-visible state machine; nothing on the data path
+// runs on the CPU.
+#include "rootless_ops.h"
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <ctime>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <utility>
+#include <vector>
+
+#include "rlo_hip.h"
+
+int total_pickup = 0;  // rootless_ops.h:46
+
+struct RLO_msg_generic {  // first member = the user view, so RLO_user_msg* and RLO_msg_t* convert
+    RLO_user_msg msg_usr;
+    int send_len;         // bytes given to RLO_msg_new_bc
+    int source;           // tree parent (MPI_SOURCE in the reference), -1 for local messages
+    uint64_t seq;         // command sequence number once posted
+    int posted;           // 1: in the command ring (or backlog), 2: consumed by the device
+    int pickup_done, fwd_done;
+    size_t dirty;         // bytes of buf written since the last clear (pool reuse)
+};
+
+struct Proposal_state {  // rootless_ops.c:184-194
+    RLO_ID pid;
+    int recv_proposal_from;
+    RLO_Vote vote;
+    int votes_needed, votes_recved;
+    RLO_Req_stat state;
+    RLO_msg_t* proposal_msg;
+    RLO_msg_t* decision_msg;
+};
+
+namespace {
+
+struct Cmd {  // a command waiting for room in the command ring
+    rlo_cmd_t c;
+    std::vector<uint8_t> payload;
+    RLO_msg_t* msg;
+};
+
+}  // namespace
+
+struct progress_engine {
+    MPI_Comm comm = MPI_COMM_NULL;
+    int rank = 0, size = 0, id = 0, device = 0;
+    rlo_world_t* w = nullptr;
+    void* stream = nullptr;
+    iar_cb_func_t judge = nullptr, action = nullptr;
+    void* ctx = nullptr;
+    uint32_t slot_bytes = 0;      // device payload capacity
+    uint32_t deliver_max = 0;     // bytes a receiver sees (reference: msg_size_max - 4, :1588)
+    int send_list_len = 0;
+    std::deque<RLO_msg_t*> pickup;   // queue_pickup (:938)
+    std::deque<Cmd> backlog;         // commands the ring had no room for yet
+    std::deque<RLO_msg_t*> wait;     // my bcasts until the device took them (queue_wait, :1594)
+    uint64_t bcast_seq = 0;
+    RLO_proposal_state own{};        // my_own_proposal (:241)
+    std::map<std::pair<int, int>, std::vector<char>> approved;  // (origin, pid) -> PBuf (queue_iar_pending)
+    long sent_bcast = 0, recved_bcast = 0;  // :1600, :586
+    bool failed = false;
+    uint32_t poll_tick = 0;
+    std::vector<uint8_t> evbuf;
+    progress_engine* next = nullptr;
+};
+
+namespace {
+
+progress_engine* g_engines = nullptr;  // Active_Engines (:40)
+int g_engines_ever = 0;
+std::vector<RLO_msg_t*> g_pool;         // recycled received messages
+
+void proposal_init(RLO_proposal_state* ps) {  // proposal_state_init :1235-1248
+    ps->pid = -1;
+    ps->recv_proposal_from = -1;
+    ps->vote = 1;
+    ps->votes_needed = -1;
+    ps->votes_recved = 0;
+    ps->state = RLO_INVALID;
+    ps->proposal_msg = nullptr;
+    ps->decision_msg = nullptr;
+}
+
+RLO_msg_t* msg_alloc(int origin) {
+    RLO_msg_t* m;
+    if (!g_pool.empty()) {
+        m = g_pool.back();
+        g_pool.pop_back();
+        std::memset(m->msg_usr.buf, 0, m->dirty);  // the data area reads as calloc'd (:290)
+    } else {
+        m = (RLO_msg_t*)std::calloc(1, sizeof(RLO_msg_t));
+        if (!m) return nullptr;
+    }
+    m->msg_usr.type = -1;  // RLO_msg_new_generic :292-294
+    m->msg_usr.pid = -1;
+    m->msg_usr.vote = -1;
+    m->msg_usr.data_len = 0;
+    m->msg_usr.data = m->msg_usr.buf + sizeof(int);
+    std::memcpy(m->msg_usr.buf, &origin, sizeof(int));
+    m->send_len = 0;
+    m->source = -1;
+    m->seq = 0;
+    m->posted = 0;
+    m->pickup_done = 0;
+    m->fwd_done = 0;
+    m->dirty = sizeof(int);
+    return m;
+}
+
+void msg_release(RLO_msg_t* m) {
+    if (!m) return;
+    if (g_pool.size() < 256) g_pool.push_back(m);
+    else std::free(m);
+}
+
+// PBuf [pid i32][vote i32][data_len u64][data] (pbuf_serialize :1369-1396)
+size_t pbuf_put(char* out, RLO_ID pid, RLO_Vote vote, uint64_t len, const void* data) {
+    std::memcpy(out, &pid, 4);
+    std::memcpy(out + 4, &vote, 4);
+    std::memcpy(out + 8, &len, 8);
+    if (len) std::memcpy(out + 16, data, len);
+    return 16 + len;
+}
+
+int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t len, RLO_msg_t* msg) {
+    if (e->backlog.empty()) {
+        int rc = rlo_host_post(e->w, e->rank, &c, payload, len);
+        if (rc == RLO_OK) {
+            if (msg) {
+                uint64_t posted = 0;
+                rlo_host_cmd_count(e->w, e->rank, nullptr, &posted);
+                msg->seq = posted;  // consumed once the device head reaches it
+                msg->posted = 1;
+            }
+            return 0;
+        }
+        if (rc != RLO_E_AGAIN) {
+            std::fprintf(stderr, "rlo: rank %d: command post failed: %s\n", e->rank, rlo_strerror(rc));
+            return -1;
+        }
+    }
+    Cmd q;
+    q.c = c;
+    q.payload.assign((const uint8_t*)payload, (const uint8_t*)payload + len);
+    q.msg = msg;
+    if (msg) msg->posted = 1;
+    e->backlog.push_back(std::move(q));
+    return 0;
+}
+
+void flush_backlog(progress_engine* e) {
+    while (!e->backlog.empty()) {
+        Cmd& q = e->backlog.front();
+        int rc = rlo_host_post(e->w, e->rank, &q.c, q.payload.data(), (uint32_t)q.payload.size());
+        if (rc == RLO_E_AGAIN) return;
+        if (rc != RLO_OK) {
+            std::fprintf(stderr, "rlo: rank %d: command post failed: %s\n", e->rank, rlo_strerror(rc));
+            e->failed = true;
+            return;
+        }
+        if (q.msg) {
+            uint64_t posted = 0;
+            rlo_host_cmd_count(e->w, e->rank, nullptr, &posted);
+            q.msg->seq = posted;
+        }
+        e->backlog.pop_front();
+    }
+}
+
+// frees my sent bcasts once the device has taken them (_wait_only_queue_cleanup :1015-1034)
+void reap_sent(progress_engine* e) {
+    if (e->wait.empty()) return;
+    uint64_t consumed = 0;
+    rlo_host_cmd_count(e->w, e->rank, &consumed, nullptr);
+    while (!e->wait.empty()) {
+        RLO_msg_t* m = e->wait.front();
+        if (m->seq == 0 || m->seq > consumed) break;
+        e->wait.pop_front();
+        m->posted = 2;
+        m->fwd_done = 1;
+        std::free(m);
+    }
+}
+
+void check_alive(progress_engine* e) {
+    if (e->failed) return;
+    if (rlo_host_running(e->w) == 1) return;
+    int rc = rlo_wait(e->w);
+    rlo_rank_stats_t st;
+    std::memset(&st, 0, sizeof st);
+    rlo_stats(e->w, &st, 1);
+    std::fprintf(stderr, "rlo: rank %d engine %d: progress kernel stopped (%s, device error %u aux %u)\n", e->rank, e->id,
+                 rlo_strerror(rc), st.error, st.error_aux);
+    e->failed = true;
+}
+
+void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* payload) {
+    switch (ev.kind) {
+        case RLO_EV_DELIVER_BCAST: {  // :583-589 -> pickup
+            RLO_msg_t* m = msg_alloc(ev.origin);
+            if (!m) return;
+            const uint32_t n = ev.len < e->deliver_max ? ev.len : e->deliver_max;
+            std::memcpy(m->msg_usr.buf + sizeof(int), payload, n);
+            m->dirty = sizeof(int) + n;
+            m->msg_usr.type = RLO_BCAST;
+            m->source = ev.from;
+            m->fwd_done = 1;  // forwarded by the device before this event was written
+            e->recved_bcast++;
+            e->pickup.push_back(m);
+            break;
+        }
+        case RLO_EV_DELIVER_DECISION: {  // _iar_decision_handler :814-859 + _user_msg_mock :920-932
+            e->approved.erase(std::make_pair(ev.origin, (int)ev.id));  // declined: proposal dropped (:833-837)
+            RLO_msg_t* m = msg_alloc(ev.origin);
+            if (!m) return;
+            char* d = m->msg_usr.buf + sizeof(int);
+            m->dirty = sizeof(int) + pbuf_put(d, (RLO_ID)ev.id, ev.vote, 7, "IAR_DEC");
+            m->msg_usr.type = RLO_IAR_DECISION;
+            m->msg_usr.pid = (RLO_ID)ev.id;
+            m->msg_usr.vote = ev.vote;
+            m->msg_usr.data_len = 7;
+            m->msg_usr.data = d + 16;
+            m->source = ev.from;
+            m->fwd_done = 1;
+            e->recved_bcast++;
+            e->pickup.push_back(m);
+            break;
+        }
+        case RLO_EV_ACTION: {  // decision 1 for a proposal I approved: action(PBuf) (:842)
+            auto it = e->approved.find(std::make_pair(ev.origin, (int)ev.id));
+            if (it != e->approved.end()) {
+                if (e->action) e->action(it->second.data(), e->ctx);
+                e->approved.erase(it);
+            }
+            break;
+        }
+        case RLO_EV_RESULT: {  // my decision went out (:560-563 + _iar_decision_bcast :908-917)
+            e->own.vote = ev.vote;
+            e->own.votes_recved = e->own.votes_needed;
+            e->own.state = RLO_COMPLETED;
+            e->sent_bcast++;  // a decision counts as a sent bcast (:1600)
+            break;
+        }
+        case RLO_EV_JUDGE: {  // judge(proposal data, ctx) (:698); data is zero-padded like the
+                              // reference's calloc'd receive buffer
+            std::vector<char> pb(RLO_MSG_SIZE_MAX + 16, 0);
+            const uint32_t n = ev.len < (uint32_t)RLO_MSG_SIZE_MAX ? ev.len : (uint32_t)RLO_MSG_SIZE_MAX;
+            std::memcpy(pb.data(), payload, n);
+            int v = e->judge ? e->judge(pb.data() + 16, e->ctx) : 1;
+            if (v != 0 && v != 1) {
+                std::printf("%s:%u - rank = %03d: unknown judgment received: %d\n", __func__, __LINE__, e->rank, v);
+                v = 0;
+            }
+            if (v == 1) e->approved[std::make_pair(ev.origin, (int)ev.id)] = std::move(pb);
+            rlo_cmd_t c;
+            std::memset(&c, 0, sizeof c);
+            c.kind = RLO_CMD_JUDGE;
+            c.origin = ev.origin;
+            c.id = (int32_t)ev.id;
+            c.pseq = ev.aux;
+            c.vote = v;
+            post(e, c, nullptr, 0, nullptr);
+            break;
+        }
+        case RLO_EV_OWN_JUDGE: {  // every vote was 1: vote = judge(my_proposal = NULL, ctx) (:770-775)
+            int v = e->judge ? e->judge(nullptr, e->ctx) : 1;
+            if (v != 0 && v != 1) v = 0;
+            rlo_cmd_t c;
+            std::memset(&c, 0, sizeof c);
+            c.kind = RLO_CMD_OWN_JUDGE;
+            c.id = (int32_t)ev.id;
+            c.vote = v;
+            post(e, c, nullptr, 0, nullptr);
+            break;
+        }
+        default:
+            std::fprintf(stderr, "rlo: rank %d: unexpected event kind %u\n", e->rank, ev.kind);
+            break;
+    }
+}
+
+// make_progress_gen (:551-641): everything the device finished since the last call
+void progress(progress_engine* e) {
+    if (!e->w || e->failed) return;
+    flush_backlog(e);
+    rlo_log_rec_t ev;
+    int got = 0;
+    for (int i = 0; i < 4096; i++) {
+        int r = rlo_host_poll(e->w, e->rank, &ev, e->evbuf.data(), (uint32_t)e->evbuf.size());
+        if (r != 1) break;
+        handle_event(e, ev, e->evbuf.data());
+        got++;
+    }
+    flush_backlog(e);
+    reap_sent(e);
+    if (!got && (++e->poll_tick & 255u) == 0) check_alive(e);
+}
+
+std::vector<std::pair<rlo_world_t*, void*>> g_grave;  // stopped engines' worlds / streams
+
+void bury() {
+    for (auto& g : g_grave) {
+        rlo_world_destroy(g.first);
+        rlo_stream_destroy(g.second);
+    }
+    g_grave.clear();
+}
+
+// The reference never frees the engine's dup'd communicator (:1461, :1524-1527) and its tests
+// use it after RLO_progress_engine_cleanup.  Keep it alive until MPI_Finalize, which deletes
+// MPI_COMM_SELF's attributes first (MPI standard, "Allowing User Functions at Process
+// Termination") -- there the retired communicators are freed.
+std::vector<MPI_Comm> g_retired;
+int g_retire_key = MPI_KEYVAL_INVALID;
+
+int free_retired(MPI_Comm, int, void*, void*) {
+    bury();
+    for (MPI_Comm& c : g_retired) MPI_Comm_free(&c);
+    g_retired.clear();
+    return MPI_SUCCESS;
+}
+
+void retire_comm(MPI_Comm c) {
+    if (g_retire_key == MPI_KEYVAL_INVALID) {
+        MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, free_retired, &g_retire_key, nullptr);
+        MPI_Comm_set_attr(MPI_COMM_SELF, g_retire_key, nullptr);
+    }
+    g_retired.push_back(c);
+}
+
+int choose_device(MPI_Comm comm, int ndev) {
+    if (const char* s = std::getenv("RLO_DEVICE")) return std::atoi(s) % ndev;
+    MPI_Comm node;
+    MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+    int lr = 0;
+    MPI_Comm_rank(node, &lr);
+    MPI_Comm_free(&node);
+    return lr % ndev;
+}
+
+}  // namespace
+
+extern "C" {
+
+RLO_user_msg* RLO_user_msg_new(RLO_msg_t* gen_msg_in) { return gen_msg_in ? &gen_msg_in->msg_usr : nullptr; }
+
+RLO_msg_t* RLO_msg_new_generic(RLO_engine_t* eng) {
+    assert(eng);
+    RLO_msg_t* m = (RLO_msg_t*)std::calloc(1, sizeof(RLO_msg_t));
+    if (!m) return nullptr;
+    m->msg_usr.type = -1;
+    m->msg_usr.pid = -1;
+    m->msg_usr.vote = -1;
+    m->msg_usr.data = m->msg_usr.buf + sizeof(int);
+    std::memcpy(m->msg_usr.buf, &eng->rank, sizeof(int));
+    m->source = -1;
+    m->dirty = sizeof(m->msg_usr.buf);
+    return m;
+}
+
+RLO_msg_t* RLO_msg_new_bc(RLO_engine_t* eng, void* buf_in, int send_size) {
+    RLO_msg_t* m = RLO_msg_new_generic(eng);
+    if (!m) return nullptr;
+    if (send_size < 0) send_size = 0;
+    if (send_size > RLO_MSG_SIZE_MAX) send_size = RLO_MSG_SIZE_MAX;  // the data area (:295)
+    if (send_size) std::memcpy(m->msg_usr.buf + sizeof(int), buf_in, (size_t)send_size);
+    m->send_len = send_size;
+    return m;
+}
+
+int RLO_msg_free(RLO_msg_t* msg_in) {
+    std::free(msg_in);
+    return 0;
+}
+
+int RLO_msg_test_isends(RLO_engine_t* eng, RLO_msg_t* msg_in) {
+    assert(eng && msg_in);
+    if (msg_in->posted == 2) return 1;
+    if (msg_in->posted == 0 || msg_in->seq == 0) return msg_in->posted == 0;  // never sent: nothing pending
+    uint64_t consumed = 0;
+    rlo_host_cmd_count(eng->w, eng->rank, &consumed, nullptr);
+    return consumed >= msg_in->seq;
+}
+
+RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb_func, void* app_ctx,
+                                      void* app_proposal_action) {
+    progress_engine* e = new progress_engine();
+    MPI_Comm_dup(mpi_comm, &e->comm);  // bcomm_init :1461
+    MPI_Comm_rank(e->comm, &e->rank);
+    MPI_Comm_size(e->comm, &e->size);
+    e->judge = (iar_cb_func_t)approv_cb_func;
+    e->action = (iar_cb_func_t)app_proposal_action;
+    e->ctx = app_ctx;
+    if (e->size < 2) {  // bcomm_init returns NULL for N < 2 (:1464-1467)
+        std::fprintf(stderr, "rlo: a rootless engine needs at least 2 ranks\n");
+        MPI_Comm_free(&e->comm);
+        delete e;
+        return nullptr;
+    }
+    size_t cap = msg_size_max ? msg_size_max : RLO_MSG_SIZE_MAX;
+    if (cap > RLO_MSG_SIZE_MAX) cap = RLO_MSG_SIZE_MAX;
+    if (cap < 64) cap = 64;
+    e->slot_bytes = (uint32_t)((cap + 15) & ~(size_t)15);
+    e->deliver_max = (uint32_t)cap - (uint32_t)sizeof(int);  // bytes [0, msg_size_max - 4) arrive (:1588)
+    e->evbuf.assign(e->slot_bytes + 16, 0);
+    int level = 0, lw = 0, scc = 0, sl[16];
+    rlo_topology(e->size, e->rank, &level, &lw, &scc, &e->send_list_len, sl);
+    proposal_init(&e->own);
+
+    // one part per rank: this process' GPU (node-local rank modulo the visible devices)
+    const int ndev = rlo_device_count();
+    int ok = ndev > 0;
+    int node_size = 0;
+    {
+        MPI_Comm node;
+        MPI_Comm_split_type(e->comm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+        MPI_Comm_size(node, &node_size);
+        MPI_Comm_free(&node);
+    }
+    if (node_size != e->size) {
+        if (e->rank == 0) std::fprintf(stderr, "rlo: the communicator must stay inside one node (hipIpc mappings)\n");
+        ok = 0;
+    }
+    int all_ok = 0;
+    MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, e->comm);
+    if (!all_ok) {
+        if (ndev <= 0) std::fprintf(stderr, "rlo: rank %d: no HIP device\n", e->rank);
+        MPI_Comm_free(&e->comm);
+        delete e;
+        return nullptr;
+    }
+    e->device = choose_device(e->comm, ndev);
+    std::vector<int> devs(e->size);
+    MPI_Allgather(&e->device, 1, MPI_INT, devs.data(), 1, MPI_INT, e->comm);
+    bool multi = false;
+    for (int d : devs) multi |= d != devs[0];
+
+    rlo_part_cfg_t pc;
+    std::memset(&pc, 0, sizeof pc);
+    pc.n_ranks = e->size;
+    pc.n_parts = e->size;
+    pc.part = e->rank;
+    pc.part_begin = nullptr;
+    pc.max_payload = e->slot_bytes;
+    pc.ring_slots = e->slot_bytes > 4096 ? 128u : 0u;
+    pc.device = e->device;
+    pc.flags = multi ? RLO_PART_UNCACHED : 0u;
+    int rc = rlo_part_create(&pc, &e->w);
+    std::vector<uint8_t> blob(RLO_PART_BLOB_BYTES, 0), blobs((size_t)RLO_PART_BLOB_BYTES * e->size, 0);
+    if (rc == RLO_OK && rlo_part_export(e->w, blob.data(), RLO_PART_BLOB_BYTES) < 0) rc = RLO_E_HIP;
+    int lok = rc == RLO_OK, gok = 0;
+    MPI_Allreduce(&lok, &gok, 1, MPI_INT, MPI_MIN, e->comm);
+    if (gok) {
+        MPI_Allgather(blob.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, blobs.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, e->comm);
+        rc = rlo_part_connect(e->w, blobs.data(), e->size);
+        if (rc == RLO_OK) {
+            rlo_host_cfg_t hc;
+            std::memset(&hc, 0, sizeof hc);
+            rc = rlo_program_host(e->w, &hc);
+        }
+        if (rc == RLO_OK) rc = rlo_stream_create(e->device, &e->stream);
+        if (rc == RLO_OK) rc = rlo_reset(e->w, e->stream);
+        lok = rc == RLO_OK;
+        MPI_Allreduce(&lok, &gok, 1, MPI_INT, MPI_MIN, e->comm);  // every part reset before any launch
+        if (gok) {
+            rc = rlo_launch_ex(e->w, e->stream, RLO_LAUNCH_NO_RESET);
+            lok = rc == RLO_OK;
+            MPI_Allreduce(&lok, &gok, 1, MPI_INT, MPI_MIN, e->comm);
+        }
+    }
+    if (!gok) {
+        std::fprintf(stderr, "rlo: rank %d: engine setup failed (%s, hip %d)\n", e->rank, rlo_strerror(rc),
+                     rlo_last_hip_error());
+        if (e->w && rlo_host_running(e->w) == 1) {
+            rlo_cmd_t q;
+            std::memset(&q, 0, sizeof q);
+            q.kind = RLO_CMD_QUIT;
+            rlo_host_post(e->w, e->rank, &q, nullptr, 0);
+            rlo_wait(e->w);
+        }
+        MPI_Barrier(e->comm);
+        if (e->w) rlo_world_destroy(e->w);
+        if (e->stream) rlo_stream_destroy(e->stream);
+        MPI_Comm_free(&e->comm);
+        delete e;
+        return nullptr;
+    }
+    e->id = ++g_engines_ever;  // engine ids 1, 2, ... (:515-517)
+    progress_engine** tail = &g_engines;
+    while (*tail) tail = &(*tail)->next;
+    *tail = e;
+    return e;
+}
+
+int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
+    assert(eng);
+    // collective quiescence (:1607-1627): every bcast and decision sent anywhere has arrived here
+    int sent = (int)eng->sent_bcast, total = 0, done = 0;
+    MPI_Request req;
+    MPI_Iallreduce(&sent, &total, 1, MPI_INT, MPI_SUM, eng->comm, &req);
+    do {
+        MPI_Test(&req, &done, MPI_STATUS_IGNORE);
+        if (!done) RLO_make_progress_all();
+    } while (!done);
+    while (!eng->failed && eng->recved_bcast + eng->sent_bcast < total) RLO_make_progress_all();
+    RLO_user_msg* u = nullptr;
+    while (RLO_user_pickup_next(eng, &u)) {  // :1628-1631
+        total_pickup++;
+        RLO_user_msg_recycle(eng, u);
+    }
+    // every rank quiescent -> stop the kernels -> nobody stores into anyone's rings any more
+    MPI_Ibarrier(eng->comm, &req);
+    done = 0;
+    do {
+        MPI_Test(&req, &done, MPI_STATUS_IGNORE);
+        if (!done) RLO_make_progress_all();
+    } while (!done);
+    rlo_cmd_t q;
+    std::memset(&q, 0, sizeof q);
+    q.kind = RLO_CMD_QUIT;
+    while (!eng->failed && rlo_host_running(eng->w) == 1) {
+        flush_backlog(eng);
+        if (eng->backlog.empty() && rlo_host_post(eng->w, eng->rank, &q, nullptr, 0) == RLO_OK) break;
+        rlo_log_rec_t ev;  // keep the pickup ring moving while the quit waits for room
+        while (rlo_host_poll(eng->w, eng->rank, &ev, eng->evbuf.data(), (uint32_t)eng->evbuf.size()) == 1) {}
+    }
+    int rc = rlo_wait(eng->w);
+    if (rc != RLO_OK && !eng->failed)
+        std::fprintf(stderr, "rlo: rank %d engine %d: kernel ended with %s\n", eng->rank, eng->id, rlo_strerror(rc));
+    MPI_Barrier(eng->comm);
+    for (RLO_msg_t* m : eng->pickup) msg_release(m);
+    for (RLO_msg_t* m : eng->wait) std::free(m);
+    retire_comm(eng->comm);  // callers keep using RLO_get_my_comm's comm after cleanup (testcases.c:329-331)
+    progress_engine** p = &g_engines;  // engine_remove (:445-466)
+    while (*p && *p != eng) p = &(*p)->next;
+    if (*p) *p = eng->next;
+    // hipFree / hipIpcCloseMemHandle may wait for the whole device, i.e. for the persistent
+    // kernel of another engine of this process: free the world once no engine kernel runs
+    g_grave.push_back(std::make_pair(eng->w, eng->stream));
+    if (!g_engines) bury();
+    delete eng;
+    return 0;
+}
+
+int RLO_make_progress_all(void) {
+    if (!g_engines) return -1;  // :540-543
+    for (progress_engine* e = g_engines; e; e = e->next) progress(e);
+    return 0;
+}
+
+int RLO_get_engine_id(RLO_engine_t* eng) {
+    assert(eng);
+    return eng->id;
+}
+
+MPI_Comm RLO_get_my_comm(RLO_engine_t* eng) {
+    assert(eng);
+    return eng->comm;
+}
+
+int RLO_bcast_gen(RLO_engine_t* eng, RLO_msg_t* msg_in, enum RLO_COMM_TAGS tag) {
+    assert(eng && msg_in);
+    if (tag != RLO_BCAST) {  // proposals / decisions are originated by the engine itself
+        std::fprintf(stderr, "rlo: RLO_bcast_gen: only RLO_BCAST is originated by callers (tag %d)\n", (int)tag);
+        return -1;
+    }
+    const uint32_t n = (uint32_t)msg_in->send_len < eng->deliver_max ? (uint32_t)msg_in->send_len : eng->deliver_max;
+    msg_in->pickup_done = 1;  // :1584
+    rlo_cmd_t c;
+    std::memset(&c, 0, sizeof c);
+    c.kind = RLO_CMD_BCAST;
+    c.id = (int32_t)++eng->bcast_seq;
+    if (post(eng, c, msg_in->msg_usr.buf + sizeof(int), n, msg_in)) return -1;
+    eng->wait.push_back(msg_in);
+    eng->sent_bcast++;
+    RLO_make_progress_all();  // :1602
+    return 0;
+}
+
+int RLO_user_pickup_next(RLO_engine_t* eng, RLO_user_msg** msg_out) {
+    assert(eng);
+    if (eng->pickup.empty()) return 0;
+    RLO_msg_t* m = eng->pickup.front();
+    eng->pickup.pop_front();
+    *msg_out = &m->msg_usr;
+    return 1;
+}
+
+int RLO_user_msg_recycle(RLO_engine_t* eng, RLO_user_msg* msg_in) {
+    assert(eng && msg_in);
+    RLO_msg_t* m = (RLO_msg_t*)msg_in;
+    m->pickup_done = 1;
+    if (m->fwd_done) {  // always: the device forwarded before the pickup event existed
+        msg_release(m);
+        return 1;
+    }
+    return 0;
+}
+
+int RLO_submit_proposal(RLO_engine_t* eng, char* proposal, size_t prop_size, RLO_ID my_proposal_id) {
+    assert(eng);
+    eng->own.pid = my_proposal_id;  // :878-883
+    eng->own.proposal_msg = nullptr;
+    eng->own.vote = 1;
+    eng->own.votes_needed = eng->send_list_len;
+    eng->own.votes_recved = 0;
+    eng->own.decision_msg = nullptr;
+    if (prop_size == 0 && proposal != nullptr) {  // pbuf_serialize rejects it (:1372-1375)
+        std::printf("pbuf_serialize failed.\n");
+        return -1;
+    }
+    if (16 + prop_size > eng->deliver_max) {
+        std::fprintf(stderr, "rlo: proposal of %zu bytes exceeds the engine's message size\n", prop_size);
+        return -1;
+    }
+    std::vector<char> pb(16 + prop_size);
+    pbuf_put(pb.data(), my_proposal_id, 1, prop_size, proposal);
+    eng->own.state = RLO_IN_PROGRESS;
+    rlo_cmd_t c;
+    std::memset(&c, 0, sizeof c);
+    c.kind = RLO_CMD_PROPOSAL;
+    c.id = my_proposal_id;
+    c.vote = 1;
+    if (post(eng, c, pb.data(), (uint32_t)pb.size(), nullptr)) return -1;
+    RLO_make_progress_all();
+    return eng->own.state == RLO_COMPLETED ? eng->own.vote : -1;
+}
+
+int RLO_check_proposal_state(RLO_engine_t* eng, int pid) {
+    (void)pid;  // ignored, as in the reference (:869-872)
+    RLO_make_progress_all();
+    return eng->own.state;
+}
+
+int RLO_get_vote_my_proposal(RLO_engine_t* eng) {
+    if (eng->own.state != RLO_COMPLETED) return -1;
+    int ret = eng->own.vote;
+    RLO_proposal_reset(&eng->own);
+    return ret;
+}
+
+int RLO_proposal_reset(RLO_proposal_state* ps) {  // :1649-1664
+    assert(ps);
+    if (ps->decision_msg) RLO_msg_free(ps->decision_msg);
+    ps->decision_msg = nullptr;
+    if (ps->proposal_msg) RLO_msg_free(ps->proposal_msg);
+    ps->proposal_msg = nullptr;
+    ps->pid = -1;
+    ps->recv_proposal_from = -1;
+    ps->state = RLO_INVALID;
+    ps->vote = -1;
+    ps->votes_needed = 0;
+    ps->votes_recved = 0;
+    return 0;
+}
+
+unsigned long RLO_get_time_usec(void) {
+    struct timeval tv;
+    gettimeofday(&tv, nullptr);
+    return 1000000ul * (unsigned long)tv.tv_sec + (unsigned long)tv.tv_usec;
+}
+
+void RLO_get_time_str(char* str_out) {
+    time_t raw;
+    time(&raw);
+    struct tm* t = localtime(&raw);
+    std::sprintf(str_out, "%d:%d:%d", t->tm_hour, t->tm_min, t->tm_sec);
+}
+
+int RLO_get_my_rank(void) {  // MPI_COMM_WORLD, as in the reference (:148-152)
+    int r = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &r);
+    return r;
+}
+
+int RLO_get_world_size(void) {
+    int n = -1;
+    MPI_Comm_size(MPI_COMM_WORLD, &n);
+    return n;
+}
+
+int RLO_user_msg_source(const RLO_user_msg* msg) { return msg ? ((const RLO_msg_t*)msg)->source : -1; }
+
+int RLO_engine_device(RLO_engine_t* eng) { return eng ? eng->device : -1; }
+
+}  // extern "C"

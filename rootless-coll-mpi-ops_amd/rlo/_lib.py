@@ -13,12 +13,17 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
 RLO_OK = 0
 RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6
 RLO_E_NOTCONNECTED = -7
+RLO_E_AGAIN = -8
 RLO_PART_BLOB_BYTES = 512
 RLO_PART_UNCACHED = 1
 RLO_LAUNCH_NO_RESET = 1
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
-DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot"}
+DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot", 7: "host command"}
+# host-service program (rlo_hip.h)
+RLO_CMD_BCAST, RLO_CMD_PROPOSAL, RLO_CMD_JUDGE, RLO_CMD_OWN_JUDGE, RLO_CMD_QUIT = 0, 2, 16, 17, 18
+RLO_EV_DELIVER_BCAST, RLO_EV_DELIVER_DECISION = 1, 1 | (4 << 8)
+RLO_EV_ACTION, RLO_EV_RESULT, RLO_EV_JUDGE, RLO_EV_OWN_JUDGE = 3, 4, 6, 7
 
 
 class WorldCfg(ctypes.Structure):
@@ -53,6 +58,16 @@ class IarCfg(ctypes.Structure):
                 ("log_cap", ctypes.c_uint32)]
 
 
+class HostCfg(ctypes.Structure):
+    _fields_ = [("cmd_slots", ctypes.c_uint32), ("pickup_slots", ctypes.c_uint32), ("idle_timeout_s", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+class Cmd(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("origin", ctypes.c_int32), ("id", ctypes.c_int32), ("pseq", ctypes.c_uint32),
+                ("vote", ctypes.c_int32), ("pad", ctypes.c_uint32)]
+
+
 class RankStats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint64) for f in (
         "bcast_delivered", "bcast_sum", "originated", "dec_delivered", "dec_approved", "actions", "judge_calls",
@@ -72,7 +87,9 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_part_create", "rlo_part_export", "rlo_part_connect", "rlo_reset", "rlo_launch_ex",
            "rlo_stream_create", "rlo_stream_destroy",
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
-           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_strerror", "rlo_last_hip_error"]
+           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_strerror", "rlo_last_hip_error",
+           "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
+           "rlo_device_count"]
 
 _lib = None
 
@@ -108,6 +125,12 @@ def load():
     L.rlo_stats.argtypes = [vp, ctypes.POINTER(RankStats), ctypes.c_int]
     L.rlo_log.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), ctypes.c_uint32, vp, ctypes.c_uint32]
     L.rlo_latencies.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    L.rlo_program_host.argtypes = [vp, ctypes.POINTER(HostCfg)]
+    L.rlo_host_post.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Cmd), vp, ctypes.c_uint32]
+    L.rlo_host_poll.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp, ctypes.c_uint32]
+    L.rlo_host_running.argtypes = [vp]
+    L.rlo_host_cmd_count.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.rlo_device_count.argtypes = []
     L.rlo_strerror.argtypes = [ctypes.c_int]
     L.rlo_strerror.restype = ctypes.c_char_p
     _lib = L

@@ -17,6 +17,9 @@ import subprocess
 import sys
 import tempfile
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import capture  # noqa: E402
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
@@ -24,12 +27,7 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
 def run(n, *args, timeout=600):
-    with tempfile.TemporaryDirectory() as td:
-        out = os.path.join(td, "out.jsonl")
-        cmd = [MPIEXEC, "-n", str(n), HARNESS, out] + [str(a) for a in args]
-        subprocess.run(cmd, check=True, timeout=timeout, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=td)
-        with open(out) as f:
-            return [json.loads(line) for line in f if line.strip()]
+    return capture.run(HARNESS, n, *args, timeout=timeout)
 
 
 def dump(name, obj):
@@ -52,30 +50,14 @@ def gen_topo(nmax=1024):
 def gen_parents(ns, length=64):
     out = {}
     for n in ns:
-        recs = run(n, "parents", length, timeout=3600)
-        parent = [[-1] * n for _ in range(n)]
-        hashes = [None] * n
-        for r in recs:
-            assert r["type"] == 0 and r["hdr_origin"] == r["origin"] and r["pid"] == -1 and r["vote"] == -1 and r["data_len"] == 0
-            assert parent[r["origin"]][r["rank"]] == -1, "duplicate delivery"
-            parent[r["origin"]][r["rank"]] = r["parent"]
-            assert hashes[r["origin"]] in (None, r["hash"])
-            hashes[r["origin"]] = r["hash"]
-        assert len(recs) == n * (n - 1)
-        out[str(n)] = {"parent": parent, "hash": hashes}
+        out[str(n)] = capture.parents(run(n, "parents", length, timeout=3600), n)
     return out
 
 
 def gen_stream(cases):
     out = []
     for n, seed, k, length in cases:
-        recs = run(n, "stream", seed, k, length)
-        per = [[] for _ in range(n)]
-        for r in recs:
-            assert r["type"] == 0
-            per[r["rank"]].append([r["bid"], r["origin"], r["parent"], r["hash"]])
-        for p in per:
-            p.sort()
+        per = capture.stream(run(n, "stream", seed, k, length), n)
         out.append({"n": n, "seed": seed, "k": k, "len": length, "deliveries": per})
     return out
 
@@ -83,26 +65,18 @@ def gen_stream(cases):
 def gen_iar(n, cases):
     out = []
     for origin, mask in cases:
-        recs = run(n, "iar", origin, mask)
-        judge = sorted([r["rank"], r["null"], r["arg"]] for r in recs if r["ev"] == "judge")
-        actions = sorted([r["rank"], r["pid"], r["vote"], r["data_len"], r["data"]] for r in recs if r["ev"] == "action")
-        pickups = sorted([r["rank"], r["type"], r["pid"], r["vote"], r["data_len"], r["data"], r["origin"]]
-                         for r in recs if r["ev"] == "pickup")
-        result = [r["vote"] for r in recs if r["ev"] == "result"]
-        assert len(result) == 1
-        out.append({"n": n, "origin": origin, "mask": mask, "judge": judge, "actions": actions, "pickups": pickups,
-                    "decision": result[0]})
+        c = capture.iar(run(n, "iar", origin, mask))
+        c.update({"n": n, "origin": origin, "mask": mask})
+        out.append(c)
     return out
 
 
 def gen_multi(n, cases):
     out = []
     for a1, mod, agree in cases:
-        recs = run(n, "multi", a1, mod, agree)
-        judge = sorted([r["rank"], r["null"], r["arg"], r["ret"]] for r in recs if r["ev"] == "judge")
-        decisions = sorted([r["rank"], r["pid"], r["vote"], r["origin"]] for r in recs if r["ev"] == "decision")
-        results = sorted([r["rank"], r["pid"], r["vote"]] for r in recs if r["ev"] == "result")
-        out.append({"n": n, "active_1": a1, "mod": mod, "agree": agree, "judge": judge, "decisions": decisions, "results": results})
+        c = capture.multi(run(n, "multi", a1, mod, agree))
+        c.update({"n": n, "active_1": a1, "mod": mod, "agree": agree})
+        out.append(c)
     return out
 
 
@@ -132,6 +106,8 @@ def main():
 
     tests = run(4, "tests", timeout=900)
     dump("testcases.json", {"n": 4, "results": tests})
+    tests2 = run(4, "tests2", timeout=900)
+    dump("testcases2.json", {"n": 4, "results": tests2})
 
 
 if __name__ == "__main__":

@@ -31,11 +31,21 @@ def test_library_loads_without_gpu():
     assert os.path.exists(rlo.LIB_PATH)
 
 
-@pytest.mark.parametrize("header", sorted(h for h in os.listdir(INCLUDE) if h.endswith(".h")))
+LIBS = {"rlo_hip.h": "librlo_hip.so", "rootless_ops.h": "librootless_ops.so"}
+
+
+def test_every_header_has_a_library():
+    assert sorted(h for h in os.listdir(INCLUDE) if h.endswith(".h")) == sorted(LIBS)
+
+
+@pytest.mark.parametrize("header", sorted(LIBS))
 def test_every_declared_symbol_is_exported(header):
     import rlo
 
-    lib = ctypes.CDLL(rlo.LIB_PATH)
+    path = os.path.join(os.path.dirname(rlo.LIB_PATH), LIBS[header])
+    if header == "rootless_ops.h" and not os.path.exists("/opt/conda/include/mpi.h"):
+        pytest.skip("no MPI in this image: librootless_ops.so is not built")
+    lib = ctypes.CDLL(path)
     names = declared_functions(header)
     assert names, header
     missing = [n for n in names if not hasattr(lib, n)]
