@@ -40,6 +40,7 @@ static constexpr int kAuxSc1 = 16;  // cache policy: sc1 (agent scope, write-thr
 static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
+static constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at candidates 192..255
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -76,7 +77,7 @@ struct Shared {
     uint32_t n_oi[kMaxOut];          // slots admitted into out-ring oi this iteration
     uint32_t R, C, nstorm, storm_base, loc_kind, lat_id, exit_now;
     // host-service mode: command run selected this iteration, pickup ring position
-    uint32_t hbase, nh, ev_n, quit;
+    uint32_t hbase, nh, ev_n, quit, gap_lo, gap_hi;
     uint64_t hhead, hin_head, pk_tail;
     int64_t prop_idx;
     uint32_t storm_ids[kPass];
@@ -486,6 +487,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     // out-ring credits is re-staged only a little past what fitted, so a hot rank does not pull
     // (and classify) hundreds of messages per iteration that cannot leave anyway
     uint32_t win_r = kMaxCand;
+    uint64_t hpoll = 0;  // host mode, wave 0: lane 0 = command-ring tail, lane 1 = pickup-ring head
+    uint32_t hskip = 0;
     bool peer_failed = false;
     uint64_t idle_since = 0;
     uint32_t idle_n = 0;
@@ -494,9 +497,10 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
         // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
         uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
         uint32_t errf = 0, sid = 0;
-        uint64_t hpoll = 0;  // host mode: lane 0 = command-ring tail, lane 1 = pickup-ring head
         if (w == 0) {
-            if (host && lane < 2) hpoll = poll64_sys(&hctl[lane == 0 ? kHctlInjTail : kHctlPkHead]);
+            // host mode: the pinned counters cost a PCIe round trip, so they are re-read only every
+            // 4th iteration while idle (every iteration during a command burst or a full pickup ring)
+            if (host && lane < 2 && hskip == 0) hpoll = poll64_sys(&hctl[lane == 0 ? kHctlInjTail : kHctlPkHead]);
             if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
             if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
             if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
@@ -531,6 +535,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (lane == 1) pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
                 const uint64_t pk_head = rdl64(hpoll, 1);
                 const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - pk_head);
+                const bool busy_h = rdl64(hpoll, 0) != S.hin_head || pk_free < P.log_cap / 2u;
+                hskip = busy_h ? 0u : (hskip == 0 ? 3u : hskip - 1u);
                 hblock = pk_free < 8u;
                 hlim = hblock ? 0u : (pk_free - 4u) / 2u;
             }
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             vin_head_r += vtake;  // merged by wave 1 before the next publish
             // in-rings: fair per-ring quotas
             const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)256) : 0u;
-            const uint32_t reserve = host ? 64u : ((P.mode & MODE_IAR) ? 2u : 0u);
+            const uint32_t reserve = host ? kPass + 1u : ((P.mode & MODE_IAR) ? 2u : 0u);  // host: stage block + decision
             const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
             const uint32_t quota = nact ? min(kMaxCand - reserve, hlim) / (uint32_t)nact : 0u;
@@ -570,18 +576,31 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (S.own_state == 2) { loc_kind = K_DEC; C++; }
                 else if (S.own_state == 0 && S.own_iter < S.own_n) { loc_kind = K_PROP; prop_idx = P.prop_off[lr] + S.own_iter; C++; }
             }
-            uint32_t hbase = C, nh = 0;
+            uint32_t hbase = C, nh = 0, gap_lo = C;
             if (host && !hblock) {
-                // commands in FIFO order: a leading run of control commands (judge verdicts, quit) is
-                // applied now; the run of originations behind it becomes candidates (a proposal only
-                // when no own proposal is active, and it ends the run)
+                // commands in FIFO order.  The pending slots (up to 64) are pulled whole into the
+                // stage block of candidates 192..255 with ONE LDS-DMA round trip; a leading run of
+                // control commands (judge verdicts, quit) is applied now, the run of originations
+                // behind it becomes candidates in place (a proposal only when no own proposal is
+                // active, and it ends the run)
                 const uint64_t pend_n = rdl64(hpoll, 0) - S.hin_head;
-                const uint32_t np = (uint32_t)min(pend_n, (uint64_t)64);
+                const uint32_t np = (uint32_t)min(pend_n, (uint64_t)kPass);
                 if (np) {
-                    u32x4 hd = {0u, 0u, 0u, 0u};
-                    if ((uint32_t)lane < np) hd = ld_sys(rh, (uint32_t)((S.hin_head + lane) & hcap_m) * P.fwd_stride);
-                    const uint32_t htag = (hd.x >> 16) & 0xffu;
+                    const uint32_t nit = np * nsmall;
+                    for (uint32_t i0 = 0; i0 < nit; i0 += 64) {
+                        const uint32_t i = i0 + lane;
+                        if (i < nit) {
+                            const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
+                            const uint32_t off = (uint32_t)((S.hin_head + mi) & hcap_m) * P.fwd_stride;
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(STG(kHostBase, 0) + (i0 << 4)), 16,
+                                                                     off + 16u * q, 0, 0, kAuxSc1 | 1);
+                        }
+                    }
+                    VM_DRAIN();
+                    asm volatile("" ::: "memory");
                     const bool inq = (uint32_t)lane < np;
+                    const u32x4 hd = inq ? *reinterpret_cast<const u32x4*>(STG(kHostBase + lane, 0)) : u32x4{0u, 0u, 0u, 0u};
+                    const uint32_t htag = (hd.x >> 16) & 0xffu;
                     const uint64_t cm = __ballot(inq && htag >= 16u);
                     const uint32_t ncp = ~cm == 0ull ? 64u : (uint32_t)__builtin_ctzll(~cm);
                     if ((uint32_t)lane < ncp) {
@@ -601,16 +620,24 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                         }
                     }
                     const bool org = inq && (uint32_t)lane >= ncp && (htag == TAG_BCAST || htag == TAG_PROPOSAL);
-                    const uint64_t om = __ballot(org) >> ncp;
+                    const uint64_t om = ncp >= 64u ? 0ull : __ballot(org) >> ncp;
                     uint32_t run = ~om == 0ull ? 64u - ncp : (uint32_t)__builtin_ctzll(~om);
-                    const uint64_t pm = (__ballot(org && htag == TAG_PROPOSAL) >> ncp) & (run >= 64 ? ~0ull : ((1ull << run) - 1ull));
+                    const uint64_t pm = ncp >= 64u ? 0ull
+                                                   : (__ballot(org && htag == TAG_PROPOSAL) >> ncp) &
+                                                         (run >= 64 ? ~0ull : ((1ull << run) - 1ull));
                     if (pm) {
                         const uint32_t fp = (uint32_t)__builtin_ctzll(pm);
                         run = (S.own_state == 0 && loc_kind != K_DEC) ? fp + 1u : fp;
                     }
-                    nh = min(run, kMaxCand - C);
+                    nh = run;
+                    gap_lo = C;
+                    hbase = kHostBase + ncp;
+                    if ((uint32_t)lane >= ncp && (uint32_t)lane < ncp + nh) {
+                        S.cand[kHostBase + lane].src = (uint32_t)((S.hin_head + lane) & hcap_m) * P.fwd_stride;
+                        S.cand[kHostBase + lane].group = kGroupLocal + K_HOST;
+                    }
                     if (lane == 0) { S.hhead = S.hin_head + ncp; S.hin_head += ncp; }
-                    C += nh;
+                    if (nh) C = hbase + nh;
                 }
             }
             if ((P.mode & MODE_STORM) && S.sched_next < S.sched_n) {
@@ -637,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 S.vtot = vtot;
                 S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
                 S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = 0;
-                S.hbase = hbase; S.nh = nh;
+                S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase;
                 S.exit_now = S.done;
                 if (P.mode & MODE_PROF) S.dbg[0] += R;
             }
@@ -686,27 +713,6 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                                 S.cand[lo + mi].group = (uint32_t)g;
                             }
                             dma16(rf, STG(lo, 0) + (i0 << 4), off + 16u * q);
-                        }
-                    }
-                }
-            }
-            if (host && S.nh) {  // the host command run: slots in pinned memory, same layout as a ring slot
-                const uint32_t hb = S.hbase, he = hb + S.nh;
-                const uint32_t lo = max(hb, c_lo), hi = min(he, c_lo + kPass);
-                if (lo < hi) {
-                    const uint64_t head = S.hhead + (lo - hb);
-                    const uint32_t nit = (hi - lo) * nsmall;
-                    for (uint32_t i0 = 0; i0 < nit; i0 += 64) {
-                        const uint32_t i = i0 + lane;
-                        if (i < nit) {
-                            const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
-                            const uint32_t off = (uint32_t)((head + mi) & hcap_m) * P.fwd_stride;
-                            if (q == 0) {
-                                S.cand[lo + mi].src = off;
-                                S.cand[lo + mi].group = kGroupLocal + K_HOST;
-                            }
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(STG(lo, 0) + (i0 << 4)), 16, off + 16u * q, 0, 0,
-                                                                     kAuxSc1 | 1);
                         }
                     }
                 }
@@ -764,7 +770,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
             // ---------------- D: classify this wave's messages
             const uint32_t c = (uint32_t)w * kPass + lane;
-            const bool active = c < C;
+            const bool active = c < C && !(c >= S.gap_lo && c < S.gap_hi);  // host mode: no candidates in the gap
             uint32_t kind = K_BAD, w0 = 0, id = 0, w2 = 0, t0 = 0, src = 0, kids = 0, group = 0;
             int from = -1, judge = 1;
             bool want_jreq = false;  // host mode: a proposal whose verdict has not been asked for yet
@@ -956,7 +962,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                                 }
                             }
                         }
-                        logidx = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, 0);
+                        // aux: device ticks (10 ns) from origination to this pickup (latency diagnostics)
+                        logidx = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1,
+                                         (uint32_t)now_ticks() - t0);
                     } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler (:668-726)
                         const int32_t pid = (int32_t)id;
                         const int k = (int)(group >> 1);
@@ -1146,6 +1154,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             PROF_STAMP(5);
         }
 
+        // host mode: every store of this iteration (pickup records + payloads included) drained, so
+        // the pickup tail is published at the end of this iteration, not after the next poll
+        if (host && (C != 0 || S.vtot != 0)) {
+            VM_DRAIN();
+            BAR();
+        }
         // ---------------- consume (wave 0): in-ring prefixes, producer counts, bookkeeping
         if (w == 0) {
             if (lane < n_in2) {
@@ -1157,12 +1171,22 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 else if (adm == tk && tk == win_r) win_r = min(2u * win_r, (uint32_t)kMaxCand);
                 if (P.mode & MODE_PROF) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
             }
+            if (host) {
+                if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(ihptr_r, in_head_r, sys); }
+                if (lane < n_in) {
+                    const uint64_t vt = S.vout_tail[lane];
+                    if (vt != pub_vout_r) { pub_vout_r = vt; pub64(vtptr_r, vt, sys); }
+                }
+            }
             {
                 const uint64_t bst = __ballot(lane < n_in2 && S.first_bad[lane] < S.ring_base[lane] + S.ring_take[lane]);
                 if (lane == 0 && bst) S.stalls += (unsigned long long)__popcll(bst);
             }
             if (lane < nout) {
                 out_tail_r += S.n_oi[lane];
+                // host mode: this iteration's stores are drained (see above): publish now, not after
+                // the next poll -- one iteration less per hop
+                if (host && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(otptr_r, out_tail_r, sys); }
                 if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
                     S.hist[32 + lane] += S.n_oi[lane];
                     S.hist[64 + lane] += S.ofree[lane] >> 4;
@@ -1185,9 +1209,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                         if (adm > S.nh) adm = S.nh;
                         S.hin_head = S.hhead + adm;
                     }
-                    S.pk_tail += S.ev_n;
-                    S.log_count += S.ev_n;
-                    S.ev_n = 0;
+                    if (S.ev_n) {
+                        S.pk_tail += S.ev_n;
+                        S.log_count += S.ev_n;
+                        S.ev_n = 0;
+                        pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
+                    }
                 }
                 S.iterations++;
                 if (S.progressed) {  // the clock is read on the 1st and every 64th idle iteration only

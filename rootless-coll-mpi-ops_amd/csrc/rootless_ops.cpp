@@ -20,8 +20,12 @@
 #include <cstdlib>
 #include <ctime>
 #include <cstring>
+#include <atomic>
+#include <chrono>
 #include <deque>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -57,6 +61,11 @@ struct Cmd {  // a command waiting for room in the command ring
     RLO_msg_t* msg;
 };
 
+struct RawEv {  // a pickup-ring event pulled off the device, not yet handled on the app thread
+    rlo_log_rec_t ev;
+    std::vector<uint8_t> payload;
+};
+
 }  // namespace
 
 struct progress_engine {
@@ -79,6 +88,11 @@ struct progress_engine {
     bool failed = false;
     uint32_t poll_tick = 0;
     std::vector<uint8_t> evbuf;
+    // the device side of the engine (command ring producer, pickup ring consumer, backlog, evq)
+    // is shared with the pump thread, which keeps both rings moving while the application is
+    // not calling progress (MPI's sends complete without it: testcases.c:690-697 relies on that)
+    std::mutex mu;
+    std::deque<RawEv> evq;
     progress_engine* next = nullptr;
 };
 
@@ -141,6 +155,7 @@ size_t pbuf_put(char* out, RLO_ID pid, RLO_Vote vote, uint64_t len, const void* 
 }
 
 int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t len, RLO_msg_t* msg) {
+    std::lock_guard<std::mutex> lk(e->mu);
     if (e->backlog.empty()) {
         int rc = rlo_host_post(e->w, e->rank, &c, payload, len);
         if (rc == RLO_OK) {
@@ -166,6 +181,7 @@ int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t l
     return 0;
 }
 
+// [e->mu held]
 void flush_backlog(progress_engine* e) {
     while (!e->backlog.empty()) {
         Cmd& q = e->backlog.front();
@@ -186,6 +202,7 @@ void flush_backlog(progress_engine* e) {
 }
 
 // frees my sent bcasts once the device has taken them (_wait_only_queue_cleanup :1015-1034)
+// [e->mu held]
 void reap_sent(progress_engine* e) {
     if (e->wait.empty()) return;
     uint64_t consumed = 0;
@@ -297,21 +314,83 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
     }
 }
 
-// make_progress_gen (:551-641): everything the device finished since the last call
-void progress(progress_engine* e) {
-    if (!e->w || e->failed) return;
+// [e->mu held] commands into the command ring, events off the pickup ring into evq
+bool pump(progress_engine* e) {
+    const size_t backlog0 = e->backlog.size();
     flush_backlog(e);
     rlo_log_rec_t ev;
     int got = 0;
-    for (int i = 0; i < 4096; i++) {
+    for (; got < 4096; got++) {
         int r = rlo_host_poll(e->w, e->rank, &ev, e->evbuf.data(), (uint32_t)e->evbuf.size());
         if (r != 1) break;
-        handle_event(e, ev, e->evbuf.data());
-        got++;
+        RawEv q;
+        q.ev = ev;
+        if (ev.payload_idx != 0xffffffffu) {
+            const uint32_t n = ev.len < (uint32_t)e->evbuf.size() ? ev.len : (uint32_t)e->evbuf.size();
+            q.payload.assign(e->evbuf.data(), e->evbuf.data() + n);
+        }
+        e->evq.push_back(std::move(q));
     }
-    flush_backlog(e);
-    reap_sent(e);
-    if (!got && (++e->poll_tick & 255u) == 0) check_alive(e);
+    if (got) flush_backlog(e);
+    return got || e->backlog.size() != backlog0;
+}
+
+// make_progress_gen (:551-641): everything the device finished since the last call
+void progress(progress_engine* e) {
+    if (!e->w || e->failed) return;
+    // like make_progress_gen, which completes at most one receive per call (its single posted
+    // ANY_SOURCE irecv, :569-624), a call surfaces at most one received message (a delivery or a
+    // proposal to judge); applications pace on that (testcases.c:666-686 stops sending exactly
+    // when its count is reached only because each progress call yields one pickup)
+    std::deque<RawEv> local;
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        pump(e);
+        while (!e->evq.empty()) {
+            const uint32_t k = e->evq.front().ev.kind;
+            local.push_back(std::move(e->evq.front()));
+            e->evq.pop_front();
+            if (k == RLO_EV_DELIVER_BCAST || k == RLO_EV_DELIVER_DECISION || k == RLO_EV_JUDGE) break;
+        }
+        reap_sent(e);
+    }
+    for (const RawEv& q : local) handle_event(e, q.ev, q.payload.data());
+    if (local.empty() && (++e->poll_tick & 255u) == 0) check_alive(e);
+}
+
+// ---- the pump thread: one per process while engines exist; it only moves ring entries
+std::mutex g_list_mu;  // guards g_engines against the pump thread
+std::thread g_pump;
+std::atomic<bool> g_pump_stop{false};
+
+void pump_loop() {
+    unsigned idle = 0;
+    while (!g_pump_stop.load(std::memory_order_relaxed)) {
+        bool did = false;
+        {
+            std::lock_guard<std::mutex> lg(g_list_mu);
+            for (progress_engine* e = g_engines; e; e = e->next) {
+                std::unique_lock<std::mutex> lk(e->mu, std::try_to_lock);
+                if (!lk.owns_lock() || e->failed || !e->w) continue;  // the app thread is on it
+                did |= pump(e);
+            }
+        }
+        if (did) idle = 0;
+        else if (++idle > 2000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::yield();
+    }
+}
+
+void pump_start() {
+    if (g_pump.joinable()) return;
+    g_pump_stop = false;
+    g_pump = std::thread(pump_loop);
+}
+
+void pump_stop() {
+    if (!g_pump.joinable()) return;
+    g_pump_stop = true;
+    g_pump.join();
 }
 
 std::vector<std::pair<rlo_world_t*, void*>> g_grave;  // stopped engines' worlds / streams
@@ -394,10 +473,11 @@ int RLO_msg_free(RLO_msg_t* msg_in) {
 int RLO_msg_test_isends(RLO_engine_t* eng, RLO_msg_t* msg_in) {
     assert(eng && msg_in);
     if (msg_in->posted == 2) return 1;
-    if (msg_in->posted == 0 || msg_in->seq == 0) return msg_in->posted == 0;  // never sent: nothing pending
+    if (msg_in->posted == 0) return 1;  // never sent: nothing pending
+    std::lock_guard<std::mutex> lk(eng->mu);
     uint64_t consumed = 0;
     rlo_host_cmd_count(eng->w, eng->rank, &consumed, nullptr);
-    return consumed >= msg_in->seq;
+    return msg_in->seq != 0 && consumed >= msg_in->seq;
 }
 
 RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb_func, void* app_ctx,
@@ -504,9 +584,13 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
         return nullptr;
     }
     e->id = ++g_engines_ever;  // engine ids 1, 2, ... (:515-517)
-    progress_engine** tail = &g_engines;
-    while (*tail) tail = &(*tail)->next;
-    *tail = e;
+    {
+        std::lock_guard<std::mutex> lg(g_list_mu);
+        progress_engine** tail = &g_engines;
+        while (*tail) tail = &(*tail)->next;
+        *tail = e;
+    }
+    pump_start();
     return e;
 }
 
@@ -536,11 +620,11 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
     rlo_cmd_t q;
     std::memset(&q, 0, sizeof q);
     q.kind = RLO_CMD_QUIT;
-    while (!eng->failed && rlo_host_running(eng->w) == 1) {
-        flush_backlog(eng);
-        if (eng->backlog.empty() && rlo_host_post(eng->w, eng->rank, &q, nullptr, 0) == RLO_OK) break;
-        rlo_log_rec_t ev;  // keep the pickup ring moving while the quit waits for room
-        while (rlo_host_poll(eng->w, eng->rank, &ev, eng->evbuf.data(), (uint32_t)eng->evbuf.size()) == 1) {}
+    post(eng, q, nullptr, 0, nullptr);
+    while (!eng->failed && rlo_host_running(eng->w) == 1) {  // keep both rings moving until the kernel ends
+        std::lock_guard<std::mutex> lk(eng->mu);
+        pump(eng);
+        eng->evq.clear();
     }
     int rc = rlo_wait(eng->w);
     if (rc != RLO_OK && !eng->failed)
@@ -549,9 +633,13 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
     for (RLO_msg_t* m : eng->pickup) msg_release(m);
     for (RLO_msg_t* m : eng->wait) std::free(m);
     retire_comm(eng->comm);  // callers keep using RLO_get_my_comm's comm after cleanup (testcases.c:329-331)
-    progress_engine** p = &g_engines;  // engine_remove (:445-466)
-    while (*p && *p != eng) p = &(*p)->next;
-    if (*p) *p = eng->next;
+    {
+        std::lock_guard<std::mutex> lg(g_list_mu);
+        progress_engine** p = &g_engines;  // engine_remove (:445-466)
+        while (*p && *p != eng) p = &(*p)->next;
+        if (*p) *p = eng->next;
+    }
+    if (!g_engines) pump_stop();
     // hipFree / hipIpcCloseMemHandle may wait for the whole device, i.e. for the persistent
     // kernel of another engine of this process: free the world once no engine kernel runs
     g_grave.push_back(std::make_pair(eng->w, eng->stream));

@@ -17,8 +17,9 @@ DROPIN_HARNESS = os.path.join(REPO, "oracle", "_ref", "dropin_harness")
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
-def run(exe, n, *args, timeout=600, env=None):
-    """mpiexec -n N exe OUT args... -> list of JSON records (rank 0 gathers every rank's lines)"""
+def run(exe, n, *args, timeout=600, env=None, want_stdout=False):
+    """mpiexec -n N exe OUT args... -> list of JSON records (rank 0 gathers every rank's lines);
+    with want_stdout, (records, combined stdout/stderr text)"""
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "out.jsonl")
         cmd = ["timeout", "-k", "10", str(timeout), MPIEXEC, "-n", str(n), exe, out] + [str(a) for a in args]
@@ -26,7 +27,8 @@ def run(exe, n, *args, timeout=600, env=None):
         if r.returncode != 0:
             raise RuntimeError("%s exited %d:\n%s" % (" ".join(cmd), r.returncode, r.stdout.decode(errors="replace")[-4000:]))
         with open(out) as f:
-            return [json.loads(line) for line in f if line.strip()]
+            recs = [json.loads(line) for line in f if line.strip()]
+        return (recs, r.stdout.decode(errors="replace")) if want_stdout else recs
 
 
 def parents(recs, n):
