@@ -32,6 +32,14 @@ sys.path.insert(0, PKG)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
+def note(msg):
+    """progress on stderr (the JSON line stays the only stdout)"""
+    print("[bench %.1fs] %s" % (time.time() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.time()
+
+
 def percentile(a, p):
     import numpy as np
 
@@ -93,6 +101,141 @@ def pmc_traffic(ranks, length, k, device, timeout_s=120):
             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, last of 2 launches; FETCH x2 (gfx950)"}, None
 
 
+def dropin_api_leg(ranks=8, timeout_s=150):
+    """The drop-in rootless_ops.h path end to end: tools/api_bench.c over librootless_ops.so
+    (one MPI process per rank, every rank's engine a persistent kernel on this GPU) beside the
+    same driver linked against the compiled reference under host MPI on the box's cores."""
+    mpiexec = "/opt/conda/bin/mpiexec"
+    ours = os.path.join(PKG, "lib", "rlo_api_bench")
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_api_bench")
+    if not (os.path.exists(mpiexec) and os.path.exists(ours)):
+        return {"error": "mpiexec or rlo_api_bench missing"}
+    out = {"ranks": ranks, "driver": "tools/api_bench.c (same calls for both)", "ours": {}, "reference_host_mpi": {}}
+    legs = [("storm", ["storm", "20000", "64"]), ("lat", ["lat", "500", "64"]), ("iar", ["iar", "2000"])]
+    for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
+        if not os.path.exists(exe):
+            out[name] = {"error": "not built"}
+            continue
+        for leg, args in legs:
+            note("api %s %s" % (name, leg))
+            try:
+                r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(ranks), exe] + args,
+                                   stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20)
+                lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+                out[name][leg] = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
+            except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
+                out[name][leg] = {"error": str(e)[:200]}
+    try:
+        o, f = out["ours"], out["reference_host_mpi"]
+        out["ratio_vs_reference"] = {
+            "bcast_per_s": round(o["storm"]["bcast_per_s"] / f["storm"]["bcast_per_s"], 2),
+            "decisions_per_s": round(o["iar"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
+            "p50_latency": round(o["lat"]["p50_us"] / f["lat"]["p50_us"], 2)}
+    except Exception:  # noqa: BLE001
+        pass
+    out["cores"] = ranks
+    return out
+
+
+def bulk_leg(dist, world, rank, local, sizes_mib=(1, 4, 16, 64), iters=5, blocks=None):
+    """BASELINE configs[2]: large-message rootless bcast (pipelined scatter + all-gather over the
+    ranks' HBM buffers, rlo_bulk.hip) from rotating originators vs rooted RCCL broadcast of the
+    same bytes from the same root.  N > 1: one rank per GPU.  N = 1: an 8-rank world on the one
+    GPU (HBM only; no RCCL counterpart).  Every receiver checks every byte."""
+    import torch
+
+    import rlo
+    from rlo.bulk import Bulk
+
+    G = world if world > 1 else 8
+    maxb = max(sizes_mib) << 20
+    blocks = blocks or (128 if world > 1 else 32)
+    if world > 1:
+        w = rlo.World.part(G, G, rank, max_payload=64, device=local, uncached=True)
+        blobs = [None] * world
+        dist.all_gather_object(blobs, w.export())
+        w.connect(blobs)
+        b = Bulk(w, maxb)
+        bb = [None] * world
+        dist.all_gather_object(bb, b.export())
+        b.connect(bb)
+        mine = [rank]
+        # rehearsal of the N-part path on one GPU (RLO_BENCH_DEVICE): RCCL refuses two ranks per GPU
+        nccl = None if os.environ.get("RLO_BENCH_DEVICE") else dist.new_group(backend="nccl")
+    else:
+        w = rlo.World(G, max_payload=64, device=local)
+        b = Bulk(w, maxb)
+        b.connect([b.export()])
+        mine = list(range(G))
+        nccl = None
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def maxr(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    out = []
+    try:
+        for mib in sizes_mib:
+            nbytes = mib << 20
+            ours, ok = [], True
+            for it in range(iters + 1):
+                o = it % G
+                gen = torch.Generator(device="cuda").manual_seed(1000 * mib + o)
+                want = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=gen)
+                if o in mine:
+                    b.tensor(o)[:nbytes].copy_(want)
+                barrier()
+                b.reset()
+                barrier()
+                b.launch(o, nbytes, blocks=blocks)
+                ms, rc = b.wait(raise_on_error=False)
+                ok &= rc == 0
+                for r in mine:
+                    if r != o:
+                        ok &= bool(torch.equal(b.tensor(r)[:nbytes], want))
+                ms = maxr(ms)
+                if it:  # the first launch is a warmup
+                    ours.append(ms)
+            if rank == 0:
+                note("bulk %d MiB ours done" % mib)
+            rec = {"MiB": mib, "ours_ms": round(sorted(ours)[len(ours) // 2], 4), "verified": ok}
+            rec["ours_algbw_GBps"] = round(nbytes / (rec["ours_ms"] * 1e-3) / 1e9, 2)
+            if nccl is not None:
+                t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                rc = []
+                for it in range(iters + 2):
+                    o = it % G
+                    barrier()
+                    e0.record()
+                    dist.broadcast(t, src=o, group=nccl)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    if it >= 2:
+                        rc.append(maxr(e0.elapsed_time(e1)))
+                rec["rccl_ms"] = round(sorted(rc)[len(rc) // 2], 4)
+                rec["rccl_algbw_GBps"] = round(nbytes / (rec["rccl_ms"] * 1e-3) / 1e9, 2)
+                rec["ours_over_rccl"] = round(rec["rccl_ms"] / rec["ours_ms"], 3)
+            else:  # one GPU: every byte written once per receiver and read once per forward
+                rec["hbm_GBps"] = round((2.0 * (G - 1) * nbytes) / (rec["ours_ms"] * 1e-3) / 1e9, 1)
+            out.append(rec)
+    finally:
+        b.close()
+        w.close()
+    return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "blocks_per_rank": blocks,
+            "algorithm": "pipelined scatter + all-gather over per-rank HBM buffers (rlo_bulk.hip)",
+            "baseline": "torch.distributed.broadcast, nccl backend (RCCL), same root" if world > 1 else None,
+            "sizes": out}
+
+
 def reference_datapoint(length):
     """The compiled reference itself under host MPI (8 ranks), if it was built and MPI exists."""
     exe = os.path.join(REPO, "oracle", "_ref", "ref_harness")
@@ -126,6 +269,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / decisions legs")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-api", action="store_true", help="skip the drop-in rootless_ops.h API leg")
+    ap.add_argument("--no-bulk", action="store_true", help="skip the large-message leg (vs RCCL at N > 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,6 +278,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("RLO_BENCH_DEVICE"):  # rehearsal of the N-part path on one GPU
         local = int(os.environ["RLO_BENCH_DEVICE"])
+
+    # the drop-in API leg runs first, before this process opens the GPU: its 8 MPI ranks each keep
+    # a persistent kernel resident, and idle hardware queues held here would share the card with them
+    api_leg = None
+    if rank == 0 and world == 1 and not args.no_api:
+        note("drop-in API leg")
+        api_leg = dropin_api_leg()
 
     import ctypes
 
@@ -144,7 +296,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")  # control plane only: blob exchange, barriers, max-reduce
+        import datetime
+
+        # control plane only: blob exchange, barriers, max-reduce (bounded: a stuck peer ends the run)
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=4))
 
     import rlo
 
@@ -246,6 +401,8 @@ def main():
         # cross-GPU tree edges per bcast: G-1 .. G; each moves header + payload over xGMI
         extras["xgmi_alg_GBps_per_gpu"] = round(k * (world - 1) * (length + 16) / world / (kernel_ms * 1e-3) / 1e9, 3)
     if not args.no_extras:
+        if rank == 0:
+            note("latency / loaded-latency / decisions legs")
         if world == 1 or mode == "replicas":
             # unloaded latency: one random originator per round (bcast completion = last pickup)
             w.program_latency(args.lat_rounds, length, seed=17)
@@ -280,6 +437,13 @@ def main():
         ok &= bool((ist["error"] == 0).all())
     lib.rlo_stream_destroy(stream)
     w.close()
+    if not args.no_bulk:
+        if rank == 0:
+            note("bulk leg")
+        try:
+            extras["bulk"] = bulk_leg(dist, world, rank, local)
+        except Exception as e:  # noqa: BLE001 - reported, never fails the headline line
+            extras["bulk"] = {"error": repr(e)[:300]}
     ok = bool(sum_over_ranks(0.0 if ok else 1.0) == 0.0)
 
     line = {
@@ -308,7 +472,10 @@ def main():
         "verified": ok,
     }
     line.update(extras)
+    if rank == 0:
+        note("storm timed: %.3f ms/step" % (elapsed / args.steps * 1e3))
     if rank == 0 and world == 1 and not args.no_pmc:
+        note("pmc passes")
         tr, why = pmc_traffic(per, length, k, local)
         if tr is not None:
             line["roofline"]["traffic"] = round(tr["bytes"] / 1e9, 4)
@@ -317,7 +484,10 @@ def main():
             line["roofline"]["traffic_detail"] = tr
         else:
             line["roofline"]["traffic_error"] = why
+    if api_leg is not None:
+        line["dropin_api"] = api_leg
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        note("cpu baseline")
         line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)

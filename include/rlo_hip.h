@@ -193,6 +193,25 @@ int rlo_host_cmd_count(rlo_world_t* w, int rank, uint64_t* consumed, uint64_t* p
 /* number of HIP devices visible to this process (0 without a GPU) */
 int rlo_device_count(void);
 
+/* ---- bulk (large-message) rootless bcast, beyond the reference's 32,764-B cap.
+ * Every rank of the world gets a receive buffer in its part's HBM (uncached; peer HBM over xGMI
+ * across GPUs).  A bcast from any originator o of `bytes` already in o's buffer reaches every
+ * other rank's buffer as a pipelined scatter (o -> stripe owners) + all-gather (owners -> the
+ * rest), chunk by chunk.  Same exchange protocol as parts: create -> export -> exchange blobs ->
+ * connect; before every bcast each part resets its flags and all parts pass a host barrier;
+ * every part then launches with the same (origin, bytes, chunk, blocks). */
+typedef struct rlo_bulk rlo_bulk_t;
+#define RLO_BULK_BLOB_BYTES 256u
+int rlo_bulk_create(rlo_world_t* w, uint64_t buf_bytes, rlo_bulk_t** out);
+int rlo_bulk_export(rlo_bulk_t* b, void* blob, uint32_t cap); /* returns RLO_BULK_BLOB_BYTES */
+int rlo_bulk_connect(rlo_bulk_t* b, const void* blobs /* n_parts x RLO_BULK_BLOB_BYTES */, int n_parts);
+void* rlo_bulk_buffer(rlo_bulk_t* b, int rank); /* device pointer of a local rank's buffer  */
+int rlo_bulk_reset(rlo_bulk_t* b, void* stream);  /* zero this part's flags (sync)           */
+/* async; chunk_bytes 0 = auto; blocks = workgroups per local rank (same on every part) */
+int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream);
+int rlo_bulk_wait(rlo_bulk_t* b, float* kernel_ms); /* RLO_E_DEVICE if a wait timed out      */
+int rlo_bulk_destroy(rlo_bulk_t* b);
+
 /* ------------------------------------------------------------------ run */
 int rlo_reset(rlo_world_t* w, void* stream);           /* zero this part's counters (sync) */
 #define RLO_LAUNCH_NO_RESET 1u

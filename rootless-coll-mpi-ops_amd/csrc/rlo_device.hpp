@@ -168,4 +168,21 @@ struct Params {
     uint64_t* hctl;               // [n_local][kHctlWords] ring counters
 };
 
+// ---- bulk (large-message) rootless bcast: pipelined scatter + all-gather (rlo_bulk.hip)
+constexpr int kMaxBulkRanks = 64;
+constexpr uint32_t kBulkBlock = 1024;     // bytes one wave moves per step (64 lanes x 16 B)
+constexpr uint32_t kBulkMaxChunks = 4096; // flags per rank and kind
+
+struct BulkParams {
+    int32_t n, rank_begin, origin, pad;
+    uint64_t bytes;                      // message size
+    uint32_t chunk, stripe, nchunks;     // chunk = stripe * (n - 1); stripe multiple of kBulkBlock
+    uint32_t buf_bytes;                  // capacity of every rank's buffer (<= 4 GiB, multiple of 1 KiB)
+    uint8_t* buf[kMaxBulkRanks];         // every rank's receive buffer (peer HBM mapped)
+    uint32_t* sflag[kMaxBulkRanks];      // every rank's scatter flags [kBulkMaxChunks]
+    uint32_t* gflag[kMaxBulkRanks];      // every rank's gather flags [kBulkMaxChunks]
+    uint64_t deadline_ticks;
+    uint32_t* err;                       // this part's error word
+};
+
 }  // namespace rlo

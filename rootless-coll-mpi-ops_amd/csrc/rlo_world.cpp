@@ -18,6 +18,7 @@
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream);
 extern "C" size_t rlo_kernel_static_lds(void);
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds);
+extern "C" hipError_t rlo_launch_bulk(const rlo::BulkParams* p, int blocks, int local_ranks, hipStream_t stream);
 
 static_assert(sizeof(rlo_rank_stats_t) == sizeof(rlo::RankStats), "stats ABI");
 static_assert(sizeof(rlo_log_rec_t) == sizeof(rlo::LogRec), "log ABI");
@@ -1017,6 +1018,187 @@ int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
     HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipMemcpy(ticks, w->d_lat_out.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+}  // extern "C"
+
+// ====================================================================== bulk bcast
+
+namespace {
+struct BulkBlob {
+    uint32_t magic, part;
+    int32_t device, pad;
+    uint64_t token, ptr, bytes, stride;
+    hipIpcMemHandle_t h;
+};
+static_assert(sizeof(BulkBlob) <= RLO_BULK_BLOB_BYTES, "bulk blob");
+constexpr uint32_t kBulkMagic = 0x524C4F42u;  // "RLOB"
+// per rank: [buffer buf_bytes][scatter flags][gather flags]
+constexpr uint64_t kBulkFlagBytes = 2ull * rlo::kBulkMaxChunks * 4ull;
+}  // namespace
+
+struct rlo_bulk {
+    rlo_world* w = nullptr;
+    uint64_t buf_bytes = 0, stride = 0;
+    uint8_t* region = nullptr;              // this part's ranks
+    std::vector<uint8_t*> base;             // every part's region, mapped here
+    std::vector<void*> opened;
+    uint32_t* err = nullptr;
+    rlo::BulkParams P{};
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool connected = false;
+};
+
+extern "C" {
+
+int rlo_bulk_create(rlo_world_t* w, uint64_t buf_bytes, rlo_bulk_t** out) {
+    if (!w || !out || buf_bytes == 0 || w->L.n > rlo::kMaxBulkRanks) return RLO_E_INVAL;
+    buf_bytes = (buf_bytes + rlo::kBulkBlock - 1) / rlo::kBulkBlock * rlo::kBulkBlock;
+    if (buf_bytes > 0xFFFF0000ull) return RLO_E_INVAL;  // one buffer resource per rank
+    HIPCHK(hipSetDevice(w->device));
+    rlo_bulk* b = new rlo_bulk();
+    b->w = w;
+    b->buf_bytes = buf_bytes;
+    b->stride = buf_bytes + kBulkFlagBytes;
+    // uncached: peers on other GPUs store into it over xGMI; receivers read it after a flag
+    hipError_t e = hipExtMallocWithFlags((void**)&b->region, b->stride * w->nl, hipDeviceMallocUncached);
+    if (e == hipSuccess) e = hipExtMallocWithFlags((void**)&b->err, 256, hipDeviceMallocUncached);
+    if (e != hipSuccess) { g_last_hip = (int)e; rlo_bulk_destroy(b); return RLO_E_HIP; }
+    (void)hipMemset(b->region, 0, b->stride * w->nl);
+    (void)hipMemset(b->err, 0, 256);
+    (void)hipStreamSynchronize(nullptr);
+    (void)hipEventCreate(&b->ev0);
+    (void)hipEventCreate(&b->ev1);
+    *out = b;
+    return RLO_OK;
+}
+
+int rlo_bulk_export(rlo_bulk_t* b, void* blob, uint32_t cap) {
+    if (!b || !blob || cap < RLO_BULK_BLOB_BYTES) return RLO_E_INVAL;
+    BulkBlob x;
+    std::memset(&x, 0, sizeof x);
+    x.magic = kBulkMagic;
+    x.part = (uint32_t)b->w->part;
+    x.device = b->w->device;
+    x.token = process_token();
+    x.ptr = (uint64_t)(uintptr_t)b->region;
+    x.bytes = b->buf_bytes;
+    x.stride = b->stride;
+    HIPCHK(hipIpcGetMemHandle(&x.h, b->region));
+    std::memset(blob, 0, RLO_BULK_BLOB_BYTES);
+    std::memcpy(blob, &x, sizeof x);
+    return (int)RLO_BULK_BLOB_BYTES;
+}
+
+int rlo_bulk_connect(rlo_bulk_t* b, const void* blobs, int n_parts) {
+    if (!b || !blobs || n_parts != b->w->L.nparts || b->connected) return RLO_E_INVAL;
+    rlo_world* w = b->w;
+    HIPCHK(hipSetDevice(w->device));
+    b->base.assign(n_parts, nullptr);
+    const uint64_t tok = process_token();
+    for (int q = 0; q < n_parts; q++) {
+        BulkBlob x;
+        std::memcpy(&x, (const uint8_t*)blobs + (size_t)q * RLO_BULK_BLOB_BYTES, sizeof x);
+        if (x.magic != kBulkMagic || (int)x.part != q || x.bytes != b->buf_bytes || x.stride != b->stride)
+            return RLO_E_INVAL;
+        if (q == w->part) {
+            b->base[q] = b->region;
+        } else if (x.token == tok) {
+            if (x.device != w->device) {
+                hipError_t e = hipDeviceEnablePeerAccess(x.device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { g_last_hip = (int)e; return RLO_E_HIP; }
+                (void)hipGetLastError();
+            }
+            b->base[q] = (uint8_t*)(uintptr_t)x.ptr;
+        } else {
+            void* p = nullptr;
+            HIPCHK(hipIpcOpenMemHandle(&p, x.h, hipIpcMemLazyEnablePeerAccess));
+            b->opened.push_back(p);
+            b->base[q] = (uint8_t*)p;
+        }
+    }
+    rlo::BulkParams& P = b->P;
+    std::memset(&P, 0, sizeof P);
+    P.n = w->L.n;
+    P.rank_begin = w->rb;
+    P.buf_bytes = (uint32_t)b->buf_bytes;
+    for (int r = 0; r < w->L.n; r++) {
+        const int q = w->L.part_of[r];
+        uint8_t* rb = b->base[q] + (uint64_t)(r - w->L.pb[q]) * b->stride;
+        P.buf[r] = rb;
+        P.sflag[r] = reinterpret_cast<uint32_t*>(rb + b->buf_bytes);
+        P.gflag[r] = P.sflag[r] + rlo::kBulkMaxChunks;
+    }
+    P.err = b->err;
+    P.deadline_ticks = 100000000ull * 20;  // 20 s per bulk bcast
+    b->connected = true;
+    return RLO_OK;
+}
+
+void* rlo_bulk_buffer(rlo_bulk_t* b, int rank) {
+    if (!b || !b->connected || rank < b->w->rb || rank >= b->w->rb + b->w->nl) return nullptr;
+    return b->P.buf[rank];
+}
+
+int rlo_bulk_reset(rlo_bulk_t* b, void* stream) {
+    if (!b || !b->connected) return RLO_E_INVAL;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(b->w->device));
+    for (int lr = 0; lr < b->w->nl; lr++)
+        HIPCHK(hipMemsetAsync(b->region + (uint64_t)lr * b->stride + b->buf_bytes, 0, kBulkFlagBytes, s));
+    HIPCHK(hipMemsetAsync(b->err, 0, 4, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return RLO_OK;
+}
+
+int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream) {
+    if (!b || !b->connected) return RLO_E_INVAL;
+    const int n = b->w->L.n;
+    if (origin < 0 || origin >= n || bytes == 0 || bytes > b->buf_bytes || blocks == 0 || blocks > 1024) return RLO_E_INVAL;
+    rlo::BulkParams& P = b->P;
+    // stripes are whole 1-KiB blocks; a chunk is (N-1) stripes; at most kBulkMaxChunks chunks
+    uint64_t want = chunk_bytes ? chunk_bytes : std::max<uint64_t>(bytes / 16, 256u * 1024u);
+    uint64_t stripe = (want / (uint64_t)(n - 1) + rlo::kBulkBlock - 1) / rlo::kBulkBlock * rlo::kBulkBlock;
+    stripe = std::max<uint64_t>(stripe, rlo::kBulkBlock);
+    uint64_t chunk = stripe * (uint64_t)(n - 1);
+    while ((bytes + chunk - 1) / chunk > rlo::kBulkMaxChunks) { stripe *= 2; chunk = stripe * (uint64_t)(n - 1); }
+    if (chunk > 0xFFFFFFFFull) return RLO_E_INVAL;
+    P.origin = origin;
+    P.bytes = bytes;
+    P.stripe = (uint32_t)stripe;
+    P.chunk = (uint32_t)chunk;
+    P.nchunks = (uint32_t)((bytes + chunk - 1) / chunk);
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(b->w->device));
+    HIPCHK(hipEventRecord(b->ev0, s));
+    hipError_t e = rlo_launch_bulk(&P, (int)blocks, b->w->nl, s);
+    if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
+    HIPCHK(hipEventRecord(b->ev1, s));
+    return RLO_OK;
+}
+
+int rlo_bulk_wait(rlo_bulk_t* b, float* ms) {
+    if (!b) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(b->w->device));
+    HIPCHK(hipEventSynchronize(b->ev1));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, b->ev0, b->ev1));
+    if (ms) *ms = t;
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, b->err, sizeof err, hipMemcpyDeviceToHost));
+    return err ? RLO_E_DEVICE : RLO_OK;
+}
+
+int rlo_bulk_destroy(rlo_bulk_t* b) {
+    if (!b) return RLO_E_INVAL;
+    (void)hipSetDevice(b->w->device);
+    for (void* p : b->opened) (void)hipIpcCloseMemHandle(p);
+    if (b->region) (void)hipFree(b->region);
+    if (b->err) (void)hipFree(b->err);
+    if (b->ev0) (void)hipEventDestroy(b->ev0);
+    if (b->ev1) (void)hipEventDestroy(b->ev1);
+    delete b;
+    return RLO_OK;
 }
 
 }  // extern "C"

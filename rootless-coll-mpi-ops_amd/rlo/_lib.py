@@ -89,7 +89,9 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_strerror", "rlo_last_hip_error",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
-           "rlo_device_count"]
+           "rlo_device_count", "rlo_bulk_create", "rlo_bulk_export", "rlo_bulk_connect", "rlo_bulk_buffer",
+           "rlo_bulk_reset", "rlo_bulk_launch", "rlo_bulk_wait", "rlo_bulk_destroy"]
+RLO_BULK_BLOB_BYTES = 256
 
 _lib = None
 
@@ -131,6 +133,15 @@ def load():
     L.rlo_host_running.argtypes = [vp]
     L.rlo_host_cmd_count.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.rlo_device_count.argtypes = []
+    L.rlo_bulk_create.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(vp)]
+    L.rlo_bulk_export.argtypes = [vp, vp, ctypes.c_uint32]
+    L.rlo_bulk_connect.argtypes = [vp, vp, ctypes.c_int]
+    L.rlo_bulk_buffer.argtypes = [vp, ctypes.c_int]
+    L.rlo_bulk_buffer.restype = vp
+    L.rlo_bulk_reset.argtypes = [vp, vp]
+    L.rlo_bulk_launch.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, vp]
+    L.rlo_bulk_wait.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.rlo_bulk_destroy.argtypes = [vp]
     L.rlo_strerror.argtypes = [ctypes.c_int]
     L.rlo_strerror.restype = ctypes.c_char_p
     _lib = L
