@@ -77,7 +77,7 @@ struct Shared {
     uint32_t n_oi[kMaxOut];          // slots admitted into out-ring oi this iteration
     uint32_t R, C, nstorm, storm_base, loc_kind, lat_id, exit_now;
     // host-service mode: command run selected this iteration, pickup ring position
-    uint32_t hbase, nh, ev_n, quit, gap_lo, gap_hi;
+    uint32_t hbase, nh, ev_n, quit, gap_lo, gap_hi, nchmax;
     uint64_t hhead, hin_head, pk_tail;
     int64_t prop_idx;
     uint32_t storm_ids[kPass];
@@ -364,6 +364,28 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     return x - v;
+}
+
+// wave-wide OR / MAX with the same DPP pattern, result uniform (lane 63 broadcast)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    uint32_t x = v;
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    uint32_t x = v;
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 // payload chunk q >= 1 of a locally originated message (payload bytes [16(q-1), 16q))
@@ -664,7 +686,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 S.vtot = vtot;
                 S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
                 S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = 0;
-                S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase;
+                S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase; S.nchmax = 0;
                 S.exit_now = S.done;
                 if (P.mode & MODE_PROF) S.dbg[0] += R;
             }
@@ -888,8 +910,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             }
             PROF_STAMP(2);
 
-            // ---------------- E: admission: credits per out-ring, FIFO prefix per source
-            for (int oi = 0; oi < nout; oi++) {
+            // ---------------- E: admission: credits per out-ring, FIFO prefix per source.  The ballot
+            // loops visit only the out-rings some lane of this wave needs (a wall rank uses about half)
+            const uint32_t wneed = wave_or(need);
+            if (lane < nout) S.wcnt[w][lane] = 0;
+            for (uint32_t m = wneed; m; m &= m - 1) {
+                const int oi = __builtin_ctz(m);
                 const uint64_t b = __ballot((need >> oi) & 1u);
                 if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
             }
@@ -902,7 +928,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 room_r = f > pre ? f - pre : 0u;
             }
             bool fits = active && judge >= 0;
-            for (int oi = 0; oi < nout; oi++) {
+            for (uint32_t m = wneed; m; m &= m - 1) {
+                const int oi = __builtin_ctz(m);
                 const bool bit = (need >> oi) & 1u;
                 const uint64_t b = __ballot(bit);
                 if (b && bit && (uint32_t)__popcll(b & lt_mask) >= rdl32(room_r, oi)) {
@@ -916,9 +943,16 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             const uint32_t an = admitted ? need : 0u;
             const uint32_t len = w2 & 0xffffffu;
             const bool isbig = admitted && ((kHdr + len + 15u) >> 4) > nsmall;
-            for (int oi = 0; oi < nout; oi++) {
+            const uint32_t wadm = wave_or(an);
+            if (lane < nout) S.wcnt[w][lane] = 0;
+            for (uint32_t m = wadm; m; m &= m - 1) {
+                const int oi = __builtin_ctz(m);
                 const uint64_t b = __ballot((an >> oi) & 1u);
                 if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
+            }
+            {  // chunks per message on the small copy path this iteration (storm: all equal)
+                const uint32_t mx = wave_max(admitted && !isbig ? (kHdr + len + 15u) >> 4 : 0u);
+                if (lane == 0 && mx) atomicMax(&S.nchmax, mx);
             }
             BAR();
             uint32_t pre_r = 0;  // lane oi: slots of out-ring oi taken by lower waves
@@ -931,10 +965,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
                 if (w == 0) S.n_oi[lane] = tot;
             }
-            for (int oi = 0; oi < nout; oi++) {
+            for (uint32_t m = wadm; m; m &= m - 1) {
+                const int oi = __builtin_ctz(m);
                 const bool bit = (an >> oi) & 1u;
                 const uint64_t b = __ballot(bit);
-                if (b && bit) {
+                if (bit) {
                     const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
                     OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : 0u));
                     if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
@@ -1095,14 +1130,16 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
             // ---------------- G2: small messages.  Out-ring oi (oi = w, w + 4, ...) receives its
             // admitted messages' staged slots as contiguous (message, chunk) items
+            const uint32_t nq = max(S.nchmax, 1u);  // items per message: the largest small message
+            const uint32_t qmagic = nq > 1 ? 0xFFFFFFFFu / nq + 1u : 0u;
             for (int oi = w; oi < nout; oi += kWaves) {
                 const uint32_t n = S.n_oi[oi];
                 if (!n) continue;
                 const uint64_t slot0 = S.out_tail0[oi];
                 const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(oring_r, oi)), oring_bytes);
-                const uint32_t nit = n * nsmall;
+                const uint32_t nit = n * nq;
                 for (uint32_t i = lane; i < nit; i += 64) {
-                    const uint32_t r = div_small(i, nmagic), q = i - r * nsmall;
+                    const uint32_t r = div_small(i, qmagic), q = i - r * nq;
                     const uint16_t e = OL(oi, r);
                     if (e & kBigFlag) continue;
                     const uint32_t nch = (kHdr + (S.cand[e].w2 & 0xffffffu) + 15u) >> 4;
