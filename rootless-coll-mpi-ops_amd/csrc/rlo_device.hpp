@@ -163,9 +163,12 @@ struct Params {
     uint32_t nout_max;            // 2 x max send_list_len over the ranks of this launch
     // host-service mode (MODE_HOST): all in pinned host memory.  Pickup records / payloads use
     // log / log_payload above as per-rank rings of log_cap slots.
-    uint8_t* hin;                 // command slots [n_local][hin_cap] x fwd_stride (forward-slot layout)
+    uint8_t* hin;                 // command slots [n_local][hin_cap] x fwd_stride (forward-slot layout),
+                                  //   uncached VRAM written by the CPU through the BAR
     uint32_t hin_cap;
-    uint64_t* hctl;               // [n_local][kHctlWords] ring counters
+    uint64_t* hctl;               // [n_local][kHctlWords] counters the DEVICE writes (pinned host memory)
+    uint64_t* hctl_dev;           // [n_local][kHctlWords] counters the HOST writes (uncached VRAM:
+                                  //   the CPU stores through the BAR, the kernel polls locally)
 };
 
 // ---- bulk (large-message) rootless bcast: pipelined scatter + all-gather (rlo_bulk.hip)

@@ -457,6 +457,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rh =
         mk_rsrc(host ? P.hin + (size_t)lr * P.hin_cap * P.fwd_stride : P.fwd_region, host ? P.hin_cap * P.fwd_stride : 16u);
     uint64_t* const hctl = host ? P.hctl + (size_t)lr * kHctlWords : nullptr;
+    uint64_t* const hctl_dev = host ? P.hctl_dev + (size_t)lr * kHctlWords : nullptr;
     const uint32_t hcap_m = host ? P.hin_cap - 1u : 0u;
 
     // ---------------- init
@@ -510,7 +511,6 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     // (and classify) hundreds of messages per iteration that cannot leave anyway
     uint32_t win_r = kMaxCand;
     uint64_t hpoll = 0;  // host mode, wave 0: lane 0 = command-ring tail, lane 1 = pickup-ring head
-    uint32_t hskip = 0;
     bool peer_failed = false;
     uint64_t idle_since = 0;
     uint32_t idle_n = 0;
@@ -520,9 +520,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
         uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
         uint32_t errf = 0, sid = 0;
         if (w == 0) {
-            // host mode: the pinned counters cost a PCIe round trip, so they are re-read only every
-            // 4th iteration while idle (every iteration during a command burst or a full pickup ring)
-            if (host && lane < 2 && hskip == 0) hpoll = poll64_sys(&hctl[lane == 0 ? kHctlInjTail : kHctlPkHead]);
+            // host mode: the host-written counters live in uncached VRAM (a local poll)
+            if (host && lane < 2) hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
             if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
             if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
             if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
@@ -557,8 +556,6 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (lane == 1) pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
                 const uint64_t pk_head = rdl64(hpoll, 1);
                 const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - pk_head);
-                const bool busy_h = rdl64(hpoll, 0) != S.hin_head || pk_free < P.log_cap / 2u;
-                hskip = busy_h ? 0u : (hskip == 0 ? 3u : hskip - 1u);
                 hblock = pk_free < 8u;
                 hlim = hblock ? 0u : (pk_free - 4u) / 2u;
             }

@@ -279,8 +279,9 @@ struct rlo_world {
     DevBuf<rlo::LogRec> d_log;
     uint32_t lat_rounds = 0;
     // host-service program (pinned host memory)
-    uint8_t* h_cmd = nullptr;       // [nl][cmd_cap][stride]
-    uint64_t* h_ctl = nullptr;      // [nl][kHctlWords]
+    uint8_t* h_cmd = nullptr;       // [nl][cmd_cap][stride]     uncached VRAM, CPU writes through the BAR
+    uint64_t* h_ctl = nullptr;      // [nl][kHctlWords]           pinned host: device-written counters
+    uint64_t* d_ctl = nullptr;      // [nl][kHctlWords]           uncached VRAM: host-written counters
     rlo::LogRec* h_ev = nullptr;    // [nl][pk_cap]
     uint8_t* h_evp = nullptr;       // [nl][pk_cap][max_payload]
     uint32_t cmd_cap = 0, pk_cap = 0;
@@ -579,7 +580,8 @@ int rlo_world_destroy(rlo_world_t* w) {
     w->d_lat_count.release(); w->d_lat_round.release(); w->d_lat_origin.release(); w->d_prop_pid.release();
     w->d_lat_out.release(); w->d_mask.release(); w->d_prop_data.release(); w->d_log_payload.release();
     w->d_isp.release(); w->d_log.release();
-    if (w->h_cmd) (void)hipHostFree(w->h_cmd);
+    if (w->h_cmd) (void)hipFree(w->h_cmd);
+    if (w->d_ctl) (void)hipFree(w->d_ctl);
     if (w->h_ctl) (void)hipHostFree(w->h_ctl);
     if (w->h_ev) (void)hipHostFree(w->h_ev);
     if (w->h_evp) (void)hipHostFree(w->h_evp);
@@ -796,11 +798,23 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
 }
 
 static void host_free(rlo_world* w) {
-    if (w->h_cmd) (void)hipHostFree(w->h_cmd);
+    if (w->h_cmd) (void)hipFree(w->h_cmd);
+    if (w->d_ctl) (void)hipFree(w->d_ctl);
     if (w->h_ctl) (void)hipHostFree(w->h_ctl);
     if (w->h_ev) (void)hipHostFree(w->h_ev);
     if (w->h_evp) (void)hipHostFree(w->h_evp);
-    w->h_cmd = nullptr; w->h_ctl = nullptr; w->h_ev = nullptr; w->h_evp = nullptr;
+    w->h_cmd = nullptr; w->d_ctl = nullptr; w->h_ctl = nullptr; w->h_ev = nullptr; w->h_evp = nullptr;
+}
+
+// uncached VRAM the CPU writes through the (large) BAR: the kernel polls it locally instead of
+// paying a PCIe round trip per poll (tools/probe/bar_write.hip: 0.10 vs 1.2 us per poll).
+// Uncached, not merely fine-grained: a fine-grained line can stay in the XCD's L2 and hide
+// the CPU's store until it is evicted (ms-long stalls measured at 8 ranks).
+static int bar_alloc(void** p, size_t bytes) {
+    hipError_t e = hipExtMallocWithFlags(p, std::max<size_t>(bytes, 256), hipDeviceMallocUncached);
+    if (e != hipSuccess) { g_last_hip = (int)e; *p = nullptr; return RLO_E_HIP; }
+    std::memset(*p, 0, std::max<size_t>(bytes, 256));  // through the BAR: also checks CPU access
+    return RLO_OK;
 }
 
 static int host_alloc(void** p, size_t bytes) {
@@ -822,7 +836,8 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     w->cmd_cap = cc;
     w->pk_cap = pc;
     const size_t nl = (size_t)w->nl;
-    if (host_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) || host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
+    if (bar_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) || bar_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8) ||
+        host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
         host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) || host_alloc((void**)&w->h_evp, nl * pc * w->max_payload)) {
         host_free(w);
         return RLO_E_HIP;
@@ -839,6 +854,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     P.hin = w->h_cmd;
     P.hin_cap = cc;
     P.hctl = w->h_ctl;
+    P.hctl_dev = w->d_ctl;
     const uint64_t idle = cfg ? cfg->idle_timeout_s : 0;
     P.timeout_ticks = idle ? 100000000ull * idle : ~0ull >> 2;
     P.deadline_ticks = ~0ull >> 2;  // serves until RLO_CMD_QUIT
@@ -851,6 +867,7 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payl
     if (len + rlo::kHdr > w->L.stride || len > 0xffffffu || (len && !payload)) return RLO_E_INVAL;
     const int lr = rank - w->rb;
     uint64_t* ctl = w->h_ctl + (size_t)lr * rlo::kHctlWords;
+    uint64_t* dctl = w->d_ctl + (size_t)lr * rlo::kHctlWords;
     const uint64_t tail = w->cmd_tail[lr];
     const uint64_t head = __atomic_load_n(&ctl[rlo::kHctlInjHead], __ATOMIC_ACQUIRE);
     if (tail - head >= w->cmd_cap) return RLO_E_AGAIN;
@@ -863,7 +880,9 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payl
     std::memcpy(slot, hdr, sizeof hdr);
     if (len) std::memcpy(slot + rlo::kHdr, payload, len);
     w->cmd_tail[lr] = tail + 1;
-    __atomic_store_n(&ctl[rlo::kHctlInjTail], tail + 1, __ATOMIC_RELEASE);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // BAR stores may be write-combined: slot before tail
+    __atomic_store_n(&dctl[rlo::kHctlInjTail], tail + 1, __ATOMIC_RELEASE);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // push the tail out now
     return RLO_OK;
 }
 
@@ -881,7 +900,8 @@ int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, ui
         std::memcpy(payload, w->h_evp + ((size_t)lr * w->pk_cap + i) * w->max_payload, n);
     }
     w->pk_head[lr] = head + 1;
-    __atomic_store_n(&ctl[rlo::kHctlPkHead], head + 1, __ATOMIC_RELEASE);
+    __atomic_store_n(&w->d_ctl[(size_t)lr * rlo::kHctlWords + rlo::kHctlPkHead], head + 1, __ATOMIC_RELEASE);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // a write-combined BAR store would otherwise linger
     return 1;
 }
 
@@ -913,6 +933,8 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     HIPCHK(hipSetDevice(w->device));
     if (w->have_program && (w->P.mode & rlo::MODE_HOST)) {  // the kernel is not running: rings restart at 0
         std::memset(w->h_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
+        std::memset(w->d_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
         std::fill(w->cmd_tail.begin(), w->cmd_tail.end(), 0);
         std::fill(w->pk_head.begin(), w->pk_head.end(), 0);
     }

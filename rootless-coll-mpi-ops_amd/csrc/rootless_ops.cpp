@@ -93,6 +93,10 @@ struct progress_engine {
     // not calling progress (MPI's sends complete without it: testcases.c:690-697 relies on that)
     std::mutex mu;
     std::deque<RawEv> evq;
+    std::atomic<int64_t> app_ns{0};  // last time the application thread made progress
+    // RLO_TRACE=1: counters printed at cleanup (diagnostics)
+    uint64_t n_progress = 0, n_events = 0, n_pumped = 0, n_judge = 0, n_result = 0;
+    int64_t t_submit = 0, sum_prop_ns = 0, max_prop_ns = 0;
     progress_engine* next = nullptr;
 };
 
@@ -101,6 +105,10 @@ namespace {
 progress_engine* g_engines = nullptr;  // Active_Engines (:40)
 int g_engines_ever = 0;
 std::vector<RLO_msg_t*> g_pool;         // recycled received messages
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 void proposal_init(RLO_proposal_state* ps) {  // proposal_state_init :1235-1248
     ps->pid = -1;
@@ -270,6 +278,12 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             break;
         }
         case RLO_EV_RESULT: {  // my decision went out (:560-563 + _iar_decision_bcast :908-917)
+            if (e->t_submit) {
+                const int64_t d = now_ns() - e->t_submit;
+                e->sum_prop_ns += d;
+                e->max_prop_ns = std::max(e->max_prop_ns, d);
+            }
+            e->n_result++;
             e->own.vote = ev.vote;
             e->own.votes_recved = e->own.votes_needed;
             e->own.state = RLO_COMPLETED;
@@ -277,6 +291,7 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             break;
         }
         case RLO_EV_JUDGE: {  // judge(proposal data, ctx) (:698); data is zero-padded like the
+            e->n_judge++;
                               // reference's calloc'd receive buffer
             std::vector<char> pb(RLO_MSG_SIZE_MAX + 16, 0);
             const uint32_t n = ev.len < (uint32_t)RLO_MSG_SIZE_MAX ? ev.len : (uint32_t)RLO_MSG_SIZE_MAX;
@@ -338,6 +353,7 @@ bool pump(progress_engine* e) {
 // make_progress_gen (:551-641): everything the device finished since the last call
 void progress(progress_engine* e) {
     if (!e->w || e->failed) return;
+    e->app_ns.store(now_ns(), std::memory_order_relaxed);
     // like make_progress_gen, which completes at most one receive per call (its single posted
     // ANY_SOURCE irecv, :569-624), a call surfaces at most one received message (a delivery or a
     // proposal to judge); applications pace on that (testcases.c:666-686 stops sending exactly
@@ -354,6 +370,8 @@ void progress(progress_engine* e) {
         }
         reap_sent(e);
     }
+    e->n_progress++;
+    e->n_events += local.size();
     for (const RawEv& q : local) handle_event(e, q.ev, q.payload.data());
     if (local.empty() && (++e->poll_tick & 255u) == 0) check_alive(e);
 }
@@ -363,26 +381,31 @@ std::mutex g_list_mu;  // guards g_engines against the pump thread
 std::thread g_pump;
 std::atomic<bool> g_pump_stop{false};
 
+// The pump steps in only for engines whose application thread has not made progress for a
+// while: a busy application moves its own rings, and the pump would only compete for its core.
 void pump_loop() {
+    constexpr int64_t kQuiet = 200000;  // ns without an application progress call
     unsigned idle = 0;
     while (!g_pump_stop.load(std::memory_order_relaxed)) {
         bool did = false;
         {
             std::lock_guard<std::mutex> lg(g_list_mu);
+            const int64_t t = now_ns();
             for (progress_engine* e = g_engines; e; e = e->next) {
+                if (t - e->app_ns.load(std::memory_order_relaxed) < kQuiet) continue;
                 std::unique_lock<std::mutex> lk(e->mu, std::try_to_lock);
                 if (!lk.owns_lock() || e->failed || !e->w) continue;  // the app thread is on it
-                did |= pump(e);
+                if (pump(e)) { did = true; e->n_pumped++; }
             }
         }
         if (did) idle = 0;
-        else if (++idle > 2000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else if (++idle > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
         else std::this_thread::yield();
     }
 }
 
 void pump_start() {
-    if (g_pump.joinable()) return;
+    if (g_pump.joinable() || std::getenv("RLO_NO_PUMP")) return;
     g_pump_stop = false;
     g_pump = std::thread(pump_loop);
 }
@@ -596,6 +619,12 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
 
 int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
     assert(eng);
+    if (std::getenv("RLO_TRACE"))
+        std::fprintf(stderr, "rlo trace rank %d engine %d: progress %llu events %llu pumped %llu judge %llu results %llu "
+                     "proposal->result avg %.1f us max %.1f us\n", eng->rank, eng->id, (unsigned long long)eng->n_progress,
+                     (unsigned long long)eng->n_events, (unsigned long long)eng->n_pumped, (unsigned long long)eng->n_judge,
+                     (unsigned long long)eng->n_result, eng->n_result ? eng->sum_prop_ns / 1e3 / eng->n_result : 0.0,
+                     eng->max_prop_ns / 1e3);
     // collective quiescence (:1607-1627): every bcast and decision sent anywhere has arrived here
     int sent = (int)eng->sent_bcast, total = 0, done = 0;
     MPI_Request req;
@@ -721,6 +750,7 @@ int RLO_submit_proposal(RLO_engine_t* eng, char* proposal, size_t prop_size, RLO
     }
     std::vector<char> pb(16 + prop_size);
     pbuf_put(pb.data(), my_proposal_id, 1, prop_size, proposal);
+    eng->t_submit = now_ns();
     eng->own.state = RLO_IN_PROGRESS;
     rlo_cmd_t c;
     std::memset(&c, 0, sizeof c);
