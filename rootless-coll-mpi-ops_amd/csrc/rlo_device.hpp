@@ -135,6 +135,8 @@ struct Params {
     uint32_t* lat_count;          // [lat_rounds] deliveries so far
     uint64_t* lat_out;            // [lat_rounds] completion ticks
     uint32_t* lat_round;          // current round (global)
+    const uint32_t* lat_own_off;  // [n_local + 1] CSR of the rounds each local rank originates
+    const uint32_t* lat_own;
     // IAR workload
     uint32_t judge_kind, judge_ppm;
     uint64_t judge_seed;

@@ -40,6 +40,7 @@ static constexpr int kAuxSc1 = 16;  // cache policy: sc1 (agent scope, write-thr
 static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
+static constexpr uint32_t kIdleSpin = 256;  // tight re-polls after an idle iteration (~0.1 ms at most)
 static constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at candidates 192..255
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
@@ -99,7 +100,7 @@ struct Shared {
     int64_t own_iter, own_n;
     // origination progress
     int64_t sched_next, sched_n;
-    uint32_t lat_next, done, error, error_aux, progressed;
+    uint32_t lat_pos, lat_pos_n, lat_own_next, done, error, error_aux, progressed;
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, iterations, busy, stalls;
@@ -477,7 +478,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             S.own_n = ((P.mode & MODE_IAR) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
             S.sched_next = 0;
             S.sched_n = (P.mode & MODE_STORM) ? (P.sched_off[lr + 1] - P.sched_off[lr]) : 0;
-            S.lat_next = 0;
+            S.lat_pos = 0;
+            S.lat_pos_n = (P.mode & MODE_LAT) ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
+            S.lat_own_next = S.lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
             S.expect_bcast = (P.mode & (MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
             S.expect_dec = ((P.mode & MODE_IAR) && !host) ? P.expect_dec[lr] : 0;
             S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
@@ -514,19 +517,34 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     bool peer_failed = false;
     uint64_t idle_since = 0;
     uint32_t idle_n = 0;
+    bool idle_prev = false;  // wave 0: the last iteration selected nothing
+    uint64_t p_in = 0, p_vin = 0, p_oh = 0, p_voh = 0, p_h = 0;  // wave 0: the last poll
+    uint32_t p_lat = 0;
 
     for (;;) {
         // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
         uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
-        uint32_t errf = 0, sid = 0;
+        uint32_t errf = 0, sid = 0, latr = 0;
         if (w == 0) {
-            // host mode: the host-written counters live in uncached VRAM (a local poll)
-            if (host && lane < 2) hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
-            if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
-            if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
-            if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
-            if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
-            if (lane == 0) errf = poll32(P.error_flag);
+            // After an iteration that selected nothing, wave 0 re-polls in a tight loop until a
+            // polled word moves (the other waves wait at the barrier): a message arriving at an
+            // idle rank is seen one poll round trip later instead of after a whole idle iteration.
+            // Bounded, so the idle clock and the deadline still tick.
+            for (uint32_t sp = 0;; sp++) {
+                // host mode: the host-written counters live in uncached VRAM (a local poll)
+                if (host && lane < 2) hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
+                if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
+                if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
+                if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
+                if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
+                if (lane == 0) errf = poll32(P.error_flag);
+                if ((P.mode & MODE_LAT) && lane == 1) latr = poll32(P.lat_round);  // the round in progress
+                if (!idle_prev || sp >= kIdleSpin) break;
+                const bool moved = in_tail_r != p_in || vin_tail_r != p_vin || out_head_r != p_oh ||
+                                   vout_head_r != p_voh || hpoll != p_h || latr != p_lat || errf != 0;
+                if (__ballot(moved)) break;
+            }
+            p_in = in_tail_r; p_vin = vin_tail_r; p_oh = out_head_r; p_voh = vout_head_r; p_h = hpoll; p_lat = latr;
             const int64_t sn = S.sched_next;
             if ((P.mode & MODE_STORM) && sn + lane < S.sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[P.sched_off[lr] + sn + lane];
@@ -675,8 +693,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
             if ((P.mode & MODE_LAT) && C < kMaxCand) {
-                while (S.lat_next < P.lat_rounds && P.lat_origin[S.lat_next] != me) S.lat_next++;
-                if (S.lat_next < P.lat_rounds && poll32(P.lat_round) == S.lat_next) { lat_id = S.lat_next; C++; }
+                // my next round (prefetched) starts when the previous round completed everywhere
+                if (S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
             }
             if (lane == 0) {
                 S.ract = ract;
@@ -689,6 +707,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             }
         }
         BAR();  // selection visible
+        PROF_STAMP(7);
         if (S.exit_now) break;  // the final counters are published
         const uint32_t R = S.R, C = S.C;
         const uint32_t nstorm = S.nstorm, storm_base = S.storm_base, loc_kind = S.loc_kind;
@@ -980,18 +999,17 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             const int vote = (int)(int8_t)(w0 >> 24);
             const uint32_t pseq = w2 >> 24;
             uint32_t logidx = ~0u;
+            bool lat_deliv = false;
+            uint32_t lat_tn = 0;
             if (admitted) {
                 if (kind == K_RING) {
                     if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
                         if (P.mode & (MODE_HIST | MODE_LAT)) {
                             const uint64_t tn = now_ticks();
                             if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)tn - t0)], 1u);
-                            if (P.mode & MODE_LAT) {
-                                uint32_t old = atomicAdd(&P.lat_count[id], 1u);
-                                if (old + 1u == (uint32_t)(P.n - 1)) {
-                                    P.lat_out[id] = (uint64_t)((uint32_t)tn - t0);
-                                    __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                }
+                            if (P.mode & MODE_LAT) {  // round bookkeeping after the forwards are issued (G)
+                                lat_deliv = true;
+                                lat_tn = (uint32_t)tn - t0;
                             }
                         }
                         // aux: device ticks (10 ns) from origination to this pickup (latency diagnostics)
@@ -1048,7 +1066,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     S.own_pid = -1;  // RLO_proposal_reset via RLO_get_vote_my_proposal (:1649-1673)
                     S.own_iter++;
                 } else if (kind == K_LAT) {
-                    S.lat_next = id + 1;
+                    const uint32_t np = S.lat_pos + 1u;
+                    S.lat_pos = np;
+                    S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
                 }
             }
             if (active) {
@@ -1185,6 +1205,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     stage_big();  // loads behind this iteration's stores drain in order (only when > stage2)
                 }
             }
+            if (lat_deliv) {  // latency program: the last of N-1 pickups completes the round
+                const uint32_t old = atomicAdd(&P.lat_count[id], 1u);
+                if (old + 1u == (uint32_t)(P.n - 1)) {
+                    P.lat_out[id] = (uint64_t)lat_tn;
+                    __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             PROF_STAMP(5);
         }
 
@@ -1263,10 +1290,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 bool done = true;
                 if (P.mode & MODE_STORM) done &= S.sched_next == S.sched_n;
                 if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == S.expect_bcast;
-                if (P.mode & MODE_LAT) {
-                    while (S.lat_next < P.lat_rounds && P.lat_origin[S.lat_next] != me) S.lat_next++;
-                    done &= S.lat_next >= P.lat_rounds;
-                }
+                if (P.mode & MODE_LAT) done &= S.lat_pos >= S.lat_pos_n;
                 if ((P.mode & MODE_IAR) && !host)
                     done &= S.own_iter == S.own_n && S.own_state == 0 && (int64_t)S.dec_delivered == S.expect_dec;
                 if (host) done = S.quit != 0;
@@ -1274,6 +1298,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (peer_failed) done = true;  // another rank failed: stop everyone
                 S.done = done;
             }
+            idle_prev = C == 0 && S.vtot == 0 && !S.done;
         }
         PROF_STAMP(6);
     }

@@ -272,6 +272,7 @@ struct rlo_world {
     rlo::Params P{};
     DevBuf<int64_t> d_sched_off, d_expect_bcast, d_prop_off, d_expect_dec;
     DevBuf<uint32_t> d_sched_ids, d_prop_data_off, d_prop_data_len, d_isp_off, d_lat_count, d_lat_round;
+    DevBuf<uint32_t> d_lat_own_off, d_lat_own;
     DevBuf<int32_t> d_lat_origin, d_prop_pid;
     DevBuf<uint64_t> d_lat_out;
     DevBuf<uint8_t> d_mask, d_prop_data, d_log_payload;
@@ -578,7 +579,7 @@ int rlo_world_destroy(rlo_world_t* w) {
     w->d_sched_off.release(); w->d_expect_bcast.release(); w->d_prop_off.release(); w->d_expect_dec.release();
     w->d_sched_ids.release(); w->d_prop_data_off.release(); w->d_prop_data_len.release(); w->d_isp_off.release();
     w->d_lat_count.release(); w->d_lat_round.release(); w->d_lat_origin.release(); w->d_prop_pid.release();
-    w->d_lat_out.release(); w->d_mask.release(); w->d_prop_data.release(); w->d_log_payload.release();
+    w->d_lat_out.release(); w->d_lat_own_off.release(); w->d_lat_own.release(); w->d_mask.release(); w->d_prop_data.release(); w->d_log_payload.release();
     w->d_isp.release(); w->d_log.release();
     if (w->h_cmd) (void)hipFree(w->h_cmd);
     if (w->d_ctl) (void)hipFree(w->d_ctl);
@@ -705,10 +706,19 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     for (uint32_t i = 0; i < rounds; i++) org[i] = (int32_t)(splitmix64(seed + i) % (uint64_t)n);
     for (int r = 0; r < n; r++)
         for (uint32_t i = 0; i < rounds; i++) expect[r] += org[i] != r;
+    // per local rank the rounds it originates, in order (the kernel prefetches the next one)
+    std::vector<uint32_t> own_off(w->nl + 1, 0), own;
+    for (int lr = 0; lr < w->nl; lr++) {
+        for (uint32_t i = 0; i < rounds; i++)
+            if (org[i] == w->rb + lr) own.push_back(i);
+        own_off[lr + 1] = (uint32_t)own.size();
+    }
+    if (own.empty()) own.push_back(0);
+    if (w->d_lat_own_off.upload(own_off) || w->d_lat_own.upload(own)) return RLO_E_HIP;
     if (w->d_lat_origin.upload(org) || w->d_expect_bcast.upload(expect) || w->d_lat_count.alloc(rounds) ||
         w->d_lat_out.alloc(rounds) || w->d_lat_round.alloc(1))
         return RLO_E_HIP;
-    P.mode = rlo::MODE_LAT | ((flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u);
+    P.mode = rlo::MODE_LAT | ((flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u) | ((flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
     P.len = len;
     P.seed = seed;
     P.lat_rounds = rounds;
@@ -716,6 +726,8 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     P.lat_count = w->d_lat_count.p;
     P.lat_out = w->d_lat_out.p;
     P.lat_round = w->d_lat_round.p;
+    P.lat_own_off = w->d_lat_own_off.p;
+    P.lat_own = w->d_lat_own.p;
     P.expect_bcast = w->d_expect_bcast.p;
     w->lat_rounds = rounds;
     int rc = setup_log(w, flags, 0, true);

@@ -89,8 +89,8 @@ class World:
         cfg = L.StormCfg(seed, k, length, window, flags, log_cap)
         check(self.lib.rlo_program_storm(self.h, ctypes.byref(cfg)), "rlo_program_storm")
 
-    def program_latency(self, rounds, length, seed=0x5EED, hist=False, log=False):
-        flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0)
+    def program_latency(self, rounds, length, seed=0x5EED, hist=False, log=False, prof=False):
+        flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0) | (L.RLO_FLAG_PROF if prof else 0)
         check(self.lib.rlo_program_latency(self.h, rounds, length, seed, flags), "rlo_program_latency")
         self._lat_rounds = rounds
 
