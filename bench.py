@@ -137,6 +137,39 @@ def dropin_api_leg(ranks=8, timeout_s=150):
     return out
 
 
+def size_legs(rlo, R, device, stream, sizes=(256, 1024, 4096), k=1 << 16, steps=3):
+    """The headline storm at SURVEY 8(d) C2's larger payloads (one GPU): bcast/s and the HBM
+    roofline fraction per size, 2(N-1)(S+16) algorithmic bytes per bcast as for `value`.  Every
+    step must deliver the same bytes (per-rank checksums equal across steps)."""
+    import numpy as np
+
+    out = []
+    with rlo.World(R, max_payload=max(sizes), device=device) as w:
+        for s in sizes:
+            w.program_storm(k, s, seed=0x5EED)
+            sums, kms, ok = [], [], True
+            t0 = 0.0
+            for i in range(steps + 1):  # first launch warms
+                if i == 1:
+                    t0 = time.perf_counter()
+                w.reset(stream)
+                w.launch(stream, no_reset=True)
+                ok &= w.wait(raise_on_device_error=False) == 0
+                st = w.stats()
+                ok &= bool((st["error"] == 0).all()) and int(st["originated"].sum()) == k
+                sums.append(st["bcast_sum"].copy())
+                if i:
+                    kms.append(w.kernel_ms())
+            dt = (time.perf_counter() - t0) / steps
+            ok &= all(np.array_equal(sums[0], x) for x in sums[1:])
+            kernel_ms = float(np.mean(kms))
+            gbs = k * 2.0 * (R - 1) * (s + 16) / (kernel_ms * 1e-3) / 1e9
+            out.append({"payload_bytes": s, "bcasts": k, "bcast_per_s": round(k / dt, 1),
+                        "deliveries_per_s": round(k * (R - 1) / dt, 1), "kernel_ms": round(kernel_ms, 3),
+                        "alg_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "verified": ok})
+    return out
+
+
 def bulk_leg(dist, world, rank, local, sizes_mib=(1, 4, 16, 64), iters=5, blocks=None):
     """BASELINE configs[2]: large-message rootless bcast (pipelined scatter + all-gather over the
     ranks' HBM buffers, rlo_bulk.hip) from rotating originators vs rooted RCCL broadcast of the
@@ -435,8 +468,14 @@ def main():
         extras["decisions_kernel_ms"] = round(max_over_ranks(ims), 3)
         ok &= rc == 0 and int(sum_over_ranks(float(ist["own_decided"].sum()))) == R * p * copies
         ok &= bool((ist["error"] == 0).all())
-    lib.rlo_stream_destroy(stream)
     w.close()
+    if not args.no_extras and world == 1:
+        # SURVEY 8(d) C2's payload sizes: the same storm at 256 B .. 4 KiB (roofline per size)
+        if rank == 0:
+            note("payload-size legs")
+        extras["payload_sizes"] = size_legs(rlo, R, local, stream)
+        ok &= all(s["verified"] for s in extras["payload_sizes"])
+    lib.rlo_stream_destroy(stream)
     if not args.no_bulk:
         if rank == 0:
             note("bulk leg")

@@ -18,6 +18,7 @@
  *   iar    ORIGIN MASK           single proposal, decline iff rank in MASK (arg != NULL)
  *   multi  ACTIVE1 MOD AGREE     test_iar_multi_proposal roles (testcases.c:401-486), logging decisions
  *   tests                        the reference's own test wrappers' return values
+ *   tests_safe                   the same, hacky-sack rounds run on every rank (see mode_tests_safe)
  *   tests2                       its two-engine IAR tests
  *   bench  K LEN                 storm throughput: every rank originates K bcasts
  *   lat    ROUNDS LEN SEED       unloaded latency: one random originator per round
@@ -300,6 +301,38 @@ static void mode_tests(void) {
     if (g_rank == 0) emit("{\"test\":\"test_iar_multi_proposal(1,3,1)\",\"ret\":%d}", r);
 }
 
+/* test_wrapper_hackysacking (testcases.c:726-740) stops a rank at its first failed round.  The
+ * pass flag of a round is message timing (a send inside RLO_bcast_gen's progress call can surface
+ * the next ball inside the same pickup loop, testcases.c:670-683 + rootless_ops.c:1602), and a
+ * rank that fails while its peers pass leaves them waiting in the next round's collective engine
+ * creation.  "tests_safe" runs every round on every rank (same hacky_sack_progress_engine, same
+ * result aggregation) so a timing-dependent flag can be checked instead of hanging. */
+int hacky_sack_progress_engine(MPI_Comm comm, int msg_cnt);                    /* testcases.c:638 */
+int aggregate_test_result(MPI_Comm comm, int test_passed, char* test_name);  /* testcases.c:615 */
+
+static int hackysacking_all_rounds(int cnt_round, int cnt_msg) {
+    MPI_Comm comm;
+    MPI_Comm_dup(MPI_COMM_WORLD, &comm);
+    int failed = 0;
+    for (int i = 0; i < cnt_round; i++)
+        if (hacky_sack_progress_engine(comm, cnt_msg) != 1) failed++;
+    return aggregate_test_result(comm, failed == 0, "Hackysack");
+}
+
+static void mode_tests_safe(void) {
+    int r;
+    r = test_wrapper_bcast(2);
+    if (g_rank == 0) emit("{\"test\":\"test_wrapper_bcast(2)\",\"ret\":%d}", r);
+    r = hackysacking_all_rounds(3, 100);
+    if (g_rank == 0) emit("{\"test\":\"test_wrapper_hackysacking(3,100)\",\"ret\":%d}", r);
+    r = test_IAllReduce_single_proposal(MPI_COMM_WORLD, 1, 2, 0);
+    if (g_rank == 0) emit("{\"test\":\"test_IAllReduce_single_proposal(1,2,0)\",\"ret\":%d}", r);
+    r = test_IAllReduce_single_proposal(MPI_COMM_WORLD, 1, 2, 1);
+    if (g_rank == 0) emit("{\"test\":\"test_IAllReduce_single_proposal(1,2,1)\",\"ret\":%d}", r);
+    r = test_iar_multi_proposal(MPI_COMM_WORLD, 1, 3, 1);
+    if (g_rank == 0) emit("{\"test\":\"test_iar_multi_proposal(1,3,1)\",\"ret\":%d}", r);
+}
+
 /* the reference's two-engine tests (testcases.c:110-241, :488-595) */
 int test_concurrent_iar_single_proposal(MPI_Comm comm, int starter, int no_rank, int agree);
 int test_concurrent_iar_multi_proposal(MPI_Comm comm, int active_1, int active_2_mod, int agree);
@@ -449,6 +482,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(mode, "iar")) mode_iar(atoi(argv[3]), (unsigned)strtoul(argv[4], 0, 0));
     else if (!strcmp(mode, "multi")) mode_multi(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
     else if (!strcmp(mode, "tests")) mode_tests();
+    else if (!strcmp(mode, "tests_safe")) mode_tests_safe();
     else if (!strcmp(mode, "tests2")) mode_tests2();
     else if (!strcmp(mode, "bench")) mode_bench(atoi(argv[3]), atoi(argv[4]));
     else if (!strcmp(mode, "lat")) mode_lat(atoi(argv[3]), atoi(argv[4]), strtoull(argv[5], 0, 0));

@@ -14,11 +14,12 @@
 // on every tree edge, and consecutive chunks' phases overlap.  Parity for a bulk bcast is
 // byte-exact delivery to all N-1 ranks (tests/test_gpu_bulk.py).
 //
-// Memory ordering (MI355X_MICROARCH.md "Valid forms", row 1, at system scope): every handed-off
-// byte is stored sc0 sc1 and every storing wave drains vmcnt(0) before its workgroup barrier; one
-// lane per destination then adds to the flag with a system-scope atomic.  A receiver polls with
-// one lane, joins a barrier, and every wave loads the bytes with sc0 sc1 loads.  Buffers are
-// allocated uncached.  Work is split in 1-KiB blocks so that a wave's destination is uniform.
+// Memory ordering (MI355X_MICROARCH.md "Valid forms", first bullet, at system scope): every
+// handed-off byte is stored sc0 sc1 and every storing wave drains vmcnt(0) before its workgroup
+// barrier; wave 0 then runs a system release (+ explicit vmcnt(0)) and one lane per destination
+// adds to the flag with a system-scope atomic.  A receiver polls with one lane, runs a system
+// acquire, joins a barrier, and every wave loads the bytes (sc0 sc1).  Buffers are allocated
+// uncached.  Work is split in 1-KiB blocks so that a wave's destination is uniform.
 #include <hip/hip_runtime.h>
 
 #include "rlo_device.hpp"
@@ -46,6 +47,19 @@ __device__ bool bk_wait(uint32_t* p, uint32_t target, uint64_t deadline, uint32_
         }
     }
     return true;
+}
+
+// System-scope release / acquire around the flags (MI355X_MICROARCH.md "Valid forms", first
+// bullet; the sc1-loads-instead-of-acquire form is measured for hipMalloc memory and agent-scope
+// flags only, while these buffers are uncached and the flags system scope).  The wait after the
+// release is explicit: the compiler may drop it (same section, "Compiler hazard").
+__device__ __forceinline__ void bk_release() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void bk_acquire() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __global__ __launch_bounds__(256) void rlo_bulk_kernel(BulkParams P) {
@@ -85,12 +99,18 @@ __global__ __launch_bounds__(256) void rlo_bulk_kernel(BulkParams P) {
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid < n - 1) {  // one lane per owner: this workgroup's share of chunk c has landed
-                const int owner = (o + 1 + tid) % n;
-                __hip_atomic_fetch_add(&P.sflag[owner][c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tid < 64) {  // wave 0 releases, then one lane per owner: this workgroup's share has landed
+                bk_release();
+                if (tid < n - 1) {
+                    const int owner = (o + 1 + tid) % n;
+                    __hip_atomic_fetch_add(&P.sflag[owner][c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         } else {  // ---- all-gather: my stripe of chunk c, once the originator delivered it
-            if (tid == 0 && !bk_wait(&P.sflag[me][c], B, deadline, P.err)) ok = 0;
+            if (tid == 0) {
+                if (!bk_wait(&P.sflag[me][c], B, deadline, P.err)) ok = 0;
+                bk_acquire();
+            }
             __syncthreads();
             if (!ok) break;
             const uint32_t s0 = (uint32_t)kme * slen;
@@ -118,10 +138,13 @@ __global__ __launch_bounds__(256) void rlo_bulk_kernel(BulkParams P) {
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid < n - 1) {
-                const int dst = (o + 1 + tid) % n;
-                if (dst != me)
-                    __hip_atomic_fetch_add(&P.gflag[dst][c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tid < 64) {
+                bk_release();
+                if (tid < n - 1) {
+                    const int dst = (o + 1 + tid) % n;
+                    if (dst != me)
+                        __hip_atomic_fetch_add(&P.gflag[dst][c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
     }

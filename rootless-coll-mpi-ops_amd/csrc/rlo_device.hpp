@@ -40,6 +40,8 @@ enum Mode : uint32_t {
     MODE_LOG = 16u,    // record every event (+ delivered payload bytes) for parity tests
     MODE_HIST = 32u,   // per-delivery latency histogram
     MODE_PROF = 64u,   // per-phase shader-clock accounting (diagnostic build of the same kernel)
+    MODE_LAZYPUB = 256u,  // diagnostic: publish counters after the next poll (the pre-eager scheme)
+    MODE_NOSPIN = 512u,   // diagnostic: no tight re-poll after an idle iteration
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };

@@ -972,6 +972,14 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
         if (rc) return rc;
     }
     HIPCHK(hipEventRecord(w->ev0, s));
+    // diagnostic A/B switch: publish producer counters after the next poll instead of at the end
+    // of the iteration that drained the stores
+    static const bool lazy = std::getenv("RLO_LAZY_PUB") != nullptr;
+    if (lazy) w->P.mode |= rlo::MODE_LAZYPUB;
+    else w->P.mode &= ~rlo::MODE_LAZYPUB;
+    static const bool nospin = std::getenv("RLO_NO_IDLE_SPIN") != nullptr;  // diagnostic
+    if (nospin) w->P.mode |= rlo::MODE_NOSPIN;
+    else w->P.mode &= ~rlo::MODE_NOSPIN;
     hipError_t e = rlo_launch_progress(&w->P, w->nl, w->dyn_lds, s);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));

@@ -97,6 +97,7 @@ struct progress_engine {
     // RLO_TRACE=1: counters printed at cleanup (diagnostics)
     uint64_t n_progress = 0, n_events = 0, n_pumped = 0, n_judge = 0, n_result = 0;
     int64_t t_submit = 0, sum_prop_ns = 0, max_prop_ns = 0;
+    int64_t t_moved = 0, t_dump = 0;  // RLO_WATCHDOG: last event / last state dump
     progress_engine* next = nullptr;
 };
 
@@ -350,6 +351,24 @@ bool pump(progress_engine* e) {
     return got || e->backlog.size() != backlog0;
 }
 
+// RLO_WATCHDOG=seconds (diagnostics): an engine whose application keeps calling progress but
+// sees no event for that long prints its host- and ring-side state once per period
+void watchdog(progress_engine* e, bool moved, int64_t period_ns) {
+    const int64_t t = now_ns();
+    if (moved || e->t_moved == 0) { e->t_moved = t; return; }
+    if (t - e->t_moved < period_ns || t - e->t_dump < period_ns) return;
+    e->t_dump = t;
+    std::lock_guard<std::mutex> lk(e->mu);  // backlog / evq are shared with the pump thread
+    uint64_t consumed = 0, posted = 0;
+    rlo_host_cmd_count(e->w, e->rank, &consumed, &posted);
+    std::fprintf(stderr, "rlo watchdog rank %d engine %d: %.1f s without events; sent %ld recved %ld pickup %zu "
+                 "backlog %zu wait %zu evq %zu commands consumed %llu / posted %llu, kernel running %d, "
+                 "progress calls %llu events %llu\n", e->rank, e->id, (t - e->t_moved) * 1e-9, e->sent_bcast,
+                 e->recved_bcast, e->pickup.size(), e->backlog.size(), e->wait.size(), e->evq.size(),
+                 (unsigned long long)consumed, (unsigned long long)posted, rlo_host_running(e->w),
+                 (unsigned long long)e->n_progress, (unsigned long long)e->n_events);
+}
+
 // make_progress_gen (:551-641): everything the device finished since the last call
 void progress(progress_engine* e) {
     if (!e->w || e->failed) return;
@@ -374,6 +393,8 @@ void progress(progress_engine* e) {
     e->n_events += local.size();
     for (const RawEv& q : local) handle_event(e, q.ev, q.payload.data());
     if (local.empty() && (++e->poll_tick & 255u) == 0) check_alive(e);
+    static const double wd = std::getenv("RLO_WATCHDOG") ? std::atof(std::getenv("RLO_WATCHDOG")) : 0.0;
+    if (wd > 0) watchdog(e, !local.empty(), (int64_t)(wd * 1e9));
 }
 
 // ---- the pump thread: one per process while engines exist; it only moves ring entries

@@ -25,28 +25,42 @@ def _fill(t, nbytes, seed):
     t[:nbytes].copy_(torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g))
 
 
-@pytest.mark.parametrize("n,nbytes,origin,blocks,chunk", [
-    (2, 1 << 20, 1, 8, 0), (3, 3 * (1 << 20) + 123, 0, 16, 0), (8, 4 << 20, 5, 16, 0),
-    (8, 1000, 7, 4, 0), (5, (1 << 20) + 16, 2, 8, 64 << 10), (16, 2 << 20, 9, 8, 0)])
-def test_bulk_one_part(rlo, n, nbytes, origin, blocks, chunk):
+def _check(b, n, origin, nbytes, src, rep):
+    import torch
+
+    for r in range(n):
+        if r == origin:
+            continue
+        got = b.tensor(r)[:nbytes]
+        if not torch.equal(got, src[:nbytes]):
+            bad = torch.nonzero(got != src[:nbytes]).flatten()
+            stale = int((got[bad] == 0xA5).sum())
+            raise AssertionError("rank %d rep %d: %d bytes differ in [%d, %d], %d still 0xA5" %
+                                 (r, rep, bad.numel(), int(bad[0]), int(bad[-1]), stale))
+
+
+@pytest.mark.parametrize("n,nbytes,origin,blocks,chunk,reps", [
+    (2, 1 << 20, 1, 8, 0, 2), (3, 3 * (1 << 20) + 123, 0, 16, 0, 2), (8, 4 << 20, 5, 16, 0, 2),
+    (8, 1000, 7, 4, 0, 2), (5, (1 << 20) + 16, 2, 8, 64 << 10, 2), (16, 2 << 20, 9, 8, 0, 2),
+    (3, 3 * (1 << 20) + 123, 0, 16, 0, 40), (8, (4 << 20) + 80, 3, 32, 0, 40)])
+def test_bulk_one_part(rlo, n, nbytes, origin, blocks, chunk, reps):
     import torch
 
     from rlo.bulk import Bulk
 
     with rlo.World(n, max_payload=64) as w, Bulk(w, 8 << 20) as b:
         b.connect([b.export()])
-        for r in range(n):  # stale bytes must be overwritten, not trusted
-            b.tensor(r).fill_(0xA5)
         src = b.tensor(origin)
         _fill(src, nbytes, seed=n * 1000 + origin)
-        torch.cuda.synchronize()
-        for rep in range(2):  # reusable: flags reset between bcasts
+        for rep in range(reps):  # reusable: flags reset between bcasts
+            for r in range(n):  # stale bytes must be overwritten, not trusted
+                if r != origin:
+                    b.tensor(r).fill_(0xA5)
+            torch.cuda.synchronize()
             b.reset()
             b.launch(origin, nbytes, blocks=blocks, chunk=chunk)
             b.wait()
-            for r in range(n):
-                if r != origin:
-                    assert torch.equal(b.tensor(r)[:nbytes], src[:nbytes]), (r, rep)
+            _check(b, n, origin, nbytes, src, rep)
 
 
 def test_bulk_two_parts_inprocess(rlo):

@@ -1,0 +1,56 @@
+"""Repeat a small logged storm and report every delivered payload that differs from the oracle's
+bytes, with what the wrong bytes match (another bcast's payload = a stale ring slot; zeros = not
+yet written).  python tools/stress_storm_logged.py [--n 4 --k 64 --len 64 --seed 7 --reps 200]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rootless-coll-mpi-ops_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import pyoracle as orc  # noqa: E402
+import rlo  # noqa: E402
+
+LOG_DELIVER = 1
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=4)
+ap.add_argument("--k", type=int, default=64)
+ap.add_argument("--len", type=int, default=64)
+ap.add_argument("--seed", type=int, default=7)
+ap.add_argument("--reps", type=int, default=200)
+ap.add_argument("--max-payload", type=int, default=4096)
+a = ap.parse_args()
+n, k, ln, seed = a.n, a.k, a.len, a.seed
+want = {b: orc.payload(orc.origin_of(seed, b, n), b, ln) for b in range(k)}
+ref = orc.storm(n, seed, k, ln)
+bad_runs = 0
+with rlo.World(n, max_payload=a.max_payload) as w:
+    for rep in range(a.reps):
+        w.program_storm(k, ln, seed=seed, log=True, log_cap=k + 8)
+        w.run()
+        st = w.stats()
+        sums_ok = np.array_equal(st["bcast_sum"], ref["sum"])
+        found = []
+        for r in range(n):
+            rows, payload = w.log(r, cap=k + 8, payload=True)
+            for row in rows:
+                if row[0] != LOG_DELIVER:
+                    continue
+                bid, idx = row[4], row[8]
+                got = bytes(payload[idx][:ln])
+                if got != want[bid]:
+                    diff = [i for i in range(ln) if got[i] != want[bid][i]]
+                    like = [b for b in range(k) if b != bid and want[b][diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16]
+                            == got[diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16]]
+                    found.append("rank %d bid %d origin %d parent %d: %d bytes differ (first %d, last %d), "
+                                 "16-B chunk like bids %s, zero chunk %s" %
+                                 (r, bid, row[2], row[3], len(diff), diff[0], diff[-1], like[:4],
+                                  got[diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16] == bytes(16)))
+        if found or not sums_ok:
+            bad_runs += 1
+            print("rep %d: sums_ok %s" % (rep, sums_ok), flush=True)
+            for f in found[:10]:
+                print("   " + f, flush=True)
+print("bad runs: %d of %d" % (bad_runs, a.reps), flush=True)
