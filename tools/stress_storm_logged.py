@@ -33,12 +33,18 @@ with rlo.World(n, max_payload=a.max_payload) as w:
         st = w.stats()
         sums_ok = np.array_equal(st["bcast_sum"], ref["sum"])
         found = []
+        orig_st = st["originated"].astype(np.int64).tolist()
+        orig_ref = [sum(1 for b in range(k) if orc.origin_of(seed, b, n) == r) for r in range(n)]
+        if orig_st != orig_ref:
+            found.append("originated per rank %s, oracle %s" % (orig_st, orig_ref))
         for r in range(n):
             rows, payload = w.log(r, cap=k + 8, payload=True)
             for row in rows:
                 if row[0] != LOG_DELIVER:
                     continue
                 bid, idx = row[4], row[8]
+                if row[2] != orc.origin_of(seed, bid, n):
+                    found.append("rank %d bid %d: origin %d, oracle %d" % (r, bid, row[2], orc.origin_of(seed, bid, n)))
                 got = bytes(payload[idx][:ln])
                 if got != want[bid]:
                     diff = [i for i in range(ln) if got[i] != want[bid][i]]
