@@ -42,6 +42,7 @@ enum Mode : uint32_t {
     MODE_PROF = 64u,   // per-phase shader-clock accounting (diagnostic build of the same kernel)
     MODE_LAZYPUB = 256u,  // diagnostic: publish counters after the next poll (the pre-eager scheme)
     MODE_NOSPIN = 512u,   // diagnostic: no tight re-poll after an idle iteration
+    MODE_NOACQ = 1024u,   // diagnostic (UNSAFE): no agent acquire between iterations (A/B of its cost)
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };

@@ -121,6 +121,12 @@ struct Shared {
         asm volatile("" ::: "memory");                     \
     } while (0)
 #define VM_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+// agent-scope acquire without the leading vmcnt(0) of __builtin_amdgcn_fence: callers have drained
+// their loads already (MODE_NOACQ: diagnostic A/B of its cost, unsafe)
+#define ACQ_NEXT()                                                             \
+    do {                                                                       \
+        if (!(P.mode & MODE_NOACQ)) asm volatile("buffer_inv sc1" ::: "memory"); \
+    } while (0)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
@@ -761,6 +767,15 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
             VM_DRAIN();  // this wave's stage loads (wave 1: and its vote loads)
+            // Agent acquire for the NEXT iteration's ring loads.  LDS-DMA is not a load to registers,
+            // so its sc1 bit is not the measured stand-in for an acquire (MI355X_MICROARCH.md, "Valid
+            // forms"): a 128-B line staged now also holds the head of the next slot (stride S + 16),
+            // maybe not yet written, and an L1 copy of it staged next iteration would be stale (seen:
+            // zero / previous-world headers in ~1 of 10 suite runs).  This wave's ring loads are
+            // drained, so none refills L1 behind the invalidate; it completes under the rest of the
+            // iteration, and phase A's VM_DRAIN (or the eager drain) waits for it before any wave
+            // stages again.  stage_big() repeats it after its own LDS-DMA loads.
+            ACQ_NEXT();
             PROF_STAMP(1);
 
             // ---------------- B1 (wave 1): merge the votes (_iar_vote_handler :743-812)
@@ -1142,6 +1157,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     }
                 }
                 VM_DRAIN();
+                ACQ_NEXT();  // this wave's LDS-DMA of ring slots (see D0)
             };
             if (nbig) {
                 if (tid == 0) { S.bm = 0; S.bq0 = 0; }

@@ -980,6 +980,9 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool nospin = std::getenv("RLO_NO_IDLE_SPIN") != nullptr;  // diagnostic
     if (nospin) w->P.mode |= rlo::MODE_NOSPIN;
     else w->P.mode &= ~rlo::MODE_NOSPIN;
+    static const bool noacq = std::getenv("RLO_NO_ACQUIRE") != nullptr;  // diagnostic A/B, unsafe
+    if (noacq) w->P.mode |= rlo::MODE_NOACQ;
+    else w->P.mode &= ~rlo::MODE_NOACQ;
     hipError_t e = rlo_launch_progress(&w->P, w->nl, w->dyn_lds, s);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));

@@ -21,42 +21,82 @@ ap.add_argument("--len", type=int, default=64)
 ap.add_argument("--seed", type=int, default=7)
 ap.add_argument("--reps", type=int, default=200)
 ap.add_argument("--max-payload", type=int, default=4096)
+ap.add_argument("--fresh", action="store_true",
+                help="a new World per rep, n alternating n / n+1 (the test suite's allocation pattern); "
+                     "a mismatching log is read a second time to tell a stale read from a wrong delivery")
 a = ap.parse_args()
 n, k, ln, seed = a.n, a.k, a.len, a.seed
-want = {b: orc.payload(orc.origin_of(seed, b, n), b, ln) for b in range(k)}
-ref = orc.storm(n, seed, k, ln)
+
+
+def check(w, n, reps_tag):
+    want = {b: orc.payload(orc.origin_of(seed, b, n), b, ln) for b in range(k)}
+    ref = orc.storm(n, seed, k, ln, want_parent=True)
+    st = w.stats()
+    sums_ok = np.array_equal(st["bcast_sum"], ref["sum"])
+    found = []
+    orig_st = st["originated"].astype(np.int64).tolist()
+    orig_ref = [sum(1 for b in range(k) if orc.origin_of(seed, b, n) == r) for r in range(n)]
+    if orig_st != orig_ref:
+        found.append("originated per rank %s, oracle %s" % (orig_st, orig_ref))
+    bad_ranks = []
+    for r in range(n):
+        rows, payload = w.log(r, cap=k + 8, payload=True)
+        nbad = 0
+        for row in rows:
+            if row[0] != LOG_DELIVER:
+                found.append("rank %d: record kind %d" % (r, row[0]))
+                nbad += 1
+                continue
+            bid, idx = row[4], row[8]
+            if bid >= k or row[2] != orc.origin_of(seed, bid, n) or row[3] != int(ref["parent"][bid, r]):
+                found.append("rank %d bid %d: origin %d parent %d (oracle %s)" %
+                             (r, bid, row[2], row[3],
+                              (orc.origin_of(seed, bid, n), int(ref["parent"][bid, r])) if bid < k else "-"))
+                nbad += 1
+                continue
+            got = bytes(payload[idx][:ln])
+            if got != want[bid]:
+                nbad += 1
+                diff = [i for i in range(ln) if got[i] != want[bid][i]]
+                like = [b for b in range(k) if b != bid and want[b][diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16]
+                        == got[diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16]]
+                found.append("rank %d bid %d origin %d parent %d: %d bytes differ (first %d, last %d), "
+                             "16-B chunk like bids %s, zero chunk %s" %
+                             (r, bid, row[2], row[3], len(diff), diff[0], diff[-1], like[:4],
+                              got[diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16] == bytes(16)))
+        if nbad:
+            bad_ranks.append((r, nbad, len(rows)))
+    return sums_ok, found, bad_ranks
+
+
 bad_runs = 0
+if a.fresh:
+    import torch
+    for rep in range(a.reps):
+        nn = n + (rep & 1)
+        with rlo.World(nn, max_payload=a.max_payload) as w:
+            w.program_storm(k, ln, seed=seed, log=True, log_cap=k + 8)
+            w.run()
+            sums_ok, found, bad_ranks = check(w, nn, rep)
+            if found or not sums_ok:
+                bad_runs += 1
+                print("rep %d n %d: sums_ok %s, bad (rank, records, of) %s" % (rep, nn, sums_ok, bad_ranks), flush=True)
+                for f in found[:10]:
+                    print("   " + f, flush=True)
+                torch.cuda.synchronize()
+                s2, f2, b2 = check(w, nn, rep)
+                print("   second read after a device sync: %d findings, bad %s" % (len(f2), b2), flush=True)
+    print("bad runs: %d of %d" % (bad_runs, a.reps), flush=True)
+    sys.exit(0)
+
 with rlo.World(n, max_payload=a.max_payload) as w:
     for rep in range(a.reps):
         w.program_storm(k, ln, seed=seed, log=True, log_cap=k + 8)
         w.run()
-        st = w.stats()
-        sums_ok = np.array_equal(st["bcast_sum"], ref["sum"])
-        found = []
-        orig_st = st["originated"].astype(np.int64).tolist()
-        orig_ref = [sum(1 for b in range(k) if orc.origin_of(seed, b, n) == r) for r in range(n)]
-        if orig_st != orig_ref:
-            found.append("originated per rank %s, oracle %s" % (orig_st, orig_ref))
-        for r in range(n):
-            rows, payload = w.log(r, cap=k + 8, payload=True)
-            for row in rows:
-                if row[0] != LOG_DELIVER:
-                    continue
-                bid, idx = row[4], row[8]
-                if row[2] != orc.origin_of(seed, bid, n):
-                    found.append("rank %d bid %d: origin %d, oracle %d" % (r, bid, row[2], orc.origin_of(seed, bid, n)))
-                got = bytes(payload[idx][:ln])
-                if got != want[bid]:
-                    diff = [i for i in range(ln) if got[i] != want[bid][i]]
-                    like = [b for b in range(k) if b != bid and want[b][diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16]
-                            == got[diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16]]
-                    found.append("rank %d bid %d origin %d parent %d: %d bytes differ (first %d, last %d), "
-                                 "16-B chunk like bids %s, zero chunk %s" %
-                                 (r, bid, row[2], row[3], len(diff), diff[0], diff[-1], like[:4],
-                                  got[diff[0] // 16 * 16:(diff[0] // 16 + 1) * 16] == bytes(16)))
+        sums_ok, found, bad_ranks = check(w, n, rep)
         if found or not sums_ok:
             bad_runs += 1
-            print("rep %d: sums_ok %s" % (rep, sums_ok), flush=True)
+            print("rep %d: sums_ok %s, bad %s" % (rep, sums_ok, bad_ranks), flush=True)
             for f in found[:10]:
                 print("   " + f, flush=True)
 print("bad runs: %d of %d" % (bad_runs, a.reps), flush=True)
