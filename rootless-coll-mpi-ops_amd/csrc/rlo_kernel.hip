@@ -121,8 +121,8 @@ struct Shared {
         asm volatile("" ::: "memory");                     \
     } while (0)
 #define VM_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-// agent-scope acquire without the leading vmcnt(0) of __builtin_amdgcn_fence: callers have drained
-// their loads already (MODE_NOACQ: diagnostic A/B of its cost, unsafe)
+// agent-scope acquire after LDS-DMA of ring slots (large messages), without the leading vmcnt(0)
+// of __builtin_amdgcn_fence: callers have drained their loads (MODE_NOACQ: diagnostic A/B, unsafe)
 #define ACQ_NEXT()                                                             \
     do {                                                                       \
         if (!(P.mode & MODE_NOACQ)) asm volatile("buffer_inv sc1" ::: "memory"); \
@@ -741,41 +741,55 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
 
-            // ---------------- D0: this wave's ring slots -> LDS (LDS-DMA), coalesced per in-ring run
+            // ---------------- D0: this wave's ring slots -> registers (sc1 loads) -> LDS, ONE round trip.
+            // Loads to registers, not LDS-DMA: sc1 loads to registers behind the counter poll are the
+            // measured hand-off form without an acquire (MI355X_MICROARCH.md, "Valid forms", row 1);
+            // LDS-DMA is not (its lines can stay in L1, and a 128-B line also holds the head of the
+            // next, maybe unwritten, slot: seen as stale headers in ~1 of 10 suite runs).
             const uint32_t c_lo = (uint32_t)w * kPass, c_hi = min(c_lo + kPass, R);
             if (c_lo < c_hi) {
-                for (uint64_t m = S.ract; m; m &= m - 1) {  // active in-rings (uniform loop)
+                // lane g = in-ring g: its run of candidates, read once (no LDS round trip per ring)
+                uint32_t gb = 0, ge = 0, gdat = 0;
+                uint64_t gh = 0;
+                if (lane < n_in2) {
+                    gb = S.ring_base[lane];
+                    ge = gb + S.ring_take[lane];
+                    gh = S.ring_head[lane];
+                    gdat = t.in_data[lane >> 1][lane & 1];
+                }
+                const uint64_t hit = __ballot(lane < n_in2 && max(gb, c_lo) < min(ge, c_hi));
+                // lane = candidate c_lo + lane: its in-ring and slot offset
+                const uint32_t cc = c_lo + (uint32_t)lane;
+                uint32_t src = 0;
+                for (uint64_t m = hit; m; m &= m - 1) {  // rings with candidates in this wave (uniform loop)
                     const int g = __builtin_ctzll(m);
-                    const uint32_t gb = S.ring_base[g], ge = gb + S.ring_take[g];
-                    const uint32_t lo = max(gb, c_lo), hi = min(ge, c_hi);
-                    if (lo >= hi) continue;
-                    const uint64_t head = S.ring_head[g] + (lo - gb);
-                    const uint32_t gdat = t.in_data[g >> 1][g & 1];
-                    const uint32_t nit = (hi - lo) * nsmall;
-                    for (uint32_t i0 = 0; i0 < nit; i0 += 64) {
-                        const uint32_t i = i0 + lane;
-                        if (i < nit) {
-                            const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
-                            const uint32_t off = gdat + (uint32_t)((head + mi) & fcap_m) * P.fwd_stride;
-                            if (q == 0) {
-                                S.cand[lo + mi].src = off;
-                                S.cand[lo + mi].group = (uint32_t)g;
-                            }
-                            dma16(rf, STG(lo, 0) + (i0 << 4), off + 16u * q);
-                        }
+                    const uint32_t b0 = rdl32(gb, g), e0 = rdl32(ge, g), gd = rdl32(gdat, g);
+                    const uint64_t h0 = rdl64(gh, g);
+                    if (cc >= b0 && cc < e0) {
+                        src = gd + (uint32_t)((h0 + (cc - b0)) & fcap_m) * P.fwd_stride;
+                        S.cand[cc].src = src;
+                        S.cand[cc].group = (uint32_t)g;
                     }
                 }
+                // item i = (candidate i / nsmall, chunk i % nsmall); nsmall <= 8, so <= 8 loads per lane
+                const uint32_t nit = (c_hi - c_lo) * nsmall;
+                u32x4 sv[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    if ((uint32_t)u * 64u < nit) {  // uniform: every lane takes part in the shuffle
+                        const uint32_t i = (uint32_t)u * 64u + (uint32_t)lane;
+                        const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
+                        const uint32_t so = (uint32_t)__shfl((int)src, (int)(mi & 63u));
+                        if (i < nit) sv[u] = ld_sc1(rf, so + 16u * q);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t i = (uint32_t)u * 64u + (uint32_t)lane;
+                    if (i < nit) *reinterpret_cast<u32x4*>(STG(c_lo, 0) + (i << 4)) = sv[u];
+                }
             }
-            VM_DRAIN();  // this wave's stage loads (wave 1: and its vote loads)
-            // Agent acquire for the NEXT iteration's ring loads.  LDS-DMA is not a load to registers,
-            // so its sc1 bit is not the measured stand-in for an acquire (MI355X_MICROARCH.md, "Valid
-            // forms"): a 128-B line staged now also holds the head of the next slot (stride S + 16),
-            // maybe not yet written, and an L1 copy of it staged next iteration would be stale (seen:
-            // zero / previous-world headers in ~1 of 10 suite runs).  This wave's ring loads are
-            // drained, so none refills L1 behind the invalidate; it completes under the rest of the
-            // iteration, and phase A's VM_DRAIN (or the eager drain) waits for it before any wave
-            // stages again.  stage_big() repeats it after its own LDS-DMA loads.
-            ACQ_NEXT();
+            VM_DRAIN();  // wave 1: its vote loads
             PROF_STAMP(1);
 
             // ---------------- B1 (wave 1): merge the votes (_iar_vote_handler :743-812)
@@ -1157,7 +1171,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     }
                 }
                 VM_DRAIN();
-                ACQ_NEXT();  // this wave's LDS-DMA of ring slots (see D0)
+                // agent acquire (without the leading vmcnt(0) of the fence builtin: drained above):
+                // these LDS-DMA loads may leave lines in L1 that straddle into the next, maybe
+                // unwritten, slot, and the next iteration must not read them from there.  It completes
+                // under the stores, and phase A's VM_DRAIN (or the eager drain) waits for it
+                ACQ_NEXT();
             };
             if (nbig) {
                 if (tid == 0) { S.bm = 0; S.bq0 = 0; }

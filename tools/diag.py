@@ -6,7 +6,9 @@ sys.path.insert(0, os.path.join(REPO, "rootless-coll-mpi-ops_amd"))
 import numpy as np
 import rlo
 
-PH = ["poll", "votes+select", "classify", "admit", "effects", "copy", "publish"]
+# prof[] slots in the kernel's stamp order: 0 poll (+drain), 1 stage (LDS-DMA + vote loads), 2 classify,
+# 3 admit, 4 effects, 5 copy, 6 consume (bookkeeping + eager publish), 7 select
+PH = ["poll", "stage", "classify", "admit", "effects", "copy", "consume", "select"]
 
 
 def report(name, w, ms, deliveries):
@@ -14,7 +16,7 @@ def report(name, w, ms, deliveries):
     it = st["iterations"].astype(np.float64)
     busy = st["busy_iterations"].astype(np.float64)
     prof = st["prof"].astype(np.float64)
-    cyc_per_it = prof.sum(axis=0)[:7] / it.sum()
+    cyc_per_it = prof.sum(axis=0)[:8] / it.sum()
     print("%-28s kernel %.3f ms | iters/rank %.0f busy %.0f | deliveries/busy-iter %.1f | stalls/rank %.0f | err %d"
           % (name, ms, it.mean(), busy.mean(), deliveries / max(busy.sum(), 1), st["stalls"].mean(), st["error"].max()))
     print("   cycles/iter: " + "  ".join("%s %.0f" % (p, c) for p, c in zip(PH, cyc_per_it)) + "  | total %.0f" % cyc_per_it.sum())
