@@ -604,8 +604,30 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             const uint32_t reserve = host ? kPass + 1u : ((P.mode & MODE_IAR) ? 2u : 0u);  // host: stage block + decision
             const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
-            const uint32_t quota = nact ? min(kMaxCand - reserve, hlim) / (uint32_t)nact : 0u;
-            const uint32_t take = hblock ? 0u : min(min(ra, quota), win_r);
+            // max-min fair (water-filling) quotas: a ring's share that a short ring leaves unused goes
+            // to the long rings, so a rank fed mostly by one hot parent (a wall rank) drains it in big
+            // batches instead of 256/nact per iteration (the per-iteration cost hardly depends on the
+            // batch size)
+            const uint32_t budget = min(kMaxCand - reserve, hlim);
+            const uint32_t want = hblock ? 0u : min(ra, win_r);
+            uint32_t take = want;
+            {
+                uint32_t wtot = 0;
+                if (nact) wave_excl_scan(want, &wtot);
+                if (wtot > budget) {
+                    uint32_t lvl = budget / (uint32_t)nact;
+                    for (int it = 0; it < 4; it++) {
+                        uint32_t s = 0;
+                        wave_excl_scan(min(want, lvl), &s);
+                        const uint32_t nabove = (uint32_t)__popcll(__ballot(want > lvl));
+                        if (!nabove || s >= budget) break;
+                        const uint32_t add = (budget - s) / nabove;
+                        if (!add) break;
+                        lvl += add;
+                    }
+                    take = min(want, lvl);
+                }
+            }
             const bool backlog = __ballot(ra > take) != 0;
             uint32_t R;
             const uint32_t base = wave_excl_scan(take, &R);
