@@ -187,6 +187,9 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
     return ((uint64_t)rdl32((uint32_t)(v >> 32), l) << 32) | rdl32((uint32_t)v, l);
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)(uint32_t)uni((int)(v >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)v);
+}
 
 // i / d for the small d = nsmall (<= 8) and i < 2^16: multiply-high by ceil(2^32 / d)
 __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { return magic ? __umulhi(i, magic) : i; }
@@ -511,14 +514,17 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     const uint32_t inbox = (uint32_t)uni((int)t.inbox_ctrl), outbox = (uint32_t)uni((int)t.outbox_ctrl);
     const uint32_t sl_r = lane < sll ? (uint32_t)t.send_list[lane] : 0u;
     const bool sys = P.sys_scope != 0;
-    const uint64_t oring_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;  // out-ring data (child's part)
     const uint32_t oring_bytes = P.fwd_cap * P.fwd_stride;
     // wave 0 owns the ring counters: lane g = in-ring g, lane oi = out-ring oi, lane j = vote ring j;
     // each counter is published by a store into the part that polls it
-    const uint64_t otptr_r = lane < nout ? t.out_tail[lane >> 1][lane & 1] : 0ull;
-    const uint64_t ihptr_r = lane < n_in2 ? t.in_head[lane >> 1][lane & 1] : 0ull;
-    const uint64_t vhptr_r = lane < sll ? t.vin_head[lane] : 0ull;
-    const uint64_t vtptr_r = lane < n_in ? t.vout_tail[lane] : 0ull;
+    // remote counter / ring addresses are read from the LDS copy of the topology where they are
+    // used (lane = out-ring / in-ring / vote ring), not kept in registers: the kernel sits at the
+    // VGPR limit of two waves per SIMD
+#define OTPTR t.out_tail[lane >> 1][lane & 1]
+#define IHPTR t.in_head[lane >> 1][lane & 1]
+#define VHPTR t.vin_head[lane]
+#define VTPTR t.vout_tail[lane]
+#define ORING(oi) uni64(t.out_ring[(oi) >> 1][(oi) & 1])
     uint64_t in_head_r = 0, pub_in_r = 0, out_tail_r = 0, pub_out_r = 0, vin_head_r = 0, pub_vin_r = 0, pub_vout_r = 0;
     // per in-ring window: messages worth staging next iteration.  A ring whose prefix was cut by
     // out-ring credits is re-staged only a little past what fitted, so a hot rank does not pull
@@ -566,12 +572,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
         // ---------------- C (wave 0): publish the previous iteration, select this one
         if (w == 0) {
-            if (lane < nout && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(otptr_r, out_tail_r, sys); }
-            if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(ihptr_r, in_head_r, sys); }
-            if (lane < sll && vin_head_r != pub_vin_r) { pub_vin_r = vin_head_r; pub64(vhptr_r, vin_head_r, sys); }
+            if (lane < nout && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
+            if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(IHPTR, in_head_r, sys); }
+            if (lane < sll && vin_head_r != pub_vin_r) { pub_vin_r = vin_head_r; pub64(VHPTR, vin_head_r, sys); }
             if (lane < n_in) {
                 const uint64_t vt = S.vout_tail[lane];
-                if (vt != pub_vout_r) { pub_vout_r = vt; pub64(vtptr_r, vt, sys); }
+                if (vt != pub_vout_r) { pub_vout_r = vt; pub64(VTPTR, vt, sys); }
                 S.vout_head[lane] = vout_head_r;
             }
             peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
@@ -992,15 +998,25 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
             }
             BAR();
+#ifdef RLO_PROF_SPLIT
+            PROF_STAMP(2);
+#endif
             uint32_t room_r = 0;  // lane oi: free slots of out-ring oi left for this wave
+            bool tight_l = false;  // lane oi: the whole workgroup wants more of out-ring oi than is free
             if (lane < nout) {
-                uint32_t pre = 0;
-                for (int v = 0; v < w; v++) pre += S.wcnt[v][lane];
+                uint32_t pre = 0, tot = 0;
+                for (int v = 0; v < kWaves; v++) {
+                    const uint32_t x = S.wcnt[v][lane];
+                    if (v < w) pre += x;
+                    tot += x;
+                }
                 const uint32_t f = S.ofree[lane];
                 room_r = f > pre ? f - pre : 0u;
+                tight_l = tot > f;
             }
             bool fits = active && judge >= 0;
-            for (uint32_t m = wneed; m; m &= m - 1) {
+            // only a tight out-ring can refuse a message (a wall rank has ~2 of its ~15)
+            for (uint32_t m = wneed & (uint32_t)__ballot(tight_l); m; m &= m - 1) {
                 const int oi = __builtin_ctz(m);
                 const bool bit = (need >> oi) & 1u;
                 const uint64_t b = __ballot(bit);
@@ -1015,9 +1031,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             const uint32_t an = admitted ? need : 0u;
             const uint32_t len = w2 & 0xffffffu;
             const bool isbig = admitted && ((kHdr + len + 15u) >> 4) > nsmall;
+            const uint32_t nch_s = (kHdr + len + 15u) >> 4;  // small path: chunks, kept in the olist entry
             const uint32_t wadm = wave_or(an);
-            if (lane < nout) S.wcnt[w][lane] = 0;
-            for (uint32_t m = wadm; m; m &= m - 1) {
+            // this wave's admitted count per out-ring differs from its wanted count (wcnt, above) only
+            // where a refused message wanted that ring: recount just those
+            for (uint32_t m = wave_or(active && !admitted ? need : 0u); m; m &= m - 1) {
                 const int oi = __builtin_ctz(m);
                 const uint64_t b = __ballot((an >> oi) & 1u);
                 if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
@@ -1043,7 +1061,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 const uint64_t b = __ballot(bit);
                 if (bit) {
                     const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
-                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : 0u));
+                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 8)));
                     if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
                 }
             }
@@ -1210,22 +1228,39 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             // admitted messages' staged slots as contiguous (message, chunk) items
             const uint32_t nq = max(S.nchmax, 1u);  // items per message: the largest small message
             const uint32_t qmagic = nq > 1 ? 0xFFFFFFFFu / nq + 1u : 0u;
+            // a lane walks items i = lane, lane + 64, ... as (message r, chunk q) pairs stepped
+            // incrementally (no division or quarter-rate multiply per item: with one wave per SIMD
+            // this loop is instruction-latency bound), two independent items per round
+            const uint32_t dr = div_small(64u, qmagic), dq = 64u - dr * nq;
+            const uint32_t r0 = div_small((uint32_t)lane, qmagic), q0 = (uint32_t)lane - r0 * nq;
+            const uint32_t stg_msg = nsmall << 4, stride = P.fwd_stride;
             for (int oi = w; oi < nout; oi += kWaves) {
                 const uint32_t n = S.n_oi[oi];
                 if (!n) continue;
-                const uint64_t slot0 = S.out_tail0[oi];
-                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(oring_r, oi)), oring_bytes);
+                const uint32_t s0 = (uint32_t)S.out_tail0[oi];  // slot arithmetic mod fwd_cap (pow2)
+                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
                 const uint32_t nit = n * nq;
-                for (uint32_t i = lane; i < nit; i += 64) {
-                    const uint32_t r = div_small(i, qmagic), q = i - r * nq;
-                    const uint16_t e = OL(oi, r);
-                    if (e & kBigFlag) continue;
-                    const uint32_t nch = (kHdr + (S.cand[e].w2 & 0xffffffu) + 15u) >> 4;
-                    if (q < nch)
-                        st_ring(ro, (uint32_t)((slot0 + r) & fcap_m) * P.fwd_stride + 16u * q,
-                                *reinterpret_cast<const u32x4*>(STG(e, q)), sys);
+                uint32_t r = r0, q = q0;
+                for (uint32_t i = (uint32_t)lane; i < nit; i += 128u) {
+                    uint32_t rb = r + dr, qb = q + dq;
+                    if (qb >= nq) { qb -= nq; rb++; }
+                    const uint32_t ea = OL(oi, r);
+                    const uint32_t eb = i + 64u < nit ? (uint32_t)OL(oi, rb) : (uint32_t)kBigFlag;
+                    const bool va = !(ea & kBigFlag) && q < ((ea >> 8) & 0xfu);
+                    const bool vb = !(eb & kBigFlag) && qb < ((eb >> 8) & 0xfu);
+                    u32x4 xa = {0u, 0u, 0u, 0u}, xb = {0u, 0u, 0u, 0u};
+                    if (va) xa = *reinterpret_cast<const u32x4*>(stage + __umul24(ea & 0xffu, stg_msg) + (q << 4));
+                    if (vb) xb = *reinterpret_cast<const u32x4*>(stage + __umul24(eb & 0xffu, stg_msg) + (qb << 4));
+                    if (va) st_ring(ro, __umul24((s0 + r) & fcap_m, stride) + (q << 4), xa, sys);
+                    if (vb) st_ring(ro, __umul24((s0 + rb) & fcap_m, stride) + (qb << 4), xb, sys);
+                    r = rb + dr;
+                    q = qb + dq;
+                    if (q >= nq) { q -= nq; r++; }
                 }
             }
+#ifdef RLO_PROF_SPLIT
+            PROF_STAMP(5);
+#endif
             if (admitted && !isbig && kind == K_RING && tag == TAG_BCAST) {  // pickup: checksum (+ log payload)
                 const uint32_t nch = (kHdr + len + 15u) >> 4;
                 acc_sum += chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, id, TAG_BCAST, len});
@@ -1249,7 +1284,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                         for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
                             const int oi = __builtin_ctz(a2);
                             const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
-                            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(oring_r, oi)), oring_bytes);
+                            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
                             if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
                         }
                         if (q < nch && cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
@@ -1273,7 +1308,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+#ifdef RLO_PROF_SPLIT
+            PROF_STAMP(7);
+#else
             PROF_STAMP(5);
+#endif
         }
 
         // every store of this iteration (payloads, votes, pickup records) drained, so the producer
@@ -1294,10 +1333,10 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (P.mode & MODE_PROF) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
             }
             if (eager) {
-                if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(ihptr_r, in_head_r, sys); }
+                if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(IHPTR, in_head_r, sys); }
                 if (lane < n_in) {
                     const uint64_t vt = S.vout_tail[lane];
-                    if (vt != pub_vout_r) { pub_vout_r = vt; pub64(vtptr_r, vt, sys); }
+                    if (vt != pub_vout_r) { pub_vout_r = vt; pub64(VTPTR, vt, sys); }
                 }
             }
             {
@@ -1308,7 +1347,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 out_tail_r += S.n_oi[lane];
                 // this iteration's stores are drained (see above): publish now, not after the next
                 // poll -- one poll round trip less per hop
-                if (eager && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(otptr_r, out_tail_r, sys); }
+                if (eager && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
                 if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
                     S.hist[32 + lane] += S.n_oi[lane];
                     S.hist[64 + lane] += S.ofree[lane] >> 4;
@@ -1365,6 +1404,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     }
 #undef STG
 #undef OL
+#undef OTPTR
+#undef IHPTR
+#undef VHPTR
+#undef VTPTR
+#undef ORING
 
     // ---------------- flush statistics
     atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
