@@ -99,13 +99,12 @@ struct Shared {
     uint32_t own_word, own_needed, own_state, own_decision, own_pseq;
     int64_t own_iter, own_n;
     // origination progress
-    int64_t sched_next, sched_n;
-    uint32_t lat_pos, lat_pos_n, lat_own_next, done, error, error_aux, progressed;
+    uint32_t lat_pos, lat_pos_n, lat_own_next, error, error_aux, progressed;
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
-    unsigned long long own_decided, own_approved, proposals_recv, log_count, iterations, busy, stalls;
+    unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls;
     uint64_t prof[8], prof_t, dbg[8];
-    int64_t expect_bcast, expect_dec;
+    int64_t expect_dec;
     uint32_t hist[kHistBins];
 };
 
@@ -490,17 +489,14 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             S.own_word = 0; S.own_needed = 0; S.own_state = 0; S.own_decision = 0; S.own_pseq = 0;
             S.own_iter = 0;
             S.own_n = ((P.mode & MODE_IAR) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
-            S.sched_next = 0;
-            S.sched_n = (P.mode & MODE_STORM) ? (P.sched_off[lr + 1] - P.sched_off[lr]) : 0;
             S.lat_pos = 0;
             S.lat_pos_n = (P.mode & MODE_LAT) ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
             S.lat_own_next = S.lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
-            S.expect_bcast = (P.mode & (MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
             S.expect_dec = ((P.mode & MODE_IAR) && !host) ? P.expect_dec[lr] : 0;
             S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
-            S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.iterations = S.busy = S.stalls = 0;
-            S.error = 0; S.error_aux = 0; S.done = 0; S.exit_now = 0; S.progressed = 0;
+            S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = 0;
+            S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0;
         }
     }
     BAR();
@@ -537,6 +533,15 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     bool idle_prev = false;  // wave 0: the last iteration selected nothing
     uint64_t p_in = 0, p_vin = 0, p_oh = 0, p_voh = 0, p_h = 0;  // wave 0: the last poll
     uint32_t p_lat = 0;
+    // wave 0's own bookkeeping, kept in registers (LDS read-modify-writes by one lane are a serial
+    // chain of LDS round trips on the critical path of every iteration)
+    const int64_t sched_base = (P.mode & MODE_STORM) ? P.sched_off[lr] : 0;
+    const int64_t sched_n = (P.mode & MODE_STORM) ? P.sched_off[lr + 1] - sched_base : 0;
+    const int64_t expect_bcast = (P.mode & (MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
+    int64_t sched_next = 0;
+    uint64_t n_iter = 0, n_busy = 0, n_stalls = 0;
+    bool done_w0 = false;
+    uint32_t rbase_r = 0, rtake_r = 0, noi_r = 0;  // lane g / oi: this iteration's selection, admitted counts
 
     for (;;) {
         // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
@@ -562,9 +567,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (__ballot(moved)) break;
             }
             p_in = in_tail_r; p_vin = vin_tail_r; p_oh = out_head_r; p_voh = vout_head_r; p_h = hpoll; p_lat = latr;
-            const int64_t sn = S.sched_next;
-            if ((P.mode & MODE_STORM) && sn + lane < S.sched_n && (uint32_t)lane < P.window)
-                sid = P.sched_ids[P.sched_off[lr] + sn + lane];
+            if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
+                sid = P.sched_ids[sched_base + sched_next + lane];
         }
         VM_DRAIN();
         BAR();  // every payload / vote store of the previous iteration has left its wave
@@ -638,6 +642,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             uint32_t R;
             const uint32_t base = wave_excl_scan(take, &R);
             if (lane < n_in2) { S.ring_base[lane] = base; S.ring_take[lane] = take; S.ring_head[lane] = in_head_r; }
+            rbase_r = base;
+            rtake_r = take;
+            noi_r = 0;
             if (lane < nout) {
                 S.out_tail0[lane] = out_tail_r;
                 S.ofree[lane] = P.fwd_cap - (uint32_t)(out_tail_r - out_head_r);
@@ -716,13 +723,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (nh) C = hbase + nh;
                 }
             }
-            if ((P.mode & MODE_STORM) && S.sched_next < S.sched_n) {
+            if ((P.mode & MODE_STORM) && sched_next < sched_n) {
                 // throttle: originate only into shallow out-rings so forwarding never waits behind originations
                 const bool deep = lane < nout && (out_tail_r - out_head_r) * 2 >= P.fwd_cap;
                 const bool allow = !backlog && R < 2 * kPass && __ballot(deep) == 0;
                 if ((P.mode & MODE_PROF) && lane == 0) { if (!allow) S.dbg[5]++; else S.dbg[2]++; }
                 if (allow) {
-                    const int64_t rem = S.sched_n - S.sched_next;
+                    const int64_t rem = sched_n - sched_next;
                     uint32_t ww = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
                     if (ww > kMaxCand - C) ww = kMaxCand - C;
                     storm_base = C;
@@ -741,7 +748,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
                 S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = 0;
                 S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase; S.nchmax = 0;
-                S.exit_now = S.done;
+                S.exit_now = done_w0;
                 if (P.mode & MODE_PROF) S.dbg[0] += R;
             }
         }
@@ -1053,7 +1060,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (v < w) pre_r += x;
                     tot += x;
                 }
-                if (w == 0) S.n_oi[lane] = tot;
+                if (w == 0) { S.n_oi[lane] = tot; noi_r = tot; }
             }
             for (uint32_t m = wadm; m; m &= m - 1) {
                 const int oi = __builtin_ctz(m);
@@ -1228,24 +1235,30 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             // admitted messages' staged slots as contiguous (message, chunk) items
             const uint32_t nq = max(S.nchmax, 1u);  // items per message: the largest small message
             const uint32_t qmagic = nq > 1 ? 0xFFFFFFFFu / nq + 1u : 0u;
-            // a lane walks items i = lane, lane + 64, ... as (message r, chunk q) pairs stepped
-            // incrementally (no division or quarter-rate multiply per item: with one wave per SIMD
-            // this loop is instruction-latency bound), two independent items per round
+            // the (out-ring, message, chunk) items of all out-rings form one sequence split evenly over
+            // the four waves (a rank whose traffic sits on every other out-ring -- rank 0 sends on the
+            // wrapped channel only -- would otherwise store from two waves).  A lane walks its items as
+            // (message r, chunk q) pairs stepped incrementally (no division or quarter-rate multiply per
+            // item: with one wave per SIMD this loop is instruction-latency bound), two per round
             const uint32_t dr = div_small(64u, qmagic), dq = 64u - dr * nq;
-            const uint32_t r0 = div_small((uint32_t)lane, qmagic), q0 = (uint32_t)lane - r0 * nq;
             const uint32_t stg_msg = nsmall << 4, stride = P.fwd_stride;
-            for (int oi = w; oi < nout; oi += kWaves) {
-                const uint32_t n = S.n_oi[oi];
-                if (!n) continue;
+            const uint32_t nit_r = lane < nout ? S.n_oi[lane] * nq : 0u;
+            uint32_t items = 0;
+            const uint32_t ibase_r = wave_excl_scan(nit_r, &items);
+            const uint32_t lo = (items * (uint32_t)w) >> 2, hi = (items * (uint32_t)(w + 1)) >> 2;
+            for (uint64_t mo = __ballot(nit_r != 0 && ibase_r < hi && ibase_r + nit_r > lo); mo; mo &= mo - 1) {
+                const int oi = __builtin_ctzll(mo);
+                const uint32_t ib = rdl32(ibase_r, oi), ie = ib + rdl32(nit_r, oi);
+                const uint32_t a = max(lo, ib) - ib, b = min(hi, ie) - ib;  // this wave's items of ring oi
                 const uint32_t s0 = (uint32_t)S.out_tail0[oi];  // slot arithmetic mod fwd_cap (pow2)
                 const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
-                const uint32_t nit = n * nq;
-                uint32_t r = r0, q = q0;
-                for (uint32_t i = (uint32_t)lane; i < nit; i += 128u) {
+                uint32_t i = a + (uint32_t)lane;
+                uint32_t r = div_small(i, qmagic), q = i - r * nq;
+                for (; i < b; i += 128u) {
                     uint32_t rb = r + dr, qb = q + dq;
                     if (qb >= nq) { qb -= nq; rb++; }
                     const uint32_t ea = OL(oi, r);
-                    const uint32_t eb = i + 64u < nit ? (uint32_t)OL(oi, rb) : (uint32_t)kBigFlag;
+                    const uint32_t eb = i + 64u < b ? (uint32_t)OL(oi, rb) : (uint32_t)kBigFlag;
                     const bool va = !(ea & kBigFlag) && q < ((ea >> 8) & 0xfu);
                     const bool vb = !(eb & kBigFlag) && qb < ((eb >> 8) & 0xfu);
                     u32x4 xa = {0u, 0u, 0u, 0u}, xb = {0u, 0u, 0u, 0u};
@@ -1324,7 +1337,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
         // ---------------- consume (wave 0): in-ring prefixes, producer counts, bookkeeping
         if (w == 0) {
             if (lane < n_in2) {
-                const uint32_t bse = S.ring_base[lane], tk = S.ring_take[lane], fb = S.first_bad[lane];
+                const uint32_t bse = rbase_r, tk = rtake_r, fb = S.first_bad[lane];
+                if (fb < bse + tk) n_stalls++;  // lane 0's copy is flushed (sum over lanes at exit)
                 uint32_t adm = fb == 0xffffffffu ? tk : (fb > bse ? fb - bse : 0u);
                 if (adm > tk) adm = tk;
                 in_head_r += adm;
@@ -1339,17 +1353,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (vt != pub_vout_r) { pub_vout_r = vt; pub64(VTPTR, vt, sys); }
                 }
             }
-            {
-                const uint64_t bst = __ballot(lane < n_in2 && S.first_bad[lane] < S.ring_base[lane] + S.ring_take[lane]);
-                if (lane == 0 && bst) S.stalls += (unsigned long long)__popcll(bst);
-            }
             if (lane < nout) {
-                out_tail_r += S.n_oi[lane];
+                out_tail_r += noi_r;
                 // this iteration's stores are drained (see above): publish now, not after the next
                 // poll -- one poll round trip less per hop
                 if (eager && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
                 if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
-                    S.hist[32 + lane] += S.n_oi[lane];
+                    S.hist[32 + lane] += noi_r;
                     S.hist[64 + lane] += S.ofree[lane] >> 4;
                 }
                 if (P.mode & MODE_PROF)
@@ -1361,7 +1371,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     const uint32_t fb = S.first_bad[kGroupLocal + K_STORM];
                     uint32_t adm = fb == 0xffffffffu ? nstorm : (fb > storm_base ? fb - storm_base : 0u);
                     if (adm > nstorm) adm = nstorm;
-                    S.sched_next += adm;
+                    sched_next += adm;
                 }
                 if (host) {
                     if (S.nh) {
@@ -1377,28 +1387,30 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                         pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
                     }
                 }
-                S.iterations++;
+                n_iter++;
                 if (S.progressed) {  // the clock is read on the 1st and every 64th idle iteration only
-                    S.busy++;
+                    n_busy++;
                     idle_n = 0;
                 } else if ((++idle_n & 63u) == 1u) {
                     const uint64_t tn = now_ticks();
                     if (idle_n == 1) idle_since = tn;
                     else if (tn - idle_since > P.timeout_ticks) set_error(S, P, ERR_TIMEOUT, 0);
                 }
-                if ((S.iterations & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
+                if ((n_iter & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
                 bool done = true;
-                if (P.mode & MODE_STORM) done &= S.sched_next == S.sched_n;
-                if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == S.expect_bcast;
+                if (P.mode & MODE_STORM) done &= sched_next == sched_n;
+                if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == expect_bcast;
                 if (P.mode & MODE_LAT) done &= S.lat_pos >= S.lat_pos_n;
                 if ((P.mode & MODE_IAR) && !host)
                     done &= S.own_iter == S.own_n && S.own_state == 0 && (int64_t)S.dec_delivered == S.expect_dec;
                 if (host) done = S.quit != 0;
                 if (S.error == ERR_TIMEOUT) done = true;
                 if (peer_failed) done = true;  // another rank failed: stop everyone
-                S.done = done;
+                done_w0 = done;
             }
-            idle_prev = C == 0 && S.vtot == 0 && !S.done && !(P.mode & MODE_NOSPIN);
+            done_w0 = __builtin_amdgcn_readfirstlane((int)done_w0) != 0;  // lane 0 updated these
+            sched_next = (int64_t)uni64((uint64_t)sched_next);
+            idle_prev = C == 0 && S.vtot == 0 && !done_w0 && !(P.mode & MODE_NOSPIN);
         }
         PROF_STAMP(6);
     }
@@ -1411,6 +1423,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 #undef ORING
 
     // ---------------- flush statistics
+    if (w == 0) atomicAdd((unsigned long long*)&S.stalls, (unsigned long long)n_stalls);
     atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
     for (int i = tid; i < kHistBins; i += kBlock) P.stats[lr].hist[i] = S.hist[i];
     if (tid < 8) { P.stats[lr].prof[tid] = S.prof[tid]; P.stats[lr].dbg[tid] = S.dbg[tid]; }
@@ -1425,8 +1438,8 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
         st.own_decided = S.own_decided;
         st.own_approved = S.own_approved;
         st.proposals_recv = S.proposals_recv;
-        st.iterations = S.iterations;
-        st.busy_iterations = S.busy;
+        st.iterations = n_iter;
+        st.busy_iterations = n_busy;
         st.stalls = S.stalls;
         st.log_count = S.log_count;
         st.t_start = t_start;
