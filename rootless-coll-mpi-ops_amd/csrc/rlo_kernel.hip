@@ -94,6 +94,9 @@ struct Shared {
     uint32_t blk_c[64], blk_q0[64];      // large-message blocks staged in stage2
     // vote rings towards my parents (LDS atomics from every wave)
     uint64_t vout_tail[kMaxIn], vout_head[kMaxIn];
+    // wave 0: last published counter per lane (in-ring heads, out-ring tails, vote-in heads, vote-out
+    // tails) and the last poll per lane (in tails, vote-in tails, out heads, vote-out heads)
+    uint64_t pubw[4][64], snap[4][64];
     // own proposal (my_own_proposal, :241)
     int32_t own_pid;
     uint32_t own_word, own_needed, own_state, own_decision, own_pseq;
@@ -481,6 +484,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
         for (int i = tid; i < (int)(sizeof(RankTopo) / 4); i += kBlock) dst[i] = src[i];
         for (int i = tid; i < 2 * P.n; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
         for (int i = tid; i < kHistBins; i += kBlock) S.hist[i] = 0;
+        for (int i = tid; i < 4 * 64; i += kBlock) { (&S.pubw[0][0])[i] = 0; (&S.snap[0][0])[i] = 0; }
         if (tid < kMaxIn) { S.vout_tail[tid] = 0; S.vout_head[tid] = 0; }
         if (tid < 8) { S.prof[tid] = 0; S.dbg[tid] = 0; }
         if (tid == 0) {
@@ -521,7 +525,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 #define VHPTR t.vin_head[lane]
 #define VTPTR t.vout_tail[lane]
 #define ORING(oi) uni64(t.out_ring[(oi) >> 1][(oi) & 1])
-    uint64_t in_head_r = 0, pub_in_r = 0, out_tail_r = 0, pub_out_r = 0, vin_head_r = 0, pub_vin_r = 0, pub_vout_r = 0;
+    uint64_t in_head_r = 0, out_tail_r = 0, vin_head_r = 0;
+    // wave 0's last published counters and last poll, lane-indexed, in LDS (not registers: the
+    // kernel sits at the VGPR limit of two waves per SIMD)
+#define PUB_IN S.pubw[0][lane]
+#define PUB_OUT S.pubw[1][lane]
+#define PUB_VIN S.pubw[2][lane]
+#define PUB_VOUT S.pubw[3][lane]
     // per in-ring window: messages worth staging next iteration.  A ring whose prefix was cut by
     // out-ring credits is re-staged only a little past what fitted, so a hot rank does not pull
     // (and classify) hundreds of messages per iteration that cannot leave anyway
@@ -531,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
     uint64_t idle_since = 0;
     uint32_t idle_n = 0;
     bool idle_prev = false;  // wave 0: the last iteration selected nothing
-    uint64_t p_in = 0, p_vin = 0, p_oh = 0, p_voh = 0, p_h = 0;  // wave 0: the last poll
+    uint64_t p_h = 0;  // wave 0: the last poll (host counters; the ring counters are in S.snap)
     uint32_t p_lat = 0;
     // wave 0's own bookkeeping, kept in registers (LDS read-modify-writes by one lane are a serial
     // chain of LDS round trips on the critical path of every iteration)
@@ -562,11 +572,13 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (lane == 0) errf = poll32(P.error_flag);
                 if ((P.mode & MODE_LAT) && lane == 1) latr = poll32(P.lat_round);  // the round in progress
                 if (!idle_prev || sp >= kIdleSpin) break;
-                const bool moved = in_tail_r != p_in || vin_tail_r != p_vin || out_head_r != p_oh ||
-                                   vout_head_r != p_voh || hpoll != p_h || latr != p_lat || errf != 0;
+                const bool moved = in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] ||
+                                   out_head_r != S.snap[2][lane] || vout_head_r != S.snap[3][lane] || hpoll != p_h ||
+                                   latr != p_lat || errf != 0;
                 if (__ballot(moved)) break;
             }
-            p_in = in_tail_r; p_vin = vin_tail_r; p_oh = out_head_r; p_voh = vout_head_r; p_h = hpoll; p_lat = latr;
+            S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
+            S.snap[3][lane] = vout_head_r; p_h = hpoll; p_lat = latr;
             if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
         }
@@ -576,12 +588,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
         // ---------------- C (wave 0): publish the previous iteration, select this one
         if (w == 0) {
-            if (lane < nout && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
-            if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(IHPTR, in_head_r, sys); }
-            if (lane < sll && vin_head_r != pub_vin_r) { pub_vin_r = vin_head_r; pub64(VHPTR, vin_head_r, sys); }
+            if (lane < nout && out_tail_r != PUB_OUT) { PUB_OUT = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
+            if (lane < n_in2 && in_head_r != PUB_IN) { PUB_IN = in_head_r; pub64(IHPTR, in_head_r, sys); }
+            if (lane < sll && vin_head_r != PUB_VIN) { PUB_VIN = vin_head_r; pub64(VHPTR, vin_head_r, sys); }
             if (lane < n_in) {
                 const uint64_t vt = S.vout_tail[lane];
-                if (vt != pub_vout_r) { pub_vout_r = vt; pub64(VTPTR, vt, sys); }
+                if (vt != PUB_VOUT) { PUB_VOUT = vt; pub64(VTPTR, vt, sys); }
                 S.vout_head[lane] = vout_head_r;
             }
             peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
@@ -1183,19 +1195,37 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
             // ---------------- G1: stage the first group of large messages (before any store)
             const uint32_t nbig = S.nbig;
-            auto plan_big = [&]() {  // thread 0: next (message, 64-chunk block) pairs for stage2
-                if (tid == 0) {
-                    uint32_t bm = S.bm, bq0 = S.bq0, nblk = 0;
-                    while (bm < nbig && nblk < s2_blocks && nblk < 64) {
-                        const uint32_t cc = S.big[bm];
+            auto plan_big = [&]() {  // wave 0: next (message, 64-chunk block) pairs for stage2, lane-parallel
+                if (w == 0) {
+                    const uint32_t bm = S.bm, bq0 = S.bq0;
+                    const uint32_t lim = min(s2_blocks, 64u);
+                    const uint32_t mi = bm + (uint32_t)lane;
+                    uint32_t nb = 0, cc = 0, q0 = 0;
+                    if (mi < nbig) {
+                        cc = S.big[mi];
                         const uint32_t nch = (kHdr + (S.cand[cc].w2 & 0xffffffu) + 15u) >> 4;
-                        S.blk_c[nblk] = cc;
-                        S.blk_q0[nblk] = bq0;
-                        nblk++;
-                        bq0 += 64;
-                        if (bq0 >= nch) { bm++; bq0 = 0; }
+                        q0 = lane == 0 ? bq0 : 0u;
+                        nb = (nch - q0 + 63u) >> 6;
                     }
-                    S.bm = bm; S.bq0 = bq0; S.nblk = nblk;
+                    uint32_t tot;
+                    const uint32_t st = wave_excl_scan(nb, &tot);
+                    for (uint32_t k = 0; k < nb && st + k < lim; k++) {
+                        S.blk_c[st + k] = cc;
+                        S.blk_q0[st + k] = q0 + 64u * k;
+                    }
+                    const uint64_t cut = __ballot(nb != 0 && st + nb > lim);  // the first cut message is the cursor
+                    uint32_t nbm, nbq0, nblk;
+                    if (cut) {
+                        const int l = __builtin_ctzll(cut);
+                        nbm = bm + (uint32_t)l;
+                        nbq0 = rdl32(q0, l) + 64u * (lim - rdl32(st, l));
+                        nblk = lim;
+                    } else {
+                        nbm = min(bm + 64u, nbig);
+                        nbq0 = 0;
+                        nblk = tot;
+                    }
+                    if (lane == 0) { S.bm = nbm; S.bq0 = nbq0; S.nblk = nblk; }
                 }
             };
             auto stage_big = [&]() {  // wave w stages (and later stores) blocks b = w, w + 4, ...
@@ -1347,17 +1377,17 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (P.mode & MODE_PROF) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
             }
             if (eager) {
-                if (lane < n_in2 && in_head_r != pub_in_r) { pub_in_r = in_head_r; pub64(IHPTR, in_head_r, sys); }
+                if (lane < n_in2 && in_head_r != PUB_IN) { PUB_IN = in_head_r; pub64(IHPTR, in_head_r, sys); }
                 if (lane < n_in) {
                     const uint64_t vt = S.vout_tail[lane];
-                    if (vt != pub_vout_r) { pub_vout_r = vt; pub64(VTPTR, vt, sys); }
+                    if (vt != PUB_VOUT) { PUB_VOUT = vt; pub64(VTPTR, vt, sys); }
                 }
             }
             if (lane < nout) {
                 out_tail_r += noi_r;
                 // this iteration's stores are drained (see above): publish now, not after the next
                 // poll -- one poll round trip less per hop
-                if (eager && out_tail_r != pub_out_r) { pub_out_r = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
+                if (eager && out_tail_r != PUB_OUT) { PUB_OUT = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
                 if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
                     S.hist[32 + lane] += noi_r;
                     S.hist[64 + lane] += S.ofree[lane] >> 4;
@@ -1421,6 +1451,10 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 #undef VHPTR
 #undef VTPTR
 #undef ORING
+#undef PUB_IN
+#undef PUB_OUT
+#undef PUB_VIN
+#undef PUB_VOUT
 
     // ---------------- flush statistics
     if (w == 0) atomicAdd((unsigned long long*)&S.stalls, (unsigned long long)n_stalls);
