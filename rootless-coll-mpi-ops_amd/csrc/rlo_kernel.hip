@@ -205,6 +205,17 @@ __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { retu
             S.prof_t = c_;                              \
         }                                               \
     } while (0)
+// RLO_PROF_SPLIT (diagnostic build): slots 1-6 split the wave-0 phases (1 publish, 2 quotas,
+// 3 originations, 4 in-ring heads, 5 out-ring tails, 6 lane-0 bookkeeping); the all-wave phases go to 7
+#ifdef RLO_PROF_SPLIT
+#define PST(a, b) PROF_STAMP(b)
+#define PSX(b) PROF_STAMP(b)
+#else
+#define PST(a, b) PROF_STAMP(a)
+#define PSX(b) \
+    do {       \
+    } while (0)
+#endif
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + kGolden64;
@@ -597,6 +608,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 S.vout_head[lane] = vout_head_r;
             }
             peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
+            PSX(1);
             // host mode: publish the command head / pickup tail of the previous iteration; the pickup
             // ring bounds this iteration's events: a ring message makes <= 2 (action + decision), plus
             // <= 2 of the own proposal (final-judge request, result)
@@ -664,6 +676,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             }
             if (lane < kGroups) S.first_bad[lane] = 0xffffffffu;
             if (lane + 64 < kGroups) S.first_bad[lane + 64] = 0xffffffffu;
+            PSX(2);
             // local originations
             uint32_t C = R, loc_kind = 0, nstorm = 0, storm_base = 0, lat_id = 0xffffffffu;
             int64_t prop_idx = -1;
@@ -765,7 +778,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             }
         }
         BAR();  // selection visible
-        PROF_STAMP(7);
+        PST(7, 3);
         if (S.exit_now) break;  // the final counters are published
         const uint32_t R = S.R, C = S.C;
         const uint32_t nstorm = S.nstorm, storm_base = S.storm_base, loc_kind = S.loc_kind;
@@ -837,7 +850,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
             VM_DRAIN();  // wave 1: its vote loads
-            PROF_STAMP(1);
+            PST(1, 7);
 
             // ---------------- B1 (wave 1): merge the votes (_iar_vote_handler :743-812)
             if (w == 1 && vtot) {
@@ -1005,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 for (uint32_t q = (uint32_t)lane; 16u * q < plen && 16u * q < P.log_stride; q += 64u)
                     st_sys16(dst + 16u * q, ld_sc1(rf, lsrc + kHdr + 16u * q));
             }
-            PROF_STAMP(2);
+            PST(2, 7);
 
             // ---------------- E: admission: credits per out-ring, FIFO prefix per source.  The ballot
             // loops visit only the out-rings some lane of this wave needs (a wall rank uses about half)
@@ -1017,9 +1030,6 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (lane == 0) S.wcnt[w][oi] = (uint32_t)__popcll(b);
             }
             BAR();
-#ifdef RLO_PROF_SPLIT
-            PROF_STAMP(2);
-#endif
             uint32_t room_r = 0;  // lane oi: free slots of out-ring oi left for this wave
             bool tight_l = false;  // lane oi: the whole workgroup wants more of out-ring oi than is free
             if (lane < nout) {
@@ -1085,7 +1095,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
             const uint64_t amask = __ballot(admitted);
-            PROF_STAMP(3);
+            PST(3, 7);
 
             // ---------------- F: side effects of admitted messages
             const uint32_t tag = (w0 >> 16) & 0xffu;
@@ -1191,7 +1201,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
             BAR();  // olist / cand / n_oi / big complete
-            PROF_STAMP(4);
+            PST(4, 7);
 
             // ---------------- G1: stage the first group of large messages (before any store)
             const uint32_t nbig = S.nbig;
@@ -1301,9 +1311,6 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (q >= nq) { q -= nq; r++; }
                 }
             }
-#ifdef RLO_PROF_SPLIT
-            PROF_STAMP(5);
-#endif
             if (admitted && !isbig && kind == K_RING && tag == TAG_BCAST) {  // pickup: checksum (+ log payload)
                 const uint32_t nch = (kHdr + len + 15u) >> 4;
                 acc_sum += chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, id, TAG_BCAST, len});
@@ -1351,11 +1358,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
-#ifdef RLO_PROF_SPLIT
-            PROF_STAMP(7);
-#else
-            PROF_STAMP(5);
-#endif
+            PST(5, 7);
         }
 
         // every store of this iteration (payloads, votes, pickup records) drained, so the producer
@@ -1376,6 +1379,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 else if (adm == tk && tk == win_r) win_r = min(2u * win_r, (uint32_t)kMaxCand);
                 if (P.mode & MODE_PROF) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
             }
+            PSX(4);
             if (eager) {
                 if (lane < n_in2 && in_head_r != PUB_IN) { PUB_IN = in_head_r; pub64(IHPTR, in_head_r, sys); }
                 if (lane < n_in) {
@@ -1396,6 +1400,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     atomicMax((unsigned long long*)&S.dbg[7], (unsigned long long)(out_tail_r - S.out_tail0[lane] +
                                                                                    (P.fwd_cap - S.ofree[lane])));
             }
+            PSX(5);
             if (lane == 0) {
                 if (nstorm) {
                     const uint32_t fb = S.first_bad[kGroupLocal + K_STORM];
