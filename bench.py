@@ -436,23 +436,35 @@ def main():
     if not args.no_extras:
         if rank == 0:
             note("latency / loaded-latency / decisions legs")
+        # unloaded latency: one random originator per round, round i+1 starts when every rank has
+        # picked up round i
+        w.program_latency(args.lat_rounds, length, seed=17)
+        step()
         if world == 1 or mode == "replicas":
-            # unloaded latency: one random originator per round (bcast completion = last pickup)
-            w.program_latency(args.lat_rounds, length, seed=17)
-            step()
+            # one-way: origination -> last pickup, both on this GPU's clock
             lat_us = w.latencies_ticks().astype(np.float64) * 0.01
             extras["p50_us"] = round(percentile(lat_us, 50), 2)
             extras["p99_us"] = round(percentile(lat_us, 99), 2)
-        # loaded per-delivery latency inside the storm
-        w.program_storm(k, length, seed=seed, hist=True)
-        step()
-        hist = w.stats()["hist"].sum(axis=0).astype(np.float64)
-        if dist is not None:
-            t = torch.tensor(hist)
-            dist.all_reduce(t)
-            hist = t.numpy()
-        extras["storm_delivery_p50_us"] = round(rlo.hist_percentile(hist, 50) * 0.01, 2)
-        extras["storm_delivery_p99_us"] = round(rlo.hist_percentile(hist, 99) * 0.01, 2)
+        if rank == 0:
+            # closed-loop round time on ONE clock (world rank 0 observes every completion), the form
+            # that stays valid when the world spans GPUs whose clocks are not synchronised
+            obs = w.round_ticks().astype(np.float64)
+            rt_us = np.diff(obs[obs > 0]) * 0.01
+            if len(rt_us):
+                extras["round_p50_us"] = round(percentile(rt_us, 50), 2)
+                extras["round_p99_us"] = round(percentile(rt_us, 99), 2)
+        # loaded per-delivery latency inside the storm (origination clock vs pickup clock: one
+        # GPU's clock only when the world is on one GPU, so not reported for sharded N > 1)
+        if world == 1 or mode == "replicas":
+            w.program_storm(k, length, seed=seed, hist=True)
+            step()
+            hist = w.stats()["hist"].sum(axis=0).astype(np.float64)
+            if dist is not None:
+                t = torch.tensor(hist)
+                dist.all_reduce(t)
+                hist = t.numpy()
+            extras["storm_delivery_p50_us"] = round(rlo.hist_percentile(hist, 50) * 0.01, 2)
+            extras["storm_delivery_p99_us"] = round(rlo.hist_percentile(hist, 99) * 0.01, 2)
         # consensus: every rank keeps one outstanding proposal (approve-all)
         p = args.iar_p
         props = [(r, it * R + r, b"0123456789abcdef") for it in range(p) for r in range(R)]

@@ -113,7 +113,11 @@ typedef struct {
 int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg);
 
 /* one bcast per round, round i from splitmix64(seed + i) % N; round i+1 starts when every
- * rank has picked up round i.  rlo_latencies() returns per-round completion ticks (10 ns). */
+ * rank has picked up round i.  rlo_latencies() returns per-round completion ticks (10 ns):
+ * origination -> last pickup, on one clock only when the world is one part.  Worlds split over
+ * parts (processes / GPUs, <= 8192 rounds) share the round word through part 0; there
+ * rlo_round_ticks() (on the part holding world rank 0) returns the clock of world rank 0 when it
+ * saw round i complete: successive differences are closed-loop round times on ONE clock. */
 int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags);
 
 #define RLO_JUDGE_APPROVE 0u /* approve everything                                           */
@@ -243,6 +247,7 @@ typedef struct {
 int rlo_stats(rlo_world_t* w, rlo_rank_stats_t* out, int n);
 int rlo_log(rlo_world_t* w, int rank, rlo_log_rec_t* out, uint32_t cap, uint8_t* payload, uint32_t payload_stride);
 int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap);
+int rlo_round_ticks(rlo_world_t* w, uint64_t* ticks, uint32_t cap);
 
 const char* rlo_strerror(int code);
 int rlo_last_hip_error(void);

@@ -29,6 +29,11 @@ constexpr int kStagePasses = 4;  // 4 x 64 messages per progress iteration
 constexpr int kHistBins = 128;    // latency histogram: 4 sub-bins per octave of 10 ns ticks
 constexpr int kMaxParts = 64;     // parts (processes x GPUs) of one world
 constexpr int kCtrlHdrWords = 16; // per-part control words before the rank blocks: [0] error flag
+// latency program of a world split over parts: the round word and the per-round delivery counts are
+// one world-wide copy in part 0's control region (peer-mapped like the ring counters), after its rank
+// blocks: [round word, own 128-B line][counts: kLatCap x u32]
+constexpr int kLatCap = 8192;
+constexpr int kLatWords = 16 + kLatCap / 2;
 
 // message classes == enum RLO_COMM_TAGS (rootless_ops.h:50-61)
 enum Tag : uint32_t { TAG_BCAST = 0, TAG_PROPOSAL = 2, TAG_VOTE = 3, TAG_DECISION = 4 };
@@ -137,7 +142,8 @@ struct Params {
     const int32_t* lat_origin;    // [lat_rounds]
     uint32_t* lat_count;          // [lat_rounds] deliveries so far
     uint64_t* lat_out;            // [lat_rounds] completion ticks
-    uint32_t* lat_round;          // current round (global)
+    uint32_t* lat_round;          // current round (global; part 0's control region when sharded)
+    uint64_t* lat_obs;            // [lat_rounds] observer clock (world rank 0) when round i completed
     const uint32_t* lat_own_off;  // [n_local + 1] CSR of the rounds each local rank originates
     const uint32_t* lat_own;
     // IAR workload

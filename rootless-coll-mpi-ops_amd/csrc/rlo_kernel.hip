@@ -102,7 +102,7 @@ struct Shared {
     uint32_t own_word, own_needed, own_state, own_decision, own_pseq;
     int64_t own_iter, own_n;
     // origination progress
-    uint32_t lat_pos, lat_pos_n, lat_own_next, error, error_aux, progressed;
+    uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls;
@@ -505,6 +505,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             S.own_iter = 0;
             S.own_n = ((P.mode & MODE_IAR) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
             S.lat_pos = 0;
+            S.lat_seen = 0;
             S.lat_pos_n = (P.mode & MODE_LAT) ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
             S.lat_own_next = S.lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
             S.expect_dec = ((P.mode & MODE_IAR) && !host) ? P.expect_dec[lr] : 0;
@@ -581,7 +582,9 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
                 if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
                 if (lane == 0) errf = poll32(P.error_flag);
-                if ((P.mode & MODE_LAT) && lane == 1) latr = poll32(P.lat_round);  // the round in progress
+                if ((P.mode & MODE_LAT) && lane == 1)  // the round in progress (part 0's word when sharded)
+                    latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                               : poll32(P.lat_round);
                 if (!idle_prev || sp >= kIdleSpin) break;
                 const bool moved = in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] ||
                                    out_head_r != S.snap[2][lane] || vout_head_r != S.snap[3][lane] || hpoll != p_h ||
@@ -590,6 +593,14 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             }
             S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
             S.snap[3][lane] = vout_head_r; p_h = hpoll; p_lat = latr;
+            if ((P.mode & MODE_LAT) && me == 0) {  // world rank 0 observes round completions on its clock
+                const uint32_t done_r = rdl32(latr, 1), seen = S.lat_seen;
+                if (done_r > seen) {
+                    const uint64_t tn = now_ticks();
+                    for (uint32_t k = seen + (uint32_t)lane; k < done_r && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
+                    if (lane == 0) S.lat_seen = done_r;
+                }
+            }
             if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
         }
@@ -1352,10 +1363,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 }
             }
             if (lat_deliv) {  // latency program: the last of N-1 pickups completes the round
-                const uint32_t old = atomicAdd(&P.lat_count[id], 1u);
+                const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                         : atomicAdd(&P.lat_count[id], 1u);
                 if (old + 1u == (uint32_t)(P.n - 1)) {
-                    P.lat_out[id] = (uint64_t)lat_tn;
-                    __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    P.lat_out[id] = (uint64_t)lat_tn;  // one clock only when the world is one part
+                    if (sys) __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    else __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             PST(5, 7);

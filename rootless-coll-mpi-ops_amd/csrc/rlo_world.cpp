@@ -140,6 +140,7 @@ struct Layout {
     std::vector<uint64_t> fwd_bytes, vote_bytes, ctrl_words;  // per part
     std::vector<uint64_t> fwd_off, vote_off;                  // per edge (vc 0 ring; vc 1 follows)
     std::vector<uint32_t> inbox, outbox;                      // per rank: word index in its part's ctrl
+    std::vector<uint64_t> lat_base;                           // per part: the shared latency block (rlo_device.hpp)
 };
 
 int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uint32_t ring_slots, Layout& L) {
@@ -207,6 +208,7 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
     // control words: per part a header (word 0 = error flag), then per rank an inbox block
     // (tails of its in-rings + vote in-rings) and an outbox block (heads), 128-B aligned
     L.ctrl_words.assign(nparts, 0);
+    L.lat_base.clear();
     L.inbox.assign(n, 0);
     L.outbox.assign(n, 0);
     for (int p = 0; p < nparts; p++) {
@@ -217,6 +219,8 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
             L.outbox[r] = (uint32_t)words;
             words += (2 * L.T[r].sll + L.in_edges[r].size() + 15) & ~15ull;
         }
+        L.lat_base.push_back(words);
+        words += rlo::kLatWords;
         L.ctrl_words[p] = words;
     }
     return RLO_OK;
@@ -274,7 +278,7 @@ struct rlo_world {
     DevBuf<uint32_t> d_sched_ids, d_prop_data_off, d_prop_data_len, d_isp_off, d_lat_count, d_lat_round;
     DevBuf<uint32_t> d_lat_own_off, d_lat_own;
     DevBuf<int32_t> d_lat_origin, d_prop_pid;
-    DevBuf<uint64_t> d_lat_out;
+    DevBuf<uint64_t> d_lat_out, d_lat_obs;
     DevBuf<uint8_t> d_mask, d_prop_data, d_log_payload;
     DevBuf<char> d_isp;
     DevBuf<rlo::LogRec> d_log;
@@ -697,15 +701,16 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
 int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags) {
     if (!w || rounds == 0 || len > w->max_payload) return RLO_E_INVAL;
     if (!w->connected) return RLO_E_NOTCONNECTED;
-    if (w->L.nparts != 1) return RLO_E_INVAL;  // the round counter is one device word
+    // sharded: the round word and counts are part 0's copy, peer-mapped (rlo_device.hpp kLatWords)
+    if (w->L.nparts != 1 && rounds > (uint32_t)rlo::kLatCap) return RLO_E_INVAL;
     base_params(w);
     rlo::Params& P = w->P;
     const int n = w->L.n;
     std::vector<int32_t> org(rounds);
-    std::vector<int64_t> expect(n, 0);
+    std::vector<int64_t> expect(w->nl, 0);  // per LOCAL rank (the kernel indexes by workgroup)
     for (uint32_t i = 0; i < rounds; i++) org[i] = (int32_t)(splitmix64(seed + i) % (uint64_t)n);
-    for (int r = 0; r < n; r++)
-        for (uint32_t i = 0; i < rounds; i++) expect[r] += org[i] != r;
+    for (int lr = 0; lr < w->nl; lr++)
+        for (uint32_t i = 0; i < rounds; i++) expect[lr] += org[i] != w->rb + lr;
     // per local rank the rounds it originates, in order (the kernel prefetches the next one)
     std::vector<uint32_t> own_off(w->nl + 1, 0), own;
     for (int lr = 0; lr < w->nl; lr++) {
@@ -716,7 +721,7 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     if (own.empty()) own.push_back(0);
     if (w->d_lat_own_off.upload(own_off) || w->d_lat_own.upload(own)) return RLO_E_HIP;
     if (w->d_lat_origin.upload(org) || w->d_expect_bcast.upload(expect) || w->d_lat_count.alloc(rounds) ||
-        w->d_lat_out.alloc(rounds) || w->d_lat_round.alloc(1))
+        w->d_lat_out.alloc(rounds) || w->d_lat_round.alloc(1) || w->d_lat_obs.alloc(rounds))
         return RLO_E_HIP;
     P.mode = rlo::MODE_LAT | ((flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u) | ((flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
     P.len = len;
@@ -726,6 +731,12 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     P.lat_count = w->d_lat_count.p;
     P.lat_out = w->d_lat_out.p;
     P.lat_round = w->d_lat_round.p;
+    P.lat_obs = w->d_lat_obs.p;
+    if (w->L.nparts != 1) {
+        uint64_t* blk = w->pc[0] + w->L.lat_base[0];
+        P.lat_round = reinterpret_cast<uint32_t*>(blk);
+        P.lat_count = reinterpret_cast<uint32_t*>(blk + 16);
+    }
     P.lat_own_off = w->d_lat_own_off.p;
     P.lat_own = w->d_lat_own.p;
     P.expect_bcast = w->d_expect_bcast.p;
@@ -956,6 +967,8 @@ int rlo_reset(rlo_world_t* w, void* stream) {
         HIPCHK(hipMemsetAsync(w->d_lat_count.p, 0, sizeof(uint32_t) * w->lat_rounds, s));
         HIPCHK(hipMemsetAsync(w->d_lat_out.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
         HIPCHK(hipMemsetAsync(w->d_lat_round.p, 0, sizeof(uint32_t), s));
+        HIPCHK(hipMemsetAsync(w->d_lat_obs.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
+        // sharded: part 0's control memset above clears the shared round word and counts
     }
     HIPCHK(hipStreamSynchronize(s));
     return RLO_OK;
@@ -1062,6 +1075,15 @@ int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
     uint32_t n = std::min(cap, w->lat_rounds);
     HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipMemcpy(ticks, w->d_lat_out.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    return (int)n;
+}
+
+int rlo_round_ticks(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
+    if (!w || !ticks || !w->d_lat_obs.p) return RLO_E_INVAL;
+    if (w->rb != 0) return RLO_E_INVAL;  // the observer is world rank 0
+    uint32_t n = std::min(cap, w->lat_rounds);
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipMemcpy(ticks, w->d_lat_obs.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return (int)n;
 }
 

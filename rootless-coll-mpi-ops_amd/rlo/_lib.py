@@ -87,7 +87,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_part_create", "rlo_part_export", "rlo_part_connect", "rlo_reset", "rlo_launch_ex",
            "rlo_stream_create", "rlo_stream_destroy",
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
-           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_strerror", "rlo_last_hip_error",
+           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_strerror", "rlo_last_hip_error",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
            "rlo_device_count", "rlo_bulk_create", "rlo_bulk_export", "rlo_bulk_connect", "rlo_bulk_buffer",
            "rlo_bulk_reset", "rlo_bulk_launch", "rlo_bulk_wait", "rlo_bulk_destroy"]
@@ -127,6 +127,7 @@ def load():
     L.rlo_stats.argtypes = [vp, ctypes.POINTER(RankStats), ctypes.c_int]
     L.rlo_log.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), ctypes.c_uint32, vp, ctypes.c_uint32]
     L.rlo_latencies.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    L.rlo_round_ticks.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     L.rlo_program_host.argtypes = [vp, ctypes.POINTER(HostCfg)]
     L.rlo_host_post.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Cmd), vp, ctypes.c_uint32]
     L.rlo_host_poll.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp, ctypes.c_uint32]

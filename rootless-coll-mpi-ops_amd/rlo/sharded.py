@@ -6,7 +6,9 @@ run_processes(): one spawned process per part; blobs are exchanged through a que
                  regions are mapped with hipIpc (dmabuf), launches start after a barrier
                  that follows every part's reset.
 A program spec is a dict: {"kind": "storm", "k", "len", "seed", "window", "log"} or
-{"kind": "iar", "props": [(origin, pid, bytes)], "judge", "mask", "isp", "seed", "ppm", "log"}.
+{"kind": "iar", "props": [(origin, pid, bytes)], "judge", "mask", "isp", "seed", "ppm", "log"} or
+{"kind": "lat", "rounds", "len", "seed"} (the round word lives in part 0; st["round_ticks"] is world
+rank 0's clock at each round's completion).
 """
 import ctypes
 import multiprocessing as mp
@@ -27,6 +29,8 @@ def _program(w, spec):
         w.program_iar(spec["props"], judge=spec.get("judge", L.RLO_JUDGE_APPROVE), mask=spec.get("mask"),
                       isp=spec.get("isp"), seed=spec.get("seed", 0), ppm=spec.get("ppm", 0),
                       log=spec.get("log", False), log_cap=spec.get("log_cap", 0))
+    elif spec["kind"] == "lat":
+        w.program_latency(spec["rounds"], spec["len"], seed=spec.get("seed", 0x5EED))
     else:
         raise ValueError(spec["kind"])
 
@@ -34,6 +38,8 @@ def _program(w, spec):
 def _collect(w, spec):
     st = w.stats()
     out = {"rank_begin": w.rank_begin, "stats": st, "ms": w.kernel_ms(), "info": dict(w.info)}
+    if spec["kind"] == "lat" and w.rank_begin == 0:
+        out["rounds"] = w.round_ticks()
     if spec.get("log"):
         cap = spec.get("log_cap", 0) or 1024
         out["logs"] = {r: w.log(r, cap=cap, payload=spec["kind"] == "storm") for r in range(w.rank_begin, w.rank_end)}
@@ -49,6 +55,8 @@ def merge(results):
     logs = {}
     for r in results:
         logs.update(r.get("logs", {}))
+        if "rounds" in r:
+            st["round_ticks"] = r["rounds"]
     return st, logs, [r["ms"] for r in results]
 
 

@@ -181,6 +181,12 @@ class World:
         n = check(self.lib.rlo_latencies(self.h, arr, self._lat_rounds), "rlo_latencies")
         return np.array(arr[:n], dtype=np.uint64)
 
+    def round_ticks(self):
+        """Clock of world rank 0 (10 ns ticks) when it saw each round complete (the part holding rank 0)."""
+        arr = (ctypes.c_uint64 * self._lat_rounds)()
+        n = check(self.lib.rlo_round_ticks(self.h, arr, self._lat_rounds), "rlo_round_ticks")
+        return np.array(arr[:n], dtype=np.uint64)
+
 
 def hist_percentile(hist, p):
     """Percentile (in 10 ns ticks) from the device log-bucket histogram (4 sub-bins per octave)."""

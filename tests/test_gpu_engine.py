@@ -218,8 +218,11 @@ def test_latency_program(rlo):
         w.program_latency(rounds, 64, seed=5)
         w.run()
         lat = w.latencies_ticks()
+        rt = w.round_ticks().astype(np.int64)
         st = w.stats()
     assert (st["error"] == 0).all()
     assert len(lat) == rounds and (lat > 0).all()
+    seen = rt[rt > 0]  # rank 0's clock at each completion it saw
+    assert len(seen) >= rounds - 1 and (np.diff(seen) >= 0).all()
     org = [orc.origin_of(5, i, n) for i in range(rounds)]
     assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]

@@ -124,3 +124,34 @@ def test_iar_sharded_processes(rlo):
     assert int(st["own_approved"].sum()) == n * p
     assert (st["dec_delivered"] == (n - 1) * p).all()
     assert (st["actions"] == (n - 1) * p).all()
+
+
+def _check_lat(st, n, rounds, seed):
+    assert (st["error"] == 0).all(), (st["error"], st["error_aux"])
+    org = [orc.origin_of(seed, i, n) for i in range(rounds)]
+    assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]
+    rt = st["round_ticks"].astype(np.int64)
+    seen = rt[rt > 0]
+    # world rank 0 saw (nearly) every round complete, on its own clock, in order
+    assert len(seen) >= rounds - 1 and (np.diff(seen) >= 0).all()
+
+
+@pytest.mark.parametrize("n,bounds", [(32, [0, 16, 32]), (64, [0, 10, 40, 64])])
+def test_latency_sharded_inprocess(rlo, n, bounds):
+    """Latency program over parts: the round word and counts are part 0's, peer-mapped."""
+    from rlo import sharded
+
+    rounds, seed = 64, 5
+    (st, _, _), rcs = sharded.run_inprocess(n, bounds, {"kind": "lat", "rounds": rounds, "len": 64, "seed": seed})
+    assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
+    _check_lat(st, n, rounds, seed)
+
+
+def test_latency_sharded_processes(rlo):
+    from rlo import sharded
+
+    n, rounds, seed = 16, 48, 9
+    (st, _, _), rcs = sharded.run_processes(n, [0, 8, 16], {"kind": "lat", "rounds": rounds, "len": 64, "seed": seed},
+                                            uncached=True)
+    assert rcs == [0, 0], (st["error"], st["error_aux"])
+    _check_lat(st, n, rounds, seed)
