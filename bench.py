@@ -380,6 +380,7 @@ def main():
             R = per
             w = rlo.World(R, max_payload=max(64, length), device=local)
             sharded_error = [e for e in errs if e][0]
+    waves = int(w.info.get("waves", 4))  # rank-workgroup width the world was sized with (4 or 8)
     lib = rlo.abi.load()
     stream = ctypes.c_void_p()
     rlo.abi.check(lib.rlo_stream_create(local, ctypes.byref(stream)), "rlo_stream_create")
@@ -514,6 +515,7 @@ def main():
                                "random originators, %d bcasts per step; value = delivered bcast messages/s "
                                "(each bcast reaches %d ranks)" % (R, per, length, k, R - 1),
                    "ranks_per_gpu": per, "world_ranks": R, "payload_bytes": length, "bcasts_per_step": k,
+                   "waves_per_rank": waves,
                    "parallelism": ("one world sharded over %d GPU(s), contiguous rank ranges" % world) if mode == "sharded"
                    else "%d independent %d-rank worlds, one per GPU" % (world, R)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

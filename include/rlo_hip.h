@@ -69,7 +69,9 @@ typedef struct {
     uint64_t fwd_bytes, vote_bytes, ctrl_bytes; /* this part's regions                    */
     int32_t cus, blocks_per_cu;
     int32_t part, n_parts, rank_begin, rank_end; /* ranks [rank_begin, rank_end) are local */
-    int32_t sys_scope, pad2;                     /* 1: parts span GPUs (system-scope stores) */
+    int32_t sys_scope;                           /* 1: parts span GPUs (system-scope stores) */
+    int32_t waves;                               /* waves per rank-workgroup: 8 (512 messages per
+                                                    iteration) or 4 (256), chosen at creation     */
 } rlo_world_info_t;
 
 /* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522

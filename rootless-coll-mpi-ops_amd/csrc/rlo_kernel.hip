@@ -41,7 +41,6 @@ static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
 static constexpr uint32_t kIdleSpin = 256;  // tight re-polls after an idle iteration (~0.1 ms at most)
-static constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at candidates 192..255
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -67,7 +66,12 @@ struct CandL {          // one message of this iteration, kept for the copy phas
     uint32_t kind, group;
 };
 
+// W waves per rank-workgroup (rlo_device.hpp kBlock documents the 4-wave form): 64 W candidate
+// messages per iteration.  8 waves (512 candidates, two waves per SIMD) when every rank has a CU
+// of its own; 4 waves when two rank-workgroups share a CU (worlds larger than the GPU)
+template <int W>
 struct Shared {
+    static constexpr int kWaves = W, kMaxCand = 64 * W;
     RankTopo t;
     // selection of this iteration (wave 0)
     uint64_t ring_head[2 * kMaxIn];  // consumer count of in-ring g at iteration start
@@ -287,7 +291,8 @@ __device__ __forceinline__ uint32_t hist_bin(uint64_t d) {
     return b < kHistBins ? b : kHistBins - 1;
 }
 
-__device__ __forceinline__ void set_error(Shared& S, const Params& P, uint32_t code, uint32_t aux) {
+template <class SH>
+__device__ __forceinline__ void set_error(SH& S, const Params& P, uint32_t code, uint32_t aux) {
     if (atomicCAS(&S.error, 0u, code) == 0u) {
         S.error_aux = aux;
         atomicCAS(P.error_flag, 0u, code);
@@ -328,7 +333,8 @@ __device__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, ui
 
 // one event record: the parity log (MODE_LOG, linear) or the host pickup ring (MODE_HOST, the
 // slot after this iteration's earlier events; the selection phase guaranteed the room)
-__device__ __forceinline__ uint32_t log_put(Shared& S, const Params& P, int lr, uint32_t kind, int origin, int from,
+template <class SH>
+__device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint32_t kind, int origin, int from,
                                             uint32_t id, uint32_t len, int vote, uint32_t aux) {
     if (!(P.mode & (MODE_LOG | MODE_HOST))) return ~0u;
     uint32_t i;
@@ -357,7 +363,8 @@ __device__ __forceinline__ uint32_t log_put(Shared& S, const Params& P, int lr, 
 }
 
 // vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741)
-__device__ __forceinline__ void emit_vote(Shared& S, const Params& P, int me, uint32_t k,
+template <class SH>
+__device__ __forceinline__ void emit_vote(SH& S, const Params& P, int me, uint32_t k,
                                           int origin, int32_t pid, uint32_t pseq, int vote) {
     unsigned long long p = atomicAdd((unsigned long long*)&S.vout_tail[k], 1ull);
     if (p - S.vout_head[k] >= P.vote_cap) {
@@ -454,18 +461,21 @@ __device__ __forceinline__ u32x4 gen_chunk(const Params& P, uint32_t kind, int m
 
 // ------------------------------------------------------------------ the kernel
 
-__global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
+    constexpr int kWaves = W, kBlock = 64 * W, kMaxCand = 64 * W;
+    constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at the last 64 candidates
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    __shared__ Shared S;
+    __shared__ Shared<W> S;
     const uint32_t nsmall = P.nsmall;  // chunks per staged message
     const uint32_t nmagic = nsmall > 1 ? 0xFFFFFFFFu / nsmall + 1u : 0u;
     PendState* pend = reinterpret_cast<PendState*>(dyn_lds);                        // [2 * n]
     uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + 32u * (uint32_t)P.n);  // [oi][256]
-    uint8_t* stage = dyn_lds + 32u * (uint32_t)P.n + P.nout_max * 512u;             // [message][q] x 16 B
+    uint8_t* stage = dyn_lds + 32u * (uint32_t)P.n + P.nout_max * (2u * kMaxCand);  // [message][q] x 16 B
     uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
     const uint32_t s2_blocks = P.stage2_bytes / 1024u;
 #define STG(c, q) (stage + (((uint32_t)(c) * nsmall + (uint32_t)(q)) << 4))
-#define OL(oi, r) olist[((uint32_t)(oi) << 8) + (uint32_t)(r)]
+#define OL(oi, r) olist[(uint32_t)(oi) * (uint32_t)kMaxCand + (uint32_t)(r)]
 
     const int lr = blockIdx.x;
     const int me = P.rank_begin + lr;
@@ -645,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             if (lane < sll) { S.vbase[lane] = vex; S.va[lane] = vtake; S.vhead[lane] = vin_head_r; }
             vin_head_r += vtake;  // merged by wave 1 before the next publish
             // in-rings: fair per-ring quotas
-            const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)256) : 0u;
+            const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)kMaxCand) : 0u;
             const uint32_t reserve = host ? kPass + 1u : ((P.mode & MODE_IAR) ? 2u : 0u);  // host: stage block + decision
             const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
@@ -1101,7 +1111,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                 const uint64_t b = __ballot(bit);
                 if (bit) {
                     const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
-                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 8)));
+                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 9)));  // c < 512: 9 bits
                     if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
                 }
             }
@@ -1296,7 +1306,7 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
             const uint32_t nit_r = lane < nout ? S.n_oi[lane] * nq : 0u;
             uint32_t items = 0;
             const uint32_t ibase_r = wave_excl_scan(nit_r, &items);
-            const uint32_t lo = (items * (uint32_t)w) >> 2, hi = (items * (uint32_t)(w + 1)) >> 2;
+            const uint32_t lo = items * (uint32_t)w / (uint32_t)kWaves, hi = items * (uint32_t)(w + 1) / (uint32_t)kWaves;
             for (uint64_t mo = __ballot(nit_r != 0 && ibase_r < hi && ibase_r + nit_r > lo); mo; mo &= mo - 1) {
                 const int oi = __builtin_ctzll(mo);
                 const uint32_t ib = rdl32(ibase_r, oi), ie = ib + rdl32(nit_r, oi);
@@ -1310,11 +1320,11 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
                     if (qb >= nq) { qb -= nq; rb++; }
                     const uint32_t ea = OL(oi, r);
                     const uint32_t eb = i + 64u < b ? (uint32_t)OL(oi, rb) : (uint32_t)kBigFlag;
-                    const bool va = !(ea & kBigFlag) && q < ((ea >> 8) & 0xfu);
-                    const bool vb = !(eb & kBigFlag) && qb < ((eb >> 8) & 0xfu);
+                    const bool va = !(ea & kBigFlag) && q < ((ea >> 9) & 0xfu);
+                    const bool vb = !(eb & kBigFlag) && qb < ((eb >> 9) & 0xfu);
                     u32x4 xa = {0u, 0u, 0u, 0u}, xb = {0u, 0u, 0u, 0u};
-                    if (va) xa = *reinterpret_cast<const u32x4*>(stage + __umul24(ea & 0xffu, stg_msg) + (q << 4));
-                    if (vb) xb = *reinterpret_cast<const u32x4*>(stage + __umul24(eb & 0xffu, stg_msg) + (qb << 4));
+                    if (va) xa = *reinterpret_cast<const u32x4*>(stage + __umul24(ea & 0x1ffu, stg_msg) + (q << 4));
+                    if (vb) xb = *reinterpret_cast<const u32x4*>(stage + __umul24(eb & 0x1ffu, stg_msg) + (qb << 4));
                     if (va) st_ring(ro, __umul24((s0 + r) & fcap_m, stride) + (q << 4), xa, sys);
                     if (vb) st_ring(ro, __umul24((s0 + rb) & fcap_m, stride) + (qb << 4), xb, sys);
                     r = rb + dr;
@@ -1503,11 +1513,12 @@ __global__ __launch_bounds__(kBlock) void rlo_progress_kernel(Params P) {
 
 }  // namespace rlo
 
-// C-ABI launch shim used by rlo_world.cpp
+// C-ABI launch shims used by rlo_world.cpp; waves = 4 or 8 (the Shared / LDS layout depends on it)
+template <int W>
 static hipError_t grant_dyn_lds(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {  // > 64 KiB of dynamic LDS must be requested explicitly
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel,
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
@@ -1515,17 +1526,25 @@ static hipError_t grant_dyn_lds(size_t dyn_lds) {
     return hipSuccess;
 }
 
-extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
-    hipError_t e = grant_dyn_lds(dyn_lds);
+extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int waves) {
+    hipError_t e = waves == 8 ? grant_dyn_lds<8>(dyn_lds) : grant_dyn_lds<4>(dyn_lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rlo::rlo_progress_kernel, dim3(blocks), dim3(rlo::kBlock), dyn_lds, stream, *p);
+    if (waves == 8) hipLaunchKernelGGL(rlo::rlo_progress_kernel<8>, dim3(blocks), dim3(512), dyn_lds, stream, *p);
+    else hipLaunchKernelGGL(rlo::rlo_progress_kernel<4>, dim3(blocks), dim3(256), dyn_lds, stream, *p);
     return hipGetLastError();
 }
 
-extern "C" size_t rlo_kernel_static_lds(void) { return sizeof(rlo::Shared); }
+extern "C" size_t rlo_kernel_static_lds(int waves) {
+    return waves == 8 ? sizeof(rlo::Shared<8>) : sizeof(rlo::Shared<4>);
+}
 
-extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds) {
-    hipError_t e = grant_dyn_lds(dyn_lds);
+extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int waves) {
+    if (waves == 8) {
+        hipError_t e = grant_dyn_lds<8>(dyn_lds);
+        if (e != hipSuccess) return e;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<8>, 512, dyn_lds);
+    }
+    hipError_t e = grant_dyn_lds<4>(dyn_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel, rlo::kBlock, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<4>, 256, dyn_lds);
 }

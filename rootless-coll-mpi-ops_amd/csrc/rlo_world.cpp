@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -15,9 +16,9 @@
 #include "rlo_device.hpp"
 #include "rlo_hip.h"
 
-extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream);
-extern "C" size_t rlo_kernel_static_lds(void);
-extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds);
+extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int waves);
+extern "C" size_t rlo_kernel_static_lds(int waves);
+extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int waves);
 extern "C" hipError_t rlo_launch_bulk(const rlo::BulkParams* p, int blocks, int local_ranks, hipStream_t stream);
 
 static_assert(sizeof(rlo_rank_stats_t) == sizeof(rlo::RankStats), "stats ABI");
@@ -295,6 +296,7 @@ struct rlo_world {
     float last_ms = 0.f;
     size_t dyn_lds = 0;
     uint32_t nsmall = 8, stage2 = 1024;
+    int waves = 4;  // rank-workgroup width: 8 (512 candidates per iteration) when each rank has a CU
 };
 
 namespace {
@@ -311,21 +313,22 @@ int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
 // co-residency of the part's rank-workgroups: largest small-path stage (nsmall chunks per
 // message, <= 8) and then the largest stage2 (<= 64 KiB) at which the occupancy calculator
 // (LDS allocation granularity, registers, waves) still co-schedules them
-int size_lds(rlo_world* w) {
+int size_lds_waves(rlo_world* w, int waves) {
     const Layout& L = w->L;
     const size_t lds_cu = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
     const int need_bpc = (w->nl + w->cus - 1) / w->cus;
     const size_t per_block = lds_cu / need_bpc;
+    const size_t cand = (size_t)64 * waves, stat = rlo_kernel_static_lds(waves);
     int api = 0;
     bool ok = false;
     for (uint32_t ns = std::min<uint32_t>(8u, L.stride / 16u); ns >= 1 && !ok; ns--) {
-        const size_t fixed = rlo_kernel_static_lds() + (size_t)32 * L.n + (size_t)2 * L.max_fan * 256 * 2 +
-                             (size_t)rlo::kMaxCand * ns * 16;
+        // [pending proposals 2N x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2]
+        const size_t fixed = stat + (size_t)32 * L.n + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16;
         if (per_block < fixed + 1024 + 512) continue;
         size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
         for (;;) {
-            w->dyn_lds = fixed - rlo_kernel_static_lds() + s2;
-            if (rlo_occupancy(&api, w->dyn_lds) != hipSuccess) api = 0;
+            w->dyn_lds = fixed - stat + s2;
+            if (rlo_occupancy(&api, w->dyn_lds, waves) != hipSuccess) api = 0;
             if (api >= need_bpc) { ok = true; break; }
             if (s2 <= 1024) break;
             s2 -= 1024;
@@ -334,9 +337,23 @@ int size_lds(rlo_world* w) {
         w->stage2 = (uint32_t)s2;
     }
     if (!ok) return RLO_E_OCCUPANCY;
+    w->waves = waves;
     w->blocks_per_cu = std::max(1, api);
     if (w->nl > w->blocks_per_cu * w->cus) return RLO_E_OCCUPANCY;
     return RLO_OK;
+}
+
+// 8-wave rank-workgroups (512 candidates per iteration) when every local rank gets a CU of its own,
+// every message fits the small copy path (slot <= 8 chunks: payloads <= 112 B) and the 8-wave layout
+// fits; else 4 waves (larger slots need the LDS for the large-message stage: 64 B storm 12.1 -> 16.0 M
+// bcast/s with 8 waves, but 256 B .. 4 KiB 30-40 % slower).  RLO_WAVES=4 / 8 forces one (A/B)
+int size_lds(rlo_world* w) {
+    const char* env = std::getenv("RLO_WAVES");
+    const int force = env ? std::atoi(env) : 0;
+    const bool small = w->L.stride <= 8u * 16u;
+    if (force != 4 && (small || force == 8) && w->nl <= w->cus && size_lds_waves(w, 8) == RLO_OK) return RLO_OK;
+    if (force == 8) return RLO_E_OCCUPANCY;
+    return size_lds_waves(w, 4);
 }
 
 // RankTopo of every local rank, with remote ends resolved to addresses in this process
@@ -616,6 +633,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->rank_begin = w->rb;
     o->rank_end = w->rb + w->nl;
     o->sys_scope = w->sys_scope;
+    o->waves = w->waves;
     return RLO_OK;
 }
 
@@ -996,7 +1014,7 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool noacq = std::getenv("RLO_NO_ACQUIRE") != nullptr;  // diagnostic A/B, unsafe
     if (noacq) w->P.mode |= rlo::MODE_NOACQ;
     else w->P.mode &= ~rlo::MODE_NOACQ;
-    hipError_t e = rlo_launch_progress(&w->P, w->nl, w->dyn_lds, s);
+    hipError_t e = rlo_launch_progress(&w->P, w->nl, w->dyn_lds, s, w->waves);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));
     return RLO_OK;

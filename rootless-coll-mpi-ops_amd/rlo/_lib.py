@@ -38,7 +38,7 @@ class WorldInfo(ctypes.Structure):
                 ("vote_bytes", ctypes.c_uint64), ("ctrl_bytes", ctypes.c_uint64), ("cus", ctypes.c_int32),
                 ("blocks_per_cu", ctypes.c_int32), ("part", ctypes.c_int32), ("n_parts", ctypes.c_int32),
                 ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),
-                ("pad2", ctypes.c_int32)]
+                ("waves", ctypes.c_int32)]
 
 
 class PartCfg(ctypes.Structure):
