@@ -428,7 +428,9 @@ def main():
     alg_bytes = k * 2.0 * (R - 1) * (length + 16) * copies / world
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
-    extras = {"bcast_per_s": round(bcast_per_s, 1), "world_ranks": R, "mode": mode}
+    extras = {"bcast_per_s": round(bcast_per_s, 1), "world_ranks": R, "mode": mode,
+              # staged slots whose header lacked the slot mark (each one a device error; 0 expected)
+              "unmarked_slots": int(sum_over_ranks(float(st["unmarked_slots"].sum())))}
     if mode == "replicas":
         extras["sharded_error"] = sharded_error
     if world > 1 and mode == "sharded":

@@ -242,6 +242,7 @@ typedef struct {
                           admit, effects, copy, publish) */
     uint64_t dbg[8];   /* RLO_FLAG_PROF: engine counters (DESIGN.md "Diagnostics") */
     uint32_t hist[128];
+    uint64_t unmarked_slots; /* staged ring slots whose header lacked the slot mark (RLO_DERR_BAD_SLOT) */
 } rlo_rank_stats_t;
 
 

@@ -17,6 +17,8 @@
 
 namespace rlo {
 
+// the 4-wave rank-workgroup; the kernel is templated on the wave count (4 or 8: 256 or 512
+// messages per iteration, rlo_kernel.hip) and the host picks the width per world (rlo_world.cpp)
 constexpr int kBlock = 256;       // threads per rank-workgroup: 4 waves, one 64-message pass each
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxFanout = 16;    // send_list_len <= ceil(log2 N) <= 16  (N <= 65536)
@@ -71,7 +73,8 @@ enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_
 // Slot header, 16 bytes:
 //   w0 = origin (16 b) | tag (8 b) << 16 | vote (8 b) << 24
 //   w1 = id   (bcast id / proposal pid)
-//   w2 = len  (24 b, payload bytes) | pseq (8 b) << 24   (pseq: per-origin proposal sequence)
+//   w2 = len (16 b, payload bytes) | mark 0xA5 (8 b) << 16 | pseq (8 b) << 24 (pseq: per-origin
+//        proposal sequence; the mark, set at origination, tells a written slot from zeroed ring memory)
 //   w3 = t0   (low 32 bits of s_memrealtime at origination, 100 MHz)
 // Vote slot, 16 bytes: w0 = origin | vote << 24, w1 = pid, w2 = pseq, w3 = voter
 
@@ -105,6 +108,7 @@ struct RankStats {
     uint64_t dbg[8];                      // MODE_PROF: ring cands, admitted, storm-allowed iters, storm offered,
                                           //   shallow-blocked, backlog-blocked, child copies, max out-ring fill
     uint32_t hist[kHistBins];
+    uint64_t unmarked_slots;               // staged ring slots whose header lacked the slot mark (an error)
 };
 
 struct LogRec {            // 32 bytes

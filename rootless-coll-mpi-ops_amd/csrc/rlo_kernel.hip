@@ -109,7 +109,7 @@ struct Shared {
     uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
-    unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls;
+    unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
     uint64_t prof[8], prof_t, dbg[8];
     int64_t expect_dec;
     uint32_t hist[kHistBins];
@@ -245,6 +245,10 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 __device__ __forceinline__ uint32_t chunk_mix(uint32_t q, u32x4 w) {
     return fmix32(w.x ^ fmix32(w.y ^ fmix32(w.z ^ fmix32(w.w ^ (q * kGolden32 + 0x7F4A7C15u)))));
 }
+
+// slot mark (w2 bits 16..23 of every slot header, rlo_device.hpp): rings are zeroed at creation,
+// so a staged header without the mark is a slot whose bytes were not visible yet
+static constexpr uint32_t kSlotMark = 0xA5u;
 
 __device__ __forceinline__ uint32_t mask_bytes(uint32_t w, int keep) {  // keep the low `keep` bytes
     return keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.expect_dec = ((P.mode & MODE_IAR) && !host) ? P.expect_dec[lr] : 0;
             S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
-            S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = 0;
+            S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0;
         }
     }
@@ -936,14 +940,21 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 kind = K_RING;
                 const int origin = (int)(w0 & 0xffffu);
                 const uint32_t tag = (w0 >> 16) & 0xffu;
-                if (origin >= P.n || (tag == TAG_BCAST && (P.mode & MODE_LAT) && id >= P.lat_rounds)) {
+                if (((w2 >> 16) & 0xffu) != kSlotMark) {
+                    // a slot whose bytes were not visible behind its published tail: every header
+                    // carries the mark from its origination, so this is a protocol violation -- stop
+                    // loudly instead of forwarding zeros (rings are uncached, rlo_world.cpp)
+                    atomicAdd(&S.stale, 1ull);
+                    set_error(S, P, ERR_BAD_SLOT, 0x57A1Eu);
+                    kind = K_BAD;
+                } else if (origin >= P.n || (tag == TAG_BCAST && (P.mode & MODE_LAT) && id >= P.lat_rounds)) {
                     set_error(S, P, ERR_BAD_SLOT, w0);
                     kind = K_BAD;  // consumed, never forwarded, no side effects
                 } else if (tag == TAG_BCAST || tag == TAG_DECISION) {
                     kids = kids_of(me, origin, from, level, last_wall, scc, sll, sl_r);
                 } else if (tag == TAG_PROPOSAL) {
                     // PBuf [pid][vote][data_len u64][data] at slot + 16 (rootless_ops.c:1402-1410)
-                    const uint32_t plen = w2 & 0xffffffu;
+                    const uint32_t plen = w2 & 0xffffu;
                     if (host) {  // the host judges: hold the proposal at the head of its ring until the verdict
                         PendState* ps = &pend[2 * origin + ((w2 >> 24) & 1u)];
                         const uint8_t pv = ps->valid;
@@ -981,12 +992,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     id = h.y;
                     if (((h.x >> 16) & 0xffu) == TAG_PROPOSAL) {  // RLO_submit_proposal :876-906 (payload = PBuf)
                         w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
-                        w2 = (h.z & 0xffffffu) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                        w2 = (h.z & 0xffffu) | ((uint32_t)(S.own_iter & 0xff) << 24);
                     } else {
                         w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
-                        w2 = h.z & 0xffffffu;
+                        w2 = h.z & 0xffffu;
                     }
-                    if ((w2 & 0xffffffu) + kHdr > P.fwd_stride) {
+                    if ((w2 & 0xffffu) + kHdr > P.fwd_stride) {
                         set_error(S, P, ERR_HOST_CMD, h.x);
                         kind = K_BAD;
                         kids = 0;
@@ -1012,13 +1023,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
                     w2 = P.len;
                 }
-                // stage the header (+ the payload of a small message) like a received slot
-                const uint32_t nch = (kHdr + (w2 & 0xffffffu) + 15u) >> 4;
+                // stage the header (+ the payload of a small message) like a received slot; the header
+                // carries the slot mark every hop checks
+                w2 = (w2 & 0xff00ffffu) | (kSlotMark << 16);
+                const uint32_t nch = (kHdr + (w2 & 0xffffu) + 15u) >> 4;
                 *reinterpret_cast<u32x4*>(STG(c, 0)) = u32x4{w0, id, w2, t0};
                 if (nch <= nsmall && kind != K_HOST && kind != K_BAD)
                     for (uint32_t q = 1; q < nch; q++)
                         *reinterpret_cast<u32x4*>(STG(c, q)) =
-                            gen_chunk(P, kind, me, id, w2 & 0xffffffu, src, (int)(int8_t)(w0 >> 24), q);
+                            gen_chunk(P, kind, me, id, w2 & 0xffffu, src, (int)(int8_t)(w0 >> 24), q);
             }
             const int origin = (int)(w0 & 0xffffu);
             const uint32_t need = active ? need_of(kids, origin, sll, sl_r) : 0u;
@@ -1026,7 +1039,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const int l = __builtin_ctzll(jb);
                 const uint32_t lsrc = rdl32(src, l), lw2 = rdl32(w2, l), lid = rdl32(id, l);
                 const int lorg = (int)(rdl32(w0, l) & 0xffffu), lfrom = (int)rdl32((uint32_t)from, l);
-                const uint32_t plen = lw2 & 0xffffffu;
+                const uint32_t plen = lw2 & 0xffffu;
                 uint32_t slot = 0;
                 if (lane == 0) {
                     PendState* ps = &pend[2 * lorg + ((lw2 >> 24) & 1u)];
@@ -1079,7 +1092,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             BAR();  // every wave has read wcnt and posted its first misfit per source
             const bool admitted = active && fits && c < S.first_bad[group];
             const uint32_t an = admitted ? need : 0u;
-            const uint32_t len = w2 & 0xffffffu;
+            const uint32_t len = w2 & 0xffffu;
             const bool isbig = admitted && ((kHdr + len + 15u) >> 4) > nsmall;
             const uint32_t nch_s = (kHdr + len + 15u) >> 4;  // small path: chunks, kept in the olist entry
             const uint32_t wadm = wave_or(an);
@@ -1234,7 +1247,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     uint32_t nb = 0, cc = 0, q0 = 0;
                     if (mi < nbig) {
                         cc = S.big[mi];
-                        const uint32_t nch = (kHdr + (S.cand[cc].w2 & 0xffffffu) + 15u) >> 4;
+                        const uint32_t nch = (kHdr + (S.cand[cc].w2 & 0xffffu) + 15u) >> 4;
                         q0 = lane == 0 ? bq0 : 0u;
                         nb = (nch - q0 + 63u) >> 6;
                     }
@@ -1264,7 +1277,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 for (uint32_t b = (uint32_t)w; b < nblk; b += kWaves) {
                     const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
                     const CandL& cl = S.cand[cc];
-                    const uint32_t nch = (kHdr + (cl.w2 & 0xffffffu) + 15u) >> 4;
+                    const uint32_t nch = (kHdr + (cl.w2 & 0xffffu) + 15u) >> 4;
                     uint8_t* dst = stage2 + (b << 10);
                     if (cl.kind == K_RING) {
                         if (q < nch) dma16(rf, dst, cl.src + 16u * q);
@@ -1275,7 +1288,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     } else if (q < nch) {
                         *reinterpret_cast<u32x4*>(dst + 16u * lane) =
                             q == 0 ? u32x4{cl.w0, cl.id, cl.w2, cl.t0}
-                                   : gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), q);
+                                   : gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), q);
                     }
                 }
                 VM_DRAIN();
@@ -1350,7 +1363,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     for (uint32_t b = (uint32_t)w; b < nblk; b += kWaves) {
                         const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
                         const CandL& cl = S.cand[cc];
-                        const uint32_t blen = cl.w2 & 0xffffffu, nch = (kHdr + blen + 15u) >> 4;
+                        const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
                         const u32x4 v = *reinterpret_cast<const u32x4*>(stage2 + (b << 10) + 16u * lane);
                         for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
                             const int oi = __builtin_ctz(a2);
@@ -1503,6 +1516,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         st.iterations = n_iter;
         st.busy_iterations = n_busy;
         st.stalls = S.stalls;
+        st.unmarked_slots = S.stale;
         st.log_count = S.log_count;
         st.t_start = t_start;
         st.t_end = now_ticks();

@@ -458,7 +458,13 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return RLO_E_NODEVICE;
     rlo_world* w = new rlo_world();
     w->max_payload = (std::max<uint32_t>(cfg->max_payload ? cfg->max_payload : 4096u, 16u) + 15u) & ~15u;
+    if (w->max_payload > 65520u) { delete w; return RLO_E_INVAL; }  // slot header: 16-bit length (rlo_device.hpp)
     w->flags = cfg->flags;
+    // rings and counters in uncached memory for every world, not only for parts on other GPUs: a
+    // line of ring memory left in some XCD's L2 by an earlier kernel (the creation / reset fill) is
+    // not invalidated by another XCD's write-through stores, and a consumer on that XCD read the
+    // zeros (seen as unmarked slot headers that never became visible).  RLO_CACHED_RINGS=1: A/B only
+    if (!std::getenv("RLO_CACHED_RINGS")) w->flags |= RLO_PART_UNCACHED;
     int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, w->L);
     if (rc) { delete w; return rc; }
     w->part = cfg->part;
@@ -980,6 +986,9 @@ int rlo_reset(rlo_world_t* w, void* stream) {
         std::fill(w->pk_head.begin(), w->pk_head.end(), 0);
     }
     HIPCHK(hipMemsetAsync(w->ctrl, 0, w->L.ctrl_words[w->part] * 8, s));
+    // zeroed rings: a slot whose bytes are not visible yet reads without the header's slot mark
+    // (rlo_device.hpp) and is reloaded, in every launch, not only in a fresh world
+    HIPCHK(hipMemsetAsync(w->fwd, 0, w->L.fwd_bytes[w->part], s));
     HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->nl, s));
     if (w->have_program && (w->P.mode & rlo::MODE_LAT)) {
         HIPCHK(hipMemsetAsync(w->d_lat_count.p, 0, sizeof(uint32_t) * w->lat_rounds, s));

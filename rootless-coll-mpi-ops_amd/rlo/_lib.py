@@ -74,7 +74,7 @@ class RankStats(ctypes.Structure):
         "own_decided", "own_approved", "proposals_recv", "iterations", "busy_iterations", "stalls", "log_count",
         "t_start", "t_end")] + [("error", ctypes.c_uint32), ("error_aux", ctypes.c_uint32), ("prof", ctypes.c_uint64 * 8),
                            ("dbg", ctypes.c_uint64 * 8),
-                           ("hist", ctypes.c_uint32 * 128)]
+                           ("hist", ctypes.c_uint32 * 128), ("unmarked_slots", ctypes.c_uint64)]
 
 
 class LogRec(ctypes.Structure):
