@@ -182,7 +182,7 @@ def bulk_leg(dist, world, rank, local, sizes_mib=(1, 4, 16, 64), iters=5, blocks
 
     G = world if world > 1 else 8
     maxb = max(sizes_mib) << 20
-    blocks = blocks or (128 if world > 1 else 32)
+    blocks = blocks or 0  # 0: the library sizes workgroups and chunks (rlo_bulk_launch)
     if world > 1:
         w = rlo.World.part(G, G, rank, max_payload=64, device=local, uncached=True)
         blobs = [None] * world
@@ -263,7 +263,7 @@ def bulk_leg(dist, world, rank, local, sizes_mib=(1, 4, 16, 64), iters=5, blocks
     finally:
         b.close()
         w.close()
-    return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "blocks_per_rank": blocks,
+    return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "blocks_per_rank": blocks or "auto",
             "algorithm": "pipelined scatter + all-gather over per-rank HBM buffers (rlo_bulk.hip)",
             "baseline": "torch.distributed.broadcast, nccl backend (RCCL), same root" if world > 1 else None,
             "sizes": out}

@@ -213,7 +213,9 @@ int rlo_bulk_export(rlo_bulk_t* b, void* blob, uint32_t cap); /* returns RLO_BUL
 int rlo_bulk_connect(rlo_bulk_t* b, const void* blobs /* n_parts x RLO_BULK_BLOB_BYTES */, int n_parts);
 void* rlo_bulk_buffer(rlo_bulk_t* b, int rank); /* device pointer of a local rank's buffer  */
 int rlo_bulk_reset(rlo_bulk_t* b, void* stream);  /* zero this part's flags (sync)           */
-/* async; chunk_bytes 0 = auto; blocks = workgroups per local rank (same on every part) */
+/* async; chunk_bytes 0 = auto (one chunk when every part shares a GPU, ~sqrt(bytes / 4 MiB)
+ * chunks across GPUs); blocks = workgroups per local rank, 0 = auto (bytes / 64 KiB in
+ * [32, 128]); the same arguments on every part */
 int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream);
 int rlo_bulk_wait(rlo_bulk_t* b, float* kernel_ms); /* RLO_E_DEVICE if a wait timed out      */
 int rlo_bulk_destroy(rlo_bulk_t* b);

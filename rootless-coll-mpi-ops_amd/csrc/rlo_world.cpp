@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1121,7 +1122,7 @@ int rlo_round_ticks(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
 namespace {
 struct BulkBlob {
     uint32_t magic, part;
-    int32_t device, pad;
+    int32_t device, pci;  // pci: PCI domain/bus/device of the part's GPU (auto chunking)
     uint64_t token, ptr, bytes, stride;
     hipIpcMemHandle_t h;
 };
@@ -1141,7 +1142,16 @@ struct rlo_bulk {
     rlo::BulkParams P{};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool connected = false;
+    bool cross_gpu = false;  // some part sits on another GPU: links, not HBM, bound the copy
 };
+
+namespace {
+int32_t pci_of(int device) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return -1;
+    return (p.pciDomainID << 16) | (p.pciBusID << 8) | p.pciDeviceID;
+}
+}  // namespace
 
 extern "C" {
 
@@ -1174,6 +1184,7 @@ int rlo_bulk_export(rlo_bulk_t* b, void* blob, uint32_t cap) {
     x.magic = kBulkMagic;
     x.part = (uint32_t)b->w->part;
     x.device = b->w->device;
+    x.pci = pci_of(b->w->device);
     x.token = process_token();
     x.ptr = (uint64_t)(uintptr_t)b->region;
     x.bytes = b->buf_bytes;
@@ -1195,6 +1206,9 @@ int rlo_bulk_connect(rlo_bulk_t* b, const void* blobs, int n_parts) {
         std::memcpy(&x, (const uint8_t*)blobs + (size_t)q * RLO_BULK_BLOB_BYTES, sizeof x);
         if (x.magic != kBulkMagic || (int)x.part != q || x.bytes != b->buf_bytes || x.stride != b->stride)
             return RLO_E_INVAL;
+        int32_t pci0;
+        std::memcpy(&pci0, (const uint8_t*)blobs + offsetof(BulkBlob, pci), sizeof pci0);
+        if (x.pci != pci0 || x.pci < 0) b->cross_gpu = true;  // the same answer on every part
         if (q == w->part) {
             b->base[q] = b->region;
         } else if (x.token == tok) {
@@ -1248,10 +1262,23 @@ int rlo_bulk_reset(rlo_bulk_t* b, void* stream) {
 int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream) {
     if (!b || !b->connected) return RLO_E_INVAL;
     const int n = b->w->L.n;
-    if (origin < 0 || origin >= n || bytes == 0 || bytes > b->buf_bytes || blocks == 0 || blocks > 1024) return RLO_E_INVAL;
+    if (origin < 0 || origin >= n || bytes == 0 || bytes > b->buf_bytes || blocks > 1024) return RLO_E_INVAL;
     rlo::BulkParams& P = b->P;
+    // Auto sizing (tools/bulk_sweep.py, profiles/r1s5_bulk_sweep.jsonl).  Every chunk costs each
+    // workgroup a system release + flag adds + (receivers) a poll and an acquire, and the cost grows
+    // with the workgroups: on one GPU a single chunk is fastest at every size (64 MiB, 128 blocks:
+    // 157 us for 1 chunk, 458 us for 16).  Across GPUs a phase is xGMI-link bound, so pipelining
+    // the scatter under the all-gather pays: T ~ D(1 + 1/k) + k c  =>  k ~ sqrt(D / c), i.e.
+    // k = floor(sqrt(bytes / 4 MiB)) chunks (1 MiB, 4 MiB: 1; 16 MiB: 2; 64 MiB: 4).
+    if (blocks == 0) blocks = (uint32_t)std::min<uint64_t>(128, std::max<uint64_t>(32, bytes >> 16));
+    uint64_t want = chunk_bytes;
+    if (want == 0) {
+        uint64_t k = 1;
+        if (b->cross_gpu)
+            while ((k + 1) * (k + 1) * (4ull << 20) <= bytes && k < rlo::kBulkMaxChunks) k++;
+        want = (bytes + k - 1) / k;
+    }
     // stripes are whole 1-KiB blocks; a chunk is (N-1) stripes; at most kBulkMaxChunks chunks
-    uint64_t want = chunk_bytes ? chunk_bytes : std::max<uint64_t>(bytes / 16, 256u * 1024u);
     uint64_t stripe = (want / (uint64_t)(n - 1) + rlo::kBulkBlock - 1) / rlo::kBulkBlock * rlo::kBulkBlock;
     stripe = std::max<uint64_t>(stripe, rlo::kBulkBlock);
     uint64_t chunk = stripe * (uint64_t)(n - 1);

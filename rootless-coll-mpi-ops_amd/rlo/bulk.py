@@ -46,7 +46,8 @@ class Bulk:
     def reset(self, stream=None):
         check(self.lib.rlo_bulk_reset(self.h, stream), "rlo_bulk_reset")
 
-    def launch(self, origin, nbytes, blocks=64, chunk=0, stream=None):
+    def launch(self, origin, nbytes, blocks=0, chunk=0, stream=None):
+        """blocks 0 / chunk 0: sized by the library (rlo_bulk_launch in rlo_hip.h)"""
         check(self.lib.rlo_bulk_launch(self.h, origin, nbytes, chunk, blocks, stream), "rlo_bulk_launch")
 
     def wait(self, raise_on_error=True):

@@ -40,9 +40,12 @@ def _check(b, n, origin, nbytes, src, rep):
 
 
 @pytest.mark.parametrize("n,nbytes,origin,blocks,chunk,reps", [
-    (2, 1 << 20, 1, 8, 0, 2), (3, 3 * (1 << 20) + 123, 0, 16, 0, 2), (8, 4 << 20, 5, 16, 0, 2),
+    # chunk 0 is the library's choice (one chunk on one GPU); explicit chunks keep the pipelined
+    # scatter / all-gather covered; blocks 0 is the library's choice too
+    (2, 1 << 20, 1, 8, 256 << 10, 2), (3, 3 * (1 << 20) + 123, 0, 16, 0, 2), (8, 4 << 20, 5, 16, 256 << 10, 2),
     (8, 1000, 7, 4, 0, 2), (5, (1 << 20) + 16, 2, 8, 64 << 10, 2), (16, 2 << 20, 9, 8, 0, 2),
-    (3, 3 * (1 << 20) + 123, 0, 16, 0, 40), (8, (4 << 20) + 80, 3, 32, 0, 40)])
+    (3, 3 * (1 << 20) + 123, 0, 16, 192 << 10, 40), (8, (4 << 20) + 80, 3, 32, 0, 40),
+    (8, (4 << 20) + 80, 3, 0, 0, 4), (4, (5 << 20) + 7, 1, 0, 512 << 10, 4)])
 def test_bulk_one_part(rlo, n, nbytes, origin, blocks, chunk, reps):
     import torch
 
