@@ -257,8 +257,9 @@ def bulk_leg(dist, world, rank, local, sizes_mib=(1, 4, 16, 64), iters=5, blocks
                 rec["rccl_ms"] = round(sorted(rc)[len(rc) // 2], 4)
                 rec["rccl_algbw_GBps"] = round(nbytes / (rec["rccl_ms"] * 1e-3) / 1e9, 2)
                 rec["ours_over_rccl"] = round(rec["rccl_ms"] / rec["ours_ms"], 3)
-            else:  # one GPU: every byte written once per receiver and read once per forward
-                rec["hbm_GBps"] = round((2.0 * (G - 1) * nbytes) / (rec["ours_ms"] * 1e-3) / 1e9, 1)
+            else:  # one GPU: every receiver's copy written once (N-1)S; the originator reads S to
+                # scatter, the stripe owners read S between them to all-gather: (N+1)S HBM bytes
+                rec["hbm_GBps"] = round(((G + 1) * nbytes) / (rec["ours_ms"] * 1e-3) / 1e9, 1)
             out.append(rec)
     finally:
         b.close()
