@@ -108,7 +108,7 @@ typedef struct {
     uint64_t seed;       /* originator of bcast b = splitmix64(seed + b) % N              */
     int64_t k;           /* bcasts in the storm                                            */
     uint32_t len;        /* payload bytes (<= max_payload)                                 */
-    uint32_t window;     /* max originations per rank per progress iteration (0 = 32)      */
+    uint32_t window;     /* max originations per rank per progress iteration (0 = 64, max 64) */
     uint32_t flags;      /* RLO_FLAG_*                                                      */
     uint32_t log_cap;    /* log records per rank when RLO_FLAG_LOG                          */
 } rlo_storm_cfg_t;

@@ -186,7 +186,10 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         vrings[L.part_of[e.src]] += 1;
     }
     const uint64_t max_rings = *std::max_element(rings.begin(), rings.end());
-    uint32_t cap = ring_slots ? pow2_ceil(ring_slots) : 512u;
+    // default depth (tools/sweep.py, profiles/r1s5_sweep64.log): small slots (the 8-wave path,
+    // payload <= 112 B) keep the wall ranks' hot rings from refusing: 64 B storm at 256 ranks
+    // 512 slots 16.1M, 1024 25.8M, 2048 29.2M, 4096 29.4M bcast/s; larger slots stay at 512
+    uint32_t cap = ring_slots ? pow2_ceil(ring_slots) : (L.stride <= 128u ? 2048u : 512u);
     const uint64_t limit = 0xFFFF0000ull;
     if (max_rings * cap * L.stride > limit) cap = pow2_floor(limit / (max_rings * L.stride));
     if (cap < 16) return RLO_E_INVAL;
@@ -713,7 +716,7 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
              ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
     P.seed = cfg->seed;
     P.len = cfg->len;
-    P.window = std::min<uint32_t>(cfg->window ? cfg->window : 32, 64u);  // one wave prefetches the ids
+    P.window = std::min<uint32_t>(cfg->window ? cfg->window : 64, 64u);  // one wave prefetches the ids
     P.sched_off = w->d_sched_off.p;
     P.sched_ids = w->d_sched_ids.p;
     P.expect_bcast = w->d_expect_bcast.p;

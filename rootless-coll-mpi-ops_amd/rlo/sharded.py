@@ -22,7 +22,7 @@ def even_bounds(n, parts):
 
 def _program(w, spec):
     if spec["kind"] == "storm":
-        w.program_storm(spec["k"], spec["len"], seed=spec.get("seed", 0x5EED), window=spec.get("window", 32),
+        w.program_storm(spec["k"], spec["len"], seed=spec.get("seed", 0x5EED), window=spec.get("window", 64),
                         log=spec.get("log", False), log_cap=spec.get("log_cap", 0), hist=spec.get("hist", False))
     elif spec["kind"] == "iar":
         from . import _lib as L

@@ -84,7 +84,7 @@ class World:
             pass
 
     # ------------------------------------------------------------ programs
-    def program_storm(self, k, length, seed=0x5EED, window=32, log=False, hist=False, log_cap=0, prof=False):
+    def program_storm(self, k, length, seed=0x5EED, window=64, log=False, hist=False, log_cap=0, prof=False):
         flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0) | (L.RLO_FLAG_PROF if prof else 0)
         cfg = L.StormCfg(seed, k, length, window, flags, log_cap)
         check(self.lib.rlo_program_storm(self.h, ctypes.byref(cfg)), "rlo_program_storm")
