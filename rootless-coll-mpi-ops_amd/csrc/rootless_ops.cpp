@@ -584,7 +584,11 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
     pc.part = e->rank;
     pc.part_begin = nullptr;
     pc.max_payload = e->slot_bytes;
-    pc.ring_slots = e->slot_bytes > 4096 ? 128u : 0u;
+    // 512 slots for small slots (the library default is 2048 there, tuned for device storms; the
+    // drop-in's few ranks per GPU gain nothing from it: profiles/r1s5_api_slots.jsonl); RLO_RING_SLOTS
+    // overrides it for diagnostics
+    pc.ring_slots = e->slot_bytes > 4096 ? 128u : 512u;
+    if (const char* rs = std::getenv("RLO_RING_SLOTS")) pc.ring_slots = (uint32_t)std::strtoul(rs, nullptr, 10);
     pc.device = e->device;
     pc.flags = multi ? RLO_PART_UNCACHED : 0u;
     int rc = rlo_part_create(&pc, &e->w);
