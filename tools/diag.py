@@ -43,7 +43,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=256)
 ap.add_argument("--k", type=int, default=1 << 18)
 args = ap.parse_args()
-for ln, win in ((64, 32), (4096, 32)):
+for ln, win in ((64, 64), (4096, 32)):
     w = rlo.World(args.n, max_payload=max(64, ln))
     k = args.k if ln <= 1024 else args.k // 8
     w.program_storm(k, ln, window=win)
