@@ -217,6 +217,10 @@ int rlo_bulk_reset(rlo_bulk_t* b, void* stream);  /* zero this part's flags (syn
  * chunks across GPUs); blocks = workgroups per local rank, 0 = auto (bytes / 64 KiB in
  * [32, 128]); the same arguments on every part */
 int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream);
+/* the launch geometry rlo_bulk_launch uses (pure host arithmetic, no GPU): stripe bytes per
+ * owner per chunk (whole 1-KiB blocks), chunk bytes ((n-1) stripes), chunk count, workgroups */
+typedef struct { uint32_t stripe, chunk, nchunks, blocks; } rlo_bulk_plan_t;
+int rlo_bulk_plan(int n, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, int cross_gpu, rlo_bulk_plan_t* out);
 int rlo_bulk_wait(rlo_bulk_t* b, float* kernel_ms); /* RLO_E_DEVICE if a wait timed out      */
 int rlo_bulk_destroy(rlo_bulk_t* b);
 

@@ -1262,11 +1262,8 @@ int rlo_bulk_reset(rlo_bulk_t* b, void* stream) {
     return RLO_OK;
 }
 
-int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream) {
-    if (!b || !b->connected) return RLO_E_INVAL;
-    const int n = b->w->L.n;
-    if (origin < 0 || origin >= n || bytes == 0 || bytes > b->buf_bytes || blocks > 1024) return RLO_E_INVAL;
-    rlo::BulkParams& P = b->P;
+int rlo_bulk_plan(int n, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, int cross_gpu, rlo_bulk_plan_t* out) {
+    if (!out || n < 2 || n > rlo::kMaxBulkRanks || bytes == 0 || blocks > 1024) return RLO_E_INVAL;
     // Auto sizing (tools/bulk_sweep.py, profiles/r1s5_bulk_sweep.jsonl).  Every chunk costs each
     // workgroup a system release + flag adds + (receivers) a poll and an acquire, and the cost grows
     // with the workgroups: on one GPU a single chunk is fastest at every size (64 MiB, 128 blocks:
@@ -1277,7 +1274,7 @@ int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_by
     uint64_t want = chunk_bytes;
     if (want == 0) {
         uint64_t k = 1;
-        if (b->cross_gpu)
+        if (cross_gpu)
             while ((k + 1) * (k + 1) * (4ull << 20) <= bytes && k < rlo::kBulkMaxChunks) k++;
         want = (bytes + k - 1) / k;
     }
@@ -1287,11 +1284,27 @@ int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_by
     uint64_t chunk = stripe * (uint64_t)(n - 1);
     while ((bytes + chunk - 1) / chunk > rlo::kBulkMaxChunks) { stripe *= 2; chunk = stripe * (uint64_t)(n - 1); }
     if (chunk > 0xFFFFFFFFull) return RLO_E_INVAL;
+    out->stripe = (uint32_t)stripe;
+    out->chunk = (uint32_t)chunk;
+    out->nchunks = (uint32_t)((bytes + chunk - 1) / chunk);
+    out->blocks = blocks;
+    return RLO_OK;
+}
+
+int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream) {
+    if (!b || !b->connected) return RLO_E_INVAL;
+    const int n = b->w->L.n;
+    if (origin < 0 || origin >= n || bytes > b->buf_bytes) return RLO_E_INVAL;
+    rlo_bulk_plan_t plan;
+    const int rc = rlo_bulk_plan(n, bytes, chunk_bytes, blocks, b->cross_gpu ? 1 : 0, &plan);
+    if (rc != RLO_OK) return rc;
+    blocks = plan.blocks;
+    rlo::BulkParams& P = b->P;
     P.origin = origin;
     P.bytes = bytes;
-    P.stripe = (uint32_t)stripe;
-    P.chunk = (uint32_t)chunk;
-    P.nchunks = (uint32_t)((bytes + chunk - 1) / chunk);
+    P.stripe = plan.stripe;
+    P.chunk = plan.chunk;
+    P.nchunks = plan.nchunks;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(b->w->device));
     HIPCHK(hipEventRecord(b->ev0, s));

@@ -77,6 +77,11 @@ class RankStats(ctypes.Structure):
                            ("hist", ctypes.c_uint32 * 128), ("unmarked_slots", ctypes.c_uint64)]
 
 
+class BulkPlan(ctypes.Structure):
+    _fields_ = [("stripe", ctypes.c_uint32), ("chunk", ctypes.c_uint32), ("nchunks", ctypes.c_uint32),
+                ("blocks", ctypes.c_uint32)]
+
+
 class LogRec(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_uint32), ("origin", ctypes.c_int32), ("from_", ctypes.c_int32), ("id", ctypes.c_uint32),
                 ("len", ctypes.c_uint32), ("vote", ctypes.c_int32), ("aux", ctypes.c_uint32), ("payload_idx", ctypes.c_uint32)]
@@ -90,7 +95,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_strerror", "rlo_last_hip_error",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
            "rlo_device_count", "rlo_bulk_create", "rlo_bulk_export", "rlo_bulk_connect", "rlo_bulk_buffer",
-           "rlo_bulk_reset", "rlo_bulk_launch", "rlo_bulk_wait", "rlo_bulk_destroy"]
+           "rlo_bulk_reset", "rlo_bulk_launch", "rlo_bulk_wait", "rlo_bulk_destroy", "rlo_bulk_plan"]
 RLO_BULK_BLOB_BYTES = 256
 
 _lib = None
@@ -141,6 +146,8 @@ def load():
     L.rlo_bulk_buffer.restype = vp
     L.rlo_bulk_reset.argtypes = [vp, vp]
     L.rlo_bulk_launch.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, vp]
+    L.rlo_bulk_plan.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                ctypes.POINTER(BulkPlan)]
     L.rlo_bulk_wait.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.rlo_bulk_destroy.argtypes = [vp]
     L.rlo_strerror.argtypes = [ctypes.c_int]

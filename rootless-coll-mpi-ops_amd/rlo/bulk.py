@@ -12,6 +12,14 @@ from . import _lib as L
 from ._lib import check
 
 
+def plan(n, nbytes, chunk=0, blocks=0, cross_gpu=False):
+    """rlo_bulk_plan: the geometry rlo_bulk_launch would use (host arithmetic, no GPU needed)"""
+    lib = L.load()
+    out = L.BulkPlan()
+    check(lib.rlo_bulk_plan(n, nbytes, chunk, blocks, 1 if cross_gpu else 0, ctypes.byref(out)), "rlo_bulk_plan")
+    return {"stripe": out.stripe, "chunk": out.chunk, "nchunks": out.nchunks, "blocks": out.blocks}
+
+
 class _CAI:
     def __init__(self, ptr, nbytes):
         self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}

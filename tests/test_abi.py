@@ -96,3 +96,39 @@ def test_children_cover_exact_spanning_tree():
                 seen.add(r)
                 frontier += [(c, r) for c in rlo.children(n, r, o, frm)]
             assert len(seen) == n
+
+
+def test_bulk_plan_geometry():
+    """rlo_bulk_plan (host arithmetic behind rlo_bulk_launch): stripes are whole 1-KiB blocks, a chunk
+    is (n-1) stripes, the chunks cover the message, at most 4096 chunks; library defaults: one chunk
+    on one GPU, floor(sqrt(bytes / 4 MiB)) chunks across GPUs, bytes / 64 KiB workgroups in [32, 128]."""
+    import math
+
+    from rlo.bulk import plan
+
+    MiB = 1 << 20
+    for n in (2, 3, 5, 8, 16, 64):
+        for nbytes in (1, 1000, 1024, MiB, MiB + 16, 3 * MiB + 123, 16 * MiB, 64 * MiB, 1 << 30):
+            for chunk in (0, 4096, 64 << 10, MiB):
+                for cross in (False, True):
+                    p = plan(n, nbytes, chunk=chunk, cross_gpu=cross)
+                    assert p["stripe"] % 1024 == 0 and p["stripe"] >= 1024, (n, nbytes, p)
+                    assert p["chunk"] == p["stripe"] * (n - 1)
+                    assert p["nchunks"] == -(-nbytes // p["chunk"]) <= 4096
+                    assert p["blocks"] == min(128, max(32, nbytes >> 16))
+                    if chunk == 0:
+                        want = 1 if not cross else max(1, math.isqrt(nbytes // (4 * MiB)))
+                        # the stripe rounds up to whole blocks, so the chunk count can only shrink
+                        assert p["nchunks"] <= want, (n, nbytes, cross, p)
+                        if nbytes >= 64 * (n - 1) * 1024 and want <= 4096:
+                            assert p["nchunks"] == want or p["nchunks"] == want - 1, (n, nbytes, cross, p)
+    assert plan(8, 64 * MiB, cross_gpu=True)["nchunks"] == 4
+    assert plan(8, 16 * MiB, cross_gpu=True)["nchunks"] == 2
+    assert plan(8, 4 * MiB, cross_gpu=True)["nchunks"] == 1
+    assert plan(8, 64 * MiB, cross_gpu=False)["nchunks"] == 1
+    assert plan(8, MiB, blocks=7)["blocks"] == 7
+    import rlo
+
+    for bad in ((1, MiB), (65, MiB), (8, 0)):
+        with pytest.raises(rlo.RloError):
+            plan(*bad)
