@@ -111,6 +111,11 @@ def dropin_api_leg(ranks=8, timeout_s=150):
     if not (os.path.exists(mpiexec) and os.path.exists(ours)):
         return {"error": "mpiexec or rlo_api_bench missing"}
     out = {"ranks": ranks, "driver": "tools/api_bench.c (same calls for both)", "ours": {}, "reference_host_mpi": {}}
+    # all ranks' persistent kernels share the one GPU here: 2 hardware queues per single-engine rank
+    # process keep their queues within the GPU's slots (deployment note)
+    env = dict(os.environ)
+    env.setdefault("GPU_MAX_HW_QUEUES", "2")
+    out["env"] = {"GPU_MAX_HW_QUEUES": env["GPU_MAX_HW_QUEUES"]}
     legs = [("storm", ["storm", "20000", "64"]), ("lat", ["lat", "500", "64"]), ("iar", ["iar", "2000"])]
     for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
         if not os.path.exists(exe):
@@ -120,7 +125,7 @@ def dropin_api_leg(ranks=8, timeout_s=150):
             note("api %s %s" % (name, leg))
             try:
                 r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(ranks), exe] + args,
-                                   stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20)
+                                   stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20, env=env)
                 lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
                 out[name][leg] = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
             except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
