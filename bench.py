@@ -14,8 +14,9 @@ sharded contiguously (256 ranks per GPU); every bcast's tree crosses the GPUs ov
 xGMI through peer-HBM ring stores (no collective on the data path; gloo only
 exchanges the ring-mapping blobs and runs the barriers).  K bcasts per step at every
 N, so each GPU delivers ~K x 256 messages per step: weak scaling.  `value` is
-delivered bcast messages per second over all ranks (K x (R - 1) per step);
-`bcast_per_s` is reported beside it.  One JSON line is printed by rank 0.
+rootless bcast messages per second (BASELINE.json's metric: originated bcasts that
+reached every other rank); `deliveries_per_s` (K x (R - 1) per step) is reported
+beside it.  One JSON line is printed by rank 0.
 """
 import argparse
 import json
@@ -58,7 +59,7 @@ def cpu_baseline(n, length, seed, target_s):
     t = time.perf_counter()
     res = orc.storm(n, seed, k, length)
     dt = time.perf_counter() - t
-    out = {"value": res["deliveries"] / dt, "unit": "msgs/s", "bcast_per_s": k / dt, "cores": 1, "kind": "port",
+    out = {"value": k / dt, "unit": "msgs/s", "deliveries_per_s": res["deliveries"] / dt, "cores": 1, "kind": "port",
            "sample": "oracle/rlo_oracle.c storm, %d virtual ranks, %d B, %d bcasts (%d deliveries), %.1f s, 1 thread"
                      % (n, length, k, res["deliveries"], dt)}
     ref = reference_datapoint(length)
@@ -427,14 +428,14 @@ def main():
         ok &= bool(np.array_equal(ref_sum, st["bcast_sum"]))  # every step delivers the same bytes
 
     deliveries = k * (R - 1) * args.steps * copies
-    value = deliveries / elapsed
     bcast_per_s = k * copies * args.steps / elapsed
+    value = bcast_per_s  # BASELINE metric: rootless bcast msgs/s (each reached all R - 1 other ranks)
     kernel_ms = max_over_ranks(float(np.mean(kms)))
     # 2(N-1)(S+16) HBM bytes per bcast; this GPU's share is its ranks' receipts
     alg_bytes = k * 2.0 * (R - 1) * (length + 16) * copies / world
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
-    extras = {"bcast_per_s": round(bcast_per_s, 1), "world_ranks": R, "mode": mode,
+    extras = {"deliveries_per_s": round(deliveries / elapsed, 1), "world_ranks": R, "mode": mode,
               # staged slots whose header lacked the slot mark (each one a device error; 0 expected)
               "unmarked_slots": int(sum_over_ranks(float(st["unmarked_slots"].sum())))}
     if mode == "replicas":
@@ -520,8 +521,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {"workload": "rootless bcast storm over one world of %d workgroup-ranks (%d per GPU), %d B payload, "
-                               "random originators, %d bcasts per step; value = delivered bcast messages/s "
-                               "(each bcast reaches %d ranks)" % (R, per, length, k, R - 1),
+                               "random originators, %d bcasts per step; value = rootless bcasts/s, each delivered "
+                               "to all %d other ranks" % (R, per, length, k, R - 1),
                    "ranks_per_gpu": per, "world_ranks": R, "payload_bytes": length, "bcasts_per_step": k,
                    "waves_per_rank": waves,
                    "parallelism": ("one world sharded over %d GPU(s), contiguous rank ranges" % world) if mode == "sharded"
