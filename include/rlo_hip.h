@@ -46,6 +46,8 @@ extern "C" {
 #define RLO_DERR_LOG_FULL 5
 #define RLO_DERR_BAD_SLOT 6
 #define RLO_DERR_HOST_CMD 7      /* malformed / unexpected host-service command                */
+#define RLO_DERR_BULK 8          /* a bulk-message index / job field out of range (a bug: reported
+                                    instead of touching memory outside the heaps)                  */
 
 /* ------------------------------------------------------------------ topology (host only) */
 /* skip-ring overlay, restated from rootless_ops.c:1416-1579; usable without a GPU */
@@ -61,6 +63,12 @@ typedef struct {
     uint32_t max_payload; /* payload bytes per slot (rounded up to 16); default 4096       */
     uint32_t ring_slots;  /* forward ring capacity (power of two); 0 = auto               */
     int32_t device;       /* HIP device ordinal; -1 = current                              */
+    /* bulk messages (longer than max_payload, up to bulk_max bytes): announced through the
+     * rings, moved by mover workgroups of the same launch (DESIGN.md "Bulk messages").
+     * bulk_max 0 = no bulk messages */
+    uint64_t bulk_max;
+    uint32_t bulk_slots;  /* heap slots per origin (power of two <= 8, N * slots <= 256); 0 = 2 */
+    uint32_t movers;      /* mover workgroups of the part (>= 2, half scatter, half gather); 0 = auto */
 } rlo_world_cfg_t;
 
 typedef struct {
@@ -72,6 +80,8 @@ typedef struct {
     int32_t sys_scope;                           /* 1: parts span GPUs (system-scope stores) */
     int32_t waves;                               /* waves per rank-workgroup: 8 (512 messages per
                                                     iteration) or 4 (256), chosen at creation     */
+    uint32_t bulk_slots, movers;                 /* bulk: heap slots per origin, mover workgroups   */
+    uint64_t bulk_max, heap_bytes;               /* bulk: largest message, this part's heap bytes   */
 } rlo_world_info_t;
 
 /* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522
@@ -92,6 +102,8 @@ typedef struct {
     uint32_t max_payload, ring_slots;
     int32_t device;            /* -1 = current                                              */
     uint32_t flags;            /* RLO_PART_*                                                */
+    uint64_t bulk_max;         /* as rlo_world_cfg_t (the same on every part)               */
+    uint32_t bulk_slots, movers;
 } rlo_part_cfg_t;
 int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out);
 int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap); /* returns RLO_PART_BLOB_BYTES */
@@ -104,13 +116,19 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 #define RLO_FLAG_HIST 2u /* per-delivery latency histogram                                  */
 #define RLO_FLAG_PROF 4u /* per-phase cycle accounting (diagnostic)                         */
 
+#define RLO_ORDER_RANDOM 0u /* origin of bcast b = splitmix64(seed + b) % N                      */
+#define RLO_ORDER_SLOTS 1u  /* origin of bcast b = b % N: every rank originates in every "slot" of N
+                               bcasts (BASELINE configs[4]: collision-heavy simultaneous originators) */
 typedef struct {
-    uint64_t seed;       /* originator of bcast b = splitmix64(seed + b) % N              */
+    uint64_t seed;       /* workload seed                                                  */
     int64_t k;           /* bcasts in the storm                                            */
-    uint32_t len;        /* payload bytes (<= max_payload)                                 */
+    uint32_t len;        /* payload bytes (<= max_payload, or <= bulk_max with bulk)        */
     uint32_t window;     /* max originations per rank per progress iteration (0 = 64, max 64) */
     uint32_t flags;      /* RLO_FLAG_*                                                      */
     uint32_t log_cap;    /* log records per rank when RLO_FLAG_LOG                          */
+    uint32_t len_max;    /* > len: mixed sizes, bcast b has storm_len(seed, b) in [len, len_max]
+                            (piecewise log-uniform, oracle/rlo_testvec.h rlo_tv_len)           */
+    uint32_t order;      /* RLO_ORDER_*                                                     */
 } rlo_storm_cfg_t;
 int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg);
 
@@ -140,7 +158,9 @@ typedef struct {
 int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, const int32_t* origin, const int32_t* pid,
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len);
 
-/* one event record (parity log / host pickup ring) */
+/* one event record (parity log / host pickup ring).  A bulk delivery (kind 1 | 10 << 8) logs
+ * len = message bytes and, once its VERIFY job ran, aux | payload_idx << 32 = the message checksum
+ * (the oracle's orc_msg_checksum) */
 typedef struct {
     uint32_t kind; /* 1 deliver | 2 judge | 3 action | 4 result | 5 error | 6 judge req | 7 own judge req; | tag << 8 */
     int32_t origin, from;
@@ -171,6 +191,8 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg);
 #define RLO_CMD_JUDGE 16u     /* verdict for an RLO_EV_JUDGE event: origin, pid, pseq, vote     */
 #define RLO_CMD_OWN_JUDGE 17u /* verdict of the originator's final judge(NULL) (:773): vote      */
 #define RLO_CMD_QUIT 18u      /* stop this rank's progress (after everything before it)          */
+#define RLO_CMD_BULK 10u      /* bulk origination: payload = {u32 len, u32 q}; use rlo_host_bulk_send */
+#define RLO_CMD_BULK_RELEASE 19u /* a bulk delivery was copied out: origin, pseq = heap slot        */
 typedef struct {
     uint32_t kind;
     int32_t origin; /* RLO_CMD_JUDGE: origin of the proposal                                  */
@@ -185,6 +207,8 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* cmd, const void* pa
 /* pickup events (rlo_log_rec_t.kind) */
 #define RLO_EV_DELIVER_BCAST (1u | (0u << 8))    /* origin, from (tree parent), id, len + payload */
 #define RLO_EV_DELIVER_DECISION (1u | (4u << 8)) /* origin, id = pid, vote = decision             */
+#define RLO_EV_DELIVER_BULK (1u | (10u << 8))   /* origin, from, id, len, aux = heap slot: the bytes
+                                                   are in this rank's heap (rlo_host_bulk_recv)   */
 #define RLO_EV_ACTION 3u    /* decision 1 for a proposal this rank approved: run action (:842)   */
 #define RLO_EV_RESULT 4u    /* my own proposal decided: id = pid, vote = decision                */
 #define RLO_EV_JUDGE 6u     /* call judge(data): origin, from, id = pid, aux = pseq,
@@ -199,30 +223,18 @@ int rlo_host_cmd_count(rlo_world_t* w, int rank, uint64_t* consumed, uint64_t* p
 /* number of HIP devices visible to this process (0 without a GPU) */
 int rlo_device_count(void);
 
-/* ---- bulk (large-message) rootless bcast, beyond the reference's 32,764-B cap.
- * Every rank of the world gets a receive buffer in its part's HBM (uncached; peer HBM over xGMI
- * across GPUs).  A bcast from any originator o of `bytes` already in o's buffer reaches every
- * other rank's buffer as a pipelined scatter (o -> stripe owners) + all-gather (owners -> the
- * rest), chunk by chunk.  Same exchange protocol as parts: create -> export -> exchange blobs ->
- * connect; before every bcast each part resets its flags and all parts pass a host barrier;
- * every part then launches with the same (origin, bytes, chunk, blocks). */
-typedef struct rlo_bulk rlo_bulk_t;
-#define RLO_BULK_BLOB_BYTES 256u
-int rlo_bulk_create(rlo_world_t* w, uint64_t buf_bytes, rlo_bulk_t** out);
-int rlo_bulk_export(rlo_bulk_t* b, void* blob, uint32_t cap); /* returns RLO_BULK_BLOB_BYTES */
-int rlo_bulk_connect(rlo_bulk_t* b, const void* blobs /* n_parts x RLO_BULK_BLOB_BYTES */, int n_parts);
-void* rlo_bulk_buffer(rlo_bulk_t* b, int rank); /* device pointer of a local rank's buffer  */
-int rlo_bulk_reset(rlo_bulk_t* b, void* stream);  /* zero this part's flags (sync)           */
-/* async; chunk_bytes 0 = auto (one chunk when every part shares a GPU, ~sqrt(bytes / 4 MiB)
- * chunks across GPUs); blocks = workgroups per local rank, 0 = auto (bytes / 64 KiB in
- * [32, 128]); the same arguments on every part */
-int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream);
-/* the launch geometry rlo_bulk_launch uses (pure host arithmetic, no GPU): stripe bytes per
- * owner per chunk (whole 1-KiB blocks), chunk bytes ((n-1) stripes), chunk count, workgroups */
-typedef struct { uint32_t stripe, chunk, nchunks, blocks; } rlo_bulk_plan_t;
-int rlo_bulk_plan(int n, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, int cross_gpu, rlo_bulk_plan_t* out);
-int rlo_bulk_wait(rlo_bulk_t* b, float* kernel_ms); /* RLO_E_DEVICE if a wait timed out      */
-int rlo_bulk_destroy(rlo_bulk_t* b);
+/* ---- bulk messages in the host-service program (the drop-in's RLO_bcast_gen beyond a slot).
+ * rlo_host_bulk_stage: takes local rank `rank`'s next bulk sequence q, waits (RLO_E_AGAIN after
+ * timeout_us) until every receiver released heap slot q mod B, and copies `len` bytes into the
+ * rank's own heap slot; then post RLO_CMD_BULK with payload {u32 len, u32 q}.
+ * rlo_host_bulk_copy: copies the message of an RLO_EV_DELIVER_BULK event (ev->len bytes) out of
+ * this rank's heap; then post RLO_CMD_BULK_RELEASE with origin = ev->origin, pseq = ev->aux. */
+/* the chunk / stripe / tile plan every rank derives for a bulk message of len bytes in an N-rank
+ * world (cross: parts span GPUs); pure host arithmetic (rlo_device.hpp bulk_plan) */
+typedef struct { uint32_t nchunks, stripe, chunk, tile, total_tiles, pad; } rlo_bulk_plan_t;
+int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out);
+int rlo_host_bulk_stage(rlo_world_t* w, int rank, const void* data, uint64_t len, uint32_t timeout_us, uint32_t* q);
+int rlo_host_bulk_copy(rlo_world_t* w, int rank, const rlo_log_rec_t* ev, void* dst);
 
 /* ------------------------------------------------------------------ run */
 int rlo_reset(rlo_world_t* w, void* stream);           /* zero this part's counters (sync) */
@@ -258,6 +270,12 @@ int rlo_log(rlo_world_t* w, int rank, rlo_log_rec_t* out, uint32_t cap, uint8_t*
 int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap);
 int rlo_round_ticks(rlo_world_t* w, uint64_t* ticks, uint32_t cap);
 
+/* this part's device error word (ctrl word 0): the first RLO_DERR_* code any workgroup of any part
+ * raised (0 = none) and, for RLO_DERR_BULK, aux = site << 24 | value */
+int rlo_device_error(rlo_world_t* w, uint32_t* code, uint32_t* aux);
+/* diagnostics of a bulk world: its part's job-ring control words (rlo_device.hpp kJctl*: posted and
+ * head per class, exited progress workgroups, tiles moved per class, gather waits) */
+int rlo_bulk_debug(rlo_world_t* w, uint64_t* out, uint32_t cap);
 const char* rlo_strerror(int code);
 int rlo_last_hip_error(void);
 

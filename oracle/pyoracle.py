@@ -53,10 +53,21 @@ def lib():
         L.orc_msg_checksum.restype = ctypes.c_uint64
         L.orc_region_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.orc_region_hash.restype = ctypes.c_uint64
+        L.orc_fnv1a.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_fnv1a.restype = ctypes.c_uint64
         L.orc_storm.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, i32p, i64p, u64p]
         L.orc_storm.restype = ctypes.c_int64
         L.orc_storm_expected.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, i64p, u64p]
         L.orc_storm_expected.restype = ctypes.c_int64
+        u32 = ctypes.c_uint32
+        L.orc_storm2.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, i32p, i64p, u64p]
+        L.orc_storm2.restype = ctypes.c_int64
+        L.orc_storm_expected2.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, i64p, u64p]
+        L.orc_storm_expected2.restype = ctypes.c_int64
+        L.orc_len_of.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u32, u32]
+        L.orc_len_of.restype = u32
+        L.orc_origin_of2.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u32, u32]
+        L.orc_origin_of2.restype = u32
         L.orc_judge_hash.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32]
         L.orc_judge_hash.restype = ctypes.c_uint32
         L.orc_iar.argtypes = [ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_char_p, i32p, i32p, ctypes.POINTER(JudgeCfg),
@@ -99,8 +110,14 @@ def payload(origin, bid, length):
     return buf.raw[:length]
 
 
-def origin_of(seed, bid, n):
-    return lib().orc_origin_of(seed, bid, n)
+def origin_of(seed, bid, n, order=0):
+    """origin of bcast bid: order 0 random (splitmix64(seed + bid) % n), 1 slots (bid % n)"""
+    return lib().orc_origin_of2(seed, bid, n, order)
+
+
+def len_of(seed, bid, lo, hi):
+    """payload bytes of bcast bid in a mixed-size storm (rlo_testvec.h rlo_tv_len)"""
+    return lib().orc_len_of(seed, bid, lo, hi)
 
 
 def msg_checksum(origin, bid, tag, data):
@@ -111,20 +128,26 @@ def region_hash(data):
     return lib().orc_region_hash(data, len(data))
 
 
-def storm(n, seed, k, length, want_parent=False):
+def fnv1a(data):
+    return lib().orc_fnv1a(data, len(data))
+
+
+def storm(n, seed, k, length, want_parent=False, len_max=0, order=0):
     parent = np.full(k * n, -1, dtype=np.int32) if want_parent else None
     count = np.zeros(n, dtype=np.int64)
     ssum = np.zeros(n, dtype=np.uint64)
-    d = lib().orc_storm(n, seed, k, length, _p(parent, ctypes.c_int32), _p(count, ctypes.c_int64), _p(ssum, ctypes.c_uint64))
+    d = lib().orc_storm2(n, seed, k, length, max(length, len_max), order, _p(parent, ctypes.c_int32),
+                         _p(count, ctypes.c_int64), _p(ssum, ctypes.c_uint64))
     if d < 0:
         raise RuntimeError("oracle storm failed")
     return {"deliveries": d, "count": count, "sum": ssum, "parent": parent.reshape(k, n) if want_parent else None}
 
 
-def storm_expected(n, seed, k, length):
+def storm_expected(n, seed, k, length, len_max=0, order=0):
     count = np.zeros(n, dtype=np.int64)
     ssum = np.zeros(n, dtype=np.uint64)
-    d = lib().orc_storm_expected(n, seed, k, length, _p(count, ctypes.c_int64), _p(ssum, ctypes.c_uint64))
+    d = lib().orc_storm_expected2(n, seed, k, length, max(length, len_max), order, _p(count, ctypes.c_int64),
+                                  _p(ssum, ctypes.c_uint64))
     return {"deliveries": d, "count": count, "sum": ssum}
 
 

@@ -183,6 +183,45 @@ static void mode_stream(uint64_t seed, int K, int len) {
     free(buf);
 }
 
+/* ---------------------------------------------------------------- bulk stream (drop-in extension)
+ * Mixed sizes lo..hi (rlo_tv_len), bcast b from rank b % N (every rank originates in every slot).
+ * Bcasts longer than the reference's data region are the drop-in's bulk extension; they arrive with
+ * data_len = their size (the reference cannot send them at all).  Per delivery: bid,
+ * origin, tree parent, data_len and the FNV-1a of the delivered bytes (the data region for ring
+ * bcasts, data_len bytes for bulk ones). */
+static void mode_bulkstream(uint64_t seed, int K, int lo, int hi) {
+    RLO_engine_t* eng = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, NULL, NULL, NULL);
+    uint8_t* buf = calloc(1, (size_t)hi + 8);
+    int mine = 0;
+    for (int b = 0; b < K; b++) if (b % g_size == g_rank) mine++;
+    int expect = K - mine, got = 0, next_b = g_rank;
+    MPI_Barrier(MPI_COMM_WORLD);
+    while (got < expect || next_b < K) {
+        if (next_b < K) {
+            int len = (int)rlo_tv_len(seed, (uint64_t)next_b, (uint32_t)lo, (uint32_t)hi);
+            rlo_tv_payload(g_rank, next_b, buf, len);
+            RLO_msg_t* m = RLO_msg_new_bc(eng, buf, len);
+            if (!m || RLO_bcast_gen(eng, m, RLO_BCAST) != 0) { fprintf(stderr, "bulkstream: send failed\n"); break; }
+            next_b += g_size;
+        }
+        RLO_make_progress_all();
+        RLO_user_msg* u = NULL;
+        while (RLO_user_pickup_next(eng, &u)) {
+            uint64_t w0;
+            memcpy(&w0, u->data, 8);
+            size_t n = u->data_len ? u->data_len : RLO_TV_DATA_REGION;
+            uint64_t h = rlo_tv_fnv1a((const uint8_t*)u->data, n, RLO_TV_FNV_INIT);
+            emit("{\"rank\":%d,\"bid\":%u,\"origin\":%d,\"parent\":%d,\"type\":%d,\"len\":%zu,\"hash\":\"%016llx\"}",
+                 g_rank, (unsigned)(w0 >> 32), *(int*)u->buf, msg_parent(u), u->type, (size_t)u->data_len,
+                 (unsigned long long)h);
+            RLO_user_msg_recycle(eng, u);
+            got++;
+        }
+    }
+    RLO_progress_engine_cleanup(eng);
+    free(buf);
+}
+
 /* ---------------------------------------------------------------- iar */
 typedef struct { unsigned mask; int rank; } MaskCtx;
 
@@ -479,6 +518,7 @@ int main(int argc, char** argv) {
     if (!strcmp(mode, "topo")) mode_topo(atoi(argv[3]));
     else if (!strcmp(mode, "parents")) mode_parents(atoi(argv[3]));
     else if (!strcmp(mode, "stream")) mode_stream(strtoull(argv[3], 0, 0), atoi(argv[4]), atoi(argv[5]));
+    else if (!strcmp(mode, "bulkstream")) mode_bulkstream(strtoull(argv[3], 0, 0), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]));
     else if (!strcmp(mode, "iar")) mode_iar(atoi(argv[3]), (unsigned)strtoul(argv[4], 0, 0));
     else if (!strcmp(mode, "multi")) mode_multi(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
     else if (!strcmp(mode, "tests")) mode_tests();

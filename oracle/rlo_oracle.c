@@ -130,6 +130,7 @@ int orc_fwd_send_cnt(int n, int rank, int origin, int from) {
 void orc_payload(uint32_t origin, uint32_t bid, uint8_t* out, size_t len) { rlo_tv_payload(origin, bid, out, len); }
 uint32_t orc_origin_of(uint64_t seed, uint64_t bid, uint32_t n) { return rlo_tv_origin(seed, bid, n); }
 uint64_t orc_region_hash(const uint8_t* p, size_t len) { return rlo_tv_region_hash(p, len); }
+uint64_t orc_fnv1a(const uint8_t* p, size_t len) { return rlo_tv_fnv1a(p, len, RLO_TV_FNV_INIT); }
 
 static inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
@@ -163,6 +164,8 @@ typedef struct {
     int32_t tag, origin, from, id, vote;
     uint32_t len;
     uint8_t* data; /* owned copy: every hop copies the bytes, like an MPI send */
+    uint64_t cs;   /* storm: checksum of a bulk message (beyond the reference's 32,764-B cap, its
+                      bytes are a pure function of (origin, bid, len) and are not copied per hop) */
 } omsg;
 
 typedef struct {
@@ -197,7 +200,7 @@ static int post(ofifo* inbox, int to, int me, const omsg* m) {
     omsg c = *m;
     c.from = me;
     c.data = NULL;
-    if (m->len) {
+    if (m->len && m->data) {
         c.data = malloc(m->len);
         if (!c.data) return -1;
         memcpy(c.data, m->data, m->len);
@@ -212,7 +215,7 @@ int orc_tree(int n, int origin, int32_t* parent) {
     ofifo* inbox = calloc(n, sizeof(ofifo));
     topo_t* t = malloc(n * sizeof(topo_t));
     for (int r = 0; r < n; r++) { topo_init(n, r, &t[r]); parent[r] = -1; }
-    omsg m = {ORC_BCAST, origin, -1, 0, -1, 0, NULL};
+    omsg m = {ORC_BCAST, origin, -1, 0, -1, 0, NULL, 0};
     int kids[ORC_MAX_FANOUT], cnt = 0, busy = 1;
     int k = children_t(&t[origin], origin, origin, -1, kids);
     for (int i = 0; i < k; i++) post(inbox, kids[i], origin, &m);
@@ -239,12 +242,16 @@ int orc_tree(int n, int origin, int32_t* parent) {
 
 /* ------------------------------------------------------------------ storm */
 
-int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent, int64_t* count, uint64_t* sum) {
+#define ORC_COPY_MAX 32764 /* the reference's deliverable data region (rootless_ops.c:1588) */
+
+int64_t orc_storm2(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order, int32_t* parent,
+                   int64_t* count, uint64_t* sum) {
     if (n < 2 || k < 0) return -1;
+    if (len_hi < len_lo) len_hi = len_lo;
     ofifo* inbox = calloc(n, sizeof(ofifo));
     topo_t* t = malloc(n * sizeof(topo_t));
     int64_t* next = calloc(n + 1, sizeof(int64_t)); /* next bid index scan position per rank */
-    uint8_t* buf = malloc(len ? len : 1);
+    uint8_t* buf = malloc(len_hi ? len_hi : 1);
     int64_t deliveries = 0, originated = 0;
     for (int r = 0; r < n; r++) {
         topo_init(n, r, &t[r]);
@@ -256,10 +263,10 @@ int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent
     /* per-rank origination lists (CSR) */
     int64_t* off = calloc(n + 1, sizeof(int64_t));
     int64_t* ids = malloc((k ? k : 1) * sizeof(int64_t));
-    for (int64_t b = 0; b < k; b++) off[rlo_tv_origin(seed, b, n) + 1]++;
+    for (int64_t b = 0; b < k; b++) off[rlo_tv_origin2(seed, b, n, order) + 1]++;
     for (int r = 0; r < n; r++) off[r + 1] += off[r];
     for (int64_t b = 0; b < k; b++) {
-        uint32_t o = rlo_tv_origin(seed, b, n);
+        uint32_t o = rlo_tv_origin2(seed, b, n, order);
         ids[off[o] + next[o]++] = b;
     }
     memset(next, 0, (n + 1) * sizeof(int64_t));
@@ -271,8 +278,13 @@ int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent
             /* originate one bcast (RLO_msg_new_bc + RLO_bcast_gen, rootless_ops.c:311, :1581) */
             if (off[r] + next[r] < off[r + 1]) {
                 uint32_t bid = (uint32_t)ids[off[r] + next[r]++];
+                uint32_t len = rlo_tv_len(seed, bid, len_lo, len_hi);
                 rlo_tv_payload(r, bid, buf, len);
-                omsg m = {ORC_BCAST, r, -1, (int32_t)bid, -1, len, buf};
+                omsg m = {ORC_BCAST, r, -1, (int32_t)bid, -1, len, buf, 0};
+                if (len > ORC_COPY_MAX) { /* a bulk message: every receiver gets exactly these bytes */
+                    m.cs = orc_msg_checksum(r, bid, ORC_BCAST, buf, len);
+                    m.data = NULL;
+                }
                 int kk = children_t(&t[r], r, r, -1, kids);
                 for (int i = 0; i < kk; i++) post(inbox, kids[i], r, &m);
                 originated++;
@@ -284,7 +296,7 @@ int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent
                 busy = 1;
                 deliveries++;
                 if (count) count[r]++;
-                if (sum) sum[r] += orc_msg_checksum(in.origin, in.id, ORC_BCAST, in.data, in.len);
+                if (sum) sum[r] += in.data || in.len == 0 ? orc_msg_checksum(in.origin, in.id, ORC_BCAST, in.data, in.len) : in.cs;
                 if (parent) parent[(int64_t)in.id * n + r] = in.from;
                 int kk = children_t(&t[r], r, in.origin, in.from, kids);
                 for (int i = 0; i < kk; i++) post(inbox, kids[i], r, &in);
@@ -297,14 +309,21 @@ int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent
     return originated == k ? deliveries : -1;
 }
 
-int64_t orc_storm_expected(int n, uint64_t seed, int64_t k, uint32_t len, int64_t* count, uint64_t* sum) {
+int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent, int64_t* count, uint64_t* sum) {
+    return orc_storm2(n, seed, k, len, len, 0, parent, count, sum);
+}
+
+int64_t orc_storm_expected2(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order,
+                            int64_t* count, uint64_t* sum) {
     if (n < 2 || k < 0) return -1;
-    uint8_t* buf = malloc(len ? len : 1);
+    if (len_hi < len_lo) len_hi = len_lo;
+    uint8_t* buf = malloc(len_hi ? len_hi : 1);
     uint64_t total = 0;
     int64_t* own_cnt = calloc(n, sizeof(int64_t));
     uint64_t* own_sum = calloc(n, sizeof(uint64_t));
     for (int64_t b = 0; b < k; b++) {
-        uint32_t o = rlo_tv_origin(seed, b, n);
+        uint32_t o = rlo_tv_origin2(seed, b, n, order);
+        uint32_t len = rlo_tv_len(seed, b, len_lo, len_hi);
         rlo_tv_payload(o, (uint32_t)b, buf, len);
         uint64_t cs = orc_msg_checksum(o, (uint32_t)b, ORC_BCAST, buf, len);
         total += cs;
@@ -317,6 +336,15 @@ int64_t orc_storm_expected(int n, uint64_t seed, int64_t k, uint32_t len, int64_
     }
     free(buf); free(own_cnt); free(own_sum);
     return k * (int64_t)(n - 1);
+}
+
+int64_t orc_storm_expected(int n, uint64_t seed, int64_t k, uint32_t len, int64_t* count, uint64_t* sum) {
+    return orc_storm_expected2(n, seed, k, len, len, 0, count, sum);
+}
+
+uint32_t orc_len_of(uint64_t seed, uint64_t bid, uint32_t lo, uint32_t hi) { return rlo_tv_len(seed, bid, lo, hi); }
+uint32_t orc_origin_of2(uint64_t seed, uint64_t bid, uint32_t n, uint32_t order) {
+    return rlo_tv_origin2(seed, bid, n, order);
 }
 
 /* ------------------------------------------------------------------ IAR */
@@ -409,19 +437,19 @@ static void submit(iar_sim* s, int r, int32_t pid, const char* data, uint32_t dl
     o->recvd = 0;
     o->state = 1;
     uint32_t total = 16 + dl;
-    omsg m = {ORC_PROPOSAL, r, -1, pid, 1, total, pbuf_make(pid, 1, dl, data, total)};
+    omsg m = {ORC_PROPOSAL, r, -1, pid, 1, total, pbuf_make(pid, 1, dl, data, total), 0};
     bcast_from(s, r, &m);
     free(m.data);
 }
 
 static void vote_to(iar_sim* s, int r, int parent, int32_t pid, int32_t vote) { /* _vote_back :728-741 */
-    omsg v = {ORC_VOTE, r, -1, pid, vote, 0, NULL};
+    omsg v = {ORC_VOTE, r, -1, pid, vote, 0, NULL, 0};
     post(s->inbox, parent, r, &v);
 }
 
 /* _iar_decision_bcast :908-917: PBuf(pid, decision, 7, "IAR_DEC") in a 64-byte buffer */
 static void decision_bcast(iar_sim* s, int r, int32_t pid, int32_t d) {
-    omsg m = {ORC_DECISION, r, -1, pid, d, 64, pbuf_make(pid, d, 7, "IAR_DEC", 64)};
+    omsg m = {ORC_DECISION, r, -1, pid, d, 64, pbuf_make(pid, d, 7, "IAR_DEC", 64), 0};
     bcast_from(s, r, &m);
     free(m.data);
     s->decisions++;

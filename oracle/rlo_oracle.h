@@ -41,6 +41,7 @@ uint32_t orc_origin_of(uint64_t seed, uint64_t bid, uint32_t n);
 uint32_t orc_chunk_mix(uint32_t q, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3);
 uint64_t orc_msg_checksum(uint32_t origin, uint32_t bid, uint32_t tag, const uint8_t* payload, uint32_t len);
 uint64_t orc_region_hash(const uint8_t* payload, size_t len);
+uint64_t orc_fnv1a(const uint8_t* p, size_t len); /* FNV-1a 64 of exactly len bytes */
 
 /* ---- storm: every bid b in [0,k) originates at orc_origin_of(seed,b,n) with a len-byte payload.
  * Message-passing simulation: per-rank FIFO inbox, payload copied on every tree edge.
@@ -49,6 +50,16 @@ uint64_t orc_region_hash(const uint8_t* payload, size_t len);
 int64_t orc_storm(int n, uint64_t seed, int64_t k, uint32_t len, int32_t* parent, int64_t* count, uint64_t* sum);
 /* same outputs, computed analytically (every non-origin receives every bcast exactly once) */
 int64_t orc_storm_expected(int n, uint64_t seed, int64_t k, uint32_t len, int64_t* count, uint64_t* sum);
+/* the same with mixed payload sizes (bcast b has rlo_tv_len(seed, b, len_lo, len_hi) bytes) and an
+ * origin order (0 random, 1 slots: b % n).  Messages longer than the reference's 32,764-B data region
+ * are bulk messages: delivered to every other rank byte for byte like the rest, their
+ * bytes are not copied per hop in the simulation (a pure function of origin, bid and len) */
+int64_t orc_storm2(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order, int32_t* parent,
+                   int64_t* count, uint64_t* sum);
+int64_t orc_storm_expected2(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order,
+                            int64_t* count, uint64_t* sum);
+uint32_t orc_len_of(uint64_t seed, uint64_t bid, uint32_t lo, uint32_t hi);
+uint32_t orc_origin_of2(uint64_t seed, uint64_t bid, uint32_t n, uint32_t order);
 
 /* ---- IAR (proposal / vote / decision): rootless_ops.c:668-917, :1036-1070 */
 enum { ORC_JUDGE_APPROVE = 0, ORC_JUDGE_MASK = 1, ORC_JUDGE_ISP = 2, ORC_JUDGE_HASH = 3 };

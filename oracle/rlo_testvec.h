@@ -47,6 +47,30 @@ static inline uint32_t rlo_tv_origin(uint64_t seed, uint64_t b, uint32_t n) {
     return (uint32_t)(rlo_tv_splitmix64(seed + b) % n);
 }
 
+/* storm origins, by order: 0 random (above), 1 "slots": bcast b originates at rank b % n, so in
+ * every slot of n consecutive bcasts every rank originates (BASELINE configs[4]) */
+static inline uint32_t rlo_tv_origin2(uint64_t seed, uint64_t b, uint32_t n, uint32_t order) {
+    return order == 1 ? (uint32_t)(b % n) : rlo_tv_origin(seed, b, n);
+}
+
+/* mixed payload sizes (BASELINE configs[4]): length of bcast b in [lo, hi], piecewise log-uniform --
+ * an octave [2^e, 2^(e+1)) uniform over the octaves of [lo, hi), then uniform inside it; integer
+ * only (the device's storm_len_of in rlo_device.hpp states the same) */
+static inline uint32_t rlo_tv_len(uint64_t seed, uint64_t b, uint32_t lo, uint32_t hi) {
+    if (hi <= lo) return lo;
+    if (lo == 0) lo = 1;
+    const int elo = 31 - __builtin_clz(lo), ehi = 31 - __builtin_clz(hi);
+    const uint64_t x = rlo_tv_splitmix64(seed ^ 0xC5C5C5C5C5C5C5C5ull ^ (b * RLO_TV_GOLDEN));
+    const uint32_t noct = (uint32_t)(ehi - elo) + ((hi & (hi - 1u)) ? 1u : 0u);
+    if (noct == 0) return lo;
+    const uint32_t e = (uint32_t)elo + (uint32_t)(x % noct);
+    const uint64_t base = 1ull << e;
+    uint64_t v = base + ((x >> 32) % base);
+    if (v < lo) v = lo;
+    if (v > hi) v = hi;
+    return (uint32_t)v;
+}
+
 static inline uint64_t rlo_tv_fnv1a(const uint8_t* p, size_t len, uint64_t h) {
     for (size_t i = 0; i < len; i++) { h ^= p[i]; h *= 0x100000001b3ull; }
     return h;

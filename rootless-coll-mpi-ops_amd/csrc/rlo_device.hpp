@@ -37,8 +37,10 @@ constexpr int kCtrlHdrWords = 16; // per-part control words before the rank bloc
 constexpr int kLatCap = 8192;
 constexpr int kLatWords = 16 + kLatCap / 2;
 
-// message classes == enum RLO_COMM_TAGS (rootless_ops.h:50-61)
-enum Tag : uint32_t { TAG_BCAST = 0, TAG_PROPOSAL = 2, TAG_VOTE = 3, TAG_DECISION = 4 };
+// message classes == enum RLO_COMM_TAGS (rootless_ops.h:50-61); TAG_BULK (beyond RLO_ANY_TAG) is
+// the announcement of a bulk message (longer than a ring slot): payload = BulkDesc, the bytes move
+// through the mover workgroups (below), the user sees an RLO_BCAST
+enum Tag : uint32_t { TAG_BCAST = 0, TAG_PROPOSAL = 2, TAG_VOTE = 3, TAG_DECISION = 4, TAG_BULK = 10 };
 
 enum Mode : uint32_t {
     MODE_STORM = 1u,   // every rank originates its share of K bcasts (random originators)
@@ -55,8 +57,9 @@ enum Mode : uint32_t {
 };
 
 // host-service command kinds (tag field of a command slot); tags < 16 are originations
-// (TAG_BCAST: RLO_bcast_gen :1581, TAG_PROPOSAL: RLO_submit_proposal :876)
-enum HostCmd : uint32_t { CMD_JUDGE = 16, CMD_OWN_JUDGE = 17, CMD_QUIT = 18 };
+// (TAG_BCAST: RLO_bcast_gen :1581, TAG_PROPOSAL: RLO_submit_proposal :876, TAG_BULK: a bulk
+// bcast whose bytes the host put in the origin's own heap slot)
+enum HostCmd : uint32_t { CMD_JUDGE = 16, CMD_OWN_JUDGE = 17, CMD_QUIT = 18, CMD_BULK_RELEASE = 19 };
 // per local rank, 64 host words (one 128-B line per counter)
 constexpr int kHctlWords = 64;
 constexpr int kHctlInjTail = 0, kHctlInjHead = 16, kHctlPkTail = 32, kHctlPkHead = 48;
@@ -68,7 +71,8 @@ enum LogKind : uint32_t { LOG_DELIVER = 1, LOG_JUDGE = 2, LOG_ACTION = 3, LOG_RE
                           LOG_OWN_JREQ = 7 };// host mode: the originator's final judge(NULL) request (:773)
 
 enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_COLLISION = 3, ERR_VOTE_ORPHAN = 4,
-                      ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6, ERR_HOST_CMD = 7 };
+                      ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6, ERR_HOST_CMD = 7,
+                      ERR_BULK = 8 };  // a bulk index / job field out of range (error_aux: site << 24 | value)
 
 // Slot header, 16 bytes:
 //   w0 = origin (16 b) | tag (8 b) << 16 | vote (8 b) << 24
@@ -184,23 +188,152 @@ struct Params {
     uint64_t* hctl;               // [n_local][kHctlWords] counters the DEVICE writes (pinned host memory)
     uint64_t* hctl_dev;           // [n_local][kHctlWords] counters the HOST writes (uncached VRAM:
                                   //   the CPU stores through the BAR, the kernel polls locally)
+    // bulk messages (the BULK kernel instantiation only; rlo_device.hpp "bulk messages" below)
+    uint32_t bulk_slots, bulk_cap;  // B (power of two) heap slots per origin, bytes per slot (x 64 KiB)
+    uint32_t n_local, nmov;         // progress workgroups, mover workgroups (blocks [n_local, n_local + nmov))
+    uint32_t bulk_cross;            // parts span GPUs: chunked (pipelined) plan
+    uint32_t len_lo, len_hi;        // storm payload lengths: len_hi > len_lo -> storm_len_of per bcast
+    uint32_t ring_cap;              // payload bytes a ring slot carries (longer -> bulk)
+    const uint64_t* bheap;          // [n_parts] heap base of every part, mapped in this process
+    const uint64_t* bflag;          // [n_parts] flag-region base of every part, mapped in this process
+    const int32_t* part_of;         // [n] part of every rank
+    const int32_t* part_begin;      // [n_parts + 1]
+    struct BulkJob* jobs;           // [2][jslots] this part's job rings (class A, class B)
+    uint32_t jslots, bpend_off;     // job ring slots per class (power of two, >= every job that can be
+                                    //   unfinished at once); dynamic-LDS byte offset of the pending table
+    uint64_t* jctl;                 // [kJctlWords] posted / head counters, exited progress workgroups
+    uint64_t* jclaim;               // [2][jslots] seq << 32 | next tile to claim
+    uint64_t* jfree;                // [2][jslots] slot j % J takes job j once jfree == j
+    uint32_t* jdone;                // [2][jslots] finished tiles of the slot's job
+    uint64_t* jsum;                 // [2][jslots] VERIFY checksum accumulator
 };
 
-// ---- bulk (large-message) rootless bcast: pipelined scatter + all-gather (rlo_bulk.hip)
-constexpr int kMaxBulkRanks = 64;
-constexpr uint32_t kBulkBlock = 1024;     // bytes one wave moves per step (64 lanes x 16 B)
-constexpr uint32_t kBulkMaxChunks = 4096; // flags per rank and kind
+// ---- bulk messages (longer than a ring slot; SURVEY §8(f)1, BASELINE configs[2], [4]).
+// Rootless: the origin's progress workgroup originates a TAG_BULK announcement that travels the
+// skip-ring tree like any bcast; the bytes move as a pipelined scatter + all-gather between the
+// ranks' heaps, done by MOVER workgroups of the same persistent launch:
+//   * heap slot (r, o, s) of rank r holds r's copy of origin o's bulk message with bulk sequence q,
+//     s = q mod B; every rank computes every address, so nobody allocates or asks;
+//   * the message is cut into chunks, a chunk into N-1 stripes (whole KiB), stripe k owned by
+//     rank (o + 1 + k) mod N; SCATTER tiles (origin's movers) store stripe k into its owner's slot
+//     and bump the owner's sflag[chunk] and tflag; GATHER tiles (each receiver's movers, posted when
+//     the announcement arrives) wait for their own stripe of a chunk, then store it into the other
+//     N-2 receivers' slots and bump their tflag;
+//   * a receiver's copy is complete when tflag == the message's tile count plus its own gather tiles
+//     (it may not be released before its pushes out of it are done; its progress workgroup polls);
+//     it is then delivered (device programs: a VERIFY job checksums it; host mode: a pickup
+//     event, the host copies it out), the slot's flags are cleared and done(o, s) at the origin is
+//     bumped; the origin reuses slot s for sequence q + B only when done(o, s) counts every receiver.
+// Mover classes: class A (SCATTER, VERIFY) never waits; class B (GATHER) waits only for class-A
+// scatters, so no cycle of waits exists however announcements interleave.
+constexpr uint32_t kBulkKiB = 1024;     // stripe granularity
+constexpr int kBulkMaxChunks = 16;
+constexpr uint32_t kBulkLine = 128;     // per (rank, origin, slot): sflag[16] u32 @0, tflag u32 @64
+constexpr uint32_t kBulkTflag = 16;     // word index of tflag in the line
+constexpr uint64_t kJobTileMask = (1ull << 40) - 1;  // post counter: jobs << 40 | tiles
+constexpr int kMaxPend = 256;           // pending bulk receptions per rank (N * B <= 256)
+enum JobKind : uint32_t { JOB_SCATTER = 1, JOB_GATHER = 2, JOB_VERIFY = 3 };
+enum JobClass : uint32_t { JCLS_A = 0, JCLS_B = 1 };
 
-struct BulkParams {
-    int32_t n, rank_begin, origin, pad;
-    uint64_t bytes;                      // message size
-    uint32_t chunk, stripe, nchunks;     // chunk = stripe * (n - 1); stripe multiple of kBulkBlock
-    uint32_t buf_bytes;                  // capacity of every rank's buffer (<= 4 GiB, multiple of 1 KiB)
-    uint8_t* buf[kMaxBulkRanks];         // every rank's receive buffer (peer HBM mapped)
-    uint32_t* sflag[kMaxBulkRanks];      // every rank's scatter flags [kBulkMaxChunks]
-    uint32_t* gflag[kMaxBulkRanks];      // every rank's gather flags [kBulkMaxChunks]
-    uint64_t deadline_ticks;
-    uint32_t* err;                       // this part's error word
+struct BulkJob {         // 64 B, one slot of a part's job ring
+    uint32_t seq;        // j + 1 once the slot holds job j
+    uint32_t kind;       // JobKind
+    int32_t origin, lr;  // message origin, posting (local) rank
+    uint32_t slot, bid;  // heap slot s, bcast id
+    uint32_t len, ntiles;
+    uint64_t tile_base;  // (unused)
+    int32_t from;        // VERIFY: tree parent of the announcement (log)
+    uint32_t logidx;     // VERIFY: log record to complete with the checksum, ~0u = none
+    uint32_t q, gen;     // bulk sequence; SCATTER source: 1 = heap slot (o, o, s) (host), 0 = generated
+    uint32_t pad[2];
 };
+static_assert(sizeof(BulkJob) == 64, "job slot");
+
+// part-local job-ring control words (each on its own 128-B line): [cls*16 + 0] jobs posted,
+// [cls*16 + 8] head (first job not fully claimed), [32] exited progress workgroups
+constexpr int kJctlPost = 0, kJctlClaim = 8, kJctlExited = 32, kJctlWords = 48;
+
+// stripe / chunk / tile plan of a bulk message: a pure function of (N, len, cross-GPU), so every
+// rank derives the same one (cross: parts span GPUs -> pipelined chunks, ~sqrt(len / 4 MiB) of
+// them; one GPU: one chunk).  A tile (what one mover claim moves, then one release + flag add) is
+// the stripe, cut to <= 256 KiB: small enough that many movers share one stripe, large enough
+// that the per-tile release fence stays a small share of the copy.
+constexpr uint32_t kBulkTileMax = 256u << 10;
+struct BulkPlan {
+    uint32_t nchunks, stripe, chunk, tile;  // chunk = stripe * (N - 1); stripe, tile multiples of 1 KiB
+};
+__host__ __device__ inline BulkPlan bulk_plan(int n, uint32_t len, bool cross) {
+    uint32_t k = 1;
+    if (cross)
+        while ((uint64_t)(k + 1) * (k + 1) * (4ull << 20) <= len && k < (uint32_t)kBulkMaxChunks) k++;
+    const uint32_t m = (uint32_t)(n - 1);
+    const uint64_t per = ((uint64_t)len + k - 1) / k;
+    uint64_t stripe = ((per + m - 1) / m + kBulkKiB - 1) / kBulkKiB * kBulkKiB;
+    if (stripe < kBulkKiB) stripe = kBulkKiB;
+    uint64_t chunk = stripe * m;
+    while ((len + chunk - 1) / chunk > (uint64_t)kBulkMaxChunks) { stripe *= 2; chunk = stripe * m; }
+    BulkPlan p;
+    p.stripe = (uint32_t)stripe;
+    p.chunk = (uint32_t)chunk;
+    p.nchunks = len ? (uint32_t)((len + chunk - 1) / chunk) : 0u;
+    const uint32_t parts = (p.stripe + kBulkTileMax - 1) / kBulkTileMax;
+    p.tile = (p.stripe / parts + kBulkKiB - 1) / kBulkKiB * kBulkKiB;
+    return p;
+}
+// bytes of stripe k in chunk c
+__host__ __device__ inline uint32_t bulk_stripe_len(const BulkPlan& p, uint32_t len, uint32_t c, uint32_t k) {
+    const uint64_t c0 = (uint64_t)c * p.chunk;
+    const uint64_t clen = len - c0 < p.chunk ? len - c0 : p.chunk;
+    const uint64_t s0 = (uint64_t)k * p.stripe;
+    if (s0 >= clen) return 0u;
+    return (uint32_t)(clen - s0 < p.stripe ? clen - s0 : p.stripe);
+}
+__host__ __device__ inline uint32_t bulk_tiles_of(const BulkPlan& p, uint32_t bytes) {
+    return (bytes + p.tile - 1) / p.tile;
+}
+// tiles of chunk c over all its stripes
+__host__ __device__ inline uint32_t bulk_chunk_tiles(const BulkPlan& p, uint32_t len, uint32_t c) {
+    const uint64_t c0 = (uint64_t)c * p.chunk;
+    const uint32_t clen = (uint32_t)(len - c0 < p.chunk ? len - c0 : p.chunk);
+    const uint32_t full = clen / p.stripe, rem = clen % p.stripe;
+    return full * bulk_tiles_of(p, p.stripe) + bulk_tiles_of(p, rem);
+}
+// tiles of every stripe of every chunk = what reaches each receiver = its completion count
+__host__ __device__ inline uint32_t bulk_total_tiles(const BulkPlan& p, uint32_t len) {
+    uint32_t t = 0;
+    for (uint32_t c = 0; c < p.nchunks; c++) t += bulk_chunk_tiles(p, len, c);
+    return t;
+}
+// tiles of stripe k over all chunks (one receiver's GATHER job)
+__host__ __device__ inline uint32_t bulk_stripe_tiles(const BulkPlan& p, uint32_t len, uint32_t k) {
+    uint32_t t = 0;
+    for (uint32_t c = 0; c < p.nchunks; c++) t += bulk_tiles_of(p, bulk_stripe_len(p, len, c, k));
+    return t;
+}
+
+// storm workload with mixed payload sizes (BASELINE configs[4]): piecewise log-uniform length of
+// bcast b in [lo, hi]: an octave e uniform over [log2 lo, log2 hi), then uniform inside the octave
+// (integer only, so the device, the host and the oracle (rlo_testvec.h) agree bit for bit)
+__host__ __device__ inline uint64_t rlo_mix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline uint32_t storm_len_of(uint64_t seed, uint64_t b, uint32_t lo, uint32_t hi) {
+    if (hi <= lo) return lo;
+    if (lo == 0) lo = 1;
+    const int elo = 31 - __builtin_clz(lo), ehi = 31 - __builtin_clz(hi);
+    const uint64_t x = rlo_mix64(seed ^ 0xC5C5C5C5C5C5C5C5ull ^ (b * 0x9E3779B97F4A7C15ull));
+    // octaves [2^e, 2^(e+1)) for e in [elo, ehi), plus the partial top one when hi is no power of 2
+    const uint32_t noct = (uint32_t)(ehi - elo) + ((hi & (hi - 1u)) ? 1u : 0u);
+    if (noct == 0) return lo;
+    const uint32_t e = (uint32_t)elo + (uint32_t)(x % noct);
+    const uint64_t base = 1ull << e;
+    uint64_t v = base + ((x >> 32) % base);
+    if (v < lo) v = lo;
+    if (v > hi) v = hi;
+    return (uint32_t)v;
+}
 
 }  // namespace rlo

@@ -30,6 +30,8 @@
 // that precedes the counter store.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rlo_device.hpp"
 
 namespace rlo {
@@ -66,11 +68,32 @@ struct CandL {          // one message of this iteration, kept for the copy phas
     uint32_t kind, group;
 };
 
+// bulk-message state (the BULK instantiation only)
+struct BulkSh {
+    BulkJob mv_job;             // mover: the job of the claimed tile
+    uint32_t mv_ti, mv_stop;
+    unsigned long long mv_sum;
+    uint32_t bq[kPass];         // progress: storm candidate i -> bulk sequence, ~0u = a ring message
+    uint32_t blen[kPass];       // storm candidate i -> payload length
+    uint32_t bact[kMaxPend];    // pending receptions (o * B + s), compact
+    uint32_t nbact, ncomp;
+    uint64_t cmask[kMaxPend / 64];  // completion bits by position in bact (phase A poll)
+    uint64_t sdone[8];          // done(me, s), s < B
+    uint32_t bulk_q;            // my bulk originations so far
+};
+struct NoBulkSh {};
+struct BulkPend {               // dynamic LDS [N * B]: a pending bulk reception of (o, s)
+    uint32_t bid, len, ntiles;
+    int32_t from;
+    uint32_t t0, q, pad0, pad1;
+};
+
 // W waves per rank-workgroup (rlo_device.hpp kBlock documents the 4-wave form): 64 W candidate
 // messages per iteration.  8 waves (512 candidates, two waves per SIMD) when every rank has a CU
 // of its own; 4 waves when two rank-workgroups share a CU (worlds larger than the GPU)
-template <int W>
+template <int W, bool BULK>
 struct Shared {
+    typename std::conditional<BULK, BulkSh, NoBulkSh>::type b;
     static constexpr int kWaves = W, kMaxCand = 64 * W;
     RankTopo t;
     // selection of this iteration (wave 0)
@@ -312,7 +335,7 @@ __device__ __forceinline__ uint32_t judge_hash(uint64_t seed, uint32_t rank, int
 // device judge registry.  arg = proposal data at byte offset arg_off of the forward region,
 // data_len bytes, zero-extended (the reference's calloc'd receive buffer).  ISP restates
 // testcases.c:18-37.  The originator's final call passes NULL (:773): device judges approve it.
-__device__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, uint32_t my_mask, int32_t pid,
+__device__ __forceinline__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, uint32_t my_mask, int32_t pid,
                           uint32_t arg_off, uint32_t data_len) {
     switch (P.judge_kind) {
         case JUDGE_MASK:
@@ -336,10 +359,11 @@ __device__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, ui
 }
 
 // one event record: the parity log (MODE_LOG, linear) or the host pickup ring (MODE_HOST, the
-// slot after this iteration's earlier events; the selection phase guaranteed the room)
+// slot after this iteration's earlier events; the selection phase guaranteed the room).  Returns the
+// record's payload index (~0u: no payload), or with want_rec the record index itself
 template <class SH>
 __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint32_t kind, int origin, int from,
-                                            uint32_t id, uint32_t len, int vote, uint32_t aux) {
+                                            uint32_t id, uint32_t len, int vote, uint32_t aux, bool want_rec = false) {
     if (!(P.mode & (MODE_LOG | MODE_HOST))) return ~0u;
     uint32_t i;
     if (P.mode & MODE_HOST) {
@@ -363,7 +387,7 @@ __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint
     u32x4* dst = reinterpret_cast<u32x4*>(&P.log[(size_t)lr * P.log_cap + i]);
     st_sys16(dst, u32x4{r.kind, (uint32_t)r.origin, (uint32_t)r.from, r.id});
     st_sys16(dst + 1, u32x4{r.len, (uint32_t)r.vote, r.aux, r.payload_idx});
-    return r.payload_idx;
+    return want_rec ? i : r.payload_idx;
 }
 
 // vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741)
@@ -463,14 +487,400 @@ __device__ __forceinline__ u32x4 gen_chunk(const Params& P, uint32_t kind, int m
     return v;
 }
 
+// ------------------------------------------------------------------ bulk messages (rlo_device.hpp)
+
+// a bulk index out of range: report (device error ERR_BULK, aux = site << 24 | value) and stop,
+// instead of touching memory that is not the heap's.  Always on in the bulk instantiation: a wild
+// peer-memory store can take down every GPU of the node, a report costs a few compares
+__device__ __forceinline__ void bulk_fault(const Params& P, uint32_t site, uint32_t v) {
+    // this part stops (its workgroups poll the word); the other parts of a sharded world then stop at
+    // their no-progress timeout
+    uint32_t* pe = P.error_flag;
+    if (atomicCAS(pe, 0u, (uint32_t)ERR_BULK) == 0u) pe[1] = (site << 24) | (v & 0xffffffu);  // ctrl word 0, high half
+}
+#define BULK_GUARD(cond, site, v)                       \
+    do {                                                \
+        if (__builtin_expect(!(cond), 0)) bulk_fault(P, (site), (uint32_t)(v)); \
+    } while (0)
+// (r, o, s) in range: else a report and the sink line (jctl's spare words), never a wild address
+__device__ __forceinline__ bool bulk_ok(const Params& P, int r, int o, uint32_t s, uint32_t site) {
+    const bool ok = (uint32_t)r < (uint32_t)P.n && (uint32_t)o < (uint32_t)P.n && s < P.bulk_slots;
+    if (!ok) bulk_fault(P, site, ((uint32_t)r << 12) | ((uint32_t)o & 0xfffu));
+    return ok;
+}
+
+// heap slot (r, o, s), its flag line and the origin's done word, in whichever part holds r / o
+__device__ __forceinline__ uint8_t* bulk_heap(const Params& P, int r, int o, uint32_t s) {
+    if (!bulk_ok(P, r, o, s, 1)) return nullptr;  // a null rsrc base: every access is dropped
+    const int p = P.part_of[r];
+    const uint64_t lr = (uint64_t)(r - P.part_begin[p]);
+    return reinterpret_cast<uint8_t*>(P.bheap[p]) + ((lr * (uint64_t)P.n + (uint64_t)o) * P.bulk_slots + s) * P.bulk_cap;
+}
+__device__ __forceinline__ uint32_t* bulk_flags(const Params& P, int r, int o, uint32_t s) {
+    if (!bulk_ok(P, r, o, s, 2)) return reinterpret_cast<uint32_t*>(P.jctl + 40);
+    const int p = P.part_of[r];
+    const uint64_t lr = (uint64_t)(r - P.part_begin[p]);
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(P.bflag[p]) +
+                                       ((lr * (uint64_t)P.n + (uint64_t)o) * P.bulk_slots + s) * kBulkLine);
+}
+__device__ __forceinline__ uint64_t* bulk_done(const Params& P, int o, uint32_t s) {
+    if (!bulk_ok(P, o, o, s, 3)) return P.jctl + 40;
+    const int p = P.part_of[o];
+    const uint64_t lr = (uint64_t)(o - P.part_begin[p]), nlp = (uint64_t)(P.part_begin[p + 1] - P.part_begin[p]);
+    return reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(P.bflag[p]) +
+                                       (nlp * (uint64_t)P.n * P.bulk_slots + lr * P.bulk_slots + s) * kBulkLine);
+}
+__device__ __forceinline__ uint32_t bflag_ld(uint32_t* p, bool sys) {
+    return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+               : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void bflag_add(uint32_t* p, uint32_t v, bool sys) {
+    if (sys) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// release / acquire around the bulk flags (the proven form of the first bulk kernel: a fence on
+// both sides, MI355X_MICROARCH.md "Valid forms" first bullet; explicit vmcnt after the release,
+// "Compiler hazard")
+__device__ __forceinline__ void bulk_release(bool sys) {
+    if (sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void bulk_acquire(bool sys) {
+    if (sys) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// clear the flags of (r, o, s) and count r's completion at the origin (slot s may be reused once
+// every receiver did this): RLO_user_msg_recycle of a bulk delivery (rootless_ops.c:981-992)
+__device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o, uint32_t s, bool sys) {
+    atomicAdd((unsigned long long*)&P.jctl[44], 1ull);  // diagnostics: releases
+    uint32_t* f = bulk_flags(P, r, o, s);
+    for (int i = 0; i <= (int)kBulkTflag; i++) __hip_atomic_store(f + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bulk_release(sys);
+    uint64_t* d = bulk_done(P, o, s);
+    if (sys) __hip_atomic_fetch_add(d, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_fetch_add(d, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// post a job (one lane): take the next job index of the class, write the slot, then open it for
+// claims (claim word = seq << 32 | next tile).  The ring holds every job that can be unfinished at
+// once (rlo_world.cpp sizes it), so the slot is free at once; the wait is a guard.  The words are
+// BulkJob's, passed as scalars (a struct whose address is taken would live in scratch)
+__device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t kind, int origin, int lr, uint32_t slot_s,
+                                         uint32_t bid, uint32_t len, uint32_t ntiles, int from, uint32_t logidx,
+                                         uint32_t q, uint32_t gen) {
+    if (!(kind >= JOB_SCATTER && kind <= JOB_VERIFY && (uint32_t)origin < (uint32_t)P.n && (uint32_t)lr < P.n_local &&
+          slot_s < P.bulk_slots && len > 0 && len <= P.bulk_cap && ntiles > 0)) {
+        bulk_fault(P, 6, (kind << 20) | (len & 0xfffffu));
+        return;
+    }
+    const uint64_t j = atomicAdd((unsigned long long*)&P.jctl[cls * 16 + kJctlPost], 1ull);
+    const uint32_t slot = (uint32_t)(j & (P.jslots - 1u));
+    atomicAdd((unsigned long long*)&P.jctl[40 + kind], 1ull);  // diagnostics: posts by kind (41..43)
+    const uint64_t t0 = now_ticks();
+    while (__hip_atomic_load(&P.jfree[cls * P.jslots + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != j) {
+        __builtin_amdgcn_s_sleep(1);
+        if (now_ticks() - t0 > P.timeout_ticks) {  // cannot happen unless a mover died: stop loudly
+            atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+            return;
+        }
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(P.jobs + (size_t)cls * P.jslots + slot);
+    st_sys16(dst, u32x4{(uint32_t)(j + 1), kind, (uint32_t)origin, (uint32_t)lr});
+    st_sys16(dst + 1, u32x4{slot_s, bid, len, ntiles});
+    st_sys16(dst + 2, u32x4{0u, 0u, (uint32_t)from, logidx});
+    st_sys16(dst + 3, u32x4{q, gen, 0u, 0u});
+    VM_DRAIN();
+    __hip_atomic_store(&P.jclaim[cls * P.jslots + slot], (uint64_t)(j + 1) << 32, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// storm payload bytes [off, off + 16) of bcast (origin, bid, len) (off a multiple of 16)
+__device__ __forceinline__ u32x4 storm_granule(uint32_t origin, uint32_t bid, uint32_t len, uint32_t off) {
+    const int b0 = (int)len - (int)off;
+    const uint32_t k0 = off >> 3;
+    const uint64_t a = b0 > 0 ? storm_word(origin, bid, k0) : 0ull;
+    const uint64_t b = b0 > 8 ? storm_word(origin, bid, k0 + 1u) : 0ull;
+    return u32x4{mask_bytes((uint32_t)a, b0), mask_bytes((uint32_t)(a >> 32), b0 - 4), mask_bytes((uint32_t)b, b0 - 8),
+                 mask_bytes((uint32_t)(b >> 32), b0 - 12)};
+}
+
+// A mover workgroup: claims one tile at a time from its class's job stream -- the job at the
+// class head, by a CAS on that job's claim word (seq << 32 | next tile; the seq tells a recycled
+// slot from the job that was read) -- and moves it.  Claims are dynamic, so the work never depends
+// on which movers are busy; a fully claimed job moves the head on.  Exits once every progress
+// workgroup of the part has exited and no job is left.
+template <int W, class SH>
+__device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
+    BulkSh& S = SS.b;
+    constexpr int kT = 64 * W;
+    const uint32_t mi = blockIdx.x - P.n_local;
+    const uint32_t na = (P.nmov + 1u) / 2u;
+    const uint32_t cls = mi < na ? JCLS_A : JCLS_B;
+    const bool sys = P.sys_scope != 0;
+    const int n = P.n;
+    const uint32_t jm = P.jslots - 1u;
+    uint64_t* posted = &P.jctl[cls * 16 + kJctlPost];
+    uint64_t* head = &P.jctl[cls * 16 + kJctlClaim];
+    BulkJob* ring = P.jobs + (size_t)cls * P.jslots;
+    uint64_t* jclaim = P.jclaim + (size_t)cls * P.jslots;
+    uint64_t acq_key = ~0ull;  // (job, chunk) the last acquire covered
+    const uint64_t t_launch = now_ticks();
+    for (;;) {
+        // ---- claim one tile
+        if (tid == 0) {
+            uint32_t stop = 0, spins = 0;
+            for (;;) {
+                const uint64_t h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t slot = (uint32_t)(h & jm);
+                const uint64_t c = __hip_atomic_load(&jclaim[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((c >> 32) > h + 1) {  // a later job holds the slot: job h finished and was recycled
+                    atomicCAS((unsigned long long*)head, (unsigned long long)h, (unsigned long long)(h + 1));
+                    continue;
+                }
+                if ((c >> 32) != h + 1) {  // job h not open yet: idle
+                    if (__hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= h) {
+                        // every progress workgroup exited (after its last post): nothing more will come
+                        if (__hip_atomic_load(&P.jctl[kJctlExited], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.n_local &&
+                            __hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= h) {
+                            stop = 1;
+                            break;
+                        }
+                    }
+                    if (poll32(P.error_flag)) { stop = 1; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                    if ((++spins & 1023u) == 0 && now_ticks() - t_launch > P.deadline_ticks) {
+                        atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                        stop = 1;
+                        break;
+                    }
+                    continue;
+                }
+                const u32x4* js = reinterpret_cast<const u32x4*>(&ring[slot]);
+                u32x4 jv[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) jv[q] = __builtin_nontemporal_load(js + q);
+                if (jv[0].x != (uint32_t)(h + 1)) continue;  // recycled under us: re-read the head
+                const uint32_t T = jv[1].w;                   // BulkJob.ntiles
+                if ((uint32_t)c >= T) {                       // fully claimed: move the head on
+                    atomicCAS((unsigned long long*)head, (unsigned long long)h, (unsigned long long)(h + 1));
+                    continue;
+                }
+                if (atomicCAS((unsigned long long*)&jclaim[slot], (unsigned long long)c, (unsigned long long)(c + 1)) == c) {
+                    u32x4* jd = reinterpret_cast<u32x4*>(&S.mv_job);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) jd[q] = jv[q];
+                    S.mv_ti = (uint32_t)c;
+                    break;
+                }
+            }
+            S.mv_stop = stop;
+        }
+        BAR();
+        if (S.mv_stop) return;
+        const BulkJob jb = S.mv_job;  // uniform (LDS broadcast)
+        const uint32_t ti = S.mv_ti;
+        if (!(jb.kind >= JOB_SCATTER && jb.kind <= JOB_VERIFY && (uint32_t)jb.origin < (uint32_t)n &&
+              (uint32_t)jb.lr < P.n_local && jb.slot < P.bulk_slots && jb.len > 0 && jb.len <= P.bulk_cap &&
+              ti < jb.ntiles)) {
+            if (tid == 0) bulk_fault(P, 4, (jb.kind << 20) | (jb.seq & 0xfffffu));
+            return;
+        }
+        const uint32_t len = jb.len, s = jb.slot;
+        const int o = jb.origin;
+        const int me = P.rank_begin + jb.lr;
+        const BulkPlan pl = bulk_plan(n, len, P.bulk_cross != 0);
+        const uint32_t jslot = (jb.seq - 1u) & jm;
+
+        if (jb.kind == JOB_SCATTER || jb.kind == JOB_GATHER) {
+            // tile -> (chunk c, stripe k, tile i of that stripe-chunk)
+            uint32_t u = ti, c = 0, k = 0, i = 0;
+            if (jb.kind == JOB_SCATTER) {
+                for (c = 0; c + 1 < pl.nchunks; c++) {
+                    const uint32_t ct = bulk_chunk_tiles(pl, len, c);
+                    if (u < ct) break;
+                    u -= ct;
+                }
+                const uint64_t c0 = (uint64_t)c * pl.chunk;
+                const uint32_t clen = (uint32_t)min((uint64_t)pl.chunk, (uint64_t)len - c0);
+                const uint32_t full = clen / pl.stripe, tf = bulk_tiles_of(pl, pl.stripe);
+                if (u < full * tf) { k = u / tf; i = u - k * tf; }
+                else { k = full; i = u - full * tf; }
+            } else {
+                k = (uint32_t)((me - o - 1 + n) % n);
+                for (c = 0; c + 1 < pl.nchunks; c++) {
+                    const uint32_t ct = bulk_tiles_of(pl, bulk_stripe_len(pl, len, c, k));
+                    if (u < ct) break;
+                    u -= ct;
+                }
+                i = u;
+            }
+            const uint32_t slen = bulk_stripe_len(pl, len, c, k);
+            const uint32_t off0 = c * pl.chunk + k * pl.stripe + i * pl.tile;
+            const uint32_t tlen = min(pl.tile, slen - i * pl.tile);
+            const uint32_t ngr = (tlen + 15u) >> 4;
+            if (jb.kind == JOB_SCATTER) {
+                const int owner = (o + 1 + (int)k) % n;
+                const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, owner, o, s), P.bulk_cap);
+                const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, o, o, s), P.bulk_cap);
+                for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
+                    u32x4 v[4];
+#pragma unroll
+                    for (int uu = 0; uu < 4; uu++) {
+                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                        if (g < ngr) v[uu] = jb.gen ? ld_sc1(rs, off0 + 16u * g) : storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g);
+                    }
+#pragma unroll
+                    for (int uu = 0; uu < 4; uu++) {
+                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                        if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
+                    }
+                }
+                VM_DRAIN();
+                __syncthreads();
+                if (tid == 0) {
+                    bulk_release(sys);
+                    uint32_t* f = bulk_flags(P, owner, o, s);
+                    bflag_add(f + c, 1u, sys);
+                    bflag_add(f + kBulkTflag, 1u, sys);
+                }
+            } else {
+                // GATHER: my stripe of chunk c must have landed (class-A scatter tiles only)
+                if (tid == 0) {
+                    uint32_t* f = bulk_flags(P, me, o, s);
+                    const uint32_t want = bulk_tiles_of(pl, slen);
+                    uint32_t spins = 0;
+                    if (bflag_ld(f + c, sys) < want) {  // diagnostics: gather tiles waiting now / last wait
+                        atomicAdd((unsigned long long*)&P.jctl[38], 1ull);
+                        P.jctl[46] = ((uint64_t)(uint32_t)o << 48) | ((uint64_t)me << 32) | ((uint64_t)s << 24) | want;
+                    }
+                    while (bflag_ld(f + c, sys) < want) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if ((++spins & 1023u) == 0 && (poll32(P.error_flag) || now_ticks() - t_launch > P.deadline_ticks)) {
+                            atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                            break;
+                        }
+                    }
+                    const uint64_t key = ((uint64_t)jb.seq << 8) | c;
+                    if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
+                    atomicAdd((unsigned long long*)&P.jctl[39], 1ull);  // diagnostics: gather waits passed
+                }
+                __syncthreads();
+                const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
+                for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
+                    u32x4 v[4];
+#pragma unroll
+                    for (int uu = 0; uu < 4; uu++) {
+                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                        if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
+                    }
+                    for (int d = 1; d < n; d++) {  // every other non-originator (uniform)
+                        const int dst = (o + d) % n;
+                        if (dst == me) continue;
+                        const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, dst, o, s), P.bulk_cap);
+#pragma unroll
+                        for (int uu = 0; uu < 4; uu++) {
+                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                            if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
+                        }
+                    }
+                }
+                VM_DRAIN();
+                __syncthreads();
+                if (tid < 64) {
+                    bulk_release(sys);
+                    // every other receiver got this tile; and so did my own count: my copy may not be
+                    // released (the origin may not reuse it) before my pushes out of it are done
+                    for (int d = 1 + tid; d < n; d += 64) {
+                        const int dst = (o + d) % n;
+                        bflag_add(bulk_flags(P, dst, o, s) + kBulkTflag, 1u, sys);
+                    }
+                }
+            }
+        } else {  // JOB_VERIFY: checksum my complete copy (the pickup read of every byte)
+            if (tid == 0) {
+                const uint64_t key = (uint64_t)jb.seq << 8;
+                if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
+            }
+            __syncthreads();
+            const uint32_t off0 = ti * pl.tile;
+            const uint32_t tlen = min(pl.tile, len - off0);
+            const uint32_t ngr = (tlen + 15u) >> 4;
+            const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
+            unsigned long long acc = 0;
+            for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
+                u32x4 v[4];
+#pragma unroll
+                for (int uu = 0; uu < 4; uu++) {
+                    const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                    if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
+                }
+#pragma unroll
+                for (int uu = 0; uu < 4; uu++) {
+                    const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                    if (g < ngr) {
+                        const uint32_t off = off0 + 16u * g;
+                        const int b0 = (int)len - (int)off;  // the reference's zero-padded tail
+                        const u32x4 w = {mask_bytes(v[uu].x, b0), mask_bytes(v[uu].y, b0 - 4), mask_bytes(v[uu].z, b0 - 8),
+                                         mask_bytes(v[uu].w, b0 - 12)};
+                        acc += chunk_mix(off >> 4, w);
+                    }
+                }
+            }
+            // workgroup sum -> the job's accumulator (returning add: ordered before the tile count)
+            for (int sh = 32; sh >= 1; sh >>= 1) acc += __shfl_xor(acc, sh);
+            if ((tid & 63) == 0) atomicAdd((unsigned long long*)&S.mv_sum, acc);
+            __syncthreads();
+            if (tid == 0) {
+                (void)__hip_atomic_fetch_add(&P.jsum[cls * P.jslots + jslot], (uint64_t)S.mv_sum, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                S.mv_sum = 0;
+            }
+        }
+        // ---- tile finished: the last one finishes the job and recycles its slot
+        if (tid == 0) {
+            atomicAdd((unsigned long long*)&P.jctl[36 + cls], 1ull);  // diagnostics: tiles moved per class
+            const uint32_t old = atomicAdd(&P.jdone[cls * P.jslots + jslot], 1u);
+            if (old + 1u == jb.ntiles) {
+                if (jb.kind == JOB_VERIFY) {
+                    const uint64_t part = __hip_atomic_load(&P.jsum[cls * P.jslots + jslot], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t tot = part + chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)o, jb.bid, TAG_BCAST, len});
+                    atomicAdd((unsigned long long*)&P.stats[jb.lr].bcast_sum, (unsigned long long)tot);
+                    if (jb.logidx != ~0u)  // the delivery record gets the message checksum
+                        st_sys16(reinterpret_cast<u32x4*>(&P.log[(size_t)jb.lr * P.log_cap + jb.logidx]) + 1,
+                                 u32x4{len, 0xffffffffu, (uint32_t)tot, (uint32_t)(tot >> 32)});
+                    bulk_slot_release(P, me, o, s, sys);
+                }
+                __hip_atomic_store(&P.jdone[cls * P.jslots + jslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&P.jsum[cls * P.jslots + jslot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&P.jfree[cls * P.jslots + jslot], (uint64_t)(jb.seq - 1u) + P.jslots, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        BAR();  // S.mv_* is rewritten by the next claim
+    }
+}
+
 // ------------------------------------------------------------------ the kernel
 
-template <int W>
+template <int W, bool BULK>
 __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     constexpr int kWaves = W, kBlock = 64 * W, kMaxCand = 64 * W;
     constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at the last 64 candidates
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    __shared__ Shared<W> S;
+    __shared__ Shared<W, BULK> S;
+    if constexpr (BULK) {
+        if (blockIdx.x >= P.n_local) {  // a mover workgroup of the same launch
+            if (threadIdx.x == 0) S.b.mv_sum = 0;
+            __syncthreads();
+            mover_run<W>(P, S, (int)threadIdx.x);
+            return;
+        }
+    }
     const uint32_t nsmall = P.nsmall;  // chunks per staged message
     const uint32_t nmagic = nsmall > 1 ? 0xFFFFFFFFu / nsmall + 1u : 0u;
     PendState* pend = reinterpret_cast<PendState*>(dyn_lds);                        // [2 * n]
@@ -501,6 +911,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint64_t* const hctl = host ? P.hctl + (size_t)lr * kHctlWords : nullptr;
     uint64_t* const hctl_dev = host ? P.hctl_dev + (size_t)lr * kHctlWords : nullptr;
     const uint32_t hcap_m = host ? P.hin_cap - 1u : 0u;
+    // bulk messages: pending receptions (o, s) in dynamic LDS [N * B] (BULK instantiation only)
+    [[maybe_unused]] BulkPend* const bpend = reinterpret_cast<BulkPend*>(dyn_lds + (BULK ? P.bpend_off : 0u));
+    [[maybe_unused]] const uint32_t bsl = BULK ? P.bulk_slots : 1u;
 
     // ---------------- init
     {
@@ -527,6 +940,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0;
+            if constexpr (BULK) {
+                S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0;
+                for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
+            }
         }
     }
     BAR();
@@ -600,13 +1017,41 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                : poll32(P.lat_round);
                 if (!idle_prev || sp >= kIdleSpin) break;
+                bool bmoved = false;
+                if constexpr (BULK) {  // a released heap slot of mine (a bulk origination may wait for it)
+                    if (lane < (int)bsl) {
+                        uint64_t* d = bulk_done(P, me, (uint32_t)lane);
+                        bmoved = (sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                      : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != S.b.sdone[lane];
+                    }
+                }
                 const bool moved = in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] ||
                                    out_head_r != S.snap[2][lane] || vout_head_r != S.snap[3][lane] || hpoll != p_h ||
-                                   latr != p_lat || errf != 0;
+                                   latr != p_lat || errf != 0 || bmoved;
                 if (__ballot(moved)) break;
             }
             S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
             S.snap[3][lane] = vout_head_r; p_h = hpoll; p_lat = latr;
+            if constexpr (BULK) {
+                // my heap slots' release counts, and which pending receptions are complete
+                if (lane < (int)bsl) {
+                    uint64_t* d = bulk_done(P, me, (uint32_t)lane);
+                    S.b.sdone[lane] = sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                const uint32_t nb = S.b.nbact;
+                for (uint32_t u = 0; u * 64u < nb; u++) {
+                    const uint32_t i = u * 64u + (uint32_t)lane;
+                    bool dn = false;
+                    if (i < nb) {
+                        const uint32_t e = S.b.bact[i];
+                        if (e >= (uint32_t)P.n * bsl) bulk_fault(P, 7, e); else
+                        dn = bflag_ld(bulk_flags(P, me, (int)(e / bsl), e % bsl) + kBulkTflag, sys) >= bpend[e].ntiles;
+                    }
+                    const uint64_t m = __ballot(dn);
+                    if (lane == 0) S.b.cmask[u] = m;
+                }
+            }
             if ((P.mode & MODE_LAT) && me == 0) {  // world rank 0 observes round completions on its clock
                 const uint32_t done_r = rdl32(latr, 1), seen = S.lat_seen;
                 if (done_r > seen) {
@@ -646,6 +1091,66 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - pk_head);
                 hblock = pk_free < 8u;
                 hlim = hblock ? 0u : (pk_free - 4u) / 2u;
+            }
+            if constexpr (BULK) {
+                // completed bulk receptions: delivered now.  Device programs: counted, logged and
+                // checksummed by a VERIFY job (which then releases the slot); host mode: one pickup
+                // event each (the host copies the bytes out and posts RLO_CMD_BULK_RELEASE)
+                const uint32_t nb = S.b.nbact;
+                if (nb) {
+                    uint32_t climit = kMaxPend;
+                    if (host) {
+                        const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - rdl64(hpoll, 1));
+                        climit = pk_free >= 24u ? (pk_free - 16u) / 2u : 0u;
+                    }
+                    uint32_t seen = 0, kept = 0;
+                    for (uint32_t u = 0; u * 64u < nb; u++) {
+                        const uint32_t i = u * 64u + (uint32_t)lane;
+                        const uint64_t m = S.b.cmask[u];
+                        bool fin = ((m >> lane) & 1ull) && seen + (uint32_t)__popcll(m & lt_mask) < climit;
+                        seen += (uint32_t)__popcll(m);
+                        const uint32_t e = i < nb ? S.b.bact[i] : 0u;
+                        if (fin) {
+                            const int o = (int)(e / bsl);
+                            const uint32_t sl = e % bsl;
+                            const BulkPend pe = bpend[e];
+                            if (host) {
+                                log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, sl);
+                            } else {
+                                atomicAdd(&S.bcast_delivered, 1ull);
+                                const uint32_t li =
+                                    log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
+                                post_job(P, JCLS_A, JOB_VERIFY, o, lr, sl, pe.bid, pe.len,
+                                         bulk_tiles_of(bulk_plan(P.n, pe.len, P.bulk_cross != 0), pe.len), pe.from, li,
+                                         pe.q, 0u);
+                                if (P.mode & MODE_LAT) {  // the last of N-1 pickups completes the round
+                                    const uint32_t old =
+                                        sys ? __hip_atomic_fetch_add(&P.lat_count[pe.bid], 1u, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_SYSTEM)
+                                            : atomicAdd(&P.lat_count[pe.bid], 1u);
+                                    if (old + 1u == (uint32_t)(P.n - 1)) {
+                                        P.lat_out[pe.bid] = (uint64_t)((uint32_t)now_ticks() - pe.t0);
+                                        if (sys) __hip_atomic_store(P.lat_round, pe.bid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                        else __hip_atomic_store(P.lat_round, pe.bid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    }
+                                }
+                            }
+                        }
+                        // compact the pending list in place (a kept entry only moves down)
+                        const bool keep = i < nb && !fin;
+                        const uint64_t km = __ballot(keep);
+                        if (keep) S.b.bact[kept + (uint32_t)__popcll(km & lt_mask)] = e;
+                        kept += (uint32_t)__popcll(km);
+                    }
+                    if (lane == 0) {
+                        S.b.nbact = kept;
+                        if (kept != nb) S.progressed = 1;
+                    }
+                    if (host && kept != nb) {  // their events count against this iteration's pickup room
+                        const uint32_t ev = nb - kept;
+                        hlim = hlim > (ev + 1u) / 2u ? hlim - (ev + 1u) / 2u : 0u;
+                    }
+                }
             }
             // votes to merge (wave 1), at most 256 per iteration: trim the ring prefixes
             const uint32_t va = (lane < sll && !hblock) ? (uint32_t)min(vin_tail_r - vin_head_r, (uint64_t)256) : 0u;
@@ -748,11 +1253,17 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             else set_error(S, P, ERR_HOST_CMD, hd.x);
                         } else if (htag == CMD_QUIT) {
                             S.quit = 1;
+                        } else if (BULK && htag == CMD_BULK_RELEASE) {  // the host copied a bulk delivery out
+                            const int og = (int)(hd.x & 0xffffu);
+                            const uint32_t sl = hd.z >> 24;
+                            if (og < P.n && og != me && sl < bsl) bulk_slot_release(P, me, og, sl, sys);
+                            else set_error(S, P, ERR_HOST_CMD, hd.x);
                         } else {
                             set_error(S, P, ERR_HOST_CMD, hd.x);
                         }
                     }
-                    const bool org = inq && (uint32_t)lane >= ncp && (htag == TAG_BCAST || htag == TAG_PROPOSAL);
+                    const bool org = inq && (uint32_t)lane >= ncp &&
+                                     (htag == TAG_BCAST || htag == TAG_PROPOSAL || (BULK && htag == TAG_BULK));
                     const uint64_t om = ncp >= 64u ? 0ull : __ballot(org) >> ncp;
                     uint32_t run = ~om == 0ull ? 64u - ncp : (uint32_t)__builtin_ctzll(~om);
                     const uint64_t pm = ncp >= 64u ? 0ull
@@ -782,6 +1293,25 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const int64_t rem = sched_n - sched_next;
                     uint32_t ww = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
                     if (ww > kMaxCand - C) ww = kMaxCand - C;
+                    if constexpr (BULK) {
+                        // per-bcast lengths; a bulk one needs its heap slot back from every receiver
+                        // of the previous use (done(me, s)); the window ends before one that does not
+                        uint32_t ln = 0, isb = 0;
+                        if ((uint32_t)lane < ww) {
+                            ln = P.len_hi > P.len_lo ? storm_len_of(P.seed, sid, P.len_lo, P.len_hi) : P.len;
+                            isb = ln > P.ring_cap ? 1u : 0u;
+                        }
+                        uint32_t nbk = 0;
+                        const uint32_t q = S.b.bulk_q + wave_excl_scan(isb, &nbk);
+                        const bool ok = !isb || S.b.sdone[q & (bsl - 1u)] >= (uint64_t)(q / bsl) * (uint64_t)(P.n - 1);
+                        const uint64_t bad = __ballot((uint32_t)lane < ww && !ok);
+                        if (bad) ww = (uint32_t)__builtin_ctzll(bad);
+                        if (bad && lane == 0) atomicAdd((unsigned long long*)&P.jctl[45], 1ull);  // diagnostics: slot waits
+                        if ((uint32_t)lane < ww) {
+                            S.b.bq[lane] = isb ? q : ~0u;
+                            S.b.blen[lane] = ln;
+                        }
+                    }
                     storm_base = C;
                     nstorm = ww;
                     C += ww;
@@ -790,7 +1320,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             if ((P.mode & MODE_LAT) && C < kMaxCand) {
                 // my next round (prefetched) starts when the previous round completed everywhere
-                if (S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
+                bool lat_ok = true;
+                if constexpr (BULK) {
+                    if (P.len > P.ring_cap) {
+                        const uint32_t q = S.b.bulk_q;
+                        lat_ok = S.b.sdone[q & (bsl - 1u)] >= (uint64_t)(q / bsl) * (uint64_t)(P.n - 1);
+                    }
+                }
+                if (lat_ok && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
             }
             if (lane == 0) {
                 S.ract = ract;
@@ -931,6 +1468,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             uint32_t kind = K_BAD, w0 = 0, id = 0, w2 = 0, t0 = 0, src = 0, kids = 0, group = 0;
             int from = -1, judge = 1;
             bool want_jreq = false;  // host mode: a proposal whose verdict has not been asked for yet
+            [[maybe_unused]] uint32_t bdesc_len = 0, bdesc_q = 0;  // a local bulk origination's descriptor
             if (active && c < R) {
                 const u32x4 h = *reinterpret_cast<const u32x4*>(STG(c, 0));
                 group = S.cand[c].group;
@@ -950,7 +1488,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else if (origin >= P.n || (tag == TAG_BCAST && (P.mode & MODE_LAT) && id >= P.lat_rounds)) {
                     set_error(S, P, ERR_BAD_SLOT, w0);
                     kind = K_BAD;  // consumed, never forwarded, no side effects
-                } else if (tag == TAG_BCAST || tag == TAG_DECISION) {
+                } else if (tag == TAG_BCAST || tag == TAG_DECISION || (BULK && tag == TAG_BULK)) {
                     kids = kids_of(me, origin, from, level, last_wall, scc, sll, sl_r);
                 } else if (tag == TAG_PROPOSAL) {
                     // PBuf [pid][vote][data_len u64][data] at slot + 16 (rootless_ops.c:1402-1410)
@@ -984,6 +1522,16 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     id = S.storm_ids[c - storm_base];
                     w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
                     w2 = P.len;
+                    if constexpr (BULK) {
+                        const uint32_t bq = S.b.bq[c - storm_base];
+                        w2 = S.b.blen[c - storm_base];
+                        if (bq != ~0u) {  // a bulk bcast: the ring carries its announcement
+                            bdesc_len = w2;
+                            bdesc_q = bq;
+                            w0 = (uint32_t)me | (TAG_BULK << 16) | (0xffu << 24);
+                            w2 = 16u;
+                        }
+                    }
                 } else if (host && c >= S.hbase && c < S.hbase + S.nh) {  // host origination (RLO_bcast_gen :1581)
                     const u32x4 h = *reinterpret_cast<const u32x4*>(STG(c, 0));
                     kind = K_HOST;
@@ -993,6 +1541,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (((h.x >> 16) & 0xffu) == TAG_PROPOSAL) {  // RLO_submit_proposal :876-906 (payload = PBuf)
                         w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
                         w2 = (h.z & 0xffffu) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                    } else if (BULK && ((h.x >> 16) & 0xffu) == TAG_BULK) {  // payload = descriptor {len, q}
+                        w0 = (uint32_t)me | (TAG_BULK << 16) | (0xffu << 24);
+                        w2 = 16u;
                     } else {
                         w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
                         w2 = h.z & 0xffffu;
@@ -1022,16 +1573,27 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     id = S.lat_id;
                     w0 = (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24);
                     w2 = P.len;
+                    if constexpr (BULK) {
+                        if (P.len > P.ring_cap) {
+                            bdesc_len = P.len;
+                            bdesc_q = S.b.bulk_q;
+                            w0 = (uint32_t)me | (TAG_BULK << 16) | (0xffu << 24);
+                            w2 = 16u;
+                        }
+                    }
                 }
                 // stage the header (+ the payload of a small message) like a received slot; the header
                 // carries the slot mark every hop checks
                 w2 = (w2 & 0xff00ffffu) | (kSlotMark << 16);
                 const uint32_t nch = (kHdr + (w2 & 0xffffu) + 15u) >> 4;
                 *reinterpret_cast<u32x4*>(STG(c, 0)) = u32x4{w0, id, w2, t0};
-                if (nch <= nsmall && kind != K_HOST && kind != K_BAD)
+                if (BULK && bdesc_len) {  // the announcement's payload: {len, bulk sequence}
+                    *reinterpret_cast<u32x4*>(STG(c, 1)) = u32x4{bdesc_len, bdesc_q, 0u, 0u};
+                } else if (nch <= nsmall && kind != K_HOST && kind != K_BAD) {
                     for (uint32_t q = 1; q < nch; q++)
                         *reinterpret_cast<u32x4*>(STG(c, q)) =
                             gen_chunk(P, kind, me, id, w2 & 0xffffu, src, (int)(int8_t)(w0 >> 24), q);
+                }
             }
             const int origin = (int)(w0 & 0xffffu);
             const uint32_t need = active ? need_of(kids, origin, sll, sl_r) : 0u;
@@ -1188,6 +1750,22 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         atomicAdd(&S.dec_delivered, 1ull);
                         if (vote != 0) atomicAdd(&S.dec_approved, 1ull);
                         log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+                    } else if constexpr (BULK) {
+                      if (tag == TAG_BULK) {
+                        // a bulk announcement: pending until my copy is complete; my movers push my
+                        // stripe on to the other receivers once the origin's scatter landed it
+                        const u32x4 dsc = *reinterpret_cast<const u32x4*>(STG(c, 1));
+                        const uint32_t sl = dsc.y & (bsl - 1u);
+                        const BulkPlan pl = bulk_plan(P.n, dsc.x, P.bulk_cross != 0);
+                        const uint32_t e = (uint32_t)origin * bsl + sl;
+                        // complete = every tile of the message landed here AND my own gather tiles (the
+                        // pushes of my stripe out of this copy) are done
+                        const uint32_t nt =
+                            P.n > 2 ? bulk_stripe_tiles(pl, dsc.x, (uint32_t)((me - origin - 1 + P.n) % P.n)) : 0u;
+                        bpend[e] = BulkPend{id, dsc.x, bulk_total_tiles(pl, dsc.x) + nt, from, t0, dsc.y, 0u, 0u};
+                        S.b.bact[atomicAdd(&S.b.nbact, 1u)] = e;
+                        if (nt) post_job(P, JCLS_B, JOB_GATHER, origin, lr, sl, id, dsc.x, nt, from, ~0u, dsc.y, 0u);
+                      }
                     }
                 } else if (kind == K_PROP || (kind == K_HOST && tag == TAG_PROPOSAL)) {
                     S.own_pid = (int32_t)id;
@@ -1206,6 +1784,20 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const uint32_t np = S.lat_pos + 1u;
                     S.lat_pos = np;
                     S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
+                    if constexpr (BULK) {
+                        if (tag == TAG_BULK) S.b.bulk_q++;
+                    }
+                }
+                if (BULK && kind != K_RING && tag == TAG_BULK) {  // my bulk bcast: scatter it (RLO_bcast_gen :1581)
+                    uint32_t blen = bdesc_len, bq = bdesc_q;
+                    if (kind == K_HOST) {  // the host wrote {len, q} and the bytes (heap slot (me, me, s))
+                        const u32x4 dsc = *reinterpret_cast<const u32x4*>(STG(c, 1));
+                        blen = dsc.x;
+                        bq = dsc.y;
+                    }
+                    post_job(P, JCLS_A, JOB_SCATTER, me, lr, bq & (bsl - 1u), id, blen,
+                             bulk_total_tiles(bulk_plan(P.n, blen, P.bulk_cross != 0), blen), -1, ~0u, bq,
+                             kind == K_HOST ? 1u : 0u);
                 }
             }
             if (active) {
@@ -1215,7 +1807,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             {  // wave-aggregated counters (one LDS op per wave instead of 64 same-address atomics)
                 const uint64_t bdel = __ballot(admitted && kind == K_RING && tag == TAG_BCAST);
-                const uint64_t borg = __ballot(admitted && (kind == K_STORM || kind == K_LAT || (kind == K_HOST && tag == TAG_BCAST)));
+                const uint64_t borg = __ballot(admitted && (kind == K_STORM || kind == K_LAT ||
+                                                            (kind == K_HOST && (tag == TAG_BCAST || tag == TAG_BULK))));
                 const uint64_t bbig = __ballot(isbig);
                 if (lane == 0) {
                     if (bdel) atomicAdd(&S.bcast_delivered, (unsigned long long)__popcll(bdel));
@@ -1437,6 +2030,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                                                                    (P.fwd_cap - S.ofree[lane])));
             }
             PSX(5);
+            if constexpr (BULK) {
+                if (nstorm) {  // the admitted prefix of the storm window used its bulk sequences
+                    const uint32_t fb = S.first_bad[kGroupLocal + K_STORM];
+                    uint32_t adm = fb == 0xffffffffu ? nstorm : (fb > storm_base ? fb - storm_base : 0u);
+                    if (adm > nstorm) adm = nstorm;
+                    const uint64_t bm = __ballot((uint32_t)lane < adm && S.b.bq[lane] != ~0u);
+                    if (lane == 0) S.b.bulk_q += (uint32_t)__popcll(bm);
+                }
+            }
             if (lane == 0) {
                 if (nstorm) {
                     const uint32_t fb = S.first_bad[kGroupLocal + K_STORM];
@@ -1481,7 +2083,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             done_w0 = __builtin_amdgcn_readfirstlane((int)done_w0) != 0;  // lane 0 updated these
             sched_next = (int64_t)uni64((uint64_t)sched_next);
-            idle_prev = C == 0 && S.vtot == 0 && !done_w0 && !(P.mode & MODE_NOSPIN);
+            // (BULK: no tight re-poll while receptions are pending: their flags are polled once per iteration)
+            bool bidle = true;
+            if constexpr (BULK) bidle = S.b.nbact == 0;
+            idle_prev = bidle && C == 0 && S.vtot == 0 && !done_w0 && !(P.mode & MODE_NOSPIN);
         }
         PROF_STAMP(6);
     }
@@ -1498,10 +2103,32 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 #undef PUB_VOUT
 
     // ---------------- flush statistics
+    if constexpr (BULK) {
+        if (tid == 0 && !(P.mode & MODE_PROF)) {  // diagnostics in stats.dbg: pending receptions at exit
+            const uint32_t nb = S.b.nbact;
+            S.dbg[0] = ((uint64_t)S.b.bulk_q << 32) | nb;
+            for (uint32_t i = 0; i < 3 && i < nb; i++) {
+                const uint32_t e = S.b.bact[i];
+                const uint32_t tf = bflag_ld(bulk_flags(P, me, (int)(e / bsl), e % bsl) + kBulkTflag, sys);
+                const uint32_t sf = bflag_ld(bulk_flags(P, me, (int)(e / bsl), e % bsl), sys);
+                S.dbg[1 + 2 * i] = ((uint64_t)e << 32) | bpend[e].ntiles;
+                S.dbg[2 + 2 * i] = ((uint64_t)sf << 32) | tf;
+            }
+            for (uint32_t i = 0; i < bsl && i < 1; i++) S.dbg[7] = S.b.sdone[0] | (S.b.sdone[bsl > 1 ? 1 : 0] << 32);
+        }
+    }
+    __syncthreads();
     if (w == 0) atomicAdd((unsigned long long*)&S.stalls, (unsigned long long)n_stalls);
     atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
     for (int i = tid; i < kHistBins; i += kBlock) P.stats[lr].hist[i] = S.hist[i];
     if (tid < 8) { P.stats[lr].prof[tid] = S.prof[tid]; P.stats[lr].dbg[tid] = S.dbg[tid]; }
+    if constexpr (BULK) {
+        if (tid == 0) {  // after every job this workgroup posted: the movers may stop once all did
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicAdd((unsigned long long*)&P.jctl[kJctlExited], 1ull);
+        }
+    }
     if (tid == 0) {
         RankStats& st = P.stats[lr];
         st.bcast_delivered = S.bcast_delivered;
@@ -1527,12 +2154,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
 }  // namespace rlo
 
-// C-ABI launch shims used by rlo_world.cpp; waves = 4 or 8 (the Shared / LDS layout depends on it)
-template <int W>
+// C-ABI launch shims used by rlo_world.cpp.  variant: 8 = 8 waves, 4 = 4 waves, 5 = 4 waves with
+// bulk messages (mover workgroups + mixed storm lengths); the Shared / LDS layout depends on it
+template <int W, bool B>
 static hipError_t grant_dyn_lds(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {  // > 64 KiB of dynamic LDS must be requested explicitly
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W>,
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
@@ -1540,25 +2168,35 @@ static hipError_t grant_dyn_lds(size_t dyn_lds) {
     return hipSuccess;
 }
 
-extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int waves) {
-    hipError_t e = waves == 8 ? grant_dyn_lds<8>(dyn_lds) : grant_dyn_lds<4>(dyn_lds);
+template <int W, bool B>
+static hipError_t launch_v(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
+    hipError_t e = grant_dyn_lds<W, B>(dyn_lds);
     if (e != hipSuccess) return e;
-    if (waves == 8) hipLaunchKernelGGL(rlo::rlo_progress_kernel<8>, dim3(blocks), dim3(512), dyn_lds, stream, *p);
-    else hipLaunchKernelGGL(rlo::rlo_progress_kernel<4>, dim3(blocks), dim3(256), dyn_lds, stream, *p);
+    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
     return hipGetLastError();
 }
 
-extern "C" size_t rlo_kernel_static_lds(int waves) {
-    return waves == 8 ? sizeof(rlo::Shared<8>) : sizeof(rlo::Shared<4>);
+template <int W, bool B>
+static hipError_t occ_v(int* blocks, size_t dyn_lds) {
+    hipError_t e = grant_dyn_lds<W, B>(dyn_lds);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B>, 64 * W, dyn_lds);
 }
 
-extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int waves) {
-    if (waves == 8) {
-        hipError_t e = grant_dyn_lds<8>(dyn_lds);
-        if (e != hipSuccess) return e;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<8>, 512, dyn_lds);
-    }
-    hipError_t e = grant_dyn_lds<4>(dyn_lds);
-    if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<4>, 256, dyn_lds);
+extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
+    if (variant == 8) return launch_v<8, false>(p, blocks, dyn_lds, stream);
+    if (variant == 5) return launch_v<4, true>(p, blocks, dyn_lds, stream);
+    return launch_v<4, false>(p, blocks, dyn_lds, stream);
+}
+
+extern "C" size_t rlo_kernel_static_lds(int variant) {
+    if (variant == 8) return sizeof(rlo::Shared<8, false>);
+    if (variant == 5) return sizeof(rlo::Shared<4, true>);
+    return sizeof(rlo::Shared<4, false>);
+}
+
+extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant) {
+    if (variant == 8) return occ_v<8, false>(blocks, dyn_lds);
+    if (variant == 5) return occ_v<4, true>(blocks, dyn_lds);
+    return occ_v<4, false>(blocks, dyn_lds);
 }

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -17,10 +18,10 @@
 #include "rlo_device.hpp"
 #include "rlo_hip.h"
 
-extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int waves);
-extern "C" size_t rlo_kernel_static_lds(int waves);
-extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int waves);
-extern "C" hipError_t rlo_launch_bulk(const rlo::BulkParams* p, int blocks, int local_ranks, hipStream_t stream);
+// variant: 8 = 8-wave, 4 = 4-wave, 5 = 4-wave with bulk messages (rlo_kernel.hip)
+extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant);
+extern "C" size_t rlo_kernel_static_lds(int variant);
+extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant);
 
 static_assert(sizeof(rlo_rank_stats_t) == sizeof(rlo::RankStats), "stats ABI");
 static_assert(sizeof(rlo_log_rec_t) == sizeof(rlo::LogRec), "log ABI");
@@ -143,9 +144,15 @@ struct Layout {
     std::vector<uint64_t> fwd_off, vote_off;                  // per edge (vc 0 ring; vc 1 follows)
     std::vector<uint32_t> inbox, outbox;                      // per rank: word index in its part's ctrl
     std::vector<uint64_t> lat_base;                           // per part: the shared latency block (rlo_device.hpp)
+    // bulk messages (rlo_device.hpp): heap slot (r, o, s) and flag line (r, o, s) in r's part, then
+    // the done lines (o, s) of the part's origins
+    uint64_t bulk_max = 0;
+    uint32_t bslots = 0, bcap = 0;
+    std::vector<uint64_t> heap_bytes, bflag_bytes;            // per part
 };
 
-int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uint32_t ring_slots, Layout& L) {
+int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uint32_t ring_slots, uint64_t bulk_max,
+                 uint32_t bulk_slots, Layout& L) {
     if (n < 2 || n > 65535 || nparts < 1 || nparts > rlo::kMaxParts) return RLO_E_INVAL;
     L.n = n;
     L.nparts = nparts;
@@ -228,6 +235,20 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         words += rlo::kLatWords;
         L.ctrl_words[p] = words;
     }
+    L.heap_bytes.assign(nparts, 0);
+    L.bflag_bytes.assign(nparts, 0);
+    if (bulk_max) {
+        L.bslots = bulk_slots ? bulk_slots : 2u;
+        if ((L.bslots & (L.bslots - 1)) || L.bslots > 8 || (uint64_t)n * L.bslots > (uint64_t)rlo::kMaxPend) return RLO_E_INVAL;
+        if (bulk_max > 0xFFF00000ull) return RLO_E_INVAL;  // a slot is addressed by one buffer resource
+        L.bulk_max = bulk_max;
+        L.bcap = (uint32_t)((bulk_max + 65535u) & ~65535ull);
+        for (int p = 0; p < nparts; p++) {
+            const uint64_t nlp = (uint64_t)(L.pb[p + 1] - L.pb[p]);
+            L.heap_bytes[p] = nlp * (uint64_t)n * L.bslots * L.bcap;
+            L.bflag_bytes[p] = (nlp * (uint64_t)n * L.bslots + nlp * L.bslots) * rlo::kBulkLine;
+        }
+    }
     return RLO_OK;
 }
 
@@ -241,6 +262,8 @@ struct PartBlob {
     uint64_t fwd_bytes, vote_bytes, ctrl_bytes;
     char bus[32];
     hipIpcMemHandle_t hf, hv, hc;
+    uint64_t heap_ptr, bflag_ptr, heap_bytes, bflag_bytes;
+    hipIpcMemHandle_t hh, hb;
 };
 static_assert(sizeof(PartBlob) <= RLO_PART_BLOB_BYTES, "blob");
 constexpr uint32_t kBlobMagic = 0x524C4F50u;  // "RLOP"
@@ -300,7 +323,20 @@ struct rlo_world {
     float last_ms = 0.f;
     size_t dyn_lds = 0;
     uint32_t nsmall = 8, stage2 = 1024;
-    int waves = 4;  // rank-workgroup width: 8 (512 candidates per iteration) when each rank has a CU
+    int waves = 4;    // rank-workgroup width: 8 (512 candidates per iteration) when each rank has a CU
+    int variant = 4;  // kernel instantiation: 8 / 4 waves, 5 = 4 waves with bulk messages
+    // bulk messages (rlo_device.hpp): this part's heap, flag region and job rings (all uncached),
+    // every part's heap / flag region as mapped here, and the device tables the kernel indexes
+    uint8_t* heap = nullptr;
+    uint8_t* bflag = nullptr;
+    uint8_t* jmem = nullptr;
+    uint64_t jmem_bytes = 0;
+    uint32_t nmov = 0, jslots = 0, bpend_off = 0;
+    std::vector<uint8_t*> ph, pbf;
+    DevBuf<uint64_t> d_bheap, d_bflag;
+    DevBuf<int32_t> d_part_of, d_part_begin;
+    std::vector<uint64_t> jfree_init;      // [2][jslots] iota: slot i takes job i first
+    std::vector<uint32_t> host_bulk_q;     // host mode: next bulk sequence of each local rank
 };
 
 namespace {
@@ -314,36 +350,58 @@ int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
     return RLO_OK;
 }
 
-// co-residency of the part's rank-workgroups: largest small-path stage (nsmall chunks per
-// message, <= 8) and then the largest stage2 (<= 64 KiB) at which the occupancy calculator
-// (LDS allocation granularity, registers, waves) still co-schedules them
-int size_lds_waves(rlo_world* w, int waves) {
+// job-ring memory of a part (uncached, part-local): [jobs 2J x 64 B][jctl][jclaim 2J][jfree 2J][jdone 2J][jsum 2J]
+struct JobMem {
+    uint64_t jobs, jctl, jclaim, jfree, jdone, jsum, bytes;
+};
+JobMem job_mem(uint32_t J) {
+    JobMem m;
+    m.jobs = 0;
+    m.jctl = m.jobs + 2ull * J * sizeof(rlo::BulkJob);
+    m.jclaim = m.jctl + (uint64_t)rlo::kJctlWords * 8;
+    m.jfree = m.jclaim + 2ull * J * 8;
+    m.jdone = m.jfree + 2ull * J * 8;
+    m.jsum = (m.jdone + 2ull * J * 4 + 127) & ~127ull;
+    m.bytes = m.jsum + 2ull * J * 8;
+    return m;
+}
+
+// co-residency of the part's workgroups (rank-workgroups, plus the mover workgroups of a bulk
+// world): largest small-path stage (nsmall chunks per message, <= 8) and then the largest stage2
+// (<= 64 KiB) at which the occupancy calculator (LDS allocation granularity, registers, waves)
+// still co-schedules them
+int size_lds_variant(rlo_world* w, int variant) {
     const Layout& L = w->L;
+    const int waves = variant == 8 ? 8 : 4;
     const size_t lds_cu = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
-    const int need_bpc = (w->nl + w->cus - 1) / w->cus;
+    const int nblk = w->nl + (variant == 5 ? (int)w->nmov : 0);
+    const int need_bpc = (nblk + w->cus - 1) / w->cus;
     const size_t per_block = lds_cu / need_bpc;
-    const size_t cand = (size_t)64 * waves, stat = rlo_kernel_static_lds(waves);
+    const size_t cand = (size_t)64 * waves, stat = rlo_kernel_static_lds(variant);
+    const size_t bpend = variant == 5 ? (size_t)L.n * L.bslots * 32 : 0;  // pending bulk receptions
     int api = 0;
     bool ok = false;
     for (uint32_t ns = std::min<uint32_t>(8u, L.stride / 16u); ns >= 1 && !ok; ns--) {
-        // [pending proposals 2N x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2]
-        const size_t fixed = stat + (size_t)32 * L.n + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16;
+        // [pending proposals 2N x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
+        const size_t fixed = stat + (size_t)32 * L.n + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
         if (per_block < fixed + 1024 + 512) continue;
         size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
         for (;;) {
             w->dyn_lds = fixed - stat + s2;
-            if (rlo_occupancy(&api, w->dyn_lds, waves) != hipSuccess) api = 0;
+            if (rlo_occupancy(&api, w->dyn_lds, variant) != hipSuccess) api = 0;
             if (api >= need_bpc) { ok = true; break; }
             if (s2 <= 1024) break;
             s2 -= 1024;
         }
         w->nsmall = ns;
         w->stage2 = (uint32_t)s2;
+        w->bpend_off = (uint32_t)(fixed - stat - bpend + s2);
     }
     if (!ok) return RLO_E_OCCUPANCY;
     w->waves = waves;
+    w->variant = variant;
     w->blocks_per_cu = std::max(1, api);
-    if (w->nl > w->blocks_per_cu * w->cus) return RLO_E_OCCUPANCY;
+    if (nblk > w->blocks_per_cu * w->cus) return RLO_E_OCCUPANCY;
     return RLO_OK;
 }
 
@@ -352,12 +410,13 @@ int size_lds_waves(rlo_world* w, int waves) {
 // fits; else 4 waves (larger slots need the LDS for the large-message stage: 64 B storm 12.1 -> 16.0 M
 // bcast/s with 8 waves, but 256 B .. 4 KiB 30-40 % slower).  RLO_WAVES=4 / 8 forces one (A/B)
 int size_lds(rlo_world* w) {
+    if (w->L.bulk_max) return size_lds_variant(w, 5);  // bulk worlds: the 4-wave kernel with movers
     const char* env = std::getenv("RLO_WAVES");
     const int force = env ? std::atoi(env) : 0;
     const bool small = w->L.stride <= 8u * 16u;
-    if (force != 4 && (small || force == 8) && w->nl <= w->cus && size_lds_waves(w, 8) == RLO_OK) return RLO_OK;
+    if (force != 4 && (small || force == 8) && w->nl <= w->cus && size_lds_variant(w, 8) == RLO_OK) return RLO_OK;
     if (force == 8) return RLO_E_OCCUPANCY;
-    return size_lds_waves(w, 4);
+    return size_lds_variant(w, 4);
 }
 
 // RankTopo of every local rank, with remote ends resolved to addresses in this process
@@ -469,7 +528,8 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     // not invalidated by another XCD's write-through stores, and a consumer on that XCD read the
     // zeros (seen as unmarked slot headers that never became visible).  RLO_CACHED_RINGS=1: A/B only
     if (!std::getenv("RLO_CACHED_RINGS")) w->flags |= RLO_PART_UNCACHED;
-    int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, w->L);
+    int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, cfg->bulk_max,
+                          cfg->bulk_slots, w->L);
     if (rc) { delete w; return rc; }
     w->part = cfg->part;
     w->rb = w->L.pb[w->part];
@@ -479,6 +539,15 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, w->device) != hipSuccess) { delete w; return RLO_E_HIP; }
     w->cus = prop.multiProcessorCount;
+    if (w->L.bulk_max) {
+        // movers: half scatter / verify (never wait), half gather (wait only for scatters).  Auto:
+        // 4 per local rank (>= 16), within the CUs the rank-workgroups leave (one workgroup per CU)
+        int mv = (int)cfg->movers;
+        if (mv == 0) mv = std::min(std::max(16, 4 * w->nl), w->cus - w->nl) & ~1;
+        if (mv < 2) { delete w; return RLO_E_OCCUPANCY; }
+        w->nmov = (uint32_t)mv;
+        w->jslots = pow2_ceil((uint32_t)w->nl * (uint32_t)(w->L.n + 1) * w->L.bslots + 64u);
+    }
     rc = size_lds(w);
     if (rc) { delete w; return rc; }
     const int me = w->part;
@@ -486,6 +555,20 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         alloc_region(w, (void**)&w->ctrl, w->L.ctrl_words[me] * 8)) {
         rlo_world_destroy(w);
         return RLO_E_HIP;
+    }
+    if (w->L.bulk_max) {  // heap, flags and job rings: uncached (peers and other XCDs write them)
+        w->jmem_bytes = job_mem(w->jslots).bytes;
+        const uint32_t keep = w->flags;
+        w->flags |= RLO_PART_UNCACHED;
+        const int e = alloc_region(w, (void**)&w->heap, w->L.heap_bytes[me]) ||
+                      alloc_region(w, (void**)&w->bflag, w->L.bflag_bytes[me]) || alloc_region(w, (void**)&w->jmem, w->jmem_bytes);
+        w->flags = keep;
+        if (e) { rlo_world_destroy(w); return RLO_E_HIP; }
+        (void)hipMemset(w->bflag, 0, w->L.bflag_bytes[me]);
+        w->jfree_init.resize(2ull * w->jslots);
+        for (uint32_t c = 0; c < 2; c++)
+            for (uint32_t i = 0; i < w->jslots; i++) w->jfree_init[(size_t)c * w->jslots + i] = i;
+        w->host_bulk_q.assign(w->nl, 0);
     }
     (void)hipMemset(w->fwd, 0, std::max<uint64_t>(w->L.fwd_bytes[me], 1));
     (void)hipMemset(w->vote, 0, std::max<uint64_t>(w->L.vote_bytes[me], 1));
@@ -524,6 +607,14 @@ int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap) {
     HIPCHK(hipIpcGetMemHandle(&b.hf, w->fwd));
     HIPCHK(hipIpcGetMemHandle(&b.hv, w->vote));
     HIPCHK(hipIpcGetMemHandle(&b.hc, w->ctrl));
+    if (w->L.bulk_max) {
+        b.heap_ptr = (uint64_t)(uintptr_t)w->heap;
+        b.bflag_ptr = (uint64_t)(uintptr_t)w->bflag;
+        b.heap_bytes = w->L.heap_bytes[w->part];
+        b.bflag_bytes = w->L.bflag_bytes[w->part];
+        HIPCHK(hipIpcGetMemHandle(&b.hh, w->heap));
+        HIPCHK(hipIpcGetMemHandle(&b.hb, w->bflag));
+    }
     std::memset(blob, 0, RLO_PART_BLOB_BYTES);
     std::memcpy(blob, &b, sizeof b);
     return (int)RLO_PART_BLOB_BYTES;
@@ -536,6 +627,8 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
     w->pf.assign(n_parts, nullptr);
     w->pv.assign(n_parts, nullptr);
     w->pc.assign(n_parts, nullptr);
+    w->ph.assign(n_parts, nullptr);
+    w->pbf.assign(n_parts, nullptr);
     char mybus[32] = {0};
     HIPCHK(hipDeviceGetPCIBusId(mybus, sizeof mybus, w->device));
     const uint64_t tok = process_token();
@@ -545,11 +638,13 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
         std::memcpy(&b, (const uint8_t*)blobs + (size_t)q * RLO_PART_BLOB_BYTES, sizeof b);
         if (b.magic != kBlobMagic || b.part != q || b.nparts != n_parts || b.n != L.n || b.cap != L.cap ||
             b.stride != L.stride || b.vote_cap != L.vote_cap || b.fwd_bytes != L.fwd_bytes[q] ||
-            b.vote_bytes != L.vote_bytes[q] || b.ctrl_bytes != L.ctrl_words[q] * 8)
+            b.vote_bytes != L.vote_bytes[q] || b.ctrl_bytes != L.ctrl_words[q] * 8 || b.heap_bytes != L.heap_bytes[q] ||
+            b.bflag_bytes != L.bflag_bytes[q])
             return RLO_E_INVAL;
         if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->sys_scope = 1;
         if (q == w->part) {
             w->pf[q] = w->fwd; w->pv[q] = w->vote; w->pc[q] = w->ctrl;
+            w->ph[q] = w->heap; w->pbf[q] = w->bflag;
         } else if (b.token == tok) {  // same process: the addresses are usable as they are
             if (b.device != w->device) {
                 hipError_t e = hipDeviceEnablePeerAccess(b.device, 0);
@@ -559,6 +654,8 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
             w->pf[q] = (uint8_t*)(uintptr_t)b.fwd_ptr;
             w->pv[q] = (uint8_t*)(uintptr_t)b.vote_ptr;
             w->pc[q] = (uint64_t*)(uintptr_t)b.ctrl_ptr;
+            w->ph[q] = (uint8_t*)(uintptr_t)b.heap_ptr;
+            w->pbf[q] = (uint8_t*)(uintptr_t)b.bflag_ptr;
         } else {  // another process: map its regions (dmabuf IPC; xGMI when on another GPU)
             void* p = nullptr;
             HIPCHK(hipIpcOpenMemHandle(&p, b.hf, hipIpcMemLazyEnablePeerAccess));
@@ -570,10 +667,28 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
             HIPCHK(hipIpcOpenMemHandle(&p, b.hc, hipIpcMemLazyEnablePeerAccess));
             w->opened.push_back(p);
             w->pc[q] = (uint64_t*)p;
+            if (L.bulk_max) {
+                HIPCHK(hipIpcOpenMemHandle(&p, b.hh, hipIpcMemLazyEnablePeerAccess));
+                w->opened.push_back(p);
+                w->ph[q] = (uint8_t*)p;
+                HIPCHK(hipIpcOpenMemHandle(&p, b.hb, hipIpcMemLazyEnablePeerAccess));
+                w->opened.push_back(p);
+                w->pbf[q] = (uint8_t*)p;
+            }
         }
     }
     build_topo(w);
     if (w->d_topo.upload(w->topo)) return RLO_E_HIP;
+    if (L.bulk_max) {  // the tables the movers and progress workgroups address the heaps with
+        std::vector<uint64_t> hb(n_parts), fb(n_parts);
+        for (int q = 0; q < n_parts; q++) {
+            hb[q] = (uint64_t)(uintptr_t)w->ph[q];
+            fb[q] = (uint64_t)(uintptr_t)w->pbf[q];
+        }
+        std::vector<int32_t> po(L.part_of.begin(), L.part_of.end()), pbv(L.pb.begin(), L.pb.end());
+        if (w->d_bheap.upload(hb) || w->d_bflag.upload(fb) || w->d_part_of.upload(po) || w->d_part_begin.upload(pbv))
+            return RLO_E_HIP;
+    }
     w->connected = true;
     return RLO_OK;
 }
@@ -588,6 +703,9 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
     pc.max_payload = cfg->max_payload;
     pc.ring_slots = cfg->ring_slots;
     pc.device = cfg->device;
+    pc.bulk_max = cfg->bulk_max;
+    pc.bulk_slots = cfg->bulk_slots;
+    pc.movers = cfg->movers;
     rlo_world* w = nullptr;
     int rc = rlo_part_create(&pc, &w);
     if (rc) return rc;
@@ -606,6 +724,10 @@ int rlo_world_destroy(rlo_world_t* w) {
     if (w->fwd) (void)hipFree(w->fwd);
     if (w->vote) (void)hipFree(w->vote);
     if (w->ctrl) (void)hipFree(w->ctrl);
+    if (w->heap) (void)hipFree(w->heap);
+    if (w->bflag) (void)hipFree(w->bflag);
+    if (w->jmem) (void)hipFree(w->jmem);
+    w->d_bheap.release(); w->d_bflag.release(); w->d_part_of.release(); w->d_part_begin.release();
     w->d_topo.release(); w->d_stats.release();
     w->d_sched_off.release(); w->d_expect_bcast.release(); w->d_prop_off.release(); w->d_expect_dec.release();
     w->d_sched_ids.release(); w->d_prop_data_off.release(); w->d_prop_data_len.release(); w->d_isp_off.release();
@@ -644,6 +766,10 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->rank_end = w->rb + w->nl;
     o->sys_scope = w->sys_scope;
     o->waves = w->waves;
+    o->bulk_slots = w->L.bslots;
+    o->movers = w->nmov;
+    o->bulk_max = w->L.bulk_max;
+    o->heap_bytes = w->L.heap_bytes[w->part];
     return RLO_OK;
 }
 
@@ -673,6 +799,27 @@ static void base_params(rlo_world* w) {
     P.timeout_ticks = 100000000ull * 10;   // 10 s without progress on a rank
     P.deadline_ticks = 100000000ull * 120; // 120 s per launch
     P.window = 32;
+    P.n_local = (uint32_t)w->nl;
+    P.ring_cap = w->L.stride - rlo::kHdr;
+    if (w->L.bulk_max) {
+        const JobMem m = job_mem(w->jslots);
+        P.bulk_slots = w->L.bslots;
+        P.bulk_cap = w->L.bcap;
+        P.nmov = w->nmov;
+        P.bulk_cross = (uint32_t)w->sys_scope;
+        P.bheap = w->d_bheap.p;
+        P.bflag = w->d_bflag.p;
+        P.part_of = w->d_part_of.p;
+        P.part_begin = w->d_part_begin.p;
+        P.jslots = w->jslots;
+        P.bpend_off = w->bpend_off;
+        P.jobs = reinterpret_cast<rlo::BulkJob*>(w->jmem + m.jobs);
+        P.jctl = reinterpret_cast<uint64_t*>(w->jmem + m.jctl);
+        P.jclaim = reinterpret_cast<uint64_t*>(w->jmem + m.jclaim);
+        P.jfree = reinterpret_cast<uint64_t*>(w->jmem + m.jfree);
+        P.jdone = reinterpret_cast<uint32_t*>(w->jmem + m.jdone);
+        P.jsum = reinterpret_cast<uint64_t*>(w->jmem + m.jsum);
+    }
 }
 
 static int setup_log(rlo_world* w, uint32_t flags, uint32_t log_cap, bool payload) {
@@ -692,7 +839,11 @@ static int setup_log(rlo_world* w, uint32_t flags, uint32_t log_cap, bool payloa
 }
 
 int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
-    if (!w || !cfg || cfg->k < 0 || cfg->len > w->max_payload || cfg->k > 0xFFFFFFFFll) return RLO_E_INVAL;
+    if (!w || !cfg || cfg->k < 0 || cfg->k > 0xFFFFFFFFll || cfg->order > RLO_ORDER_SLOTS) return RLO_E_INVAL;
+    const uint32_t hi = std::max(cfg->len, cfg->len_max);
+    // longer than a slot: a bulk message (bulk worlds only); mixed lengths: the bulk kernel only
+    if (hi > (w->L.bulk_max ? w->L.bulk_max : w->max_payload)) return RLO_E_INVAL;
+    if (cfg->len_max > cfg->len && !w->L.bulk_max) return RLO_E_INVAL;
     if (!w->connected) return RLO_E_NOTCONNECTED;
     base_params(w);
     rlo::Params& P = w->P;
@@ -701,7 +852,8 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
     std::vector<int64_t> off(nl + 1, 0), expect(nl, 0), per(n, 0);
     std::vector<uint32_t> org((size_t)std::max<int64_t>(cfg->k, 1));
     for (int64_t b = 0; b < cfg->k; b++) {
-        org[b] = (uint32_t)(splitmix64(cfg->seed + (uint64_t)b) % (uint64_t)n);
+        org[b] = cfg->order == RLO_ORDER_SLOTS ? (uint32_t)(b % n)
+                                               : (uint32_t)(splitmix64(cfg->seed + (uint64_t)b) % (uint64_t)n);
         per[org[b]]++;
         if ((int)org[b] >= rb && (int)org[b] < rb + nl) off[org[b] - rb + 1]++;
     }
@@ -716,6 +868,8 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
              ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
     P.seed = cfg->seed;
     P.len = cfg->len;
+    P.len_lo = cfg->len;
+    P.len_hi = hi;
     P.window = std::min<uint32_t>(cfg->window ? cfg->window : 64, 64u);  // one wave prefetches the ids
     P.sched_off = w->d_sched_off.p;
     P.sched_ids = w->d_sched_ids.p;
@@ -727,7 +881,7 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
 }
 
 int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags) {
-    if (!w || rounds == 0 || len > w->max_payload) return RLO_E_INVAL;
+    if (!w || rounds == 0 || len > (w->L.bulk_max ? w->L.bulk_max : w->max_payload)) return RLO_E_INVAL;
     if (!w->connected) return RLO_E_NOTCONNECTED;
     // sharded: the round word and counts are part 0's copy, peer-mapped (rlo_device.hpp kLatWords)
     if (w->L.nparts != 1 && rounds > (uint32_t)rlo::kLatCap) return RLO_E_INVAL;
@@ -994,6 +1148,13 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     // (rlo_device.hpp) and is reloaded, in every launch, not only in a fresh world
     HIPCHK(hipMemsetAsync(w->fwd, 0, w->L.fwd_bytes[w->part], s));
     HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->nl, s));
+    if (w->L.bulk_max) {  // bulk flags / release counts, job rings (slot i takes job i first)
+        const JobMem m = job_mem(w->jslots);
+        HIPCHK(hipMemsetAsync(w->bflag, 0, w->L.bflag_bytes[w->part], s));
+        HIPCHK(hipMemsetAsync(w->jmem, 0, w->jmem_bytes, s));
+        HIPCHK(hipMemcpyAsync(w->jmem + m.jfree, w->jfree_init.data(), w->jfree_init.size() * 8, hipMemcpyHostToDevice, s));
+        std::fill(w->host_bulk_q.begin(), w->host_bulk_q.end(), 0u);
+    }
     if (w->have_program && (w->P.mode & rlo::MODE_LAT)) {
         HIPCHK(hipMemsetAsync(w->d_lat_count.p, 0, sizeof(uint32_t) * w->lat_rounds, s));
         HIPCHK(hipMemsetAsync(w->d_lat_out.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
@@ -1027,7 +1188,7 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool noacq = std::getenv("RLO_NO_ACQUIRE") != nullptr;  // diagnostic A/B, unsafe
     if (noacq) w->P.mode |= rlo::MODE_NOACQ;
     else w->P.mode &= ~rlo::MODE_NOACQ;
-    hipError_t e = rlo_launch_progress(&w->P, w->nl, w->dyn_lds, s, w->waves);
+    hipError_t e = rlo_launch_progress(&w->P, w->nl + (w->L.bulk_max ? (int)w->nmov : 0), w->dyn_lds, s, w->variant);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));
     return RLO_OK;
@@ -1058,6 +1219,25 @@ int rlo_wait(rlo_world_t* w) {
     uint32_t err = 0;
     HIPCHK(hipMemcpy(&err, w->ctrl, sizeof err, hipMemcpyDeviceToHost));
     return err ? RLO_E_DEVICE : RLO_OK;
+}
+
+int rlo_bulk_debug(rlo_world_t* w, uint64_t* out, uint32_t cap) {
+    if (!w || !out || !w->jmem) return RLO_E_INVAL;
+    const JobMem m = job_mem(w->jslots);
+    const uint32_t n = std::min<uint32_t>(cap, rlo::kJctlWords);
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipMemcpy(out, w->jmem + m.jctl, n * 8, hipMemcpyDeviceToHost));
+    return (int)n;
+}
+
+int rlo_device_error(rlo_world_t* w, uint32_t* code, uint32_t* aux) {
+    if (!w) return RLO_E_INVAL;
+    uint32_t v[2] = {0, 0};
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipMemcpy(v, w->ctrl, sizeof v, hipMemcpyDeviceToHost));
+    if (code) *code = v[0];
+    if (aux) *aux = v[1];
+    return RLO_OK;
 }
 
 int rlo_run(rlo_world_t* w, void* stream, float* ms) {
@@ -1120,221 +1300,52 @@ int rlo_round_ticks(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
 
 }  // extern "C"
 
-// ====================================================================== bulk bcast
-
-namespace {
-struct BulkBlob {
-    uint32_t magic, part;
-    int32_t device, pci;  // pci: PCI domain/bus/device of the part's GPU (auto chunking)
-    uint64_t token, ptr, bytes, stride;
-    hipIpcMemHandle_t h;
-};
-static_assert(sizeof(BulkBlob) <= RLO_BULK_BLOB_BYTES, "bulk blob");
-constexpr uint32_t kBulkMagic = 0x524C4F42u;  // "RLOB"
-// per rank: [buffer buf_bytes][scatter flags][gather flags]
-constexpr uint64_t kBulkFlagBytes = 2ull * rlo::kBulkMaxChunks * 4ull;
-}  // namespace
-
-struct rlo_bulk {
-    rlo_world* w = nullptr;
-    uint64_t buf_bytes = 0, stride = 0;
-    uint8_t* region = nullptr;              // this part's ranks
-    std::vector<uint8_t*> base;             // every part's region, mapped here
-    std::vector<void*> opened;
-    uint32_t* err = nullptr;
-    rlo::BulkParams P{};
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool connected = false;
-    bool cross_gpu = false;  // some part sits on another GPU: links, not HBM, bound the copy
-};
-
-namespace {
-int32_t pci_of(int device) {
-    hipDeviceProp_t p;
-    if (hipGetDeviceProperties(&p, device) != hipSuccess) return -1;
-    return (p.pciDomainID << 16) | (p.pciBusID << 8) | p.pciDeviceID;
-}
-}  // namespace
+// ====================================================================== bulk messages, host side
 
 extern "C" {
 
-int rlo_bulk_create(rlo_world_t* w, uint64_t buf_bytes, rlo_bulk_t** out) {
-    if (!w || !out || buf_bytes == 0 || w->L.n > rlo::kMaxBulkRanks) return RLO_E_INVAL;
-    buf_bytes = (buf_bytes + rlo::kBulkBlock - 1) / rlo::kBulkBlock * rlo::kBulkBlock;
-    if (buf_bytes > 0xFFFF0000ull) return RLO_E_INVAL;  // one buffer resource per rank
+int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out) {
+    if (n < 2 || !out || len == 0 || len > 0xFFF00000ull) return RLO_E_INVAL;
+    const rlo::BulkPlan p = rlo::bulk_plan(n, (uint32_t)len, cross != 0);
+    out->nchunks = p.nchunks;
+    out->stripe = p.stripe;
+    out->chunk = p.chunk;
+    out->tile = p.tile;
+    out->total_tiles = rlo::bulk_total_tiles(p, (uint32_t)len);
+    out->pad = 0;
+    return RLO_OK;
+}
+
+int rlo_host_bulk_stage(rlo_world_t* w, int rank, const void* data, uint64_t len, uint32_t timeout_us, uint32_t* q_out) {
+    if (!w || !w->h_cmd || !w->L.bulk_max || rank < w->rb || rank >= w->rb + w->nl || !q_out) return RLO_E_INVAL;
+    if (len == 0 || len > w->L.bulk_max || (len && !data)) return RLO_E_INVAL;
+    const int lr = rank - w->rb;
+    const uint32_t B = w->L.bslots, q = w->host_bulk_q[lr], s = q & (B - 1u);
+    const uint64_t need = (uint64_t)(q / B) * (uint64_t)(w->L.n - 1);
+    // done(rank, s): every receiver released the slot's previous message (read through the BAR)
+    const volatile uint64_t* done = reinterpret_cast<const volatile uint64_t*>(
+        w->bflag + ((uint64_t)w->nl * w->L.n * B + (uint64_t)lr * B + s) * rlo::kBulkLine);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*done < need) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(timeout_us)) return RLO_E_AGAIN;
+    }
     HIPCHK(hipSetDevice(w->device));
-    rlo_bulk* b = new rlo_bulk();
-    b->w = w;
-    b->buf_bytes = buf_bytes;
-    b->stride = buf_bytes + kBulkFlagBytes;
-    // uncached: peers on other GPUs store into it over xGMI; receivers read it after a flag
-    hipError_t e = hipExtMallocWithFlags((void**)&b->region, b->stride * w->nl, hipDeviceMallocUncached);
-    if (e == hipSuccess) e = hipExtMallocWithFlags((void**)&b->err, 256, hipDeviceMallocUncached);
-    if (e != hipSuccess) { g_last_hip = (int)e; rlo_bulk_destroy(b); return RLO_E_HIP; }
-    (void)hipMemset(b->region, 0, b->stride * w->nl);
-    (void)hipMemset(b->err, 0, 256);
-    (void)hipStreamSynchronize(nullptr);
-    (void)hipEventCreate(&b->ev0);
-    (void)hipEventCreate(&b->ev1);
-    *out = b;
+    uint8_t* dst = w->heap + (((uint64_t)lr * w->L.n + (uint64_t)rank) * B + s) * w->L.bcap;
+    HIPCHK(hipMemcpy(dst, data, len, hipMemcpyHostToDevice));
+    w->host_bulk_q[lr] = q + 1;
+    *q_out = q;
     return RLO_OK;
 }
 
-int rlo_bulk_export(rlo_bulk_t* b, void* blob, uint32_t cap) {
-    if (!b || !blob || cap < RLO_BULK_BLOB_BYTES) return RLO_E_INVAL;
-    BulkBlob x;
-    std::memset(&x, 0, sizeof x);
-    x.magic = kBulkMagic;
-    x.part = (uint32_t)b->w->part;
-    x.device = b->w->device;
-    x.pci = pci_of(b->w->device);
-    x.token = process_token();
-    x.ptr = (uint64_t)(uintptr_t)b->region;
-    x.bytes = b->buf_bytes;
-    x.stride = b->stride;
-    HIPCHK(hipIpcGetMemHandle(&x.h, b->region));
-    std::memset(blob, 0, RLO_BULK_BLOB_BYTES);
-    std::memcpy(blob, &x, sizeof x);
-    return (int)RLO_BULK_BLOB_BYTES;
-}
-
-int rlo_bulk_connect(rlo_bulk_t* b, const void* blobs, int n_parts) {
-    if (!b || !blobs || n_parts != b->w->L.nparts || b->connected) return RLO_E_INVAL;
-    rlo_world* w = b->w;
+int rlo_host_bulk_copy(rlo_world_t* w, int rank, const rlo_log_rec_t* ev, void* dst) {
+    if (!w || !ev || !w->L.bulk_max || rank < w->rb || rank >= w->rb + w->nl || !dst) return RLO_E_INVAL;
+    if (ev->kind != RLO_EV_DELIVER_BULK || ev->origin < 0 || ev->origin >= w->L.n || ev->aux >= w->L.bslots ||
+        ev->len > w->L.bulk_max)
+        return RLO_E_INVAL;
+    const int lr = rank - w->rb;
     HIPCHK(hipSetDevice(w->device));
-    b->base.assign(n_parts, nullptr);
-    const uint64_t tok = process_token();
-    for (int q = 0; q < n_parts; q++) {
-        BulkBlob x;
-        std::memcpy(&x, (const uint8_t*)blobs + (size_t)q * RLO_BULK_BLOB_BYTES, sizeof x);
-        if (x.magic != kBulkMagic || (int)x.part != q || x.bytes != b->buf_bytes || x.stride != b->stride)
-            return RLO_E_INVAL;
-        int32_t pci0;
-        std::memcpy(&pci0, (const uint8_t*)blobs + offsetof(BulkBlob, pci), sizeof pci0);
-        if (x.pci != pci0 || x.pci < 0) b->cross_gpu = true;  // the same answer on every part
-        if (q == w->part) {
-            b->base[q] = b->region;
-        } else if (x.token == tok) {
-            if (x.device != w->device) {
-                hipError_t e = hipDeviceEnablePeerAccess(x.device, 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { g_last_hip = (int)e; return RLO_E_HIP; }
-                (void)hipGetLastError();
-            }
-            b->base[q] = (uint8_t*)(uintptr_t)x.ptr;
-        } else {
-            void* p = nullptr;
-            HIPCHK(hipIpcOpenMemHandle(&p, x.h, hipIpcMemLazyEnablePeerAccess));
-            b->opened.push_back(p);
-            b->base[q] = (uint8_t*)p;
-        }
-    }
-    rlo::BulkParams& P = b->P;
-    std::memset(&P, 0, sizeof P);
-    P.n = w->L.n;
-    P.rank_begin = w->rb;
-    P.buf_bytes = (uint32_t)b->buf_bytes;
-    for (int r = 0; r < w->L.n; r++) {
-        const int q = w->L.part_of[r];
-        uint8_t* rb = b->base[q] + (uint64_t)(r - w->L.pb[q]) * b->stride;
-        P.buf[r] = rb;
-        P.sflag[r] = reinterpret_cast<uint32_t*>(rb + b->buf_bytes);
-        P.gflag[r] = P.sflag[r] + rlo::kBulkMaxChunks;
-    }
-    P.err = b->err;
-    P.deadline_ticks = 100000000ull * 20;  // 20 s per bulk bcast
-    b->connected = true;
-    return RLO_OK;
-}
-
-void* rlo_bulk_buffer(rlo_bulk_t* b, int rank) {
-    if (!b || !b->connected || rank < b->w->rb || rank >= b->w->rb + b->w->nl) return nullptr;
-    return b->P.buf[rank];
-}
-
-int rlo_bulk_reset(rlo_bulk_t* b, void* stream) {
-    if (!b || !b->connected) return RLO_E_INVAL;
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipSetDevice(b->w->device));
-    for (int lr = 0; lr < b->w->nl; lr++)
-        HIPCHK(hipMemsetAsync(b->region + (uint64_t)lr * b->stride + b->buf_bytes, 0, kBulkFlagBytes, s));
-    HIPCHK(hipMemsetAsync(b->err, 0, 4, s));
-    HIPCHK(hipStreamSynchronize(s));
-    return RLO_OK;
-}
-
-int rlo_bulk_plan(int n, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, int cross_gpu, rlo_bulk_plan_t* out) {
-    if (!out || n < 2 || n > rlo::kMaxBulkRanks || bytes == 0 || blocks > 1024) return RLO_E_INVAL;
-    // Auto sizing (tools/bulk_sweep.py, profiles/r1s5_bulk_sweep.jsonl).  Every chunk costs each
-    // workgroup a system release + flag adds + (receivers) a poll and an acquire, and the cost grows
-    // with the workgroups: on one GPU a single chunk is fastest at every size (64 MiB, 128 blocks:
-    // 157 us for 1 chunk, 458 us for 16).  Across GPUs a phase is xGMI-link bound, so pipelining
-    // the scatter under the all-gather pays: T ~ D(1 + 1/k) + k c  =>  k ~ sqrt(D / c), i.e.
-    // k = floor(sqrt(bytes / 4 MiB)) chunks (1 MiB, 4 MiB: 1; 16 MiB: 2; 64 MiB: 4).
-    if (blocks == 0) blocks = (uint32_t)std::min<uint64_t>(128, std::max<uint64_t>(32, bytes >> 16));
-    uint64_t want = chunk_bytes;
-    if (want == 0) {
-        uint64_t k = 1;
-        if (cross_gpu)
-            while ((k + 1) * (k + 1) * (4ull << 20) <= bytes && k < rlo::kBulkMaxChunks) k++;
-        want = (bytes + k - 1) / k;
-    }
-    // stripes are whole 1-KiB blocks; a chunk is (N-1) stripes; at most kBulkMaxChunks chunks
-    uint64_t stripe = (want / (uint64_t)(n - 1) + rlo::kBulkBlock - 1) / rlo::kBulkBlock * rlo::kBulkBlock;
-    stripe = std::max<uint64_t>(stripe, rlo::kBulkBlock);
-    uint64_t chunk = stripe * (uint64_t)(n - 1);
-    while ((bytes + chunk - 1) / chunk > rlo::kBulkMaxChunks) { stripe *= 2; chunk = stripe * (uint64_t)(n - 1); }
-    if (chunk > 0xFFFFFFFFull) return RLO_E_INVAL;
-    out->stripe = (uint32_t)stripe;
-    out->chunk = (uint32_t)chunk;
-    out->nchunks = (uint32_t)((bytes + chunk - 1) / chunk);
-    out->blocks = blocks;
-    return RLO_OK;
-}
-
-int rlo_bulk_launch(rlo_bulk_t* b, int origin, uint64_t bytes, uint32_t chunk_bytes, uint32_t blocks, void* stream) {
-    if (!b || !b->connected) return RLO_E_INVAL;
-    const int n = b->w->L.n;
-    if (origin < 0 || origin >= n || bytes > b->buf_bytes) return RLO_E_INVAL;
-    rlo_bulk_plan_t plan;
-    const int rc = rlo_bulk_plan(n, bytes, chunk_bytes, blocks, b->cross_gpu ? 1 : 0, &plan);
-    if (rc != RLO_OK) return rc;
-    blocks = plan.blocks;
-    rlo::BulkParams& P = b->P;
-    P.origin = origin;
-    P.bytes = bytes;
-    P.stripe = plan.stripe;
-    P.chunk = plan.chunk;
-    P.nchunks = plan.nchunks;
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipSetDevice(b->w->device));
-    HIPCHK(hipEventRecord(b->ev0, s));
-    hipError_t e = rlo_launch_bulk(&P, (int)blocks, b->w->nl, s);
-    if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
-    HIPCHK(hipEventRecord(b->ev1, s));
-    return RLO_OK;
-}
-
-int rlo_bulk_wait(rlo_bulk_t* b, float* ms) {
-    if (!b) return RLO_E_INVAL;
-    HIPCHK(hipSetDevice(b->w->device));
-    HIPCHK(hipEventSynchronize(b->ev1));
-    float t = 0.f;
-    HIPCHK(hipEventElapsedTime(&t, b->ev0, b->ev1));
-    if (ms) *ms = t;
-    uint32_t err = 0;
-    HIPCHK(hipMemcpy(&err, b->err, sizeof err, hipMemcpyDeviceToHost));
-    return err ? RLO_E_DEVICE : RLO_OK;
-}
-
-int rlo_bulk_destroy(rlo_bulk_t* b) {
-    if (!b) return RLO_E_INVAL;
-    (void)hipSetDevice(b->w->device);
-    for (void* p : b->opened) (void)hipIpcCloseMemHandle(p);
-    if (b->region) (void)hipFree(b->region);
-    if (b->err) (void)hipFree(b->err);
-    if (b->ev0) (void)hipEventDestroy(b->ev0);
-    if (b->ev1) (void)hipEventDestroy(b->ev1);
-    delete b;
+    const uint8_t* src = w->heap + (((uint64_t)lr * w->L.n + (uint64_t)ev->origin) * w->L.bslots + ev->aux) * w->L.bcap;
+    HIPCHK(hipMemcpy(dst, src, ev->len, hipMemcpyDeviceToHost));
     return RLO_OK;
 }
 

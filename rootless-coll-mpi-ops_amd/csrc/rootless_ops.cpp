@@ -36,6 +36,8 @@ int total_pickup = 0;  // rootless_ops.h:46
 struct RLO_msg_generic {  // first member = the user view, so RLO_user_msg* and RLO_msg_t* convert
     RLO_user_msg msg_usr;
     int send_len;         // bytes given to RLO_msg_new_bc
+    uint8_t* ext;         // a bulk message's bytes (longer than the data area), malloc'd; else null
+    size_t ext_len;
     int source;           // tree parent (MPI_SOURCE in the reference), -1 for local messages
     uint64_t seq;         // command sequence number once posted
     int posted;           // 1: in the command ring (or backlog), 2: consumed by the device
@@ -77,6 +79,7 @@ struct progress_engine {
     void* ctx = nullptr;
     uint32_t slot_bytes = 0;      // device payload capacity
     uint32_t deliver_max = 0;     // bytes a receiver sees (reference: msg_size_max - 4, :1588)
+    uint64_t bulk_max = 0;        // extension: bcasts up to this many bytes (bulk messages), 0 = off
     int send_list_len = 0;
     std::deque<RLO_msg_t*> pickup;   // queue_pickup (:938)
     std::deque<Cmd> backlog;         // commands the ring had no room for yet
@@ -139,6 +142,8 @@ RLO_msg_t* msg_alloc(int origin) {
     m->msg_usr.data = m->msg_usr.buf + sizeof(int);
     std::memcpy(m->msg_usr.buf, &origin, sizeof(int));
     m->send_len = 0;
+    m->ext = nullptr;
+    m->ext_len = 0;
     m->source = -1;
     m->seq = 0;
     m->posted = 0;
@@ -150,6 +155,9 @@ RLO_msg_t* msg_alloc(int origin) {
 
 void msg_release(RLO_msg_t* m) {
     if (!m) return;
+    std::free(m->ext);
+    m->ext = nullptr;
+    m->ext_len = 0;
     if (g_pool.size() < 256) g_pool.push_back(m);
     else std::free(m);
 }
@@ -222,6 +230,7 @@ void reap_sent(progress_engine* e) {
         e->wait.pop_front();
         m->posted = 2;
         m->fwd_done = 1;
+        std::free(m->ext);
         std::free(m);
     }
 }
@@ -249,6 +258,32 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             m->msg_usr.type = RLO_BCAST;
             m->source = ev.from;
             m->fwd_done = 1;  // forwarded by the device before this event was written
+            e->recved_bcast++;
+            e->pickup.push_back(m);
+            break;
+        }
+        case RLO_EV_DELIVER_BULK: {  // extension: a bcast beyond the data area, copied out of the heap
+            RLO_msg_t* m = msg_alloc(ev.origin);
+            if (!m) return;
+            m->ext = (uint8_t*)std::malloc(ev.len ? ev.len : 1);
+            if (!m->ext || rlo_host_bulk_copy(e->w, e->rank, &ev, m->ext) != RLO_OK) {
+                std::fprintf(stderr, "rlo: rank %d: bulk delivery of %u bytes from %d failed\n", e->rank, ev.len, ev.origin);
+                e->failed = true;
+                msg_release(m);
+                return;
+            }
+            rlo_cmd_t c;  // the heap slot can take the origin's next bulk message
+            std::memset(&c, 0, sizeof c);
+            c.kind = RLO_CMD_BULK_RELEASE;
+            c.origin = ev.origin;
+            c.pseq = ev.aux;
+            post(e, c, nullptr, 0, nullptr);
+            m->ext_len = ev.len;
+            m->msg_usr.type = RLO_BCAST;
+            m->msg_usr.data = (char*)m->ext;
+            m->msg_usr.data_len = ev.len;  // extension: the size (reference bcasts leave 0, :920-932)
+            m->source = ev.from;
+            m->fwd_done = 1;
             e->recved_bcast++;
             e->pickup.push_back(m);
             break;
@@ -385,7 +420,8 @@ void progress(progress_engine* e) {
             const uint32_t k = e->evq.front().ev.kind;
             local.push_back(std::move(e->evq.front()));
             e->evq.pop_front();
-            if (k == RLO_EV_DELIVER_BCAST || k == RLO_EV_DELIVER_DECISION || k == RLO_EV_JUDGE) break;
+            if (k == RLO_EV_DELIVER_BCAST || k == RLO_EV_DELIVER_BULK || k == RLO_EV_DELIVER_DECISION || k == RLO_EV_JUDGE)
+                break;
         }
         reap_sent(e);
     }
@@ -503,6 +539,21 @@ RLO_msg_t* RLO_msg_new_bc(RLO_engine_t* eng, void* buf_in, int send_size) {
     RLO_msg_t* m = RLO_msg_new_generic(eng);
     if (!m) return nullptr;
     if (send_size < 0) send_size = 0;
+    if ((uint64_t)send_size > eng->deliver_max && eng->bulk_max) {
+        // extension: longer than the data area -> a bulk bcast (RLO_bcast_gen moves it through the heap)
+        if ((uint64_t)send_size > eng->bulk_max) {
+            std::fprintf(stderr, "rlo: RLO_msg_new_bc: %d bytes exceed RLO_BULK_MAX (%llu)\n", send_size,
+                         (unsigned long long)eng->bulk_max);
+            std::free(m);
+            return nullptr;
+        }
+        m->ext = (uint8_t*)std::malloc((size_t)send_size);
+        if (!m->ext) { std::free(m); return nullptr; }
+        std::memcpy(m->ext, buf_in, (size_t)send_size);
+        m->ext_len = (size_t)send_size;
+        m->send_len = send_size;
+        return m;
+    }
     if (send_size > RLO_MSG_SIZE_MAX) send_size = RLO_MSG_SIZE_MAX;  // the data area (:295)
     if (send_size) std::memcpy(m->msg_usr.buf + sizeof(int), buf_in, (size_t)send_size);
     m->send_len = send_size;
@@ -510,6 +561,7 @@ RLO_msg_t* RLO_msg_new_bc(RLO_engine_t* eng, void* buf_in, int send_size) {
 }
 
 int RLO_msg_free(RLO_msg_t* msg_in) {
+    if (msg_in) std::free(msg_in->ext);
     std::free(msg_in);
     return 0;
 }
@@ -591,6 +643,14 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
     if (const char* rs = std::getenv("RLO_RING_SLOTS")) pc.ring_slots = (uint32_t)std::strtoul(rs, nullptr, 10);
     pc.device = e->device;
     pc.flags = multi ? RLO_PART_UNCACHED : 0u;
+    // extension: bcasts beyond the data area (bulk messages) up to RLO_BULK_MAX bytes (default 64 MiB;
+    // 0 turns them off); RLO_BULK_MOVERS mover workgroups per rank (default 4)
+    e->bulk_max = 64ull << 20;
+    if (const char* bm = std::getenv("RLO_BULK_MAX")) e->bulk_max = std::strtoull(bm, nullptr, 10);
+    pc.bulk_max = e->bulk_max;
+    pc.bulk_slots = 2;
+    pc.movers = 4;
+    if (const char* mv = std::getenv("RLO_BULK_MOVERS")) pc.movers = (uint32_t)std::strtoul(mv, nullptr, 10);
     int rc = rlo_part_create(&pc, &e->w);
     std::vector<uint8_t> blob(RLO_PART_BLOB_BYTES, 0), blobs((size_t)RLO_PART_BLOB_BYTES * e->size, 0);
     if (rc == RLO_OK && rlo_part_export(e->w, blob.data(), RLO_PART_BLOB_BYTES) < 0) rc = RLO_E_HIP;
@@ -730,6 +790,26 @@ int RLO_bcast_gen(RLO_engine_t* eng, RLO_msg_t* msg_in, enum RLO_COMM_TAGS tag) 
     std::memset(&c, 0, sizeof c);
     c.kind = RLO_CMD_BCAST;
     c.id = (int32_t)++eng->bcast_seq;
+    if (msg_in->ext) {  // extension: a bulk bcast -- its bytes into my heap slot once the slot is free
+        uint32_t q = 0;
+        int rc;
+        while ((rc = rlo_host_bulk_stage(eng->w, eng->rank, msg_in->ext, msg_in->ext_len, 0, &q)) == RLO_E_AGAIN) {
+            RLO_make_progress_all();
+            if (eng->failed) return -1;
+        }
+        if (rc != RLO_OK) {
+            std::fprintf(stderr, "rlo: rank %d: bulk bcast of %zu bytes failed: %s\n", eng->rank, msg_in->ext_len,
+                         rlo_strerror(rc));
+            return -1;
+        }
+        const uint32_t desc[4] = {(uint32_t)msg_in->ext_len, q, 0u, 0u};
+        c.kind = RLO_CMD_BULK;
+        if (post(eng, c, desc, sizeof desc, msg_in)) return -1;
+        eng->wait.push_back(msg_in);
+        eng->sent_bcast++;
+        RLO_make_progress_all();  // :1602
+        return 0;
+    }
     if (post(eng, c, msg_in->msg_usr.buf + sizeof(int), n, msg_in)) return -1;
     eng->wait.push_back(msg_in);
     eng->sent_bcast++;

@@ -19,16 +19,21 @@ RLO_PART_UNCACHED = 1
 RLO_LAUNCH_NO_RESET = 1
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
-DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot", 7: "host command"}
+DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot", 7: "host command",
+        8: "bulk index"}
 # host-service program (rlo_hip.h)
 RLO_CMD_BCAST, RLO_CMD_PROPOSAL, RLO_CMD_JUDGE, RLO_CMD_OWN_JUDGE, RLO_CMD_QUIT = 0, 2, 16, 17, 18
-RLO_EV_DELIVER_BCAST, RLO_EV_DELIVER_DECISION = 1, 1 | (4 << 8)
+RLO_CMD_BULK, RLO_CMD_BULK_RELEASE = 10, 19
+RLO_EV_DELIVER_BCAST, RLO_EV_DELIVER_DECISION, RLO_EV_DELIVER_BULK = 1, 1 | (4 << 8), 1 | (10 << 8)
+RLO_ORDER_RANDOM, RLO_ORDER_SLOTS = 0, 1
+TAG_BULK = 10
 RLO_EV_ACTION, RLO_EV_RESULT, RLO_EV_JUDGE, RLO_EV_OWN_JUDGE = 3, 4, 6, 7
 
 
 class WorldCfg(ctypes.Structure):
     _fields_ = [("n_ranks", ctypes.c_int32), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
-                ("device", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("bulk_max", ctypes.c_uint64), ("bulk_slots", ctypes.c_uint32),
+                ("movers", ctypes.c_uint32)]
 
 
 class WorldInfo(ctypes.Structure):
@@ -38,18 +43,21 @@ class WorldInfo(ctypes.Structure):
                 ("vote_bytes", ctypes.c_uint64), ("ctrl_bytes", ctypes.c_uint64), ("cus", ctypes.c_int32),
                 ("blocks_per_cu", ctypes.c_int32), ("part", ctypes.c_int32), ("n_parts", ctypes.c_int32),
                 ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),
-                ("waves", ctypes.c_int32)]
+                ("waves", ctypes.c_int32), ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32),
+                ("bulk_max", ctypes.c_uint64), ("heap_bytes", ctypes.c_uint64)]
 
 
 class PartCfg(ctypes.Structure):
     _fields_ = [("n_ranks", ctypes.c_int32), ("n_parts", ctypes.c_int32), ("part", ctypes.c_int32),
                 ("part_begin", ctypes.c_void_p), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
-                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32), ("bulk_max", ctypes.c_uint64),
+                ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32)]
 
 
 class StormCfg(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("k", ctypes.c_int64), ("len", ctypes.c_uint32), ("window", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32), ("log_cap", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("log_cap", ctypes.c_uint32), ("len_max", ctypes.c_uint32),
+                ("order", ctypes.c_uint32)]
 
 
 class IarCfg(ctypes.Structure):
@@ -78,8 +86,8 @@ class RankStats(ctypes.Structure):
 
 
 class BulkPlan(ctypes.Structure):
-    _fields_ = [("stripe", ctypes.c_uint32), ("chunk", ctypes.c_uint32), ("nchunks", ctypes.c_uint32),
-                ("blocks", ctypes.c_uint32)]
+    _fields_ = [("nchunks", ctypes.c_uint32), ("stripe", ctypes.c_uint32), ("chunk", ctypes.c_uint32),
+                ("tile", ctypes.c_uint32), ("total_tiles", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class LogRec(ctypes.Structure):
@@ -93,10 +101,9 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_stream_create", "rlo_stream_destroy",
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_strerror", "rlo_last_hip_error",
+           "rlo_device_error", "rlo_bulk_debug",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
-           "rlo_device_count", "rlo_bulk_create", "rlo_bulk_export", "rlo_bulk_connect", "rlo_bulk_buffer",
-           "rlo_bulk_reset", "rlo_bulk_launch", "rlo_bulk_wait", "rlo_bulk_destroy", "rlo_bulk_plan"]
-RLO_BULK_BLOB_BYTES = 256
+           "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan"]
 
 _lib = None
 
@@ -139,17 +146,12 @@ def load():
     L.rlo_host_running.argtypes = [vp]
     L.rlo_host_cmd_count.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.rlo_device_count.argtypes = []
-    L.rlo_bulk_create.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(vp)]
-    L.rlo_bulk_export.argtypes = [vp, vp, ctypes.c_uint32]
-    L.rlo_bulk_connect.argtypes = [vp, vp, ctypes.c_int]
-    L.rlo_bulk_buffer.argtypes = [vp, ctypes.c_int]
-    L.rlo_bulk_buffer.restype = vp
-    L.rlo_bulk_reset.argtypes = [vp, vp]
-    L.rlo_bulk_launch.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, vp]
-    L.rlo_bulk_plan.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
-                                ctypes.POINTER(BulkPlan)]
-    L.rlo_bulk_wait.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
-    L.rlo_bulk_destroy.argtypes = [vp]
+    L.rlo_host_bulk_stage.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_uint32)]
+    L.rlo_host_bulk_copy.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp]
+    L.rlo_bulk_plan.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(BulkPlan)]
+    L.rlo_bulk_debug.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    L.rlo_device_error.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_strerror.argtypes = [ctypes.c_int]
     L.rlo_strerror.restype = ctypes.c_char_p
     _lib = L

@@ -5,7 +5,7 @@ run_inprocess(): every part in this process, one HIP stream each (same GPU or se
 run_processes(): one spawned process per part; blobs are exchanged through a queue, the
                  regions are mapped with hipIpc (dmabuf), launches start after a barrier
                  that follows every part's reset.
-A program spec is a dict: {"kind": "storm", "k", "len", "seed", "window", "log"} or
+A program spec is a dict: {"kind": "storm", "k", "len", "seed", "window", "log", "len_max", "order"} or
 {"kind": "iar", "props": [(origin, pid, bytes)], "judge", "mask", "isp", "seed", "ppm", "log"} or
 {"kind": "lat", "rounds", "len", "seed"} (the round word lives in part 0; st["round_ticks"] is world
 rank 0's clock at each round's completion).
@@ -23,7 +23,8 @@ def even_bounds(n, parts):
 def _program(w, spec):
     if spec["kind"] == "storm":
         w.program_storm(spec["k"], spec["len"], seed=spec.get("seed", 0x5EED), window=spec.get("window", 64),
-                        log=spec.get("log", False), log_cap=spec.get("log_cap", 0), hist=spec.get("hist", False))
+                        log=spec.get("log", False), log_cap=spec.get("log_cap", 0), hist=spec.get("hist", False),
+                        len_max=spec.get("len_max", 0), order=spec.get("order", 0))
     elif spec["kind"] == "iar":
         from . import _lib as L
         w.program_iar(spec["props"], judge=spec.get("judge", L.RLO_JUDGE_APPROVE), mask=spec.get("mask"),
@@ -60,7 +61,8 @@ def merge(results):
     return st, logs, [r["ms"] for r in results]
 
 
-def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False):
+def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, **world_kw):
+    """world_kw: bulk_max / bulk_slots / movers (World.part)"""
     from . import _lib as L
     from .world import World
 
@@ -68,7 +70,7 @@ def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
     devices = devices or [0] * parts
     streams = []
     ws = [World.part(n, parts, p, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
-                     device=devices[p], uncached=uncached) for p in range(parts)]
+                     device=devices[p], uncached=uncached, **world_kw) for p in range(parts)]
     try:
         blobs = [w.export() for w in ws]
         for w in ws:
@@ -94,12 +96,13 @@ def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
             L.load().rlo_stream_destroy(s)
 
 
-def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, blob_q, blobs_q, barrier, out_q):
+def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, blob_q, blobs_q, barrier, out_q,
+            world_kw):
     try:
         from .world import World
 
         w = World.part(n, len(bounds) - 1, part, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
-                       device=device, uncached=uncached)
+                       device=device, uncached=uncached, **world_kw)
         blob_q.put((part, w.export()))
         blobs = blobs_q.get(timeout=120)
         w.connect(blobs)
@@ -116,7 +119,8 @@ def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, bl
         out_q.put((part, -99, None, repr(e)))
 
 
-def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, timeout=300):
+def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, timeout=300,
+                  **world_kw):
     parts = len(bounds) - 1
     devices = devices or [0] * parts
     ctx = mp.get_context("spawn")
@@ -124,7 +128,7 @@ def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
     blobs_qs = [ctx.Queue() for _ in range(parts)]
     barrier = ctx.Barrier(parts)
     procs = [ctx.Process(target=_worker, args=(n, bounds, p, devices[p], spec, max_payload, ring_slots, uncached,
-                                               blob_q, blobs_qs[p], barrier, out_q)) for p in range(parts)]
+                                               blob_q, blobs_qs[p], barrier, out_q, world_kw)) for p in range(parts)]
     for p in procs:
         p.start()
     try:

@@ -21,11 +21,14 @@ class World:
     """A world of n ranks.  World(n) hosts all of them on one GPU; World.part(...) creates one
     part of a sharded world (export() -> exchange blobs -> connect(blobs))."""
 
-    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None):
+    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None, bulk_max=0, bulk_slots=0, movers=0):
+        """bulk_max > 0: messages longer than max_payload (up to bulk_max bytes) are bulk messages --
+        announced through the rings, moved by `movers` mover workgroups (0 = auto) between per-rank
+        heaps of bulk_slots slots per origin (rlo_hip.h)."""
         self.lib = L.load()
         h = ctypes.c_void_p()
         if _part is None:
-            cfg = L.WorldCfg(n, max_payload, ring_slots, device)
+            cfg = L.WorldCfg(n, max_payload, ring_slots, device, bulk_max, bulk_slots, movers)
             check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
         else:
             n_parts, part, begin, flags = _part
@@ -34,7 +37,7 @@ class World:
             if begin is not None:
                 self._pb = (ctypes.c_int32 * (n_parts + 1))(*begin)
                 pb = ctypes.cast(self._pb, ctypes.c_void_p)
-            cfg = L.PartCfg(n, n_parts, part, pb, max_payload, ring_slots, device, flags)
+            cfg = L.PartCfg(n, n_parts, part, pb, max_payload, ring_slots, device, flags, bulk_max, bulk_slots, movers)
             check(self.lib.rlo_part_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_part_create")
         self.h = h
         self.n = n
@@ -42,9 +45,11 @@ class World:
         self._lat_rounds = 0
 
     @classmethod
-    def part(cls, n, n_parts, part, part_begin=None, max_payload=4096, ring_slots=0, device=-1, uncached=False):
+    def part(cls, n, n_parts, part, part_begin=None, max_payload=4096, ring_slots=0, device=-1, uncached=False,
+             bulk_max=0, bulk_slots=0, movers=0):
         return cls(n, max_payload, ring_slots, device,
-                   _part=(n_parts, part, part_begin, L.RLO_PART_UNCACHED if uncached else 0))
+                   _part=(n_parts, part, part_begin, L.RLO_PART_UNCACHED if uncached else 0), bulk_max=bulk_max,
+                   bulk_slots=bulk_slots, movers=movers)
 
     def _query(self):
         info = L.WorldInfo()
@@ -84,9 +89,12 @@ class World:
             pass
 
     # ------------------------------------------------------------ programs
-    def program_storm(self, k, length, seed=0x5EED, window=64, log=False, hist=False, log_cap=0, prof=False):
+    def program_storm(self, k, length, seed=0x5EED, window=64, log=False, hist=False, log_cap=0, prof=False,
+                      len_max=0, order=L.RLO_ORDER_RANDOM):
+        """len_max > length: mixed sizes (piecewise log-uniform per bcast); order RLO_ORDER_SLOTS: bcast b
+        originates at rank b % n (every rank originates in every slot of n bcasts)."""
         flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0) | (L.RLO_FLAG_PROF if prof else 0)
-        cfg = L.StormCfg(seed, k, length, window, flags, log_cap)
+        cfg = L.StormCfg(seed, k, length, window, flags, log_cap, len_max, order)
         check(self.lib.rlo_program_storm(self.h, ctypes.byref(cfg)), "rlo_program_storm")
 
     def program_latency(self, rounds, length, seed=0x5EED, hist=False, log=False, prof=False):
@@ -132,8 +140,16 @@ class World:
         if rc == L.RLO_E_DEVICE:
             errs = {(self.rank_begin + r, L.DERR.get(s.error, s.error), s.error_aux)
                     for r, s in enumerate(self.stats_raw()) if s.error}
-            raise L.RloError("device engine error: %s" % sorted(errs)[:8])
+            code, aux = self.device_error()
+            raise L.RloError("device engine error: %s; part error word %s aux 0x%08x" %
+                             (sorted(errs)[:8], L.DERR.get(code, code), aux))
         return check(rc, "rlo_wait")
+
+    def device_error(self):
+        """(code, aux) of this part's device error word (rlo_device_error)"""
+        c, a = ctypes.c_uint32(), ctypes.c_uint32()
+        check(self.lib.rlo_device_error(self.h, ctypes.byref(c), ctypes.byref(a)), "rlo_device_error")
+        return c.value, a.value
 
     def run(self, stream=None):
         """launch + wait; returns the kernel time in ms (HIP events on the launch stream)."""
@@ -202,6 +218,15 @@ def hist_percentile(hist, p):
     lo = (4 + sub) << (o - 2)
     hi = (5 + sub) << (o - 2)
     return 0.5 * (lo + hi)
+
+
+def bulk_plan(n, nbytes, cross=False):
+    """rlo_bulk_plan: the chunk / stripe / tile plan every rank derives for a bulk message (host
+    arithmetic, no GPU)"""
+    out = L.BulkPlan()
+    check(L.load().rlo_bulk_plan(n, nbytes, 1 if cross else 0, ctypes.byref(out)), "rlo_bulk_plan")
+    return {"nchunks": out.nchunks, "stripe": out.stripe, "chunk": out.chunk, "tile": out.tile,
+            "total_tiles": out.total_tiles}
 
 
 def topology(n, rank):

@@ -99,36 +99,55 @@ def test_children_cover_exact_spanning_tree():
 
 
 def test_bulk_plan_geometry():
-    """rlo_bulk_plan (host arithmetic behind rlo_bulk_launch): stripes are whole 1-KiB blocks, a chunk
-    is (n-1) stripes, the chunks cover the message, at most 4096 chunks; library defaults: one chunk
-    on one GPU, floor(sqrt(bytes / 4 MiB)) chunks across GPUs, bytes / 64 KiB workgroups in [32, 128]."""
+    """rlo_bulk_plan (the plan every rank derives for a bulk message, rlo_device.hpp bulk_plan):
+    stripes are whole KiB, a chunk is N-1 stripes, <= 16 chunks cover the message, one chunk on one
+    GPU and ~sqrt(len / 4 MiB) across GPUs, tiles <= 256 KiB.  The scatter tiles (every stripe of every
+    chunk, cut into tiles) cover every byte exactly once, and total_tiles -- each receiver's completion
+    count -- equals the tiles of its own stripe (scatter) plus the other stripes (gather)."""
     import math
 
-    from rlo.bulk import plan
-
-    MiB = 1 << 20
-    for n in (2, 3, 5, 8, 16, 64):
-        for nbytes in (1, 1000, 1024, MiB, MiB + 16, 3 * MiB + 123, 16 * MiB, 64 * MiB, 1 << 30):
-            for chunk in (0, 4096, 64 << 10, MiB):
-                for cross in (False, True):
-                    p = plan(n, nbytes, chunk=chunk, cross_gpu=cross)
-                    assert p["stripe"] % 1024 == 0 and p["stripe"] >= 1024, (n, nbytes, p)
-                    assert p["chunk"] == p["stripe"] * (n - 1)
-                    assert p["nchunks"] == -(-nbytes // p["chunk"]) <= 4096
-                    assert p["blocks"] == min(128, max(32, nbytes >> 16))
-                    if chunk == 0:
-                        want = 1 if not cross else max(1, math.isqrt(nbytes // (4 * MiB)))
-                        # the stripe rounds up to whole blocks, so the chunk count can only shrink
-                        assert p["nchunks"] <= want, (n, nbytes, cross, p)
-                        if nbytes >= 64 * (n - 1) * 1024 and want <= 4096:
-                            assert p["nchunks"] == want or p["nchunks"] == want - 1, (n, nbytes, cross, p)
-    assert plan(8, 64 * MiB, cross_gpu=True)["nchunks"] == 4
-    assert plan(8, 16 * MiB, cross_gpu=True)["nchunks"] == 2
-    assert plan(8, 4 * MiB, cross_gpu=True)["nchunks"] == 1
-    assert plan(8, 64 * MiB, cross_gpu=False)["nchunks"] == 1
-    assert plan(8, MiB, blocks=7)["blocks"] == 7
     import rlo
 
-    for bad in ((1, MiB), (65, MiB), (8, 0)):
+    MiB = 1 << 20
+    for n in (2, 3, 5, 8, 16, 64, 255):
+        for nbytes in (1, 1000, 1024, 5000, MiB, MiB + 16, 3 * MiB + 123, 16 * MiB, 64 * MiB + 80):
+            for cross in (False, True):
+                p = rlo.bulk_plan(n, nbytes, cross)
+                st, ch, tile = p["stripe"], p["chunk"], p["tile"]
+                assert st % 1024 == 0 and st >= 1024 and ch == st * (n - 1), (n, nbytes, p)
+                assert tile % 1024 == 0 and 1024 <= tile <= min(st, 256 << 10), (n, nbytes, p)
+                assert p["nchunks"] == -(-nbytes // ch) <= 16, (n, nbytes, p)
+                if not cross:
+                    assert p["nchunks"] == 1 or st * (n - 1) * 16 < nbytes * 2, (n, nbytes, p)
+                covered = 0
+                per_stripe = [0] * (n - 1)
+                for c in range(p["nchunks"]):
+                    clen = min(ch, nbytes - c * ch)
+                    for k in range(n - 1):
+                        slen = max(0, min(st, clen - k * st))
+                        t = -(-slen // tile)
+                        per_stripe[k] += t
+                        for i in range(t):  # tile i of stripe k of chunk c: contiguous, in order
+                            off = c * ch + k * st + i * tile
+                            assert off == covered, (n, nbytes, c, k, i)
+                            covered += min(tile, slen - i * tile)
+                assert covered == nbytes
+                assert sum(per_stripe) == p["total_tiles"]
+                if cross and nbytes >= 16 * MiB:
+                    assert p["nchunks"] >= max(1, math.isqrt(nbytes // (4 * MiB))) - 1
+    assert rlo.bulk_plan(8, 64 * MiB, True)["nchunks"] == 4
+    assert rlo.bulk_plan(8, 64 * MiB, False)["nchunks"] == 1
+    for bad in ((1, MiB), (8, 0)):
         with pytest.raises(rlo.RloError):
-            plan(*bad)
+            rlo.bulk_plan(*bad)
+
+
+def test_bulk_world_config_rejected_without_gpu_or_bad_slots():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import rlo
+
+    with pytest.raises(rlo.RloError):
+        rlo.World(8, bulk_max=1 << 20, bulk_slots=3)

@@ -66,6 +66,29 @@ def test_stream_matches_reference(harness):
         assert got == case["deliveries"], (n, case["seed"])
 
 
+@pytest.mark.parametrize("n,k", [(4, 24), (8, 40)])
+def test_bulk_bcast_through_dropin(harness, n, k):
+    """Extension beyond the reference's 32,764-byte cap: RLO_msg_new_bc / RLO_bcast_gen of up to 1 MiB,
+    every rank originating in every slot (BASELINE configs[4] sizes).  Every rank picks up every other
+    rank's bcasts exactly once, from the oracle's tree parent; bcasts within the data region arrive as
+    in the reference (data_len 0, the region's bytes), longer ones with data_len = their size and
+    exactly their bytes."""
+    import pyoracle as orc
+
+    seed, lo, hi = 21, 64, 1 << 20
+    recs = run(harness, n, "bulkstream", seed, k, lo, hi, timeout=120)
+    par = orc.storm(n, seed, k, lo, want_parent=True, len_max=hi, order=1)["parent"]
+    want = []
+    for b in range(k):
+        o, ln = b % n, orc.len_of(seed, b, lo, hi)
+        data = orc.payload(o, b, ln)
+        dl, h = (ln, orc.fnv1a(data)) if ln > 32764 else (0, orc.region_hash(data))
+        want += [(r, b, o, int(par[b, r]), dl, "%016x" % h) for r in range(n) if r != o]
+    got = [(x["rank"], x["bid"], x["origin"], x["parent"], x["len"], x["hash"]) for x in recs]
+    assert sorted(got) == sorted(want)
+    assert any(w[4] for w in want) and any(not w[4] for w in want)
+
+
 def _iar_cases():
     return [c for c in load("iar.json")["cases"] if c["n"] <= MAXN]
 
