@@ -48,23 +48,33 @@ def percentile(a, p):
 
 
 def cpu_baseline(n, length, seed, target_s):
-    """The oracle's clean-room CPU restatement ("port"), one host core, bounded sample."""
+    """The oracle's clean-room CPU restatement ("port") on the box's host cores: the same storm (n
+    virtual ranks, length-byte payloads, random originators) with every tree edge copying the bytes,
+    the ranks dealt to `threads` host threads (oracle/rlo_oracle.c orc_storm_mt), bounded sample.
+    Beside it: the compiled reference itself under host MPI at its own 4- and 8-rank worlds."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle as orc
 
+    threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU is 16
     t = time.perf_counter()
-    orc.storm(n, seed, 2000, length)
-    per = (time.perf_counter() - t) / 2000
-    k = int(max(2000, min(2_000_000, target_s / max(per, 1e-9))))
+    orc.storm_mt(n, seed, 20000, length, threads)
+    per = (time.perf_counter() - t) / 20000
+    k = int(max(20000, min(4_000_000, target_s / max(per, 1e-9))))
     t = time.perf_counter()
-    res = orc.storm(n, seed, k, length)
+    res = orc.storm_mt(n, seed, k, length, threads)
     dt = time.perf_counter() - t
-    out = {"value": k / dt, "unit": "msgs/s", "deliveries_per_s": res["deliveries"] / dt, "cores": 1, "kind": "port",
-           "sample": "oracle/rlo_oracle.c storm, %d virtual ranks, %d B, %d bcasts (%d deliveries), %.1f s, 1 thread"
-                     % (n, length, k, res["deliveries"], dt)}
-    ref = reference_datapoint(length)
-    if ref:
-        out["reference_host_mpi"] = ref
+    out = {"value": k / dt, "unit": "msgs/s", "deliveries_per_s": res["deliveries"] / dt, "cores": threads,
+           "kind": "port",
+           "sample": "oracle/rlo_oracle.c orc_storm_mt: %d virtual ranks, %d B, %d random-origin bcasts (%d deliveries, "
+                     "bytes copied on every tree edge), %.1f s on %d host threads" % (n, length, k, res["deliveries"], dt,
+                                                                                     threads)}
+    refs = {}
+    for nr in (4, 8):
+        ref = reference_datapoint(length, nr)
+        if ref:
+            refs["n%d" % nr] = ref
+    if refs:
+        out["reference_host_mpi"] = refs
     return out
 
 
@@ -102,44 +112,43 @@ def pmc_traffic(ranks, length, k, device, timeout_s=120):
             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, last of 2 launches; FETCH x2 (gfx950)"}, None
 
 
-def dropin_api_leg(ranks=8, timeout_s=150):
+def dropin_api_leg(ranks=(4, 8), timeout_s=150):
     """The drop-in rootless_ops.h path end to end: tools/api_bench.c over librootless_ops.so
     (one MPI process per rank, every rank's engine a persistent kernel on this GPU) beside the
-    same driver linked against the compiled reference under host MPI on the box's cores."""
+    same driver linked against the compiled reference under host MPI on the box's cores, at the
+    reference's own 4- and 8-rank worlds.  Runs with the box's environment as it is (recorded)."""
     mpiexec = "/opt/conda/bin/mpiexec"
     ours = os.path.join(PKG, "lib", "rlo_api_bench")
     ref = os.path.join(REPO, "oracle", "_ref", "ref_api_bench")
     if not (os.path.exists(mpiexec) and os.path.exists(ours)):
         return {"error": "mpiexec or rlo_api_bench missing"}
-    out = {"ranks": ranks, "driver": "tools/api_bench.c (same calls for both)", "ours": {}, "reference_host_mpi": {}}
-    # all ranks' persistent kernels share the one GPU here: 2 hardware queues per single-engine rank
-    # process keep their queues within the GPU's slots (INTEGRATION.md, deployment note)
-    env = dict(os.environ)
-    env.setdefault("GPU_MAX_HW_QUEUES", "2")
-    out["env"] = {"GPU_MAX_HW_QUEUES": env["GPU_MAX_HW_QUEUES"]}
+    out = {"driver": "tools/api_bench.c (same calls for both)",
+           "env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)")}}
     legs = [("storm", ["storm", "20000", "64"]), ("lat", ["lat", "500", "64"]), ("iar", ["iar", "2000"])]
-    for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
-        if not os.path.exists(exe):
-            out[name] = {"error": "not built"}
-            continue
-        for leg, args in legs:
-            note("api %s %s" % (name, leg))
-            try:
-                r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(ranks), exe] + args,
-                                   stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20, env=env)
-                lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
-                out[name][leg] = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
-            except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
-                out[name][leg] = {"error": str(e)[:200]}
-    try:
-        o, f = out["ours"], out["reference_host_mpi"]
-        out["ratio_vs_reference"] = {
-            "bcast_per_s": round(o["storm"]["bcast_per_s"] / f["storm"]["bcast_per_s"], 2),
-            "decisions_per_s": round(o["iar"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
-            "p50_latency": round(o["lat"]["p50_us"] / f["lat"]["p50_us"], 2)}
-    except Exception:  # noqa: BLE001
-        pass
-    out["cores"] = ranks
+    for nr in ranks:
+        rec = {"ranks": nr, "ours": {}, "reference_host_mpi": {}, "cores": nr}
+        for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
+            if not os.path.exists(exe):
+                rec[name] = {"error": "not built"}
+                continue
+            for leg, args in legs:
+                note("api n=%d %s %s" % (nr, name, leg))
+                try:
+                    r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(nr), exe] + args,
+                                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20)
+                    lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+                    rec[name][leg] = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
+                except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
+                    rec[name][leg] = {"error": str(e)[:200]}
+        try:
+            o, f = rec["ours"], rec["reference_host_mpi"]
+            rec["ratio_vs_reference"] = {
+                "bcast_per_s": round(o["storm"]["bcast_per_s"] / f["storm"]["bcast_per_s"], 2),
+                "decisions_per_s": round(o["iar"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
+                "p50_latency": round(o["lat"]["p50_us"] / f["lat"]["p50_us"], 2)}
+        except Exception:  # noqa: BLE001
+            pass
+        out["n%d" % nr] = rec
     return out
 
 
@@ -176,108 +185,181 @@ def size_legs(rlo, R, device, stream, sizes=(256, 1024, 4096), k=1 << 16, steps=
     return out
 
 
-def bulk_leg(dist, world, rank, local, sizes_mib=(1, 4, 16, 64), iters=5, blocks=None):
-    """BASELINE configs[2]: large-message rootless bcast (pipelined scatter + all-gather over the
-    ranks' HBM buffers, rlo_bulk.hip) from rotating originators vs rooted RCCL broadcast of the
-    same bytes from the same root.  N > 1: one rank per GPU.  N = 1: an 8-rank world on the one
-    GPU (HBM only; no RCCL counterpart).  Every receiver checks every byte."""
-    import torch
+def _step(w, stream, dist):
+    """one launch of the loaded program; every part reset before any part launches"""
+    w.reset(stream)
+    if dist is not None:
+        dist.barrier()
+    w.launch(stream, no_reset=True)
+    rc = w.wait(raise_on_device_error=False)
+    if dist is not None:
+        dist.barrier()  # no peer still stores into this part's rings / heaps
+    return rc, w.kernel_ms()
 
-    import rlo
-    from rlo.bulk import Bulk
+
+def _world(rlo, dist, R, world, rank, local, **kw):
+    """one R-rank world: whole on this GPU (world == 1) or this process's part of it"""
+    if world == 1:
+        return rlo.World(R, device=local, **kw)
+    w = rlo.World.part(R, world, rank, device=local, uncached=True, **kw)
+    blobs = [None] * world
+    dist.all_gather_object(blobs, w.export())
+    w.connect(blobs)
+    return w
+
+
+def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64), rounds=8):
+    """BASELINE configs[2] / SURVEY 8(d) C3: large-message ROOTLESS bcast through the engine -- the
+    origin alone decides to send, receivers learn of it from the announcement on the skip-ring tree,
+    the mover workgroups move the bytes (pipelined scatter + all-gather between the ranks' heaps).
+    The latency program: one bcast at a time from random originators, round i+1 starts when every
+    rank holds round i; algbw = S / round time (world rank 0's clock).  N > 1: one rank per GPU,
+    beside rooted RCCL broadcast of the same bytes from the same root.  N = 1: 8 ranks on the GPU."""
+    import numpy as np
+    import torch
 
     G = world if world > 1 else 8
     maxb = max(sizes_mib) << 20
-    blocks = blocks or 0  # 0: the library sizes workgroups and chunks (rlo_bulk_launch)
-    if world > 1:
-        w = rlo.World.part(G, G, rank, max_payload=64, device=local, uncached=True)
-        blobs = [None] * world
-        dist.all_gather_object(blobs, w.export())
-        w.connect(blobs)
-        b = Bulk(w, maxb)
-        bb = [None] * world
-        dist.all_gather_object(bb, b.export())
-        b.connect(bb)
-        mine = [rank]
-        # rehearsal of the N-part path on one GPU (RLO_BENCH_DEVICE): RCCL refuses two ranks per GPU
-        nccl = None if os.environ.get("RLO_BENCH_DEVICE") else dist.new_group(backend="nccl")
-    else:
-        w = rlo.World(G, max_payload=64, device=local)
-        b = Bulk(w, maxb)
-        b.connect([b.export()])
-        mine = list(range(G))
-        nccl = None
-
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    def maxr(x):
-        if dist is None:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
+    w = _world(rlo, dist, G, world, rank, local, max_payload=64, bulk_max=maxb)
+    # rehearsal of the N-part path on one GPU (RLO_BENCH_DEVICE): RCCL refuses two ranks per GPU
+    nccl = dist.new_group(backend="nccl") if world > 1 and not os.environ.get("RLO_BENCH_DEVICE") else None
     out = []
     try:
         for mib in sizes_mib:
             nbytes = mib << 20
-            ours, ok = [], True
-            for it in range(iters + 1):
-                o = it % G
-                gen = torch.Generator(device="cuda").manual_seed(1000 * mib + o)
-                want = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=gen)
-                if o in mine:
-                    b.tensor(o)[:nbytes].copy_(want)
-                barrier()
-                b.reset()
-                barrier()
-                b.launch(o, nbytes, blocks=blocks)
-                ms, rc = b.wait(raise_on_error=False)
-                ok &= rc == 0
-                for r in mine:
-                    if r != o:
-                        ok &= bool(torch.equal(b.tensor(r)[:nbytes], want))
-                ms = maxr(ms)
-                if it:  # the first launch is a warmup
-                    ours.append(ms)
+            w.program_latency(rounds, nbytes, seed=0xB0 + mib)
+            sums, ok, kms = [], True, []
+            for _ in range(2):  # the first launch warms; both must deliver the same bytes
+                rc, ms = _step(w, stream, dist)
+                st = w.stats()
+                ok &= rc == 0 and bool((st["error"] == 0).all())
+                ok &= int(red(float(st["bcast_delivered"].sum()), "sum")) == rounds * (G - 1)
+                sums.append(st["bcast_sum"].copy())
+                kms.append(ms)
+            ok &= bool(np.array_equal(sums[0], sums[1]))
+            rt = 0.0
+            if w.rank_begin == 0:  # world rank 0's clock saw every round complete
+                obs = w.round_ticks().astype(np.float64)
+                d = np.diff(obs[obs > 0]) * 1e-8  # 10 ns ticks -> s
+                rt = float(np.median(d)) if len(d) else 0.0
+            rt = red(rt, "max")
+            ok = red(0.0 if ok else 1.0, "max") == 0.0
+            rec = {"MiB": mib, "round_ms": round(rt * 1e3, 4), "kernel_ms_per_round": round(red(kms[1], "max") / rounds, 4),
+                   "verified": bool(ok)}
+            rec["algbw_GBps"] = round(nbytes / rt / 1e9, 2) if rt > 0 else None
+            if world == 1 and rt > 0:
+                # one GPU: every receiver's copy written once ((G-1)S), the stripes read once (S) to
+                # all-gather, every receiver reads its copy to verify ((G-1)S): (2G-1)S HBM bytes
+                rec["hbm_GBps"] = round((2 * G - 1) * nbytes / rt / 1e9, 1)
             if rank == 0:
-                note("bulk %d MiB ours done" % mib)
-            rec = {"MiB": mib, "ours_ms": round(sorted(ours)[len(ours) // 2], 4), "verified": ok}
-            rec["ours_algbw_GBps"] = round(nbytes / (rec["ours_ms"] * 1e-3) / 1e9, 2)
+                note("bulk %d MiB: %.3f ms/round" % (mib, rt * 1e3))
             if nccl is not None:
                 t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                rc = []
-                for it in range(iters + 2):
-                    o = it % G
-                    barrier()
+                rcl = []
+                for it in range(rounds + 2):
+                    torch.cuda.synchronize()
+                    dist.barrier()
                     e0.record()
-                    dist.broadcast(t, src=o, group=nccl)
+                    dist.broadcast(t, src=it % G, group=nccl)
                     e1.record()
                     torch.cuda.synchronize()
                     if it >= 2:
-                        rc.append(maxr(e0.elapsed_time(e1)))
-                rec["rccl_ms"] = round(sorted(rc)[len(rc) // 2], 4)
+                        rcl.append(red(e0.elapsed_time(e1), "max"))
+                rec["rccl_ms"] = round(float(np.median(rcl)), 4)
                 rec["rccl_algbw_GBps"] = round(nbytes / (rec["rccl_ms"] * 1e-3) / 1e9, 2)
-                rec["ours_over_rccl"] = round(rec["rccl_ms"] / rec["ours_ms"], 3)
-            else:  # one GPU: every receiver's copy written once (N-1)S; the originator reads S to
-                # scatter, the stripe owners read S between them to all-gather: (N+1)S HBM bytes
-                rec["hbm_GBps"] = round(((G + 1) * nbytes) / (rec["ours_ms"] * 1e-3) / 1e9, 1)
+                if rt > 0:
+                    rec["ours_over_rccl"] = round(rec["rccl_ms"] / (rt * 1e3), 3)
             out.append(rec)
     finally:
-        b.close()
         w.close()
-    return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "blocks_per_rank": blocks or "auto",
-            "algorithm": "pipelined scatter + all-gather over per-rank HBM buffers (rlo_bulk.hip)",
-            "baseline": "torch.distributed.broadcast, nccl backend (RCCL), same root" if world > 1 else None,
+    return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "movers_per_part": w.info.get("movers"),
+            "algorithm": "rootless: announcement on the skip-ring tree, mover workgroups scatter + all-gather "
+                         "between per-rank heaps (rlo_kernel.hip mover_run)",
+            "timing": "median round time on world rank 0's clock (announce -> every rank holds the bytes -> "
+                      "next originator starts)",
+            "baseline": "torch.distributed.broadcast, nccl backend (RCCL), same root" if nccl is not None else None,
             "sizes": out}
 
 
-def reference_datapoint(length):
-    """The compiled reference itself under host MPI (8 ranks), if it was built and MPI exists."""
+def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3):
+    """BASELINE configs[4] / SURVEY 8(d) C5: mixed sizes log-uniform in [64 B, 1 MiB], collision-heavy
+    (slots: in every slot every rank originates, origin(b) = b mod R).  R = 64 ranks per GPU, one
+    world over all GPUs, k bcasts per step (fixed: per-GPU receipts stay ~k x 64, weak scaling).
+    Messages up to 4 KiB ride the rings; longer ones are bulk messages.  HBM bytes per bcast:
+    ring 2(R-1)(S+16); bulk (2R-1)S + 2(R-1)32 (copies written, stripes read, copies verified,
+    the announcement)."""
+    import numpy as np
+
+    R = per * world
+    lo, hi, cap, seed = 64, 1 << 20, 4096, 0xC5
+    w = _world(rlo, dist, R, world, rank, local, max_payload=cap, bulk_max=hi)
+    try:
+        w.program_storm(k, lo, seed=seed, len_max=hi, order=1)
+        ok, sums, kms = True, [], []
+        t0 = 0.0
+        for i in range(steps + 1):
+            if i == 1:
+                if dist is not None:
+                    dist.barrier()
+                t0 = time.perf_counter()
+            rc, ms = _step(w, stream, dist)
+            st = w.stats()
+            ok &= rc == 0 and bool((st["error"] == 0).all())
+            sums.append(st["bcast_sum"].copy())
+            if i:
+                kms.append(ms)
+        dt = red((time.perf_counter() - t0) / steps, "max")
+        ok &= int(red(float(st["originated"].sum()), "sum")) == k
+        ok &= int(red(float(st["bcast_delivered"].sum()), "sum")) == k * (R - 1)
+        ok &= all(np.array_equal(sums[0], x) for x in sums[1:])
+        ok = red(0.0 if ok else 1.0, "max") == 0.0
+        lens = rlo.storm_lengths(seed, k, lo, hi).astype(np.float64)
+        ring = lens <= cap
+        alg = float((2.0 * (R - 1) * (lens[ring] + 16)).sum() + ((2.0 * R - 1) * lens[~ring] + 2.0 * (R - 1) * 32).sum())
+        kernel_ms = red(float(np.mean(kms)), "max")
+        gbs = alg / world / (kernel_ms * 1e-3) / 1e9
+        return {"world_ranks": R, "ranks_per_gpu": per, "bcasts_per_step": k, "bulk_bcasts": int((~ring).sum()),
+                "payload_bytes_per_step": int(lens.sum()), "bcast_per_s": round(k / dt, 1),
+                "delivered_GBps": round(float(lens.sum()) * (R - 1) / dt / 1e9, 2), "kernel_ms": round(kernel_ms, 3),
+                "hbm_alg_GBps_per_gpu": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "verified": bool(ok),
+                "movers_per_part": w.info.get("movers")}
+    finally:
+        w.close()
+
+
+def small_n_legs(rlo, local, stream, sizes=(4, 8), rounds=2000, p=512):
+    """the device engine at the reference's own small worlds (4 and 8 ranks on
+    one GPU): unloaded one-way latency (origination -> last pickup) and decisions/s with every rank
+    keeping one proposal outstanding (approve-all judge on the device)."""
+    import numpy as np
+
+    out = {}
+    for n in sizes:
+        rec = {}
+        with rlo.World(n, max_payload=64, device=local) as w:
+            w.program_latency(rounds, 64, seed=21)
+            _step(w, stream, None)
+            lat = w.latencies_ticks().astype(np.float64) * 0.01
+            rec["p50_us"] = round(percentile(lat, 50), 2)
+            rec["p99_us"] = round(percentile(lat, 99), 2)
+            w.program_iar([(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)])
+            _step(w, stream, None)
+            t = time.perf_counter()
+            rc, ms = _step(w, stream, None)
+            dt = time.perf_counter() - t
+            st = w.stats()
+            rec["decisions_per_s"] = round(n * p / dt, 1)
+            rec["decisions_per_s_kernel"] = round(n * p / (ms * 1e-3), 1)
+            rec["decision_us"] = round(ms * 1e3 / p, 2)  # one proposal round trip per rank, back to back
+            rec["verified"] = bool(rc == 0 and (st["error"] == 0).all() and int(st["own_decided"].sum()) == n * p)
+        out["n%d" % n] = rec
+    return out
+
+
+def reference_datapoint(length, ranks=8):
+    """The compiled reference itself (rootless_ops.c + our capture driver) under host MPI: one
+    process per rank on the box's cores, 2000 random-origin bcasts."""
     exe = os.path.join(REPO, "oracle", "_ref", "ref_harness")
     mpiexec = "/opt/conda/bin/mpiexec"
     if not (os.path.exists(exe) and os.path.exists(mpiexec)):
@@ -285,10 +367,11 @@ def reference_datapoint(length):
     try:
         with tempfile.TemporaryDirectory() as td:
             out = os.path.join(td, "o.jsonl")
-            subprocess.run([mpiexec, "-n", "8", exe, out, "bench", "2000", str(length)], cwd=td, timeout=120,
-                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
+            subprocess.run(["timeout", "-k", "5", "100", mpiexec, "-n", str(ranks), exe, out, "bench", "2000",
+                            str(length)], cwd=td, timeout=120, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           check=True)
             rec = json.loads(open(out).read().splitlines()[0])
-            rec["cores"] = 8
+            rec["cores"] = ranks
             rec["kind"] = "reference"
             return rec
     except Exception as e:  # noqa: BLE001 - informative only
@@ -393,15 +476,10 @@ def main():
     rlo.abi.check(lib.rlo_stream_create(local, ctypes.byref(stream)), "rlo_stream_create")
 
     def step():
-        """one launch of the loaded program; every part reset before any part launches"""
-        w.reset(stream)
-        if dist is not None:
-            dist.barrier()
-        w.launch(stream, no_reset=True)
-        rc = w.wait(raise_on_device_error=False)
-        if dist is not None:
-            dist.barrier()  # no peer still stores into this part's rings
-        return rc, w.kernel_ms()
+        return _step(w, stream, dist)
+
+    def red(x, op):
+        return {"max": max_over_ranks, "sum": sum_over_ranks}[op](x)
 
     seed = 0x5EED
     w.program_storm(k, length, seed=seed)
@@ -497,14 +575,25 @@ def main():
             note("payload-size legs")
         extras["payload_sizes"] = size_legs(rlo, R, local, stream)
         ok &= all(s["verified"] for s in extras["payload_sizes"])
-    lib.rlo_stream_destroy(stream)
+    if not args.no_extras and world == 1:
+        if rank == 0:
+            note("small-world device legs (4 and 8 ranks)")
+        extras["small_worlds"] = small_n_legs(rlo, local, stream)
+        ok &= all(v["verified"] for v in extras["small_worlds"].values())
     if not args.no_bulk:
         if rank == 0:
-            note("bulk leg")
+            note("bulk leg (C3)")
         try:
-            extras["bulk"] = bulk_leg(dist, world, rank, local)
+            extras["bulk"] = bulk_leg(rlo, dist, world, rank, local, stream, red)
         except Exception as e:  # noqa: BLE001 - reported, never fails the headline line
             extras["bulk"] = {"error": repr(e)[:300]}
+        if rank == 0:
+            note("mixed-size leg (C5)")
+        try:
+            extras["c5_mixed"] = c5_leg(rlo, dist, world, rank, local, stream, red)
+        except Exception as e:  # noqa: BLE001
+            extras["c5_mixed"] = {"error": repr(e)[:300]}
+    lib.rlo_stream_destroy(stream)
     ok = bool(sum_over_ranks(0.0 if ok else 1.0) == 0.0)
 
     line = {

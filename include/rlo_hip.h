@@ -37,6 +37,7 @@ extern "C" {
 #define RLO_E_NODEVICE (-6)  /* no HIP device                                              */
 #define RLO_E_NOTCONNECTED (-7) /* part created but rlo_part_connect not called yet          */
 #define RLO_E_AGAIN (-8)     /* host-service ring full / nothing to do, retry after progress  */
+#define RLO_E_TIMEOUT (-9)   /* shared host service: the leader did not answer in time         */
 
 /* device error codes (rlo_rank_stats_t.error) */
 #define RLO_DERR_TIMEOUT 1
@@ -233,8 +234,44 @@ int rlo_device_count(void);
  * world (cross: parts span GPUs); pure host arithmetic (rlo_device.hpp bulk_plan) */
 typedef struct { uint32_t nchunks, stripe, chunk, tile, total_tiles, pad; } rlo_bulk_plan_t;
 int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out);
+/* the storm program's payload length of bcasts 0..k-1 (rlo_storm_cfg_t len, len_max, seed): the
+ * workload generator's host side, for byte accounting (no GPU) */
+int rlo_storm_lengths(uint64_t seed, uint64_t k, uint32_t len, uint32_t len_max, uint32_t* out);
 int rlo_host_bulk_stage(rlo_world_t* w, int rank, const void* data, uint64_t len, uint32_t timeout_us, uint32_t* q);
 int rlo_host_bulk_copy(rlo_world_t* w, int rank, const rlo_log_rec_t* ev, void* dst);
+
+/* ---- the shared host service (rlo_shm.hpp): ONE process per GPU owns a host-service part and
+ * its persistent kernel; the other rank processes of that part drive their ranks through a POSIX
+ * shared-memory segment and never create GPU queues (a GPU's hardware scheduler time-slices whole
+ * processes once more of them hold queues than it maps at once: DESIGN.md "one queue-holding
+ * process per GPU").
+ * Leader: rlo_host_share(name, stage bytes) BEFORE rlo_program_host (which then builds the host-side
+ * rings in the segment and registers it with HIP), rlo_reset, rlo_launch_ex, rlo_host_wait_started;
+ * once every client attached, rlo_host_unlink.  While the kernel runs, rlo_host_proxy must be called continuously
+ * (a service thread): it moves client commands into the part's VRAM command ring, the clients'
+ * pickup heads into the counters the kernel polls, and runs bulk copies for them.
+ * Client: rlo_client_attach(name, world rank) and the rlo_client_* calls, which mirror
+ * rlo_host_post / rlo_host_poll / rlo_host_cmd_count / rlo_host_bulk_stage / rlo_host_bulk_copy. */
+int rlo_host_share(rlo_world_t* w, const char* shm_name, uint64_t stage_bytes);
+int rlo_host_unlink(rlo_world_t* w);
+int rlo_host_proxy(rlo_world_t* w);  /* one pass; returns the number of actions taken (>= 0) */
+/* waits until every local rank's kernel workgroup serves (1), or RLO_E_TIMEOUT / RLO_E_DEVICE */
+int rlo_host_wait_started(rlo_world_t* w, uint32_t timeout_ms);
+/* marks the segment failed so clients stop waiting (engine setup aborted, kernel gone) */
+int rlo_host_fail(rlo_world_t* w);
+
+typedef struct rlo_client rlo_client_t;
+int rlo_client_attach(const char* shm_name, int rank, rlo_client_t** out);
+int rlo_client_detach(rlo_client_t* c);
+int rlo_client_state(rlo_client_t* c);  /* 0 not started, 1 serving, 2 exited, RLO_E_DEVICE */
+int rlo_client_post(rlo_client_t* c, const rlo_cmd_t* cmd, const void* payload, uint32_t len);
+int rlo_client_poll(rlo_client_t* c, rlo_log_rec_t* ev, void* payload, uint32_t cap);
+int rlo_client_cmd_count(rlo_client_t* c, uint64_t* consumed, uint64_t* posted);
+int rlo_client_bulk_put(rlo_client_t* c, const void* data, uint64_t len, uint32_t timeout_us, uint32_t* q);
+int rlo_client_bulk_get(rlo_client_t* c, const rlo_log_rec_t* ev, void* dst);
+/* diagnostics, 9 words: posted, forwarded, consumed, tail seen by the kernel, pickups consumed,
+ * pickups written, pickup head seen by the kernel, kernel iterations (/4096 beat), state */
+int rlo_client_debug(rlo_client_t* c, uint64_t* out);
 
 /* ------------------------------------------------------------------ run */
 int rlo_reset(rlo_world_t* w, void* stream);           /* zero this part's counters (sync) */

@@ -62,6 +62,9 @@ def lib():
         u32 = ctypes.c_uint32
         L.orc_storm2.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, i32p, i64p, u64p]
         L.orc_storm2.restype = ctypes.c_int64
+        L.orc_storm_mt.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, ctypes.c_int, i64p,
+                                   u64p]
+        L.orc_storm_mt.restype = ctypes.c_int64
         L.orc_storm_expected2.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, i64p, u64p]
         L.orc_storm_expected2.restype = ctypes.c_int64
         L.orc_len_of.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u32, u32]
@@ -141,6 +144,17 @@ def storm(n, seed, k, length, want_parent=False, len_max=0, order=0):
     if d < 0:
         raise RuntimeError("oracle storm failed")
     return {"deliveries": d, "count": count, "sum": ssum, "parent": parent.reshape(k, n) if want_parent else None}
+
+
+def storm_mt(n, seed, k, length, threads, len_max=0, order=0):
+    """orc_storm_mt: the storm on `threads` host threads (count / sum as storm())."""
+    count = np.zeros(n, dtype=np.int64)
+    ssum = np.zeros(n, dtype=np.uint64)
+    d = lib().orc_storm_mt(n, seed, k, length, max(length, len_max), order, threads, _p(count, ctypes.c_int64),
+                           _p(ssum, ctypes.c_uint64))
+    if d < 0:
+        raise RuntimeError("oracle storm_mt failed")
+    return {"deliveries": d, "count": count, "sum": ssum}
 
 
 def storm_expected(n, seed, k, length, len_max=0, order=0):

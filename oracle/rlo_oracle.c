@@ -9,9 +9,12 @@
  * receive order = arrival order, rootless_ops.c:656), which keeps MPI's
  * per-sender non-overtaking guarantee that the IAR protocol relies on.
  */
+#define _POSIX_C_SOURCE 200809L
 #include "rlo_oracle.h"
 #include "rlo_testvec.h"
 
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -340,6 +343,218 @@ int64_t orc_storm_expected2(int n, uint64_t seed, int64_t k, uint32_t len_lo, ui
 
 int64_t orc_storm_expected(int n, uint64_t seed, int64_t k, uint32_t len, int64_t* count, uint64_t* sum) {
     return orc_storm_expected2(n, seed, k, len, len, 0, count, sum);
+}
+
+/* ------------------------------------------------------------------ storm on host threads */
+
+/* orc_storm2 on T threads.  Rank r is progressed by thread r % T only (its origination list, its
+ * deliveries, its count / sum).  A forward copies the bytes into the sending thread's outgoing
+ * batch for the receiving thread (one batch per thread pair per sweep, handed over under that
+ * thread's inbox lock): every tree edge still copies the payload, as an MPI send does. */
+typedef struct {
+    int32_t origin, from, to, id;
+    uint32_t len;
+    uint64_t off, cs; /* bytes at batch.bytes + off (ring-sized messages); cs for bulk ones */
+} mt_msg;
+
+typedef struct mt_batch {
+    mt_msg* m;
+    size_t n, cap;
+    uint8_t* bytes;
+    size_t nb, bcap;
+    struct mt_batch* next;
+} mt_batch;
+
+typedef struct {
+    pthread_mutex_t mu;
+    mt_batch* head;
+} mt_inbox;
+
+typedef struct {
+    int n, nthr, tid;
+    uint64_t seed;
+    uint32_t lo, hi;
+    const topo_t* t;
+    const int64_t *off, *ids;
+    const int* owner; /* thread of each rank */
+    mt_inbox* in;
+    atomic_llong* delivered;
+    int64_t want;
+    int64_t* count;
+    uint64_t* sum;
+    int err;
+} mt_arg;
+
+static int mt_put(mt_batch* b, int to, int from, int origin, int id, uint32_t len, const uint8_t* data, uint64_t cs) {
+    if (b->n == b->cap) {
+        size_t nc = b->cap ? 2 * b->cap : 256;
+        mt_msg* nm = realloc(b->m, nc * sizeof(mt_msg));
+        if (!nm) return -1;
+        b->m = nm;
+        b->cap = nc;
+    }
+    mt_msg* m = &b->m[b->n++];
+    *m = (mt_msg){origin, from, to, id, len, b->nb, cs};
+    if (data && len) {
+        if (b->nb + len > b->bcap) {
+            size_t nc = b->bcap ? 2 * b->bcap : 65536;
+            while (nc < b->nb + len) nc *= 2;
+            uint8_t* nb = realloc(b->bytes, nc);
+            if (!nb) return -1;
+            b->bytes = nb;
+            b->bcap = nc;
+        }
+        memcpy(b->bytes + b->nb, data, len);
+        b->nb += len;
+    }
+    return 0;
+}
+
+static void mt_forward(mt_arg* a, mt_batch** out, int me, int origin, int from, int id, uint32_t len,
+                       const uint8_t* data, uint64_t cs) {
+    int kids[ORC_MAX_FANOUT];
+    int kk = children_t(&a->t[me], me, origin, from, kids);
+    for (int i = 0; i < kk; i++) {
+        mt_batch* b = out[a->owner[kids[i]]];
+        a->err |= mt_put(b, kids[i], me, origin, id, len, data, cs);
+    }
+}
+
+static mt_batch* mt_take(mt_batch** pool) { /* recycled batches keep their buffers (no page faults) */
+    mt_batch* b = *pool;
+    if (!b) return calloc(1, sizeof(mt_batch));
+    *pool = b->next;
+    b->n = b->nb = 0;
+    b->next = NULL;
+    return b;
+}
+
+static void mt_free_list(mt_batch* b) {
+    while (b) {
+        mt_batch* nx = b->next;
+        free(b->m); free(b->bytes); free(b);
+        b = nx;
+    }
+}
+
+static void* mt_worker(void* vp) {
+    mt_arg* a = (mt_arg*)vp;
+    const int T = a->nthr;
+    mt_batch* pool = NULL;
+    /* a contiguous block of ranks per thread: every block holds the same mix of tree levels (a
+     * strided deal would give one thread every multiple of T, the skip ring's interior ranks) */
+    const int r0 = (int)((int64_t)a->tid * a->n / T), r1 = (int)((int64_t)(a->tid + 1) * a->n / T);
+    int64_t* count = calloc(a->n, sizeof(int64_t)); /* thread-private: no false sharing between */
+    uint64_t* sum = calloc(a->n, sizeof(uint64_t)); /* neighbouring ranks of different threads */
+    uint8_t* buf = malloc(a->hi ? a->hi : 1);
+    int64_t* next = calloc(a->n, sizeof(int64_t));
+    mt_batch** out = calloc(T, sizeof(mt_batch*));
+    for (int j = 0; j < T; j++) out[j] = mt_take(&pool);
+    mt_batch* local = NULL; /* batches from this thread to itself, processed next sweep */
+    while (atomic_load_explicit(a->delivered, memory_order_relaxed) < a->want && !a->err) {
+        for (int r = r0; r < r1; r++) /* originate one per rank (RLO_bcast_gen :1581) */
+            if (a->off[r] + next[r] < a->off[r + 1]) {
+                uint32_t bid = (uint32_t)a->ids[a->off[r] + next[r]++];
+                uint32_t len = rlo_tv_len(a->seed, bid, a->lo, a->hi);
+                rlo_tv_payload(r, bid, buf, len);
+                if (len > ORC_COPY_MAX)
+                    mt_forward(a, out, r, r, -1, (int)bid, len, NULL, orc_msg_checksum(r, bid, ORC_BCAST, buf, len));
+                else
+                    mt_forward(a, out, r, r, -1, (int)bid, len, buf, 0);
+            }
+        pthread_mutex_lock(&a->in[a->tid].mu); /* take everything sent to my ranks */
+        mt_batch* got = a->in[a->tid].head;
+        a->in[a->tid].head = NULL;
+        pthread_mutex_unlock(&a->in[a->tid].mu);
+        if (local) { local->next = got; got = local; local = NULL; }
+        int64_t mine = 0;
+        while (got) { /* receive, deliver (pickup), forward (make_progress_gen :569-624) */
+            mt_batch* b = got;
+            got = b->next;
+            for (size_t i = 0; i < b->n; i++) {
+                const mt_msg* m = &b->m[i];
+                const uint8_t* d = m->len && m->len <= ORC_COPY_MAX ? b->bytes + m->off : NULL;
+                mine++;
+                count[m->to]++;
+                sum[m->to] += d || m->len == 0 ? orc_msg_checksum(m->origin, m->id, ORC_BCAST, d, m->len) : m->cs;
+                mt_forward(a, out, m->to, m->origin, m->from, m->id, m->len, d, m->cs);
+            }
+            b->next = pool;
+            pool = b;
+        }
+        for (int j = 0; j < T; j++) { /* hand the outgoing batches over */
+            mt_batch* b = out[j];
+            if (!b->n) continue;
+            out[j] = mt_take(&pool);
+            if (j == a->tid) { local = b; continue; }
+            pthread_mutex_lock(&a->in[j].mu);
+            b->next = a->in[j].head;
+            a->in[j].head = b;
+            pthread_mutex_unlock(&a->in[j].mu);
+        }
+        if (mine) atomic_fetch_add_explicit(a->delivered, mine, memory_order_relaxed);
+    }
+    for (int j = 0; j < T; j++) {
+        if (out[j]->n) a->err = 1; /* nothing may be left unsent */
+        free(out[j]->m); free(out[j]->bytes); free(out[j]);
+    }
+    if (local) { a->err = 1; mt_free_list(local); }
+    for (int r = r0; r < r1; r++) {
+        a->count[r] = count[r];
+        a->sum[r] = sum[r];
+    }
+    free(count); free(sum);
+    mt_free_list(pool);
+    free(out); free(buf); free(next);
+    return NULL;
+}
+
+int64_t orc_storm_mt(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order, int threads,
+                     int64_t* count, uint64_t* sum) {
+    if (n < 2 || k < 0 || threads < 1 || !count || !sum) return -1;
+    if (threads > n) threads = n;
+    if (len_hi < len_lo) len_hi = len_lo;
+    topo_t* t = malloc(n * sizeof(topo_t));
+    mt_inbox* in = calloc(threads, sizeof(mt_inbox));
+    int64_t* off = calloc(n + 1, sizeof(int64_t));
+    int64_t* fill = calloc(n, sizeof(int64_t));
+    int64_t* ids = malloc((k ? k : 1) * sizeof(int64_t));
+    for (int r = 0; r < n; r++) {
+        topo_init(n, r, &t[r]);
+        count[r] = 0;
+        sum[r] = 0;
+    }
+    for (int i = 0; i < threads; i++) pthread_mutex_init(&in[i].mu, NULL);
+    for (int64_t b = 0; b < k; b++) off[rlo_tv_origin2(seed, b, n, order) + 1]++;
+    for (int r = 0; r < n; r++) off[r + 1] += off[r];
+    for (int64_t b = 0; b < k; b++) {
+        uint32_t o = rlo_tv_origin2(seed, b, n, order);
+        ids[off[o] + fill[o]++] = b;
+    }
+    int* owner = malloc(n * sizeof(int));
+    for (int i = 0; i < threads; i++)
+        for (int r = (int)((int64_t)i * n / threads); r < (int)((int64_t)(i + 1) * n / threads); r++) owner[r] = i;
+    atomic_llong delivered = 0;
+    mt_arg* args = calloc(threads, sizeof(mt_arg));
+    pthread_t* th = malloc(threads * sizeof(pthread_t));
+    for (int i = 0; i < threads; i++) {
+        args[i] = (mt_arg){n, threads, i, seed, len_lo, len_hi, t, off, ids, owner, in, &delivered, k * (int64_t)(n - 1),
+                           count, sum, 0};
+        pthread_create(&th[i], NULL, mt_worker, &args[i]);
+    }
+    int err = 0;
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        err |= args[i].err;
+    }
+    for (int i = 0; i < threads; i++) {
+        if (in[i].head) err = 1; /* nothing may be left in flight */
+        mt_free_list(in[i].head);
+        pthread_mutex_destroy(&in[i].mu);
+    }
+    int64_t d = atomic_load(&delivered);
+    free(t); free(in); free(off); free(fill); free(ids); free(args); free(th); free(owner);
+    return err ? -1 : d;
 }
 
 uint32_t orc_len_of(uint64_t seed, uint64_t bid, uint32_t lo, uint32_t hi) { return rlo_tv_len(seed, bid, lo, hi); }

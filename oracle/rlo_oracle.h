@@ -59,6 +59,11 @@ int64_t orc_storm2(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t le
 int64_t orc_storm_expected2(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order,
                             int64_t* count, uint64_t* sum);
 uint32_t orc_len_of(uint64_t seed, uint64_t bid, uint32_t lo, uint32_t hi);
+/* orc_storm2's workload on `threads` host threads (bench.py's multi-core cpu_baseline leg): the ranks
+ * are dealt to the threads, every rank's inbox is a mutex-guarded FIFO, and every tree edge copies
+ * the bytes (malloc + memcpy, an MPI send).  Same count / sum outputs (parents are not recorded). */
+int64_t orc_storm_mt(int n, uint64_t seed, int64_t k, uint32_t len_lo, uint32_t len_hi, uint32_t order, int threads,
+                     int64_t* count, uint64_t* sum);
 uint32_t orc_origin_of2(uint64_t seed, uint64_t bid, uint32_t n, uint32_t order);
 
 /* ---- IAR (proposal / vote / decision): rootless_ops.c:668-917, :1036-1070 */

@@ -63,6 +63,8 @@ enum HostCmd : uint32_t { CMD_JUDGE = 16, CMD_OWN_JUDGE = 17, CMD_QUIT = 18, CMD
 // per local rank, 64 host words (one 128-B line per counter)
 constexpr int kHctlWords = 64;
 constexpr int kHctlInjTail = 0, kHctlInjHead = 16, kHctlPkTail = 32, kHctlPkHead = 48;
+constexpr int kHctlState = 40;  // device-written: 1 once the rank's workgroup serves, 2 once it exited
+constexpr int kHctlBeat = 41;   // device-written heartbeat: [41] iterations, [42] command tail seen, [43] pickup head seen
 
 enum Judge : uint32_t { JUDGE_APPROVE = 0, JUDGE_MASK = 1, JUDGE_ISP = 2, JUDGE_HASH = 3 };
 

@@ -947,6 +947,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
     }
     BAR();
+    if (host && tid == 0) pub64_sys(&hctl[kHctlState], 1ull);  // serving (rlo_host_wait_started)
     const uint64_t t_start = now_ticks();
     unsigned long long acc_sum = 0;  // checksum of delivered bcast chunks (this thread's share)
 
@@ -1032,6 +1033,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
             S.snap[3][lane] = vout_head_r; p_h = hpoll; p_lat = latr;
+            // host mode: a heartbeat for the host's watchdog every 4096 iterations (what this rank's
+            // wave 0 last saw of its command tail / pickup head, and how far it got)
+            if (host && (n_iter & 4095u) == 0 && lane < 3) pub64_sys(&hctl[kHctlBeat + lane], lane == 2 ? n_iter : hpoll);
             if constexpr (BULK) {
                 // my heap slots' release counts, and which pending receptions are complete
                 if (lane < (int)bsl) {
@@ -2149,6 +2153,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         st.t_end = now_ticks();
         st.error = S.error;
         st.error_aux = S.error_aux;
+        if (host) pub64_sys(&hctl[kHctlState], 2ull);  // this rank stopped serving
     }
 }
 

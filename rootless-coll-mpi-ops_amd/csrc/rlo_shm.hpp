@@ -1,0 +1,78 @@
+// rlo_shm.hpp -- the shared host service: the host side of a host-service part (rlo_program_host)
+// in a POSIX shared-memory segment, so that rank processes with NO HIP context of their own can
+// drive their ranks of a part that another process (the GPU's leader) owns and runs.
+//
+// Why: a persistent kernel per rank process means one set of hardware queues per process.  Once
+// more processes hold queues on a GPU than its hardware scheduler maps at once, it time-slices
+// whole processes and every persistent kernel stalls for whole quanta (profiles/
+// r2_probe_oversub.txt: 8 rank processes 0.42 s, 8 beside one idle torch process 1.33 s, 9 rank
+// processes 38-48 s, 12 rank processes > 60 s for the same 8-rank-style iar run).  With the shared
+// service exactly one process per GPU holds queues, whatever the rank count.
+//
+// Segment layout (page-aligned regions, sizes in the header so a client derives them):
+//   header page | hctl [nl][kHctlWords] (device-written counters) | ev [nl][pk_cap] LogRec |
+//   evp [nl][pk_cap][max_payload] | cli [nl] ClientBox | cmd [nl][cmd_cap][stride] |
+//   stage [nl][stage_bytes]
+// The leader registers the whole segment with HIP (the kernel writes hctl / ev / evp; the proxy
+// DMAs bulk bytes through stage).  A client writes its commands into `cmd` and its counters into
+// its ClientBox; the leader's proxy (rlo_host_proxy) moves commands into the part's VRAM command
+// ring and the pickup head into the VRAM counter the kernel polls, and runs bulk copies between
+// `stage` and the heap on the client's behalf.
+#pragma once
+#include <cstdint>
+
+#include "rlo_device.hpp"
+
+namespace rlo {
+
+constexpr uint32_t kShmMagic = 0x534f4c52u;  // "RLOS"
+constexpr uint32_t kShmVersion = 1;
+
+enum ShmOp : uint32_t { SHM_OP_NONE = 0, SHM_OP_ACQUIRE = 1, SHM_OP_PUT = 2, SHM_OP_GET = 3 };
+
+struct ShmHdr {
+    uint32_t magic, version;
+    uint32_t nl, rb;                 // local ranks of the part, first world rank
+    uint32_t n, bslots;              // world size, bulk heap slots per (receiver, origin)
+    uint32_t cmd_cap, pk_cap;        // ring capacities per rank
+    uint32_t stride, max_payload;    // command slot stride, pickup payload stride
+    uint64_t bulk_max, stage_bytes;  // bulk message cap; staging window per rank
+    uint64_t off_hctl, off_ev, off_evp, off_cli, off_cmd, off_stage, total;
+    uint32_t leader_failed, pad;     // the leader gave up (its kernel could not start / ended early)
+};
+
+// one per local rank; the two sides' words on separate 128-byte lines
+struct ClientBox {
+    alignas(128) uint64_t mtail;  // client: commands written into its `cmd` ring
+    alignas(128) uint64_t mpk;    // client: pickup events consumed
+    alignas(128) uint64_t req;    // client: bulk request sequence (request fields below valid)
+    uint32_t op, arg;             // ShmOp; ACQUIRE -, PUT q, GET origin << 8 | heap slot
+    uint64_t off, len;            // byte range of the message this request moves via `stage`
+    alignas(128) uint64_t ack;    // leader: last request completed
+    int64_t rc;                   // RLO_OK / RLO_E_AGAIN (ACQUIRE: slot still busy) / error
+    uint64_t q;                   // ACQUIRE: the bulk sequence taken
+    uint64_t fwd;                 // leader: commands forwarded into the VRAM ring (diagnostics)
+};
+static_assert(sizeof(ClientBox) == 512, "ClientBox layout");
+
+struct ShmLayout {
+    uint64_t hctl, ev, evp, cli, cmd, stage, total;
+};
+
+inline uint64_t shm_page(uint64_t x) { return (x + 4095u) & ~uint64_t(4095); }
+
+inline ShmLayout shm_layout(uint32_t nl, uint32_t cmd_cap, uint32_t pk_cap, uint32_t stride, uint32_t max_payload,
+                            uint64_t stage_bytes) {
+    ShmLayout L;
+    uint64_t o = 4096;  // header page
+    L.hctl = o; o = shm_page(o + (uint64_t)nl * kHctlWords * 8);
+    L.ev = o; o = shm_page(o + (uint64_t)nl * pk_cap * sizeof(LogRec));
+    L.evp = o; o = shm_page(o + (uint64_t)nl * pk_cap * max_payload);
+    L.cli = o; o = shm_page(o + (uint64_t)nl * sizeof(ClientBox));
+    L.cmd = o; o = shm_page(o + (uint64_t)nl * cmd_cap * stride);
+    L.stage = o; o = shm_page(o + (uint64_t)nl * stage_bytes);
+    L.total = o;
+    return L;
+}
+
+}  // namespace rlo

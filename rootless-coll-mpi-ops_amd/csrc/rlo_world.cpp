@@ -2,7 +2,10 @@
 // the mailbox rings, parts (one per process / GPU) and their connection through hipIpc,
 // programs (storm / latency / iar), launch and result readout.  Exposes the C ABI of
 // include/rlo_hip.h.
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -13,10 +16,12 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rlo_device.hpp"
 #include "rlo_hip.h"
+#include "rlo_shm.hpp"
 
 // variant: 8 = 8-wave, 4 = 4-wave, 5 = 4-wave with bulk messages (rlo_kernel.hip)
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant);
@@ -319,6 +324,15 @@ struct rlo_world {
     uint8_t* h_evp = nullptr;       // [nl][pk_cap][max_payload]
     uint32_t cmd_cap = 0, pk_cap = 0;
     std::vector<uint64_t> cmd_tail, pk_head;  // host-side copies of the counters it owns
+    // shared host service (rlo_host_share): h_ctl / h_ev / h_evp live in a POSIX shared-memory
+    // segment registered with HIP; d_hctl / d_ev / d_evp are the kernel's addresses of them
+    uint8_t* shm = nullptr;
+    uint64_t shm_bytes = 0;
+    std::string shm_name;
+    bool shm_linked = false;
+    rlo::ShmLayout SL{};
+    std::vector<uint64_t> cli_req;  // last bulk request served per local rank
+    uint64_t share_stage = 0;       // rlo_host_share called: rlo_program_host builds the segment
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
     size_t dyn_lds = 0;
@@ -481,6 +495,7 @@ const char* rlo_strerror(int code) {
         case RLO_E_NODEVICE: return "no HIP device";
         case RLO_E_NOTCONNECTED: return "part not connected";
         case RLO_E_AGAIN: return "ring full, retry";
+        case RLO_E_TIMEOUT: return "shared host service: no answer in time";
         default: return "unknown";
     }
 }
@@ -717,6 +732,8 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
     return RLO_OK;
 }
 
+static void host_free(rlo_world* w);
+
 int rlo_world_destroy(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
     (void)hipSetDevice(w->device);
@@ -734,11 +751,7 @@ int rlo_world_destroy(rlo_world_t* w) {
     w->d_lat_count.release(); w->d_lat_round.release(); w->d_lat_origin.release(); w->d_prop_pid.release();
     w->d_lat_out.release(); w->d_lat_own_off.release(); w->d_lat_own.release(); w->d_mask.release(); w->d_prop_data.release(); w->d_log_payload.release();
     w->d_isp.release(); w->d_log.release();
-    if (w->h_cmd) (void)hipFree(w->h_cmd);
-    if (w->d_ctl) (void)hipFree(w->d_ctl);
-    if (w->h_ctl) (void)hipHostFree(w->h_ctl);
-    if (w->h_ev) (void)hipHostFree(w->h_ev);
-    if (w->h_evp) (void)hipHostFree(w->h_evp);
+    host_free(w);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
     delete w;
@@ -1005,9 +1018,17 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
 static void host_free(rlo_world* w) {
     if (w->h_cmd) (void)hipFree(w->h_cmd);
     if (w->d_ctl) (void)hipFree(w->d_ctl);
-    if (w->h_ctl) (void)hipHostFree(w->h_ctl);
-    if (w->h_ev) (void)hipHostFree(w->h_ev);
-    if (w->h_evp) (void)hipHostFree(w->h_evp);
+    if (w->shm) {  // h_ctl / h_ev / h_evp point into the segment
+        (void)hipHostUnregister(w->shm);
+        munmap(w->shm, (size_t)w->shm_bytes);
+        if (w->shm_linked) shm_unlink(w->shm_name.c_str());
+        w->shm = nullptr;
+        w->shm_linked = false;
+    } else {
+        if (w->h_ctl) (void)hipHostFree(w->h_ctl);
+        if (w->h_ev) (void)hipHostFree(w->h_ev);
+        if (w->h_evp) (void)hipHostFree(w->h_evp);
+    }
     w->h_cmd = nullptr; w->d_ctl = nullptr; w->h_ctl = nullptr; w->h_ev = nullptr; w->h_evp = nullptr;
 }
 
@@ -1030,6 +1051,62 @@ static int host_alloc(void** p, size_t bytes) {
     return RLO_OK;
 }
 
+// rlo_host_share's segment (rlo_shm.hpp), built by rlo_program_host once the ring sizes are known:
+// created, mapped, registered with HIP (fine-grained: the kernel's counter / event stores reach the
+// clients' polls directly) and described in its header for the clients
+static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec** dev_ev, const uint8_t** dev_evp) {
+    const uint32_t nl = (uint32_t)w->nl;
+    const uint64_t stage = w->L.bulk_max ? w->share_stage : 0;
+    const rlo::ShmLayout L = rlo::shm_layout(nl, w->cmd_cap, w->pk_cap, w->L.stride, w->max_payload, stage);
+    const char* name = w->shm_name.c_str();
+    const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) return RLO_E_INVAL;
+    if (ftruncate(fd, (off_t)L.total) != 0) { close(fd); shm_unlink(name); return RLO_E_INVAL; }
+    void* p = mmap(nullptr, (size_t)L.total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) { shm_unlink(name); return RLO_E_INVAL; }
+    // MTYPE_UC (hipExtHostRegisterUncached), as hipHostMallocCoherent: the kernel's counter / event stores
+    // must not linger in its L2 (a default registration showed ms-long delays per pickup)
+    hipError_t e = hipHostRegister(p, (size_t)L.total, hipHostRegisterMapped | hipExtHostRegisterUncached);
+    void* dp = nullptr;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
+    if (e != hipSuccess) {
+        g_last_hip = (int)e;
+        munmap(p, (size_t)L.total);
+        shm_unlink(name);
+        return RLO_E_HIP;
+    }
+    uint8_t* b = (uint8_t*)p;
+    uint8_t* db = (uint8_t*)dp;
+    w->shm = b;
+    w->shm_bytes = L.total;
+    w->shm_linked = true;
+    w->SL = L;
+    w->h_ctl = (uint64_t*)(b + L.hctl);
+    w->h_ev = (rlo::LogRec*)(b + L.ev);
+    w->h_evp = b + L.evp;
+    w->cli_req.assign(nl, 0);
+    *dev_hctl = (const uint64_t*)(db + L.hctl);
+    *dev_ev = (const rlo::LogRec*)(db + L.ev);
+    *dev_evp = db + L.evp;
+    rlo::ShmHdr* h = (rlo::ShmHdr*)b;
+    h->version = rlo::kShmVersion;
+    h->nl = nl;
+    h->rb = (uint32_t)w->rb;
+    h->n = (uint32_t)w->L.n;
+    h->bslots = w->L.bslots;
+    h->cmd_cap = w->cmd_cap;
+    h->pk_cap = w->pk_cap;
+    h->stride = w->L.stride;
+    h->max_payload = w->max_payload;
+    h->bulk_max = w->L.bulk_max;
+    h->stage_bytes = stage;
+    h->off_hctl = L.hctl; h->off_ev = L.ev; h->off_evp = L.evp; h->off_cli = L.cli; h->off_cmd = L.cmd;
+    h->off_stage = L.stage; h->total = L.total;
+    __atomic_store_n(&h->magic, rlo::kShmMagic, __ATOMIC_RELEASE);  // clients check it last
+    return RLO_OK;
+}
+
 int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     if (!w) return RLO_E_INVAL;
     if (!w->connected) return RLO_E_NOTCONNECTED;
@@ -1041,9 +1118,19 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     w->cmd_cap = cc;
     w->pk_cap = pc;
     const size_t nl = (size_t)w->nl;
-    if (bar_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) || bar_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8) ||
-        host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
-        host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) || host_alloc((void**)&w->h_evp, nl * pc * w->max_payload)) {
+    if (bar_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) || bar_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8)) {
+        host_free(w);
+        return RLO_E_HIP;
+    }
+    const uint64_t* dev_hctl = nullptr;
+    const rlo::LogRec* dev_ev = nullptr;
+    const uint8_t* dev_evp = nullptr;
+    if (!w->shm_name.empty()) {  // rlo_host_share: the host-side rings in the shared segment
+        int rc = shm_build(w, &dev_hctl, &dev_ev, &dev_evp);
+        if (rc) { host_free(w); return rc; }
+    } else if (host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
+               host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) ||
+               host_alloc((void**)&w->h_evp, nl * pc * w->max_payload)) {
         host_free(w);
         return RLO_E_HIP;
     }
@@ -1052,13 +1139,13 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     base_params(w);
     rlo::Params& P = w->P;
     P.mode = rlo::MODE_HOST | rlo::MODE_IAR;
-    P.log = w->h_ev;
+    P.log = dev_ev ? const_cast<rlo::LogRec*>(dev_ev) : w->h_ev;
     P.log_cap = pc;
-    P.log_payload = w->h_evp;
+    P.log_payload = dev_evp ? const_cast<uint8_t*>(dev_evp) : w->h_evp;
     P.log_stride = w->max_payload;
     P.hin = w->h_cmd;
     P.hin_cap = cc;
-    P.hctl = w->h_ctl;
+    P.hctl = dev_hctl ? const_cast<uint64_t*>(dev_hctl) : w->h_ctl;
     P.hctl_dev = w->d_ctl;
     const uint64_t idle = cfg ? cfg->idle_timeout_s : 0;
     P.timeout_ticks = idle ? 100000000ull * idle : ~0ull >> 2;
@@ -1139,6 +1226,11 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     if (w->have_program && (w->P.mode & rlo::MODE_HOST)) {  // the kernel is not running: rings restart at 0
         std::memset(w->h_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
         std::memset(w->d_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
+        if (w->shm) {  // shared service: the clients' boxes restart too
+            std::memset(w->shm + w->SL.cli, 0, (size_t)w->nl * sizeof(rlo::ClientBox));
+            std::fill(w->cli_req.begin(), w->cli_req.end(), 0);
+            __atomic_store_n(&((rlo::ShmHdr*)w->shm)->leader_failed, 0u, __ATOMIC_RELEASE);
+        }
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
         std::fill(w->cmd_tail.begin(), w->cmd_tail.end(), 0);
         std::fill(w->pk_head.begin(), w->pk_head.end(), 0);
@@ -1316,6 +1408,13 @@ int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out) {
     return RLO_OK;
 }
 
+int rlo_storm_lengths(uint64_t seed, uint64_t k, uint32_t len, uint32_t len_max, uint32_t* out) {
+    if (!out && k) return RLO_E_INVAL;
+    const uint32_t hi = len_max > len ? len_max : len;
+    for (uint64_t b = 0; b < k; b++) out[b] = hi > len ? rlo::storm_len_of(seed, b, len, hi) : len;
+    return RLO_OK;
+}
+
 int rlo_host_bulk_stage(rlo_world_t* w, int rank, const void* data, uint64_t len, uint32_t timeout_us, uint32_t* q_out) {
     if (!w || !w->h_cmd || !w->L.bulk_max || rank < w->rb || rank >= w->rb + w->nl || !q_out) return RLO_E_INVAL;
     if (len == 0 || len > w->L.bulk_max || (len && !data)) return RLO_E_INVAL;
@@ -1347,6 +1446,128 @@ int rlo_host_bulk_copy(rlo_world_t* w, int rank, const rlo_log_rec_t* ev, void* 
     const uint8_t* src = w->heap + (((uint64_t)lr * w->L.n + (uint64_t)ev->origin) * w->L.bslots + ev->aux) * w->L.bcap;
     HIPCHK(hipMemcpy(dst, src, ev->len, hipMemcpyDeviceToHost));
     return RLO_OK;
+}
+
+// ====================================================================== shared host service
+
+int rlo_host_share(rlo_world_t* w, const char* name, uint64_t stage_bytes) {
+    // before rlo_program_host: that call builds the segment.  (Replacing pinned rings afterwards
+    // would mean a hipHostFree, which waits for the whole device -- i.e. for the persistent kernel
+    // of another engine of this process.)
+    if (!w || !name || name[0] != '/' || std::strlen(name) > 200 || w->have_program || w->shm) return RLO_E_INVAL;
+    if (stage_bytes == 0) stage_bytes = 4ull << 20;
+    w->share_stage = (stage_bytes + 4095u) & ~uint64_t(4095);
+    w->shm_name = name;
+    return RLO_OK;
+}
+
+int rlo_host_unlink(rlo_world_t* w) {
+    if (!w || !w->shm) return RLO_E_INVAL;
+    if (w->shm_linked) shm_unlink(w->shm_name.c_str());
+    w->shm_linked = false;
+    return RLO_OK;
+}
+
+int rlo_host_fail(rlo_world_t* w) {
+    if (!w || !w->shm) return RLO_E_INVAL;
+    __atomic_store_n(&((rlo::ShmHdr*)w->shm)->leader_failed, 1u, __ATOMIC_RELEASE);
+    return RLO_OK;
+}
+
+int rlo_host_wait_started(rlo_world_t* w, uint32_t timeout_ms) {
+    if (!w || !w->h_ctl) return RLO_E_INVAL;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        int up = 0;
+        for (int lr = 0; lr < w->nl; lr++)
+            up += __atomic_load_n(&w->h_ctl[(size_t)lr * rlo::kHctlWords + rlo::kHctlState], __ATOMIC_ACQUIRE) != 0;
+        if (up == w->nl) return RLO_OK;
+        const int r = rlo_host_running(w);
+        if (r != 1) return RLO_E_DEVICE;  // the kernel already ended (or the launch failed)
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return RLO_E_TIMEOUT;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
+// One pass of the leader's proxy over its clients (rlo_shm.hpp).
+int rlo_host_proxy(rlo_world_t* w) {
+    if (!w || !w->shm) return RLO_E_INVAL;
+    int acted = 0;
+    const uint32_t cc = w->cmd_cap, stride = w->L.stride;
+    for (int lr = 0; lr < w->nl; lr++) {
+        rlo::ClientBox* box = (rlo::ClientBox*)(w->shm + w->SL.cli) + lr;
+        uint64_t* dctl = w->d_ctl + (size_t)lr * rlo::kHctlWords;
+        // commands: the client's shared ring -> the VRAM ring the kernel polls locally.  The client
+        // admitted each one only with room in its ring (mtail - device head < cmd_cap), which is
+        // room in the VRAM ring too (it holds [device head, copied) of the same sequence)
+        const uint64_t mt = __atomic_load_n(&box->mtail, __ATOMIC_ACQUIRE);
+        uint64_t c = w->cmd_tail[lr];
+        if (mt != c) {
+            const uint8_t* src = w->shm + w->SL.cmd + (size_t)lr * cc * stride;
+            uint8_t* dst = w->h_cmd + (size_t)lr * cc * stride;
+            for (; c != mt; c++) {
+                const size_t off = (size_t)(c & (cc - 1)) * stride;
+                uint32_t hdr2;
+                std::memcpy(&hdr2, src + off + 8, 4);
+                const size_t nb = std::min<size_t>(stride, ((rlo::kHdr + (hdr2 & 0xffffffu)) + 15) & ~(size_t)15);
+                std::memcpy(dst + off, src + off, nb);
+            }
+            w->cmd_tail[lr] = mt;
+            box->fwd = mt;
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);  // BAR stores may be write-combined: slots before tail
+            __atomic_store_n(&dctl[rlo::kHctlInjTail], mt, __ATOMIC_RELEASE);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            acted++;
+        }
+        const uint64_t pk = __atomic_load_n(&box->mpk, __ATOMIC_ACQUIRE);
+        if (pk != w->pk_head[lr]) {  // pickup events the client consumed: room for the kernel
+            w->pk_head[lr] = pk;
+            __atomic_store_n(&dctl[rlo::kHctlPkHead], pk, __ATOMIC_RELEASE);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            acted++;
+        }
+        const uint64_t rq = __atomic_load_n(&box->req, __ATOMIC_ACQUIRE);
+        if (rq == w->cli_req[lr]) continue;
+        w->cli_req[lr] = rq;  // one bulk request: ACQUIRE a heap slot, or move bytes through stage
+        int64_t rc = RLO_OK;
+        const int rank = w->rb + lr;
+        uint8_t* stage = w->shm + w->SL.stage + (size_t)lr * ((rlo::ShmHdr*)w->shm)->stage_bytes;
+        const uint32_t B = w->L.bslots;
+        if (!w->L.bulk_max) {
+            rc = RLO_E_INVAL;
+        } else if (box->op == rlo::SHM_OP_ACQUIRE) {
+            const uint32_t q = w->host_bulk_q[lr], s = q & (B - 1u);
+            const uint64_t need = (uint64_t)(q / B) * (uint64_t)(w->L.n - 1);
+            const volatile uint64_t* done = reinterpret_cast<const volatile uint64_t*>(
+                w->bflag + ((uint64_t)w->nl * w->L.n * B + (uint64_t)lr * B + s) * rlo::kBulkLine);
+            if (*done >= need) {
+                w->host_bulk_q[lr] = q + 1;
+                box->q = q;
+            } else {
+                rc = RLO_E_AGAIN;  // receivers still hold the slot's previous message
+            }
+        } else if (box->op == rlo::SHM_OP_PUT || box->op == rlo::SHM_OP_GET) {
+            const bool put = box->op == rlo::SHM_OP_PUT;
+            const uint32_t origin = put ? (uint32_t)rank : box->arg >> 8;
+            const uint32_t s = put ? (box->arg & (B - 1u)) : (box->arg & 0xffu);
+            const uint64_t off = box->off, len = box->len;
+            if (origin >= (uint32_t)w->L.n || s >= B || len > ((rlo::ShmHdr*)w->shm)->stage_bytes || off + len > w->L.bulk_max) {
+                rc = RLO_E_INVAL;
+            } else {
+                uint8_t* slot = w->heap + (((uint64_t)lr * w->L.n + origin) * B + s) * w->L.bcap + off;
+                hipError_t e = hipSetDevice(w->device);
+                if (e == hipSuccess)
+                    e = put ? hipMemcpy(slot, stage, len, hipMemcpyHostToDevice) : hipMemcpy(stage, slot, len, hipMemcpyDeviceToHost);
+                if (e != hipSuccess) { g_last_hip = (int)e; rc = RLO_E_HIP; }
+            }
+        } else {
+            rc = RLO_E_INVAL;
+        }
+        box->rc = rc;
+        __atomic_store_n(&box->ack, rq, __ATOMIC_RELEASE);
+        acted++;
+    }
+    return acted;
 }
 
 }  // extern "C"

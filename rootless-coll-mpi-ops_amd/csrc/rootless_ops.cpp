@@ -20,12 +20,14 @@
 #include <cstdlib>
 #include <ctime>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <deque>
 #include <map>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <utility>
 #include <vector>
 
@@ -72,9 +74,12 @@ struct RawEv {  // a pickup-ring event pulled off the device, not yet handled on
 
 struct progress_engine {
     MPI_Comm comm = MPI_COMM_NULL;
+    MPI_Comm group = MPI_COMM_NULL;  // the ranks sharing my GPU (one part of the device world)
     int rank = 0, size = 0, id = 0, device = 0;
-    rlo_world_t* w = nullptr;
-    void* stream = nullptr;
+    bool leader = false;             // group rank 0: owns the part, its kernel and the proxy
+    rlo_world_t* w = nullptr;        // leader only
+    void* stream = nullptr;          // leader only
+    rlo_client_t* cl = nullptr;      // every rank: its rank of the part, through the shared segment
     iar_cb_func_t judge = nullptr, action = nullptr;
     void* ctx = nullptr;
     uint32_t slot_bytes = 0;      // device payload capacity
@@ -112,6 +117,12 @@ std::vector<RLO_msg_t*> g_pool;         // recycled received messages
 
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// RLO_TRACE_SETUP=1: engine construction steps with timestamps on stderr (diagnostics)
+void setup_trace(int rank, const char* step) {
+    static const bool on = std::getenv("RLO_TRACE_SETUP") != nullptr;
+    if (on) std::fprintf(stderr, "rlo setup rank %d t=%.6f %s\n", rank, now_ns() * 1e-9, step);
 }
 
 void proposal_init(RLO_proposal_state* ps) {  // proposal_state_init :1235-1248
@@ -174,11 +185,11 @@ size_t pbuf_put(char* out, RLO_ID pid, RLO_Vote vote, uint64_t len, const void* 
 int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t len, RLO_msg_t* msg) {
     std::lock_guard<std::mutex> lk(e->mu);
     if (e->backlog.empty()) {
-        int rc = rlo_host_post(e->w, e->rank, &c, payload, len);
+        int rc = rlo_client_post(e->cl, &c, payload, len);
         if (rc == RLO_OK) {
             if (msg) {
                 uint64_t posted = 0;
-                rlo_host_cmd_count(e->w, e->rank, nullptr, &posted);
+                rlo_client_cmd_count(e->cl, nullptr, &posted);
                 msg->seq = posted;  // consumed once the device head reaches it
                 msg->posted = 1;
             }
@@ -202,7 +213,7 @@ int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t l
 void flush_backlog(progress_engine* e) {
     while (!e->backlog.empty()) {
         Cmd& q = e->backlog.front();
-        int rc = rlo_host_post(e->w, e->rank, &q.c, q.payload.data(), (uint32_t)q.payload.size());
+        int rc = rlo_client_post(e->cl, &q.c, q.payload.data(), (uint32_t)q.payload.size());
         if (rc == RLO_E_AGAIN) return;
         if (rc != RLO_OK) {
             std::fprintf(stderr, "rlo: rank %d: command post failed: %s\n", e->rank, rlo_strerror(rc));
@@ -211,7 +222,7 @@ void flush_backlog(progress_engine* e) {
         }
         if (q.msg) {
             uint64_t posted = 0;
-            rlo_host_cmd_count(e->w, e->rank, nullptr, &posted);
+            rlo_client_cmd_count(e->cl, nullptr, &posted);
             q.msg->seq = posted;
         }
         e->backlog.pop_front();
@@ -223,7 +234,7 @@ void flush_backlog(progress_engine* e) {
 void reap_sent(progress_engine* e) {
     if (e->wait.empty()) return;
     uint64_t consumed = 0;
-    rlo_host_cmd_count(e->w, e->rank, &consumed, nullptr);
+    rlo_client_cmd_count(e->cl, &consumed, nullptr);
     while (!e->wait.empty()) {
         RLO_msg_t* m = e->wait.front();
         if (m->seq == 0 || m->seq > consumed) break;
@@ -237,13 +248,10 @@ void reap_sent(progress_engine* e) {
 
 void check_alive(progress_engine* e) {
     if (e->failed) return;
-    if (rlo_host_running(e->w) == 1) return;
-    int rc = rlo_wait(e->w);
-    rlo_rank_stats_t st;
-    std::memset(&st, 0, sizeof st);
-    rlo_stats(e->w, &st, 1);
-    std::fprintf(stderr, "rlo: rank %d engine %d: progress kernel stopped (%s, device error %u aux %u)\n", e->rank, e->id,
-                 rlo_strerror(rc), st.error, st.error_aux);
+    const int st = rlo_client_state(e->cl);
+    if (st == 1) return;
+    std::fprintf(stderr, "rlo: rank %d engine %d: this rank's progress workgroup stopped serving (state %d%s)\n", e->rank,
+                 e->id, st, st == RLO_E_DEVICE ? ": the GPU leader marked the engine failed" : "");
     e->failed = true;
 }
 
@@ -266,7 +274,7 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             RLO_msg_t* m = msg_alloc(ev.origin);
             if (!m) return;
             m->ext = (uint8_t*)std::malloc(ev.len ? ev.len : 1);
-            if (!m->ext || rlo_host_bulk_copy(e->w, e->rank, &ev, m->ext) != RLO_OK) {
+            if (!m->ext || rlo_client_bulk_get(e->cl, &ev, m->ext) != RLO_OK) {
                 std::fprintf(stderr, "rlo: rank %d: bulk delivery of %u bytes from %d failed\n", e->rank, ev.len, ev.origin);
                 e->failed = true;
                 msg_release(m);
@@ -372,7 +380,7 @@ bool pump(progress_engine* e) {
     rlo_log_rec_t ev;
     int got = 0;
     for (; got < 4096; got++) {
-        int r = rlo_host_poll(e->w, e->rank, &ev, e->evbuf.data(), (uint32_t)e->evbuf.size());
+        int r = rlo_client_poll(e->cl, &ev, e->evbuf.data(), (uint32_t)e->evbuf.size());
         if (r != 1) break;
         RawEv q;
         q.ev = ev;
@@ -395,18 +403,25 @@ void watchdog(progress_engine* e, bool moved, int64_t period_ns) {
     e->t_dump = t;
     std::lock_guard<std::mutex> lk(e->mu);  // backlog / evq are shared with the pump thread
     uint64_t consumed = 0, posted = 0;
-    rlo_host_cmd_count(e->w, e->rank, &consumed, &posted);
+    rlo_client_cmd_count(e->cl, &consumed, &posted);
+    uint64_t d[9] = {0};
+    rlo_client_debug(e->cl, d);
+    std::fprintf(stderr, "rlo watchdog rank %d engine %d: commands posted %llu forwarded %llu consumed %llu (kernel saw "
+                 "tail %llu); pickups consumed %llu written %llu (kernel saw head %llu); kernel beat %llu state %llu\n",
+                 e->rank, e->id, (unsigned long long)d[0], (unsigned long long)d[1], (unsigned long long)d[2],
+                 (unsigned long long)d[3], (unsigned long long)d[4], (unsigned long long)d[5], (unsigned long long)d[6],
+                 (unsigned long long)d[7], (unsigned long long)d[8]);
     std::fprintf(stderr, "rlo watchdog rank %d engine %d: %.1f s without events; sent %ld recved %ld pickup %zu "
                  "backlog %zu wait %zu evq %zu commands consumed %llu / posted %llu, kernel running %d, "
                  "progress calls %llu events %llu\n", e->rank, e->id, (t - e->t_moved) * 1e-9, e->sent_bcast,
                  e->recved_bcast, e->pickup.size(), e->backlog.size(), e->wait.size(), e->evq.size(),
-                 (unsigned long long)consumed, (unsigned long long)posted, rlo_host_running(e->w),
+                 (unsigned long long)consumed, (unsigned long long)posted, rlo_client_state(e->cl),
                  (unsigned long long)e->n_progress, (unsigned long long)e->n_events);
 }
 
 // make_progress_gen (:551-641): everything the device finished since the last call
 void progress(progress_engine* e) {
-    if (!e->w || e->failed) return;
+    if (!e->cl || e->failed) return;
     e->app_ns.store(now_ns(), std::memory_order_relaxed);
     // like make_progress_gen, which completes at most one receive per call (its single posted
     // ANY_SOURCE irecv, :569-624), a call surfaces at most one received message (a delivery or a
@@ -451,7 +466,7 @@ void pump_loop() {
             for (progress_engine* e = g_engines; e; e = e->next) {
                 if (t - e->app_ns.load(std::memory_order_relaxed) < kQuiet) continue;
                 std::unique_lock<std::mutex> lk(e->mu, std::try_to_lock);
-                if (!lk.owns_lock() || e->failed || !e->w) continue;  // the app thread is on it
+                if (!lk.owns_lock() || e->failed || !e->cl) continue;  // the app thread is on it
                 if (pump(e)) { did = true; e->n_pumped++; }
             }
         }
@@ -471,6 +486,73 @@ void pump_stop() {
     if (!g_pump.joinable()) return;
     g_pump_stop = true;
     g_pump.join();
+}
+
+// ---- the proxy thread: one per leader process while it serves parts.  It moves the clients'
+// commands into the parts' VRAM command rings and their pickup heads into the counters the
+// kernels poll, and runs their bulk copies (rlo_host_proxy); it spins, since every command of every
+// rank on this GPU passes through it
+// (the thread works on its own copy of the list, refreshed when the generation moves, so it never
+// holds a lock the application threads wait for)
+std::mutex g_served_mu;
+std::vector<rlo_world_t*> g_served;  // [g_served_mu]
+std::atomic<uint64_t> g_served_gen{0}, g_proxy_seen{0};
+std::thread g_proxy;
+std::atomic<bool> g_proxy_stop{false};
+
+void proxy_loop() {
+    unsigned idle = 0;
+    uint64_t seen = ~0ull;
+    std::vector<rlo_world_t*> mine;
+    while (!g_proxy_stop.load(std::memory_order_relaxed)) {
+        const uint64_t gen = g_served_gen.load(std::memory_order_acquire);
+        if (gen != seen) {
+            {
+                std::lock_guard<std::mutex> lg(g_served_mu);
+                mine = g_served;
+            }
+            seen = gen;
+            g_proxy_seen.store(gen, std::memory_order_release);
+        }
+        int acted = 0;
+        for (rlo_world_t* w : mine) {
+            const int a = rlo_host_proxy(w);
+            if (a > 0) acted += a;
+        }
+        if (acted) idle = 0;
+        else if (++idle > (1u << 20)) std::this_thread::sleep_for(std::chrono::microseconds(20));  // long idle only
+        else __builtin_ia32_pause();
+    }
+}
+
+void served_add(rlo_world_t* w) {
+    {
+        std::lock_guard<std::mutex> lg(g_served_mu);
+        g_served.push_back(w);
+    }
+    g_served_gen.fetch_add(1, std::memory_order_acq_rel);
+}
+
+// after this returns the proxy no longer touches w
+void served_remove(rlo_world_t* w) {
+    {
+        std::lock_guard<std::mutex> lg(g_served_mu);
+        g_served.erase(std::remove(g_served.begin(), g_served.end(), w), g_served.end());
+    }
+    const uint64_t g = g_served_gen.fetch_add(1, std::memory_order_acq_rel) + 1;
+    while (g_proxy.joinable() && g_proxy_seen.load(std::memory_order_acquire) < g) std::this_thread::yield();
+}
+
+void proxy_start() {
+    if (g_proxy.joinable()) return;
+    g_proxy_stop = false;
+    g_proxy = std::thread(proxy_loop);
+}
+
+void proxy_stop() {
+    if (!g_proxy.joinable()) return;
+    g_proxy_stop = true;
+    g_proxy.join();
 }
 
 std::vector<std::pair<rlo_world_t*, void*>> g_grave;  // stopped engines' worlds / streams
@@ -503,16 +585,6 @@ void retire_comm(MPI_Comm c) {
         MPI_Comm_set_attr(MPI_COMM_SELF, g_retire_key, nullptr);
     }
     g_retired.push_back(c);
-}
-
-int choose_device(MPI_Comm comm, int ndev) {
-    if (const char* s = std::getenv("RLO_DEVICE")) return std::atoi(s) % ndev;
-    MPI_Comm node;
-    MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
-    int lr = 0;
-    MPI_Comm_rank(node, &lr);
-    MPI_Comm_free(&node);
-    return lr % ndev;
 }
 
 }  // namespace
@@ -572,7 +644,7 @@ int RLO_msg_test_isends(RLO_engine_t* eng, RLO_msg_t* msg_in) {
     if (msg_in->posted == 0) return 1;  // never sent: nothing pending
     std::lock_guard<std::mutex> lk(eng->mu);
     uint64_t consumed = 0;
-    rlo_host_cmd_count(eng->w, eng->rank, &consumed, nullptr);
+    rlo_client_cmd_count(eng->cl, &consumed, nullptr);
     return msg_in->seq != 0 && consumed >= msg_in->seq;
 }
 
@@ -601,9 +673,12 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
     rlo_topology(e->size, e->rank, &level, &lw, &scc, &e->send_list_len, sl);
     proposal_init(&e->own);
 
-    // one part per rank: this process' GPU (node-local rank modulo the visible devices)
-    const int ndev = rlo_device_count();
-    int ok = ndev > 0;
+    // One part per GPU.  The ranks are dealt to the GPUs in contiguous blocks; the first rank of
+    // each block (the leader) owns the part -- all of the block's ranks -- with its persistent
+    // kernel, and is the only process on that GPU that touches HIP.  Every rank (the leader's own
+    // too) drives its rank through the shared host segment (rlo_client_*), which the leader's proxy
+    // thread serves.  So exactly one process per GPU holds hardware queues, however many ranks
+    // share it (DESIGN.md "one queue-holding process per GPU").
     int node_size = 0;
     {
         MPI_Comm node;
@@ -611,86 +686,140 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
         MPI_Comm_size(node, &node_size);
         MPI_Comm_free(&node);
     }
-    if (node_size != e->size) {
-        if (e->rank == 0) std::fprintf(stderr, "rlo: the communicator must stay inside one node (hipIpc mappings)\n");
-        ok = 0;
-    }
-    int all_ok = 0;
-    MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, e->comm);
-    if (!all_ok) {
-        if (ndev <= 0) std::fprintf(stderr, "rlo: rank %d: no HIP device\n", e->rank);
+    int ndev = 0;
+    if (e->rank == 0 && node_size == e->size) ndev = rlo_device_count();  // rank 0 leads a GPU anyway
+    MPI_Bcast(&ndev, 1, MPI_INT, 0, e->comm);
+    if (node_size != e->size || ndev <= 0) {
+        if (e->rank == 0)
+            std::fprintf(stderr, "rlo: %s\n", ndev <= 0 ? "no HIP device" : "the communicator must stay inside one node (hipIpc mappings)");
         MPI_Comm_free(&e->comm);
         delete e;
         return nullptr;
     }
-    e->device = choose_device(e->comm, ndev);
-    std::vector<int> devs(e->size);
-    MPI_Allgather(&e->device, 1, MPI_INT, devs.data(), 1, MPI_INT, e->comm);
+    auto dev_of = [&](int r) {
+        if (const char* sd = std::getenv("RLO_DEVICE")) return std::atoi(sd) % ndev;
+        return e->size <= ndev ? r : (int)((int64_t)r * ndev / e->size);
+    };
+    e->device = dev_of(e->rank);
+    std::vector<int> part_begin;  // contiguous blocks of ranks per GPU
+    for (int r = 0; r < e->size; r++)
+        if (r == 0 || dev_of(r) != dev_of(r - 1)) part_begin.push_back(r);
+    const int n_parts = (int)part_begin.size();
+    part_begin.push_back(e->size);
+    int part = 0;
+    while (part_begin[part + 1] <= e->rank) part++;
+    e->leader = e->rank == part_begin[part];
+    MPI_Comm_split(e->comm, part, e->rank, &e->group);
+    MPI_Comm leaders;
+    MPI_Comm_split(e->comm, e->leader ? 0 : MPI_UNDEFINED, e->rank, &leaders);
+    std::vector<int> devs(n_parts);
+    for (int p = 0; p < n_parts; p++) devs[p] = dev_of(part_begin[p]);
     bool multi = false;
     for (int d : devs) multi |= d != devs[0];
 
-    rlo_part_cfg_t pc;
-    std::memset(&pc, 0, sizeof pc);
-    pc.n_ranks = e->size;
-    pc.n_parts = e->size;
-    pc.part = e->rank;
-    pc.part_begin = nullptr;
-    pc.max_payload = e->slot_bytes;
-    // 512 slots for small slots (the library default is 2048 there, tuned for device storms; the
-    // drop-in's few ranks per GPU gain nothing from it: profiles/r1s5_api_slots.jsonl); RLO_RING_SLOTS
-    // overrides it for diagnostics
-    pc.ring_slots = e->slot_bytes > 4096 ? 128u : 512u;
-    if (const char* rs = std::getenv("RLO_RING_SLOTS")) pc.ring_slots = (uint32_t)std::strtoul(rs, nullptr, 10);
-    pc.device = e->device;
-    pc.flags = multi ? RLO_PART_UNCACHED : 0u;
-    // extension: bcasts beyond the data area (bulk messages) up to RLO_BULK_MAX bytes (default 64 MiB;
-    // 0 turns them off); RLO_BULK_MOVERS mover workgroups per rank (default 4)
-    e->bulk_max = 64ull << 20;
+    e->bulk_max = 64ull << 20;  // extension: bcasts beyond the data area up to RLO_BULK_MAX bytes (0: off)
     if (const char* bm = std::getenv("RLO_BULK_MAX")) e->bulk_max = std::strtoull(bm, nullptr, 10);
-    pc.bulk_max = e->bulk_max;
-    pc.bulk_slots = 2;
-    pc.movers = 4;
-    if (const char* mv = std::getenv("RLO_BULK_MOVERS")) pc.movers = (uint32_t)std::strtoul(mv, nullptr, 10);
-    int rc = rlo_part_create(&pc, &e->w);
-    std::vector<uint8_t> blob(RLO_PART_BLOB_BYTES, 0), blobs((size_t)RLO_PART_BLOB_BYTES * e->size, 0);
-    if (rc == RLO_OK && rlo_part_export(e->w, blob.data(), RLO_PART_BLOB_BYTES) < 0) rc = RLO_E_HIP;
-    int lok = rc == RLO_OK, gok = 0;
-    MPI_Allreduce(&lok, &gok, 1, MPI_INT, MPI_MIN, e->comm);
-    if (gok) {
-        MPI_Allgather(blob.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, blobs.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, e->comm);
-        rc = rlo_part_connect(e->w, blobs.data(), e->size);
+    int rc = RLO_OK;
+    char shm_name[96] = {0};
+    auto agree = [&](int ok_local) {  // every rank of the engine learns whether every step worked
+        int g = 0;
+        MPI_Allreduce(&ok_local, &g, 1, MPI_INT, MPI_MIN, e->comm);
+        return g != 0;
+    };
+    bool ok = true, launched = false;
+    if (e->leader) {
+        rlo_part_cfg_t pc;
+        std::memset(&pc, 0, sizeof pc);
+        pc.n_ranks = e->size;
+        pc.n_parts = n_parts;
+        pc.part = part;
+        pc.part_begin = part_begin.data();
+        pc.max_payload = e->slot_bytes;
+        // 512 slots for small slots (the library default is 2048 there, tuned for device storms; the
+        // drop-in's few ranks per GPU gain nothing from it: profiles/r1s5_api_slots.jsonl); RLO_RING_SLOTS
+        // overrides it for diagnostics
+        pc.ring_slots = e->slot_bytes > 4096 ? 128u : 512u;
+        if (const char* rs = std::getenv("RLO_RING_SLOTS")) pc.ring_slots = (uint32_t)std::strtoul(rs, nullptr, 10);
+        pc.device = e->device;
+        pc.flags = multi ? RLO_PART_UNCACHED : 0u;
+        pc.bulk_max = e->bulk_max;
+        pc.bulk_slots = 2;
+        pc.movers = 4;  // RLO_BULK_MOVERS: mover workgroups of the part
+        if (const char* mv = std::getenv("RLO_BULK_MOVERS")) pc.movers = (uint32_t)std::strtoul(mv, nullptr, 10);
+        rc = rlo_part_create(&pc, &e->w);
+    }
+    setup_trace(e->rank, "part created");
+    std::vector<uint8_t> blob(RLO_PART_BLOB_BYTES, 0), blobs((size_t)RLO_PART_BLOB_BYTES * n_parts, 0);
+    if (e->leader && rc == RLO_OK && rlo_part_export(e->w, blob.data(), RLO_PART_BLOB_BYTES) < 0) rc = RLO_E_HIP;
+    ok = agree(rc == RLO_OK);
+    if (ok && e->leader) {
+        MPI_Allgather(blob.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, blobs.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, leaders);
+        rc = rlo_part_connect(e->w, blobs.data(), n_parts);
+        setup_trace(e->rank, "connected");
+        if (rc == RLO_OK) {
+            std::snprintf(shm_name, sizeof shm_name, "/rlo.%d.%d.%d", (int)getpid(), g_engines_ever + 1, part);
+            rc = rlo_host_share(e->w, shm_name, 4ull << 20);
+        }
         if (rc == RLO_OK) {
             rlo_host_cfg_t hc;
             std::memset(&hc, 0, sizeof hc);
+            hc.pickup_slots = 512;
             rc = rlo_program_host(e->w, &hc);
         }
+        setup_trace(e->rank, "programmed (shared segment)");
         if (rc == RLO_OK) rc = rlo_stream_create(e->device, &e->stream);
         if (rc == RLO_OK) rc = rlo_reset(e->w, e->stream);
-        lok = rc == RLO_OK;
-        MPI_Allreduce(&lok, &gok, 1, MPI_INT, MPI_MIN, e->comm);  // every part reset before any launch
-        if (gok) {
-            rc = rlo_launch_ex(e->w, e->stream, RLO_LAUNCH_NO_RESET);
-            lok = rc == RLO_OK;
-            MPI_Allreduce(&lok, &gok, 1, MPI_INT, MPI_MIN, e->comm);
-        }
     }
-    if (!gok) {
+    setup_trace(e->rank, "connected+programmed+shared+reset");
+    ok = ok && agree(rc == RLO_OK);  // every part reset before any part launches
+    if (ok && e->leader) {
+        rc = rlo_launch_ex(e->w, e->stream, RLO_LAUNCH_NO_RESET);
+        launched = rc == RLO_OK;
+        setup_trace(e->rank, "launch returned");
+        // the kernel is resident and serving: a launch queued behind other work on a shared hardware
+        // queue would otherwise look like a running engine that never answers
+        if (rc == RLO_OK) rc = rlo_host_wait_started(e->w, 20000);
+        if (rc != RLO_OK)
+            std::fprintf(stderr, "rlo: rank %d: the progress kernel on GPU %d did not start serving (%s)\n", e->rank,
+                         e->device, rlo_strerror(rc));
+    }
+    ok = ok && agree(rc == RLO_OK);
+    setup_trace(e->rank, "launched+started");
+    if (ok) {  // members map their ranks through the leader's segment
+        MPI_Bcast(shm_name, (int)sizeof shm_name, MPI_CHAR, 0, e->group);
+        rc = rlo_client_attach(shm_name, e->rank, &e->cl);
+        ok = agree(rc == RLO_OK);
+        if (e->leader) rlo_host_unlink(e->w);  // every client attached (or gave up): drop the name
+    }
+    setup_trace(e->rank, "attached");
+    if (ok && e->leader) {  // the proxy serves this part from now on
+        served_add(e->w);
+        proxy_start();
+    }
+    if (!ok) {
         std::fprintf(stderr, "rlo: rank %d: engine setup failed (%s, hip %d)\n", e->rank, rlo_strerror(rc),
                      rlo_last_hip_error());
-        if (e->w && rlo_host_running(e->w) == 1) {
-            rlo_cmd_t q;
-            std::memset(&q, 0, sizeof q);
-            q.kind = RLO_CMD_QUIT;
-            rlo_host_post(e->w, e->rank, &q, nullptr, 0);
-            rlo_wait(e->w);
+        if (e->w && e->leader) {
+            rlo_host_fail(e->w);
+            if (launched && rlo_host_running(e->w) == 1) {  // stop every local rank of the kernel
+                rlo_cmd_t q;
+                std::memset(&q, 0, sizeof q);
+                q.kind = RLO_CMD_QUIT;
+                for (int r = part_begin[part]; r < part_begin[part + 1]; r++) rlo_host_post(e->w, r, &q, nullptr, 0);
+                rlo_wait(e->w);
+            }
         }
         MPI_Barrier(e->comm);
+        if (e->cl) rlo_client_detach(e->cl);
         if (e->w) rlo_world_destroy(e->w);
         if (e->stream) rlo_stream_destroy(e->stream);
+        if (leaders != MPI_COMM_NULL) MPI_Comm_free(&leaders);
+        MPI_Comm_free(&e->group);
         MPI_Comm_free(&e->comm);
         delete e;
         return nullptr;
     }
+    if (leaders != MPI_COMM_NULL) MPI_Comm_free(&leaders);
     e->id = ++g_engines_ever;  // engine ids 1, 2, ... (:515-517)
     {
         std::lock_guard<std::mutex> lg(g_list_mu);
@@ -735,14 +864,18 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
     std::memset(&q, 0, sizeof q);
     q.kind = RLO_CMD_QUIT;
     post(eng, q, nullptr, 0, nullptr);
-    while (!eng->failed && rlo_host_running(eng->w) == 1) {  // keep both rings moving until the kernel ends
+    while (!eng->failed && rlo_client_state(eng->cl) == 1) {  // keep both rings moving until my rank stops
         std::lock_guard<std::mutex> lk(eng->mu);
         pump(eng);
         eng->evq.clear();
     }
-    int rc = rlo_wait(eng->w);
-    if (rc != RLO_OK && !eng->failed)
-        std::fprintf(stderr, "rlo: rank %d engine %d: kernel ended with %s\n", eng->rank, eng->id, rlo_strerror(rc));
+    MPI_Barrier(eng->group);  // every rank of my GPU's part stopped: the kernel ends
+    if (eng->leader) {
+        served_remove(eng->w);
+        int rc = rlo_wait(eng->w);
+        if (rc != RLO_OK && !eng->failed)
+            std::fprintf(stderr, "rlo: rank %d engine %d: kernel ended with %s\n", eng->rank, eng->id, rlo_strerror(rc));
+    }
     MPI_Barrier(eng->comm);
     for (RLO_msg_t* m : eng->pickup) msg_release(m);
     for (RLO_msg_t* m : eng->wait) std::free(m);
@@ -754,10 +887,19 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
         if (*p) *p = eng->next;
     }
     if (!g_engines) pump_stop();
+    bool none_served;
+    {
+        std::lock_guard<std::mutex> lg(g_served_mu);
+        none_served = g_served.empty();
+    }
+    if (none_served) proxy_stop();
+    rlo_client_detach(eng->cl);
+    eng->cl = nullptr;
     // hipFree / hipIpcCloseMemHandle may wait for the whole device, i.e. for the persistent
     // kernel of another engine of this process: free the world once no engine kernel runs
-    g_grave.push_back(std::make_pair(eng->w, eng->stream));
+    if (eng->leader) g_grave.push_back(std::make_pair(eng->w, eng->stream));
     if (!g_engines) bury();
+    MPI_Comm_free(&eng->group);
     delete eng;
     return 0;
 }
@@ -793,7 +935,7 @@ int RLO_bcast_gen(RLO_engine_t* eng, RLO_msg_t* msg_in, enum RLO_COMM_TAGS tag) 
     if (msg_in->ext) {  // extension: a bulk bcast -- its bytes into my heap slot once the slot is free
         uint32_t q = 0;
         int rc;
-        while ((rc = rlo_host_bulk_stage(eng->w, eng->rank, msg_in->ext, msg_in->ext_len, 0, &q)) == RLO_E_AGAIN) {
+        while ((rc = rlo_client_bulk_put(eng->cl, msg_in->ext, msg_in->ext_len, 0, &q)) == RLO_E_AGAIN) {
             RLO_make_progress_all();
             if (eng->failed) return -1;
         }

@@ -103,7 +103,10 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_strerror", "rlo_last_hip_error",
            "rlo_device_error", "rlo_bulk_debug",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
-           "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan"]
+           "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan",
+           "rlo_storm_lengths", "rlo_host_share", "rlo_host_unlink", "rlo_host_proxy", "rlo_host_wait_started",
+           "rlo_host_fail", "rlo_client_attach", "rlo_client_detach", "rlo_client_state", "rlo_client_post",
+           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug"]
 
 _lib = None
 
@@ -150,6 +153,22 @@ def load():
                                       ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_host_bulk_copy.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp]
     L.rlo_bulk_plan.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(BulkPlan)]
+    L.rlo_storm_lengths.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.POINTER(ctypes.c_uint32)]
+    L.rlo_host_share.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64]
+    L.rlo_host_unlink.argtypes = [vp]
+    L.rlo_host_proxy.argtypes = [vp]
+    L.rlo_host_wait_started.argtypes = [vp, ctypes.c_uint32]
+    L.rlo_host_fail.argtypes = [vp]
+    L.rlo_client_attach.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
+    L.rlo_client_detach.argtypes = [vp]
+    L.rlo_client_state.argtypes = [vp]
+    L.rlo_client_post.argtypes = [vp, ctypes.POINTER(Cmd), vp, ctypes.c_uint32]
+    L.rlo_client_poll.argtypes = [vp, ctypes.POINTER(LogRec), vp, ctypes.c_uint32]
+    L.rlo_client_cmd_count.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.rlo_client_bulk_put.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    L.rlo_client_bulk_get.argtypes = [vp, ctypes.POINTER(LogRec), vp]
+    L.rlo_client_debug.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.rlo_bulk_debug.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     L.rlo_device_error.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_strerror.argtypes = [ctypes.c_int]

@@ -229,6 +229,14 @@ def bulk_plan(n, nbytes, cross=False):
             "total_tiles": out.total_tiles}
 
 
+def storm_lengths(seed, k, length, len_max=0):
+    """rlo_storm_lengths: the payload length of each of the storm program's k bcasts (uint32 array)"""
+    out = np.zeros(max(k, 1), dtype=np.uint32)
+    check(L.load().rlo_storm_lengths(seed, k, length, len_max, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))),
+          "rlo_storm_lengths")
+    return out[:k]
+
+
 def topology(n, rank):
     lib = L.load()
     v = [ctypes.c_int() for _ in range(4)]

@@ -151,3 +151,91 @@ def test_bulk_world_config_rejected_without_gpu_or_bad_slots():
 
     with pytest.raises(rlo.RloError):
         rlo.World(8, bulk_max=1 << 20, bulk_slots=3)
+
+
+def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
+    """a shared-host-service segment as rlo_program_host + rlo_host_share lay it out (rlo_shm.hpp),
+    built here without a GPU so the client side can be exercised on CPU"""
+    import mmap
+    import struct
+
+    import rlo
+
+    page = lambda x: (x + 4095) & ~4095  # noqa: E731
+    rec = ctypes.sizeof(rlo.abi.LogRec)
+    o = 4096
+    off = {}
+    for key, size in (("hctl", nl * 64 * 8), ("ev", nl * pc * rec), ("evp", nl * pc * maxp), ("cli", nl * 512),
+                      ("cmd", nl * cc * stride), ("stage", 0)):
+        off[key] = o
+        o = page(o + size)
+    total = o
+    fd = os.open("/dev/shm" + name, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+    os.ftruncate(fd, total)
+    m = mmap.mmap(fd, total)
+    os.close(fd)
+    hdr = struct.pack("<10I9Q2I", 0, 1, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
+                      off["cli"], off["cmd"], off["stage"], total, 0, 0)
+    m[:len(hdr)] = hdr
+    m[0:4] = struct.pack("<I", 0x534F4C52)  # magic last
+    return m, off, rec
+
+
+def test_shared_service_client_protocol_without_gpu():
+    """rlo_client_*: commands land in the client's shared ring with rlo_host_post's encoding and
+    the client's tail; events the kernel would write are read back in order with their payload;
+    the ring bounds (command capacity against the device head) hold."""
+    import struct
+
+    import rlo
+
+    lib = rlo.abi.load()
+    L = rlo.abi
+    name = "/rlo.cputest.%d" % os.getpid()
+    m, off, rec = _fake_segment(name)
+    try:
+        c = ctypes.c_void_p()
+        assert lib.rlo_client_attach(b"/rlo.no-such-segment", 4, ctypes.byref(c)) == -1
+        assert lib.rlo_client_attach(name.encode(), 3, ctypes.byref(c)) == -1  # rank outside the part
+        assert lib.rlo_client_attach(name.encode(), 5, ctypes.byref(c)) == 0  # local rank 1
+        hctl = off["hctl"] + 1 * 64 * 8
+        box = off["cli"] + 1 * 512
+        assert lib.rlo_client_state(c) == 0
+        m[hctl + 40 * 8:hctl + 41 * 8] = struct.pack("<Q", 1)
+        assert lib.rlo_client_state(c) == 1
+        cmd = L.Cmd(kind=0, origin=5, id=7, pseq=0, vote=0, pad=0)
+        payload = b"hello, rootless"
+        for i in range(4):
+            assert lib.rlo_client_post(c, ctypes.byref(cmd), payload, len(payload)) == 0
+        assert lib.rlo_client_post(c, ctypes.byref(cmd), payload, len(payload)) == -8  # ring full (device head 0)
+        assert struct.unpack_from("<Q", m, box)[0] == 4  # mtail
+        slot = off["cmd"] + 1 * 4 * 80 + 2 * 80
+        w0, w1, w2, _ = struct.unpack_from("<4I", m, slot)
+        assert (w0 & 0xFFFF, (w0 >> 16) & 0xFF, w1, w2 & 0xFFFFFF) == (5, 0, 7, len(payload))
+        assert bytes(m[slot + 16:slot + 16 + len(payload)]) == payload
+        m[hctl + 16 * 8:hctl + 17 * 8] = struct.pack("<Q", 3)  # the device consumed 3
+        consumed, posted = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.rlo_client_cmd_count(c, ctypes.byref(consumed), ctypes.byref(posted))
+        assert (consumed.value, posted.value) == (3, 4)
+        assert lib.rlo_client_post(c, ctypes.byref(cmd), payload, len(payload)) == 0
+        # two pickup events written "by the kernel": records + payload, then the pickup tail
+        ev = L.LogRec()
+        got = L.LogRec()
+        buf = ctypes.create_string_buffer(64)
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0
+        for i in range(2):
+            ev.kind, ev.origin, ev.len, ev.payload_idx = 1, i, 4, i
+            at = off["ev"] + (1 * 64 + i) * rec
+            m[at:at + rec] = bytes(ev)
+            pat = off["evp"] + (1 * 64 + i) * 64
+            m[pat:pat + 4] = b"ev%02d" % i
+        m[hctl + 32 * 8:hctl + 33 * 8] = struct.pack("<Q", 2)
+        for i in range(2):
+            assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 1
+            assert (got.origin, buf.raw[:4]) == (i, b"ev%02d" % i)
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0
+        assert struct.unpack_from("<Q", m, box + 128)[0] == 2  # mpk: the proxy hands it to the kernel
+        assert lib.rlo_client_detach(c) == 0
+    finally:
+        m.close()
+        os.unlink("/dev/shm" + name)

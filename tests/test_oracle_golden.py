@@ -68,6 +68,16 @@ def test_storm_simulation_equals_analytic_checksums():
         assert np.array_equal(sim["sum"], exp["sum"])
 
 
+@pytest.mark.parametrize("n,k,lo,hi,order,threads", [(256, 3000, 64, 64, 0, 8), (7, 400, 64, 5000, 0, 4),
+                                                     (16, 120, 64, 1 << 20, 1, 3), (3, 50, 64, 64, 0, 16)])
+def test_storm_threaded_equals_single_thread(n, k, lo, hi, order, threads):
+    """bench.py's multi-core cpu_baseline restatement delivers exactly what the single-thread one does"""
+    a = orc.storm(n, 5, k, lo, len_max=hi, order=order)
+    b = orc.storm_mt(n, 5, k, lo, threads, len_max=hi, order=order)
+    assert a["deliveries"] == b["deliveries"] == k * (n - 1)
+    assert np.array_equal(a["count"], b["count"]) and np.array_equal(a["sum"], b["sum"])
+
+
 def _iar_events(n, origin, mask):
     cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=[(mask >> r) & 1 for r in range(n)])
     prop = ("proposal-from-%d" % origin).encode()
