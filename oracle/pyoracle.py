@@ -65,6 +65,8 @@ def lib():
         L.orc_storm_mt.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, ctypes.c_int, i64p,
                                    u64p]
         L.orc_storm_mt.restype = ctypes.c_int64
+        L.orc_iar_rounds.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, i32p, ctypes.c_int]
+        L.orc_iar_rounds.restype = ctypes.c_int
         L.orc_storm_expected2.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, u32, u32, u32, i64p, u64p]
         L.orc_storm_expected2.restype = ctypes.c_int64
         L.orc_len_of.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u32, u32]
@@ -196,6 +198,17 @@ def iar(n, proposals, cfg, cap=1 << 16):
     if k < 0:
         raise RuntimeError("oracle iar failed")
     return [tuple(int(x) for x in ev[6 * i:6 * i + 6]) for i in range(k)]
+
+
+def iar_rounds(n, p, cfg, cap=None):
+    """orc_iar_rounds: iar_bench's workload (one outstanding proposal per rank, pid = it * n + r) with
+    every event: list of (ev, rank, pid, a, b, c)"""
+    cap = cap or 4 * n * n * p + 1024
+    ev = np.zeros(6 * cap, dtype=np.int32)
+    k = lib().orc_iar_rounds(n, p, ctypes.byref(cfg), _p(ev, ctypes.c_int32), cap)
+    if k < 0:
+        raise RuntimeError("oracle iar_rounds failed")
+    return [tuple(int(x) for x in r) for r in ev[:6 * k].reshape(k, 6)]
 
 
 def iar_bench(n, p, cfg):

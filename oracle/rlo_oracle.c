@@ -824,10 +824,19 @@ int orc_iar(int n, int nprop, const int32_t* origin, const int32_t* pid, const c
     return nev;
 }
 
-int64_t orc_iar_bench(int n, int p, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls, int64_t* actions) {
+/* every rank keeps one outstanding proposal (pid = iter * n + rank, 16-byte body) for p iterations;
+ * the next is submitted once RLO_get_vote_my_proposal saw the previous one decided (testcases.c
+ * :401-486 drive loop, at scale).  events != NULL records them (orc_iar's format). */
+static int64_t iar_rounds(int n, int p, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls,
+                          int64_t* actions, int32_t* events, int cap, int* nev) {
     if (n < 2) return -1;
     iar_sim s;
     sim_init(&s, n, judge);
+    if (events) {
+        s.ev = events;
+        s.cap = cap;
+        s.record = 1;
+    }
     static const char body[16] = "0123456789abcdef";
     int* iter = calloc(n, sizeof(int));
     int busy = 1;
@@ -846,8 +855,19 @@ int64_t orc_iar_bench(int n, int p, const orc_judge_cfg* judge, int64_t* approve
     if (approved) *approved = s.approved;
     if (judge_calls) *judge_calls = s.judge_calls;
     if (actions) *actions = s.actions;
+    if (nev) *nev = s.overflow ? -1 : s.nev;
     int64_t d = s.decisions;
     free(iter);
     sim_free(&s);
     return d;
+}
+
+int64_t orc_iar_bench(int n, int p, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls, int64_t* actions) {
+    return iar_rounds(n, p, judge, approved, judge_calls, actions, NULL, 0, NULL);
+}
+
+int orc_iar_rounds(int n, int p, const orc_judge_cfg* judge, int32_t* events, int cap) {
+    int nev = 0;
+    if (iar_rounds(n, p, judge, NULL, NULL, NULL, events, cap, &nev) < 0) return -1;
+    return nev;
 }

@@ -96,6 +96,8 @@ int orc_iar(int n, int nprop, const int32_t* origin, const int32_t* pid, const c
  * 16-byte body) for p iterations.  Outputs totals; returns #decisions or -1.                   */
 int64_t orc_iar_bench(int n, int p, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls,
                       int64_t* actions);
+/* the same workload with every event recorded (orc_iar's format); returns #events or -1 */
+int orc_iar_rounds(int n, int p, const orc_judge_cfg* judge, int32_t* events, int cap);
 
 #ifdef __cplusplus
 }

@@ -77,7 +77,13 @@ struct BulkSh {
     uint32_t blen[kPass];       // storm candidate i -> payload length
     uint32_t bact[kMaxPend];    // pending receptions (o * B + s), compact
     uint32_t nbact, ncomp;
+    // pending entries [0, nstable) as left by the last compaction (phase C): the only ones wave 0 may
+    // evaluate in phase A, which runs before the iteration's barrier while other waves can still be
+    // appending (an append's nbact increment can be seen before its bact store lands)
+    uint32_t nstable;
     uint64_t cmask[kMaxPend / 64];  // completion bits by position in bact (phase A poll)
+    uint32_t bonw[kMaxPend / 32];   // live receptions by (o * B + s): a guard (register twice / complete
+                                    // one that is not live = a device error, never a lost reception)
     uint64_t sdone[8];          // done(me, s), s < B
     uint32_t bulk_q;            // my bulk originations so far
 };
@@ -553,9 +559,18 @@ __device__ __forceinline__ void bulk_acquire(bool sys) {
 }
 // clear the flags of (r, o, s) and count r's completion at the origin (slot s may be reused once
 // every receiver did this): RLO_user_msg_recycle of a bulk delivery (rootless_ops.c:981-992)
-__device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o, uint32_t s, bool sys) {
+__device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o, uint32_t s, bool sys,
+                                                  uint32_t want = 0u, uint32_t bid = 0u) {
     atomicAdd((unsigned long long*)&P.jctl[44], 1ull);  // diagnostics: releases
     uint32_t* f = bulk_flags(P, r, o, s);
+    if (want) {  // the reception must be complete here: a release mid-reception would lose it
+        const uint32_t tf = bflag_ld(f + kBulkTflag, sys);
+        if (tf < want && atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+                                   (0xEEull << 56) | ((uint64_t)(r & 0xff) << 48) | ((uint64_t)(o & 0xff) << 40) |
+                                       ((uint64_t)(s & 0xf) << 36) | ((uint64_t)(bid & 0xfff) << 24) | ((tf & 0xfffu) << 12) |
+                                       (want & 0xfffu)) == 0ull)
+            bulk_fault(P, 13, ((uint32_t)r << 12) | ((uint32_t)o & 0xfffu));
+    }
     for (int i = 0; i <= (int)kBulkTflag; i++) __hip_atomic_store(f + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bulk_release(sys);
     uint64_t* d = bulk_done(P, o, s);
@@ -841,8 +856,12 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
         // ---- tile finished: the last one finishes the job and recycles its slot
         if (tid == 0) {
             atomicAdd((unsigned long long*)&P.jctl[36 + cls], 1ull);  // diagnostics: tiles moved per class
+            // this tile's effects (a VERIFY's partial sum) before its count: the finisher reads them
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint32_t old = atomicAdd(&P.jdone[cls * P.jslots + jslot], 1u);
             if (old + 1u == jb.ntiles) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 if (jb.kind == JOB_VERIFY) {
                     const uint64_t part = __hip_atomic_load(&P.jsum[cls * P.jslots + jslot], __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
@@ -851,7 +870,8 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                     if (jb.logidx != ~0u)  // the delivery record gets the message checksum
                         st_sys16(reinterpret_cast<u32x4*>(&P.log[(size_t)jb.lr * P.log_cap + jb.logidx]) + 1,
                                  u32x4{len, 0xffffffffu, (uint32_t)tot, (uint32_t)(tot >> 32)});
-                    bulk_slot_release(P, me, o, s, sys);
+                    const uint32_t nt = n > 2 ? bulk_stripe_tiles(pl, len, (uint32_t)((me - o - 1 + n) % n)) : 0u;
+                    bulk_slot_release(P, me, o, s, sys, bulk_total_tiles(pl, len) + nt, jb.bid);
                 }
                 __hip_atomic_store(&P.jdone[cls * P.jslots + jslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&P.jsum[cls * P.jslots + jslot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -921,6 +941,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         uint32_t* dst = reinterpret_cast<uint32_t*>(&S.t);
         for (int i = tid; i < (int)(sizeof(RankTopo) / 4); i += kBlock) dst[i] = src[i];
         for (int i = tid; i < 2 * P.n; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
+        if constexpr (BULK) {
+            for (int i = tid; i < P.n * (int)P.bulk_slots; i += kBlock) bpend[i] = BulkPend{0u, 0u, 0u, -1, 0u, 0u, 0u, 0u};
+        }
         for (int i = tid; i < kHistBins; i += kBlock) S.hist[i] = 0;
         for (int i = tid; i < 4 * 64; i += kBlock) { (&S.pubw[0][0])[i] = 0; (&S.snap[0][0])[i] = 0; }
         if (tid < kMaxIn) { S.vout_tail[tid] = 0; S.vout_head[tid] = 0; }
@@ -941,8 +964,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0;
             if constexpr (BULK) {
-                S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0;
+                S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
+                for (int i = 0; i < kMaxPend / 32; i++) S.b.bonw[i] = 0;
             }
         }
     }
@@ -1043,7 +1067,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     S.b.sdone[lane] = sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                           : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                const uint32_t nb = S.b.nbact;
+                const uint32_t nb = S.b.nstable;
                 for (uint32_t u = 0; u * 64u < nb; u++) {
                     const uint32_t i = u * 64u + (uint32_t)lane;
                     bool dn = false;
@@ -1101,6 +1125,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // checksummed by a VERIFY job (which then releases the slot); host mode: one pickup
                 // event each (the host copies the bytes out and posts RLO_CMD_BULK_RELEASE)
                 const uint32_t nb = S.b.nbact;
+                // phase A evaluated exactly [0, nst): an entry appended since has no valid mask bit
+                // (cmask words past phase A's range keep older iterations' bits)
+                const uint32_t nst = S.b.nstable;
                 if (nb) {
                     uint32_t climit = kMaxPend;
                     if (host) {
@@ -1111,13 +1138,17 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     for (uint32_t u = 0; u * 64u < nb; u++) {
                         const uint32_t i = u * 64u + (uint32_t)lane;
                         const uint64_t m = S.b.cmask[u];
-                        bool fin = ((m >> lane) & 1ull) && seen + (uint32_t)__popcll(m & lt_mask) < climit;
-                        seen += (uint32_t)__popcll(m);
+                        const uint64_t mv = u * 64u < nst ? m & (nst - u * 64u >= 64u ? ~0ull : ((1ull << (nst - u * 64u)) - 1ull)) : 0ull;
+                        bool fin = ((mv >> lane) & 1ull) && seen + (uint32_t)__popcll(mv & lt_mask) < climit;
+                        seen += (uint32_t)__popcll(mv);
                         const uint32_t e = i < nb ? S.b.bact[i] : 0u;
                         if (fin) {
                             const int o = (int)(e / bsl);
                             const uint32_t sl = e % bsl;
                             const BulkPend pe = bpend[e];
+                            const uint32_t ob = atomicAnd(&S.b.bonw[e >> 5], ~(1u << (e & 31u)));
+                            if (!((ob >> (e & 31u)) & 1u) || pe.pad0 != (0x5A000000u | ((uint32_t)o << 8) | sl))
+                                bulk_fault(P, 11, (e << 8) | (pe.pad0 & 0xffu));
                             if (host) {
                                 log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, sl);
                             } else {
@@ -1148,6 +1179,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                     if (lane == 0) {
                         S.b.nbact = kept;
+                        S.b.nstable = kept;
                         if (kept != nb) S.progressed = 1;
                     }
                     if (host && kept != nb) {  // their events count against this iteration's pickup room
@@ -1766,7 +1798,25 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         // pushes of my stripe out of this copy) are done
                         const uint32_t nt =
                             P.n > 2 ? bulk_stripe_tiles(pl, dsc.x, (uint32_t)((me - origin - 1 + P.n) % P.n)) : 0u;
-                        bpend[e] = BulkPend{id, dsc.x, bulk_total_tiles(pl, dsc.x) + nt, from, t0, dsc.y, 0u, 0u};
+                        {  // the same message announced here twice (it must arrive exactly once)
+                            const BulkPend pv = bpend[e];
+                            if (pv.pad0 == (0x5A000000u | ((uint32_t)origin << 8) | sl) && pv.bid == id &&
+                                atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+                                          ((uint64_t)me << 56) | ((uint64_t)(e & 0xffu) << 48) | ((uint64_t)(id & 0xffffu) << 32) |
+                                              ((uint64_t)(from & 0xffff) << 16) | (pv.from & 0xffff)) == 0ull)
+                                bulk_fault(P, 12, (e << 12) | (id & 0xfffu));
+                        }
+                        const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
+                        if ((ob >> (e & 31u)) & 1u) {  // still live: which message was, which one came
+                            const BulkPend od = bpend[e];
+                            const uint32_t tf = bflag_ld(bulk_flags(P, me, origin, sl) + kBulkTflag, sys);
+                            if (atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+                                          ((uint64_t)me << 56) | ((uint64_t)(e & 0xffu) << 48) | ((uint64_t)(od.bid & 0xffffu) << 32) |
+                                              ((uint64_t)(id & 0xffffu) << 16) | ((tf & 0xffu) << 8) | (od.ntiles & 0xffu)) == 0ull)
+                                bulk_fault(P, 10, (e << 12) | (id & 0xfffu));
+                        }
+                        bpend[e] = BulkPend{id, dsc.x, bulk_total_tiles(pl, dsc.x) + nt, from, t0, dsc.y,
+                                            0x5A000000u | ((uint32_t)origin << 8) | sl, 0u};
                         S.b.bact[atomicAdd(&S.b.nbact, 1u)] = e;
                         if (nt) post_job(P, JCLS_B, JOB_GATHER, origin, lr, sl, id, dsc.x, nt, from, ~0u, dsc.y, 0u);
                       }

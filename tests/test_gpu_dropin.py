@@ -3,7 +3,8 @@
 The capture driver that produced the golden fixtures from the compiled reference
 (oracle/ref_harness.c) is rebuilt against include/rootless_ops.h + librootless_ops.so
 (oracle/_ref/dropin_harness) and run the same way, one MPI process per rank, every rank's
-engine a persistent progress kernel on this GPU.  Its records must equal the reference's:
+the ranks of this GPU one part served by one persistent kernel of the leader process (the others
+drive their ranks through the shared host segment).  Its records must equal the reference's:
   * parents:  the tree parent of every delivery, and the delivered 32,764-B region's hash;
   * stream:   per rank the (bid, origin, parent, region hash) of a random-originator stream;
   * iar:      the judge-call set (rank, NULL?, arg), action set, decision pickups, decision;
@@ -11,7 +12,8 @@ engine a persistent progress kernel on this GPU.  Its records must equal the ref
               returns, decisions seen per rank, own results;
   * tests:    the reference's own testcases.c wrappers (compiled unmodified against our
               header) return 1, including its two-engines-per-process tests.
-At most 8 ranks: with the pytest process the GPU box allows 16 GPU processes.
+Up to 13 ranks: beyond 8 rank processes the previous one-kernel-per-process design collapsed
+(profiles/r2_dropin_ab_beyond8.txt); only the leader process touches the GPU now.
 """
 import json
 import os
@@ -25,7 +27,7 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 import capture  # noqa: E402
 
 pytestmark = pytest.mark.gpu
-MAXN = 8
+MAXN = 13
 
 
 @pytest.fixture(scope="module")
@@ -48,7 +50,7 @@ def run(harness, n, *args, timeout=80):
     return capture.run(harness, n, *args, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [4, 5, 8])
+@pytest.mark.parametrize("n", [4, 5, 8, 9, 12, 13])
 def test_parents_match_reference(harness, n):
     fx = load("parents.json")
     got = capture.parents(run(harness, n, "parents", fx["len"]), n)

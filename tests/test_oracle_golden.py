@@ -78,6 +78,24 @@ def test_storm_threaded_equals_single_thread(n, k, lo, hi, order, threads):
     assert np.array_equal(a["count"], b["count"]) and np.array_equal(a["sum"], b["sum"])
 
 
+@pytest.mark.parametrize("n,p,ppm", [(8, 5, 0), (16, 3, 50000), (64, 2, 814)])
+def test_iar_rounds_events_agree_with_totals(n, p, ppm):
+    """orc_iar_rounds (the exact-set checker of tests/test_gpu_engine.py) records the same workload
+    orc_iar_bench counts: one result per proposal, judge calls / actions / approvals equal, every
+    non-origin rank picks up every decision"""
+    kind = orc.ORC_JUDGE_HASH if ppm else orc.ORC_JUDGE_APPROVE
+    cfg, keep = orc.judge_cfg(kind, seed=7, ppm=ppm)
+    ev = orc.iar_rounds(n, p, cfg)
+    tot = orc.iar_bench(n, p, cfg)
+    res = [e for e in ev if e[0] == orc.ORC_EV_RESULT]
+    assert len(res) == tot["decisions"] == n * p
+    assert sum(1 for e in res if e[3] == 1) == tot["approved"]
+    assert sum(1 for e in ev if e[0] == orc.ORC_EV_JUDGE) == tot["judge_calls"]
+    assert sum(1 for e in ev if e[0] == orc.ORC_EV_ACTION) == tot["actions"]
+    assert sum(1 for e in ev if e[0] == orc.ORC_EV_PICKUP) == (n - 1) * n * p
+    assert sorted(e[2] for e in res) == sorted(it * n + r for it in range(p) for r in range(n))
+
+
 def _iar_events(n, origin, mask):
     cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=[(mask >> r) & 1 for r in range(n)])
     prop = ("proposal-from-%d" % origin).encode()
