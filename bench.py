@@ -282,7 +282,7 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
             "sizes": out}
 
 
-def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3):
+def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3, bulk_slots=0, movers=0):
     """BASELINE configs[4] / SURVEY 8(d) C5: mixed sizes log-uniform in [64 B, 1 MiB], collision-heavy
     (slots: in every slot every rank originates, origin(b) = b mod R).  R = 64 ranks per GPU, one
     world over all GPUs, k bcasts per step (fixed: per-GPU receipts stay ~k x 64, weak scaling).
@@ -293,7 +293,7 @@ def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3):
 
     R = per * world
     lo, hi, cap, seed = 64, 1 << 20, 4096, 0xC5
-    w = _world(rlo, dist, R, world, rank, local, max_payload=cap, bulk_max=hi)
+    w = _world(rlo, dist, R, world, rank, local, max_payload=cap, bulk_max=hi, bulk_slots=bulk_slots, movers=movers)
     try:
         w.program_storm(k, lo, seed=seed, len_max=hi, order=1)
         ok, sums, kms = True, [], []
@@ -323,7 +323,7 @@ def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3):
                 "payload_bytes_per_step": int(lens.sum()), "bcast_per_s": round(k / dt, 1),
                 "delivered_GBps": round(float(lens.sum()) * (R - 1) / dt / 1e9, 2), "kernel_ms": round(kernel_ms, 3),
                 "hbm_alg_GBps_per_gpu": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "verified": bool(ok),
-                "movers_per_part": w.info.get("movers")}
+                "movers_per_part": w.info.get("movers"), "bulk_slots": w.info.get("bulk_slots")}
     finally:
         w.close()
 

@@ -208,6 +208,8 @@ struct Params {
     uint64_t* jfree;                // [2][jslots] slot j % J takes job j once jfree == j
     uint32_t* jdone;                // [2][jslots] finished tiles of the slot's job
     uint64_t* jsum;                 // [2][jslots] VERIFY checksum accumulator
+    uint32_t* bshadow;              // [n_local][kMaxPend][8] global copies of the pending-reception records
+    uint32_t storm_order;           // RLO_ORDER_SLOTS: bcast b originates at b mod N (a guard checks ring headers)
 };
 
 // ---- bulk messages (longer than a ring slot; SURVEY §8(f)1, BASELINE configs[2], [4]).
@@ -261,6 +263,10 @@ constexpr int kJctlPost = 0, kJctlClaim = 8, kJctlExited = 32, kJctlWords = 48;
 // the stripe, cut to <= 256 KiB: small enough that many movers share one stripe, large enough
 // that the per-tile release fence stays a small share of the copy.
 constexpr uint32_t kBulkTileMax = 256u << 10;
+// a VERIFY job (a receiver's read of its whole copy) is claimed in 1-MiB tiles, independent of the
+// stripe plan: at N = 64 a stripe-sized tile made ~63 claims per copy, and the claim CAS, not the
+// bytes, bounded the mixed-size storm (4.3 s per 2,048-bcast step)
+constexpr uint32_t kVerifyTile = 1u << 20;
 struct BulkPlan {
     uint32_t nchunks, stripe, chunk, tile;  // chunk = stripe * (N - 1); stripe, tile multiples of 1 KiB
 };

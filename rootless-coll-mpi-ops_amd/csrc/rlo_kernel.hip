@@ -199,7 +199,12 @@ __device__ __forceinline__ void st_ring(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 }
 // 16-B write-through store that reaches host memory (pinned pickup rings) or HBM for the log
 __device__ __forceinline__ void st_sys16(void* p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    // two 8-B system-scope stores (sc0 sc1: write-through to host memory / visible to every XCD).
+    // Not inline asm: the compiler cannot see an asm store's pending reads of its address and data
+    // registers and may reuse them at once -- job records were seen with a neighbour's words in them
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // 16-B command-slot load from pinned host memory (written by the host CPU)
 __device__ __forceinline__ u32x4 ld_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -819,8 +824,8 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                 if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
             }
             __syncthreads();
-            const uint32_t off0 = ti * pl.tile;
-            const uint32_t tlen = min(pl.tile, len - off0);
+            const uint32_t off0 = ti * kVerifyTile;
+            const uint32_t tlen = min(kVerifyTile, len - off0);
             const uint32_t ngr = (tlen + 15u) >> 4;
             const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
             unsigned long long acc = 0;
@@ -1146,6 +1151,18 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             const int o = (int)(e / bsl);
                             const uint32_t sl = e % bsl;
                             const BulkPend pe = bpend[e];
+                            {  // the LDS record must still be what registration wrote
+                                const u32x4* sh = reinterpret_cast<const u32x4*>(P.bshadow + ((size_t)lr * kMaxPend + e) * 8u);
+                                const u32x4 a = sh[0], b = sh[1];
+                                const uint32_t bad = (a.x != pe.bid) | ((a.y != pe.len) << 1) | ((a.z != pe.ntiles) << 2) |
+                                                     ((a.w != (uint32_t)pe.from) << 3) | ((b.x != pe.t0) << 4) | ((b.y != pe.q) << 5) |
+                                                     ((b.z != pe.pad0) << 6);
+                                if (bad && atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+                                                     (0xDDull << 56) | ((uint64_t)(me & 0xff) << 48) | ((uint64_t)(e & 0xff) << 40) |
+                                                         ((uint64_t)(bad & 0x7f) << 32) | ((uint64_t)(a.x & 0xffff) << 16) |
+                                                         (pe.bid & 0xffff)) == 0ull)
+                                    bulk_fault(P, 14, (e << 8) | bad);
+                            }
                             const uint32_t ob = atomicAnd(&S.b.bonw[e >> 5], ~(1u << (e & 31u)));
                             if (!((ob >> (e & 31u)) & 1u) || pe.pad0 != (0x5A000000u | ((uint32_t)o << 8) | sl))
                                 bulk_fault(P, 11, (e << 8) | (pe.pad0 & 0xffu));
@@ -1156,8 +1173,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 const uint32_t li =
                                     log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
                                 post_job(P, JCLS_A, JOB_VERIFY, o, lr, sl, pe.bid, pe.len,
-                                         bulk_tiles_of(bulk_plan(P.n, pe.len, P.bulk_cross != 0), pe.len), pe.from, li,
-                                         pe.q, 0u);
+                                         (pe.len + kVerifyTile - 1u) / kVerifyTile, pe.from, li, pe.q, 0u);
                                 if (P.mode & MODE_LAT) {  // the last of N-1 pickups completes the round
                                     const uint32_t old =
                                         sys ? __hip_atomic_fetch_add(&P.lat_count[pe.bid], 1u, __ATOMIC_RELAXED,
@@ -1815,8 +1831,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                               ((uint64_t)(id & 0xffffu) << 16) | ((tf & 0xffu) << 8) | (od.ntiles & 0xffu)) == 0ull)
                                 bulk_fault(P, 10, (e << 12) | (id & 0xfffu));
                         }
-                        bpend[e] = BulkPend{id, dsc.x, bulk_total_tiles(pl, dsc.x) + nt, from, t0, dsc.y,
-                                            0x5A000000u | ((uint32_t)origin << 8) | sl, 0u};
+                        const BulkPend np_ = BulkPend{id, dsc.x, bulk_total_tiles(pl, dsc.x) + nt, from, t0, dsc.y,
+                                                      0x5A000000u | ((uint32_t)origin << 8) | sl, 0u};
+                        bpend[e] = np_;
+                        {  // the guard's global copy (compared at completion)
+                            u32x4* sh = reinterpret_cast<u32x4*>(P.bshadow + ((size_t)lr * kMaxPend + e) * 8u);
+                            sh[0] = u32x4{np_.bid, np_.len, np_.ntiles, (uint32_t)np_.from};
+                            sh[1] = u32x4{np_.t0, np_.q, np_.pad0, np_.pad1};
+                        }
                         S.b.bact[atomicAdd(&S.b.nbact, 1u)] = e;
                         if (nt) post_job(P, JCLS_B, JOB_GATHER, origin, lr, sl, id, dsc.x, nt, from, ~0u, dsc.y, 0u);
                       }

@@ -366,9 +366,10 @@ int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
 
 // job-ring memory of a part (uncached, part-local): [jobs 2J x 64 B][jctl][jclaim 2J][jfree 2J][jdone 2J][jsum 2J]
 struct JobMem {
-    uint64_t jobs, jctl, jclaim, jfree, jdone, jsum, bytes;
+    uint64_t jobs, jctl, jclaim, jfree, jdone, jsum, shadow, bytes;
 };
-JobMem job_mem(uint32_t J) {
+// + shadow: [nl][kMaxPend] copies of the pending-reception records (a guard against LDS corruption)
+JobMem job_mem(uint32_t J, uint32_t nl) {
     JobMem m;
     m.jobs = 0;
     m.jctl = m.jobs + 2ull * J * sizeof(rlo::BulkJob);
@@ -376,7 +377,8 @@ JobMem job_mem(uint32_t J) {
     m.jfree = m.jclaim + 2ull * J * 8;
     m.jdone = m.jfree + 2ull * J * 8;
     m.jsum = (m.jdone + 2ull * J * 4 + 127) & ~127ull;
-    m.bytes = m.jsum + 2ull * J * 8;
+    m.shadow = m.jsum + 2ull * J * 8;
+    m.bytes = m.shadow + (uint64_t)nl * rlo::kMaxPend * 32;
     return m;
 }
 
@@ -556,9 +558,10 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     w->cus = prop.multiProcessorCount;
     if (w->L.bulk_max) {
         // movers: half scatter / verify (never wait), half gather (wait only for scatters).  Auto:
-        // 4 per local rank (>= 16), within the CUs the rank-workgroups leave (one workgroup per CU)
+        // every CU the rank-workgroups leave (>= 16): a bulk copy is HBM bound only with hundreds of
+        // workgroups storing (8 ranks, 64 MiB: 12.8 GB/s algbw with 32 movers); idle movers sleep
         int mv = (int)cfg->movers;
-        if (mv == 0) mv = std::min(std::max(16, 4 * w->nl), w->cus - w->nl) & ~1;
+        if (mv == 0) mv = std::max(16, w->cus - w->nl) & ~1;
         if (mv < 2) { delete w; return RLO_E_OCCUPANCY; }
         w->nmov = (uint32_t)mv;
         w->jslots = pow2_ceil((uint32_t)w->nl * (uint32_t)(w->L.n + 1) * w->L.bslots + 64u);
@@ -572,7 +575,7 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         return RLO_E_HIP;
     }
     if (w->L.bulk_max) {  // heap, flags and job rings: uncached (peers and other XCDs write them)
-        w->jmem_bytes = job_mem(w->jslots).bytes;
+        w->jmem_bytes = job_mem(w->jslots, (uint32_t)w->nl).bytes;
         const uint32_t keep = w->flags;
         w->flags |= RLO_PART_UNCACHED;
         const int e = alloc_region(w, (void**)&w->heap, w->L.heap_bytes[me]) ||
@@ -815,7 +818,7 @@ static void base_params(rlo_world* w) {
     P.n_local = (uint32_t)w->nl;
     P.ring_cap = w->L.stride - rlo::kHdr;
     if (w->L.bulk_max) {
-        const JobMem m = job_mem(w->jslots);
+        const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);
         P.bulk_slots = w->L.bslots;
         P.bulk_cap = w->L.bcap;
         P.nmov = w->nmov;
@@ -832,6 +835,7 @@ static void base_params(rlo_world* w) {
         P.jfree = reinterpret_cast<uint64_t*>(w->jmem + m.jfree);
         P.jdone = reinterpret_cast<uint32_t*>(w->jmem + m.jdone);
         P.jsum = reinterpret_cast<uint64_t*>(w->jmem + m.jsum);
+        P.bshadow = reinterpret_cast<uint32_t*>(w->jmem + m.shadow);
     }
 }
 
@@ -883,6 +887,7 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg) {
     P.len = cfg->len;
     P.len_lo = cfg->len;
     P.len_hi = hi;
+    P.storm_order = cfg->order;
     P.window = std::min<uint32_t>(cfg->window ? cfg->window : 64, 64u);  // one wave prefetches the ids
     P.sched_off = w->d_sched_off.p;
     P.sched_ids = w->d_sched_ids.p;
@@ -1241,7 +1246,7 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     HIPCHK(hipMemsetAsync(w->fwd, 0, w->L.fwd_bytes[w->part], s));
     HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->nl, s));
     if (w->L.bulk_max) {  // bulk flags / release counts, job rings (slot i takes job i first)
-        const JobMem m = job_mem(w->jslots);
+        const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);
         HIPCHK(hipMemsetAsync(w->bflag, 0, w->L.bflag_bytes[w->part], s));
         HIPCHK(hipMemsetAsync(w->jmem, 0, w->jmem_bytes, s));
         HIPCHK(hipMemcpyAsync(w->jmem + m.jfree, w->jfree_init.data(), w->jfree_init.size() * 8, hipMemcpyHostToDevice, s));
@@ -1315,7 +1320,7 @@ int rlo_wait(rlo_world_t* w) {
 
 int rlo_bulk_debug(rlo_world_t* w, uint64_t* out, uint32_t cap) {
     if (!w || !out || !w->jmem) return RLO_E_INVAL;
-    const JobMem m = job_mem(w->jslots);
+    const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);
     const uint32_t n = std::min<uint32_t>(cap, rlo::kJctlWords);
     HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipMemcpy(out, w->jmem + m.jctl, n * 8, hipMemcpyDeviceToHost));

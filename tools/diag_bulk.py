@@ -44,6 +44,15 @@ for rep in range(reps):
       g = d[47]
       if g:
           print("jctl47 %x" % g, flush=True)
+          if g >> 56 == 0xDD:
+              print("LDS-CORRUPT rank %d e %d fields %s shadow bid %d lds bid %d" % ((g >> 48) & 0xff, (g >> 40) & 0xff,
+                    bin((g >> 32) & 0x7f), (g >> 16) & 0xffff, g & 0xffff), flush=True)
+          if g >> 56 == 0xCC:
+              print("WRONG-ORIGIN at rank %d from %d: header origin %d tag %d id %d" % ((g >> 48) & 0xff, (g >> 40) & 0xff,
+                    (g >> 32) & 0xff, (g >> 24) & 0xff, g & 0xffffff), flush=True)
+          if g >> 56 == 0xEE:
+              print("EARLY-RELEASE rank %d o %d s %d bid %d tflag %d want %d" % ((g >> 48) & 0xff, (g >> 40) & 0xff,
+                    (g >> 36) & 0xf, (g >> 24) & 0xfff, (g >> 12) & 0xfff, g & 0xfff), flush=True)
           print("LIVE-REGISTER rank %d e %d old bid %d new bid %d tflag %d old target %d" % (
               g >> 56, (g >> 48) & 0xff, (g >> 32) & 0xffff, (g >> 16) & 0xffff, (g >> 8) & 0xff, g & 0xff), flush=True)
       for r in range(n):
