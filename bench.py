@@ -198,9 +198,13 @@ def _step(w, stream, dist):
 
 
 def _world(rlo, dist, R, world, rank, local, **kw):
-    """one R-rank world: whole on this GPU (world == 1) or this process's part of it"""
+    """one R-rank world: whole on this GPU (world == 1) or this process's part of it.  In the
+    one-GPU rehearsal (RLO_BENCH_DEVICE) every part shares the GPU: bulk worlds then take few mover
+    workgroups, or the parts' persistent launches could not all be resident at once"""
     if world == 1:
         return rlo.World(R, device=local, **kw)
+    if os.environ.get("RLO_BENCH_DEVICE") and kw.get("bulk_max") and not kw.get("movers"):
+        kw["movers"] = 16
     w = rlo.World.part(R, world, rank, device=local, uncached=True, **kw)
     blobs = [None] * world
     dist.all_gather_object(blobs, w.export())

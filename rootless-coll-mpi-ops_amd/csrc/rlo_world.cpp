@@ -660,6 +660,9 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
             b.bflag_bytes != L.bflag_bytes[q])
             return RLO_E_INVAL;
         if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->sys_scope = 1;
+        // parts on other GPUs store into this part's rings and heaps over xGMI: a cached part's L2
+        // could hold lines those system-scope stores do not invalidate (rlo_hip.h RLO_PART_UNCACHED)
+        if (w->sys_scope && !(w->flags & RLO_PART_UNCACHED)) return RLO_E_INVAL;
         if (q == w->part) {
             w->pf[q] = w->fwd; w->pv[q] = w->vote; w->pc[q] = w->ctrl;
             w->ph[q] = w->heap; w->pbf[q] = w->bflag;
