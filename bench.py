@@ -125,13 +125,16 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
     out = {"driver": "tools/api_bench.c (same calls for both)",
            "env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)")}}
     legs = [("storm", ["storm", "20000", "64"]), ("lat", ["lat", "500", "64"]), ("iar", ["iar", "2000"])]
+    # iardj: the same consensus loop with the approve-all judge registered on the device
+    # (RLO_progress_engine_new_dj, an extension; the reference judges with its callback only)
+    legs_ours = legs + [("iardj", ["iardj", "2000"])]
     for nr in ranks:
         rec = {"ranks": nr, "ours": {}, "reference_host_mpi": {}, "cores": nr}
         for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
             if not os.path.exists(exe):
                 rec[name] = {"error": "not built"}
                 continue
-            for leg, args in legs:
+            for leg, args in (legs_ours if name == "ours" else legs):
                 note("api n=%d %s %s" % (nr, name, leg))
                 try:
                     r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(nr), exe] + args,
@@ -145,6 +148,7 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
             rec["ratio_vs_reference"] = {
                 "bcast_per_s": round(o["storm"]["bcast_per_s"] / f["storm"]["bcast_per_s"], 2),
                 "decisions_per_s": round(o["iar"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
+                "decisions_per_s_device_judge": round(o["iardj"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
                 "p50_latency": round(o["lat"]["p50_us"] / f["lat"]["p50_us"], 2)}
         except Exception:  # noqa: BLE001
             pass

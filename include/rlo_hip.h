@@ -215,6 +215,8 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* cmd, const void* pa
 #define RLO_EV_JUDGE 6u     /* call judge(data): origin, from, id = pid, aux = pseq,
                                payload = the proposal's PBuf (len bytes)                        */
 #define RLO_EV_OWN_JUDGE 7u /* call judge(NULL) for my proposal id (all votes were 1)          */
+#define RLO_EV_JUDGED 8u    /* device judge (rlo_host_device_judge): origin, from, id = pid, vote =
+                               verdict, aux = pseq, payload = PBuf -- informational, no reply        */
 /* next event of local rank `rank`: 1 = got one (payload copied, up to cap bytes), 0 = none */
 int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, uint32_t cap);
 /* 1 while this part's kernel runs, 0 once it has ended (rlo_wait then reports its status) */
@@ -259,6 +261,12 @@ int rlo_host_proxy(rlo_world_t* w);  /* one pass; returns the number of actions 
 int rlo_host_wait_started(rlo_world_t* w, uint32_t timeout_ms);
 /* marks the segment failed so clients stop waiting (engine setup aborted, kernel gone) */
 int rlo_host_fail(rlo_world_t* w);
+/* extension: the device judge registry (judge_kind / ppm / seed / mask / isp of cfg, as in
+ * rlo_program_iar) judges this host-service part's proposals, and approves every originator's
+ * final judge(NULL), instead of RLO_EV_JUDGE / RLO_EV_OWN_JUDGE round trips to the host.  Each
+ * judged proposal is reported by a one-way RLO_EV_JUDGED event (vote = verdict, payload = PBuf), so
+ * the host can still run action(PBuf) on approval.  Call after rlo_program_host, before launch. */
+int rlo_host_device_judge(rlo_world_t* w, const rlo_iar_cfg_t* cfg);
 
 typedef struct rlo_client rlo_client_t;
 int rlo_client_attach(const char* shm_name, int rank, rlo_client_t** out);

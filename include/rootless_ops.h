@@ -133,6 +133,26 @@ int RLO_user_msg_source(const RLO_user_msg* msg);
 /* HIP device ordinal this engine's rank lives on */
 int RLO_engine_device(RLO_engine_t* eng);
 
+/* Device judges: RLO_progress_engine_new_dj creates an engine whose proposals are judged on the
+ * GPU by a registered predicate instead of approv_cb_func -- no host round trip per tree hop, and
+ * the originator's final judge(NULL) approves (as every device judge does).  action callbacks still
+ * run on this thread with the proposal's PBuf when a decision 1 arrives for a proposal this rank
+ * approved (rootless_ops.c:842).  Collective like RLO_progress_engine_new; every rank passes its
+ * own judge (kinds must agree):
+ *   RLO_DJUDGE_APPROVE  approve every proposal;
+ *   RLO_DJUDGE_ISP      testcases.c:18-37 is_proposal_approved_cb with this rank's string isp;
+ *   RLO_DJUDGE_HASH     decline iff splitmix64(seed ^ rank << 32 ^ pid) % 1e6 < ppm (testing). */
+#define RLO_HAVE_DEVICE_JUDGE 1
+enum { RLO_DJUDGE_APPROVE = 0, RLO_DJUDGE_ISP = 2, RLO_DJUDGE_HASH = 3 };
+typedef struct {
+    int kind;
+    const char* isp;
+    unsigned int ppm;
+    unsigned long long seed;
+} RLO_device_judge;
+RLO_engine_t* RLO_progress_engine_new_dj(MPI_Comm mpi_comm, size_t msg_size_max, const RLO_device_judge* judge,
+                                         void* app_ctx, void* app_proposal_action);
+
 #ifdef __cplusplus
 }
 #endif

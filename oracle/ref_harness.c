@@ -325,6 +325,45 @@ static void mode_multi(int active_1, int mod, int agree) {
     RLO_progress_engine_cleanup(eng);
 }
 
+#ifdef RLO_HAVE_DEVICE_JUDGE
+/* the multi-proposal roles of mode_multi with is_proposal_approved_cb registered on the device
+ * (RLO_progress_engine_new_dj, RLO_DJUDGE_ISP): decisions and results must equal the reference's */
+static void mode_multi_dj(int active_1, int mod, int agree) {
+    const char* mine;
+    int proposer = 0;
+    if (g_rank == active_1) { mine = "555"; proposer = 1; }
+    else if (g_rank % mod == 0) { mine = agree ? "555" : "333"; proposer = 1; }
+    else mine = agree ? "555" : "111";
+    RLO_device_judge j = {RLO_DJUDGE_ISP, mine, 0, 0};
+    RLO_engine_t* eng = RLO_progress_engine_new_dj(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &j, NULL, &proposal_action_cb);
+    int decision_needed = 1 + (g_size - 1) / mod + 1; /* testcases.c:414 */
+    MPI_Barrier(MPI_COMM_WORLD);
+    int result = -1, own_done = !proposer, got = 0;
+    int need = proposer ? decision_needed - 1 : decision_needed;
+    if (proposer) {
+        int ret = RLO_submit_proposal(eng, (char*)mine, strlen(mine), g_rank);
+        if (ret > -1) { result = RLO_get_vote_my_proposal(eng); own_done = 1; }
+    }
+    while (!own_done || got < need) {
+        RLO_make_progress_all();
+        if (!own_done && RLO_check_proposal_state(eng, 0) == RLO_COMPLETED) {
+            result = RLO_get_vote_my_proposal(eng);
+            own_done = 1;
+        }
+        RLO_user_msg* u = NULL;
+        while (RLO_user_pickup_next(eng, &u)) {
+            if (u->type == RLO_IAR_DECISION) {
+                emit("{\"ev\":\"decision\",\"rank\":%d,\"pid\":%d,\"vote\":%d,\"origin\":%d}", g_rank, u->pid, u->vote, *(int*)u->buf);
+                got++;
+            }
+            RLO_user_msg_recycle(eng, u);
+        }
+    }
+    if (proposer) emit("{\"ev\":\"result\",\"rank\":%d,\"pid\":%d,\"vote\":%d}", g_rank, g_rank, result);
+    RLO_progress_engine_cleanup(eng);
+}
+#endif
+
 /* ---------------------------------------------------------------- tests */
 static void mode_tests(void) {
     int r;
@@ -521,6 +560,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(mode, "bulkstream")) mode_bulkstream(strtoull(argv[3], 0, 0), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]));
     else if (!strcmp(mode, "iar")) mode_iar(atoi(argv[3]), (unsigned)strtoul(argv[4], 0, 0));
     else if (!strcmp(mode, "multi")) mode_multi(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
+#ifdef RLO_HAVE_DEVICE_JUDGE
+    else if (!strcmp(mode, "multi_dj")) mode_multi_dj(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
+#endif
     else if (!strcmp(mode, "tests")) mode_tests();
     else if (!strcmp(mode, "tests_safe")) mode_tests_safe();
     else if (!strcmp(mode, "tests2")) mode_tests2();

@@ -70,7 +70,8 @@ enum Judge : uint32_t { JUDGE_APPROVE = 0, JUDGE_MASK = 1, JUDGE_ISP = 2, JUDGE_
 
 enum LogKind : uint32_t { LOG_DELIVER = 1, LOG_JUDGE = 2, LOG_ACTION = 3, LOG_RESULT = 4, LOG_ERROR = 5,
                           LOG_JREQ = 6,      // host mode: judge(data) request for a received proposal (:698)
-                          LOG_OWN_JREQ = 7 };// host mode: the originator's final judge(NULL) request (:773)
+                          LOG_OWN_JREQ = 7,  // host mode: the originator's final judge(NULL) request (:773)
+                          LOG_JUDGED = 8 };  // host mode, device judge: a proposal judged here (vote, PBuf)
 
 enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_COLLISION = 3, ERR_VOTE_ORPHAN = 4,
                       ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6, ERR_HOST_CMD = 7,
@@ -209,7 +210,8 @@ struct Params {
     uint32_t* jdone;                // [2][jslots] finished tiles of the slot's job
     uint64_t* jsum;                 // [2][jslots] VERIFY checksum accumulator
     uint32_t* bshadow;              // [n_local][kMaxPend][8] global copies of the pending-reception records
-    uint32_t storm_order;           // RLO_ORDER_SLOTS: bcast b originates at b mod N (a guard checks ring headers)
+    uint32_t storm_order;           // RLO_ORDER_SLOTS: bcast b originates at b mod N
+    uint32_t host_judge;            // host mode: 1 = judges are the host's callbacks, 0 = the device registry
 };
 
 // ---- bulk messages (longer than a ring slot; SURVEY §8(f)1, BASELINE configs[2], [4]).

@@ -394,7 +394,7 @@ __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint
     r.len = len;
     r.vote = vote;
     r.aux = aux;
-    r.payload_idx = (P.log_payload && (kind == (LOG_DELIVER | (TAG_BCAST << 8)) || kind == LOG_JREQ)) ? i : ~0u;
+    r.payload_idx = (P.log_payload && (kind == (LOG_DELIVER | (TAG_BCAST << 8)) || kind == LOG_JREQ || kind == LOG_JUDGED)) ? i : ~0u;
     u32x4* dst = reinterpret_cast<u32x4*>(&P.log[(size_t)lr * P.log_cap + i]);
     st_sys16(dst, u32x4{r.kind, (uint32_t)r.origin, (uint32_t)r.from, r.id});
     st_sys16(dst + 1, u32x4{r.len, (uint32_t)r.vote, r.aux, r.payload_idx});
@@ -929,7 +929,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // +11%).  Not in the storm program: there the drain overlaps wave 0's bookkeeping and poll
     // instead (bcasts/s +4%)
     const bool eager = host || !(P.mode & (MODE_LAZYPUB | MODE_STORM));
-    const uint32_t my_mask = ((P.mode & MODE_IAR) && !host && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
+    const bool hjudge = host && P.host_judge != 0;  // host mode: the host's callbacks judge
+    const uint32_t my_mask = ((P.mode & MODE_IAR) && !hjudge && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
     // host-service mode: this rank's command ring (pinned host memory) and its counters
     const __amdgpu_buffer_rsrc_t rh =
         mk_rsrc(host ? P.hin + (size_t)lr * P.hin_cap * P.fwd_stride : P.fwd_region, host ? P.hin_cap * P.fwd_stride : 16u);
@@ -1487,13 +1488,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             const uint32_t nw = atomicAdd(&S.own_word, inc) + inc;
                             if ((nw & 0xffffu) == S.own_needed) {
                                 const int d = (nw >> 16) == 0 ? 1 : 0;
-                                if (d && host) {  // final judge(NULL) (:770-775) is the host's callback
+                                if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback
                                     log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, 1);
                                     S.own_state = 3;
                                 } else {
                                     if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
                                         atomicAdd(&S.judge_calls, 1ull);
-                                        log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                                        if (!host) log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
                                     }
                                     S.own_decision = (uint32_t)d;
                                     S.own_state = 2;
@@ -1545,7 +1546,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else if (tag == TAG_PROPOSAL) {
                     // PBuf [pid][vote][data_len u64][data] at slot + 16 (rootless_ops.c:1402-1410)
                     const uint32_t plen = w2 & 0xffffu;
-                    if (host) {  // the host judges: hold the proposal at the head of its ring until the verdict
+                    if (hjudge) {  // the host judges: hold the proposal at the head of its ring until the verdict
                         PendState* ps = &pend[2 * origin + ((w2 >> 24) & 1u)];
                         const uint8_t pv = ps->valid;
                         if ((pv == PS_JYES || pv == PS_JNO) && ps->pid == (int32_t)id) {
@@ -1775,6 +1776,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         } else {
                             atomicAdd(&S.judge_calls, 1ull);
                             if (!host) log_put(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
+                            else if (!hjudge) {  // device judge in host mode: the host learns the verdict and keeps
+                                                 // the PBuf for action() (rootless_ops.c:842), no round trip
+                                const uint32_t slot = log_put(S, P, lr, LOG_JUDGED, origin, from, (uint32_t)pid, len, judge,
+                                                              pseq);
+                                uint8_t* dst = P.log_payload + ((size_t)lr * P.log_cap + slot) * P.log_stride;
+                                for (uint32_t q = 0; 16u * q < len && 16u * q < P.log_stride; q++)
+                                    st_sys16(dst + 16u * q, ld_sc1(rf, src + kHdr + 16u * q));
+                            }
                             PendState* ps = &pend[2 * origin + (pseq & 1u)];
                             if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                                 ps->valid = PS_NONE;

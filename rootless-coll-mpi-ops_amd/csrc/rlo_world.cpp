@@ -950,6 +950,42 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     return RLO_OK;
 }
 
+// the device judge registry (rlo_kernel.hip judge_eval) and its per-rank tables, for every world
+// rank (a part uses its own ranks' entries)
+static int set_judge(rlo_world* w, const rlo_iar_cfg_t* cfg) {
+    const int n = w->L.n;
+    rlo::Params& P = w->P;
+    if (cfg->judge_kind > RLO_JUDGE_HASH) return RLO_E_INVAL;
+    P.judge_kind = cfg->judge_kind;
+    P.judge_ppm = cfg->judge_ppm;
+    P.judge_seed = cfg->judge_seed;
+    std::vector<uint8_t> mask(n, 0);
+    if (cfg->judge_kind == RLO_JUDGE_MASK) {
+        if (!cfg->judge_mask) return RLO_E_INVAL;
+        std::memcpy(mask.data(), cfg->judge_mask, n);
+    }
+    if (w->d_mask.upload(mask)) return RLO_E_HIP;
+    P.judge_mask = w->d_mask.p;
+    std::vector<char> isp;
+    std::vector<uint32_t> isp_off(n, 0);
+    if (cfg->judge_kind == RLO_JUDGE_ISP) {
+        if (!cfg->judge_isp) return RLO_E_INVAL;
+        const char* s = cfg->judge_isp;
+        for (int r = 0; r < n; r++) {
+            isp_off[r] = (uint32_t)isp.size();
+            size_t l = std::strlen(s);
+            isp.insert(isp.end(), s, s + l + 1);
+            s += l + 1;
+        }
+    } else {
+        isp.push_back(0);
+    }
+    if (w->d_isp.upload(isp) || w->d_isp_off.upload(isp_off)) return RLO_E_HIP;
+    P.judge_isp = w->d_isp.p;
+    P.judge_isp_off = w->d_isp_off.p;
+    return RLO_OK;
+}
+
 int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, const int32_t* origin, const int32_t* pid,
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len) {
     if (!w || !cfg || nprop < 0 || (nprop && (!origin || !pid || !data_off || !data_len))) return RLO_E_INVAL;
@@ -984,33 +1020,10 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
         w->d_prop_data_len.upload(pdl) || w->d_prop_data.upload(blob) || w->d_expect_dec.upload(expect))
         return RLO_E_HIP;
     P.mode = rlo::MODE_IAR | ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
-    P.judge_kind = cfg->judge_kind;
-    P.judge_ppm = cfg->judge_ppm;
-    P.judge_seed = cfg->judge_seed;
-    std::vector<uint8_t> mask(n, 0);
-    if (cfg->judge_kind == RLO_JUDGE_MASK) {
-        if (!cfg->judge_mask) return RLO_E_INVAL;
-        std::memcpy(mask.data(), cfg->judge_mask, n);
+    {
+        const int jrc = set_judge(w, cfg);
+        if (jrc) return jrc;
     }
-    if (w->d_mask.upload(mask)) return RLO_E_HIP;
-    P.judge_mask = w->d_mask.p;
-    std::vector<char> isp;
-    std::vector<uint32_t> isp_off(n, 0);
-    if (cfg->judge_kind == RLO_JUDGE_ISP) {
-        if (!cfg->judge_isp) return RLO_E_INVAL;
-        const char* s = cfg->judge_isp;
-        for (int r = 0; r < n; r++) {
-            isp_off[r] = (uint32_t)isp.size();
-            size_t l = std::strlen(s);
-            isp.insert(isp.end(), s, s + l + 1);
-            s += l + 1;
-        }
-    } else {
-        isp.push_back(0);
-    }
-    if (w->d_isp.upload(isp) || w->d_isp_off.upload(isp_off)) return RLO_E_HIP;
-    P.judge_isp = w->d_isp.p;
-    P.judge_isp_off = w->d_isp_off.p;
     P.prop_off = w->d_prop_off.p;
     P.prop_pid = w->d_prop_pid.p;
     P.prop_data_off = w->d_prop_data_off.p;
@@ -1147,6 +1160,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     base_params(w);
     rlo::Params& P = w->P;
     P.mode = rlo::MODE_HOST | rlo::MODE_IAR;
+    P.host_judge = 1;  // judge(data) / judge(NULL) are the host's callbacks (rlo_host_device_judge: the device's)
     P.log = dev_ev ? const_cast<rlo::LogRec*>(dev_ev) : w->h_ev;
     P.log_cap = pc;
     P.log_payload = dev_evp ? const_cast<uint8_t*>(dev_evp) : w->h_evp;
@@ -1479,6 +1493,15 @@ int rlo_host_unlink(rlo_world_t* w) {
 int rlo_host_fail(rlo_world_t* w) {
     if (!w || !w->shm) return RLO_E_INVAL;
     __atomic_store_n(&((rlo::ShmHdr*)w->shm)->leader_failed, 1u, __ATOMIC_RELEASE);
+    return RLO_OK;
+}
+
+int rlo_host_device_judge(rlo_world_t* w, const rlo_iar_cfg_t* cfg) {
+    if (!w || !cfg || !w->have_program || !(w->P.mode & rlo::MODE_HOST)) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
+    const int rc = set_judge(w, cfg);
+    if (rc) return rc;
+    w->P.host_judge = 0;
     return RLO_OK;
 }
 

@@ -24,6 +24,7 @@
 #include <atomic>
 #include <chrono>
 #include <deque>
+#include <string>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -356,6 +357,16 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             post(e, c, nullptr, 0, nullptr);
             break;
         }
+        case RLO_EV_JUDGED: {  // extension: the device judged a proposal here; keep the PBuf for action()
+            e->n_judge++;
+            if (ev.vote == 1) {
+                std::vector<char> pb(RLO_MSG_SIZE_MAX + 16, 0);
+                const uint32_t n = ev.len < (uint32_t)RLO_MSG_SIZE_MAX ? ev.len : (uint32_t)RLO_MSG_SIZE_MAX;
+                std::memcpy(pb.data(), payload, n);
+                e->approved[std::make_pair(ev.origin, (int)ev.id)] = std::move(pb);
+            }
+            break;
+        }
         case RLO_EV_OWN_JUDGE: {  // every vote was 1: vote = judge(my_proposal = NULL, ctx) (:770-775)
             int v = e->judge ? e->judge(nullptr, e->ctx) : 1;
             if (v != 0 && v != 1) v = 0;
@@ -648,8 +659,12 @@ int RLO_msg_test_isends(RLO_engine_t* eng, RLO_msg_t* msg_in) {
     return msg_in->seq != 0 && consumed >= msg_in->seq;
 }
 
-RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb_func, void* app_ctx,
-                                      void* app_proposal_action) {
+}  // extern "C"
+
+namespace {
+
+RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb_func, void* app_ctx,
+                         void* app_proposal_action, const RLO_device_judge* dj) {
     progress_engine* e = new progress_engine();
     MPI_Comm_dup(mpi_comm, &e->comm);  // bcomm_init :1461
     MPI_Comm_rank(e->comm, &e->rank);
@@ -712,6 +727,35 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
     MPI_Comm_split(e->comm, part, e->rank, &e->group);
     MPI_Comm leaders;
     MPI_Comm_split(e->comm, e->leader ? 0 : MPI_UNDEFINED, e->rank, &leaders);
+    // extension: device judges -- the kinds must agree; ISP strings go to the part's leader
+    int djk = dj ? dj->kind : -1, djmin = 0, djmax = 0;
+    MPI_Allreduce(&djk, &djmin, 1, MPI_INT, MPI_MIN, e->comm);
+    MPI_Allreduce(&djk, &djmax, 1, MPI_INT, MPI_MAX, e->comm);
+    std::vector<std::string> isp_local;
+    if (djmin != djmax || (dj && dj->kind != RLO_DJUDGE_APPROVE && dj->kind != RLO_DJUDGE_ISP &&
+                           dj->kind != RLO_DJUDGE_HASH)) {  // the same on every rank: all leave here
+        if (e->rank == 0) std::fprintf(stderr, "rlo: RLO_progress_engine_new_dj: every rank must pass the same known judge kind\n");
+        if (leaders != MPI_COMM_NULL) MPI_Comm_free(&leaders);
+        MPI_Comm_free(&e->group);
+        MPI_Comm_free(&e->comm);
+        delete e;
+        return nullptr;
+    }
+    {
+        const std::string mine = dj && dj->kind == RLO_DJUDGE_ISP && dj->isp ? std::string(dj->isp) : std::string();
+        int gsz = 0, grank = 0;
+        MPI_Comm_size(e->group, &gsz);
+        MPI_Comm_rank(e->group, &grank);
+        int len = (int)mine.size() + 1;
+        std::vector<int> lens(gsz, 0), offs(gsz, 0);
+        MPI_Gather(&len, 1, MPI_INT, lens.data(), 1, MPI_INT, 0, e->group);
+        int tot = 0;
+        for (int i = 0; i < gsz; i++) { offs[i] = tot; tot += lens[i]; }
+        std::vector<char> buf(e->leader ? (size_t)std::max(tot, 1) : 1, 0);
+        MPI_Gatherv(mine.c_str(), len, MPI_CHAR, buf.data(), lens.data(), offs.data(), MPI_CHAR, 0, e->group);
+        if (e->leader)
+            for (int i = 0; i < gsz; i++) isp_local.emplace_back(buf.data() + offs[i]);
+    }
     std::vector<int> devs(n_parts);
     for (int p = 0; p < n_parts; p++) devs[p] = dev_of(part_begin[p]);
     bool multi = false;
@@ -765,6 +809,21 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
             std::memset(&hc, 0, sizeof hc);
             hc.pickup_slots = 512;
             rc = rlo_program_host(e->w, &hc);
+        }
+        if (rc == RLO_OK && dj) {  // extension: the device judges (every local rank's string for ISP)
+            rlo_iar_cfg_t jc;
+            std::memset(&jc, 0, sizeof jc);
+            jc.judge_kind = (uint32_t)dj->kind;
+            jc.judge_ppm = dj->ppm;
+            jc.judge_seed = dj->seed;
+            std::string all;
+            for (int r = 0; r < e->size; r++) {
+                const int lrk = r - part_begin[part];
+                if (lrk >= 0 && lrk < (int)isp_local.size()) all += isp_local[lrk];
+                all.push_back('\0');
+            }
+            jc.judge_isp = all.data();
+            rc = rlo_host_device_judge(e->w, &jc);
         }
         setup_trace(e->rank, "programmed (shared segment)");
         if (rc == RLO_OK) rc = rlo_stream_create(e->device, &e->stream);
@@ -829,6 +888,21 @@ RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, vo
     }
     pump_start();
     return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb_func, void* app_ctx,
+                                      void* app_proposal_action) {
+    return engine_new(mpi_comm, msg_size_max, approv_cb_func, app_ctx, app_proposal_action, nullptr);
+}
+
+RLO_engine_t* RLO_progress_engine_new_dj(MPI_Comm mpi_comm, size_t msg_size_max, const RLO_device_judge* judge,
+                                         void* app_ctx, void* app_proposal_action) {
+    if (!judge) return nullptr;
+    return engine_new(mpi_comm, msg_size_max, nullptr, app_ctx, app_proposal_action, judge);
 }
 
 int RLO_progress_engine_cleanup(RLO_engine_t* eng) {

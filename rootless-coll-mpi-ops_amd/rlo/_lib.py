@@ -27,7 +27,7 @@ RLO_CMD_BULK, RLO_CMD_BULK_RELEASE = 10, 19
 RLO_EV_DELIVER_BCAST, RLO_EV_DELIVER_DECISION, RLO_EV_DELIVER_BULK = 1, 1 | (4 << 8), 1 | (10 << 8)
 RLO_ORDER_RANDOM, RLO_ORDER_SLOTS = 0, 1
 TAG_BULK = 10
-RLO_EV_ACTION, RLO_EV_RESULT, RLO_EV_JUDGE, RLO_EV_OWN_JUDGE = 3, 4, 6, 7
+RLO_EV_ACTION, RLO_EV_RESULT, RLO_EV_JUDGE, RLO_EV_OWN_JUDGE, RLO_EV_JUDGED = 3, 4, 6, 7, 8
 
 
 class WorldCfg(ctypes.Structure):
@@ -106,7 +106,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan",
            "rlo_storm_lengths", "rlo_host_share", "rlo_host_unlink", "rlo_host_proxy", "rlo_host_wait_started",
            "rlo_host_fail", "rlo_client_attach", "rlo_client_detach", "rlo_client_state", "rlo_client_post",
-           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug"]
+           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_host_device_judge"]
 
 _lib = None
 
@@ -155,6 +155,7 @@ def load():
     L.rlo_bulk_plan.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(BulkPlan)]
     L.rlo_storm_lengths.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.POINTER(ctypes.c_uint32)]
+    L.rlo_host_device_judge.argtypes = [vp, ctypes.POINTER(IarCfg)]
     L.rlo_host_share.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64]
     L.rlo_host_unlink.argtypes = [vp]
     L.rlo_host_proxy.argtypes = [vp]

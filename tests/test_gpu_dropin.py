@@ -110,6 +110,16 @@ def test_multi_proposal_matches_reference(harness, case):
         assert got[k] == case[k], k
 
 
+@pytest.mark.parametrize("case", [c for c in load("multi.json")["cases"] if c["n"] <= MAXN],
+                         ids=lambda c: "n%d-a%d-m%d-g%d" % (c["n"], c["active_1"], c["mod"], c["agree"]))
+def test_multi_proposal_device_judge_matches_reference(harness, case):
+    """extension RLO_progress_engine_new_dj: testcases.c's is_proposal_approved_cb registered on the
+    device (RLO_DJUDGE_ISP) gives the reference's decisions at every rank and its results"""
+    got = capture.multi(run(harness, case["n"], "multi_dj", case["active_1"], case["mod"], case["agree"]))
+    for k in ("decisions", "results"):
+        assert got[k] == case[k], k
+
+
 HACKY = re.compile(r"Rank (\d+) reports: Hacky sack done passive bcast (\d+) times\. total pickup (\d+) times")
 
 

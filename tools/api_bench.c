@@ -149,8 +149,21 @@ static int action_cb(const void* a, void* c) {
     return 0;
 }
 
-static void iar(int P) {
-    RLO_engine_t* eng = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &approve_cb, NULL, &action_cb);
+/* dj: the approve-all judge registered on the device (RLO_progress_engine_new_dj, an extension of
+ * this library; the reference has no such call) */
+static void iar(int P, int dj) {
+    RLO_engine_t* eng = NULL;
+#ifdef RLO_HAVE_DEVICE_JUDGE
+    if (dj) {
+        RLO_device_judge j = {RLO_DJUDGE_APPROVE, NULL, 0, 0};
+        eng = RLO_progress_engine_new_dj(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &j, NULL, &action_cb);
+    } else
+#endif
+        eng = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &approve_cb, NULL, &action_cb);
+    if (!eng) {
+        if (g_rank == 0) fprintf(g_out, "{\"mode\":\"%s\",\"error\":\"no engine\"}\n", dj ? "iardj" : "iar");
+        return;
+    }
     char prop[17] = "0123456789abcdef";
     long expect = (long)P * (g_size - 1), got = 0, approved = 0;
     int done = 0, inflight = 0;
@@ -183,8 +196,8 @@ static void iar(int P) {
     MPI_Reduce(&dt, &dtmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
     MPI_Reduce(&approved, &app, 1, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
     if (g_rank == 0)
-        fprintf(g_out, "{\"mode\":\"iar\",\"ranks\":%d,\"P\":%d,\"seconds\":%.6f,\"decisions_per_s\":%.1f,\"approved\":%ld}\n",
-               g_size, P, dtmax, g_size * (double)P / dtmax, app);
+        fprintf(g_out, "{\"mode\":\"%s\",\"ranks\":%d,\"P\":%d,\"seconds\":%.6f,\"decisions_per_s\":%.1f,\"approved\":%ld}\n",
+               dj ? "iardj" : "iar", g_size, P, dtmax, g_size * (double)P / dtmax, app);
     RLO_progress_engine_cleanup(eng);
 }
 
@@ -195,13 +208,16 @@ int main(int argc, char** argv) {
     g_out = fdopen(dup(1), "w");
     if (!g_out || !freopen("/dev/null", "w", stdout)) return 3;
     if (argc < 3) {
-        if (g_rank == 0) fprintf(stderr, "usage: api_bench storm K LEN | lat ROUNDS LEN | iar P\n");
+        if (g_rank == 0) fprintf(stderr, "usage: api_bench storm K LEN | lat ROUNDS LEN | iar P | iardj P\n");
         MPI_Finalize();
         return 2;
     }
     if (!strcmp(argv[1], "storm")) storm(atoi(argv[2]), argc > 3 ? atoi(argv[3]) : 64);
     else if (!strcmp(argv[1], "lat")) lat(atoi(argv[2]), argc > 3 ? atoi(argv[3]) : 64);
-    else if (!strcmp(argv[1], "iar")) iar(atoi(argv[2]));
+    else if (!strcmp(argv[1], "iar")) iar(atoi(argv[2]), 0);
+#ifdef RLO_HAVE_DEVICE_JUDGE
+    else if (!strcmp(argv[1], "iardj")) iar(atoi(argv[2]), 1);
+#endif
     fflush(g_out);
     MPI_Finalize();
     return 0;
