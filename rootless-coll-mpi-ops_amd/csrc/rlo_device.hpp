@@ -205,8 +205,8 @@ struct Params {
     uint32_t jslots, bpend_off;     // job ring slots per class (power of two, >= every job that can be
                                     //   unfinished at once); dynamic-LDS byte offset of the pending table
     uint64_t* jctl;                 // [kJctlWords] posted / head counters, exited progress workgroups
-    uint64_t* jclaim;               // [2][jslots] seq << 32 | next tile to claim
-    uint64_t* jfree;                // [2][jslots] slot j % J takes job j once jfree == j
+    uint64_t* jclaim;               // (unused)
+    uint64_t* jfree;                // [2][jslots] generation: slot j % J takes sub-job j once jfree == j / J
     uint32_t* jdone;                // [2][jslots] finished tiles of the slot's job
     uint64_t* jsum;                 // [2][jslots] VERIFY checksum accumulator
     uint32_t* bshadow;              // [n_local][kMaxPend][8] global copies of the pending-reception records
@@ -241,17 +241,18 @@ constexpr int kMaxPend = 256;           // pending bulk receptions per rank (N *
 enum JobKind : uint32_t { JOB_SCATTER = 1, JOB_GATHER = 2, JOB_VERIFY = 3 };
 enum JobClass : uint32_t { JCLS_A = 0, JCLS_B = 1 };
 
-struct BulkJob {         // 64 B, one slot of a part's job ring
-    uint32_t seq;        // j + 1 once the slot holds job j
+struct BulkJob {         // 64 B, one slot of a part's job ring: one SUB-job (consecutive tiles of a job)
+    uint32_t seq;        // j + 1 once the slot holds sub-job j (written last)
     uint32_t kind;       // JobKind
     int32_t origin, lr;  // message origin, posting (local) rank
     uint32_t slot, bid;  // heap slot s, bcast id
-    uint32_t len, ntiles;
-    uint64_t tile_base;  // (unused)
+    uint32_t len, ntiles;  // message bytes; tiles of this sub-job
+    uint32_t ti0, parent;  // its first tile in the job; the job's first sub-job slot (VERIFY accounting)
     int32_t from;        // VERIFY: tree parent of the announcement (log)
     uint32_t logidx;     // VERIFY: log record to complete with the checksum, ~0u = none
     uint32_t q, gen;     // bulk sequence; SCATTER source: 1 = heap slot (o, o, s) (host), 0 = generated
-    uint32_t pad[2];
+    uint32_t total;      // tiles of the whole job
+    uint32_t pjob;       // VERIFY: the parent sub-job's index, low 32 bits (its slot's generation)
 };
 static_assert(sizeof(BulkJob) == 64, "job slot");
 
@@ -262,13 +263,15 @@ constexpr int kJctlPost = 0, kJctlClaim = 8, kJctlExited = 32, kJctlWords = 48;
 // stripe / chunk / tile plan of a bulk message: a pure function of (N, len, cross-GPU), so every
 // rank derives the same one (cross: parts span GPUs -> pipelined chunks, ~sqrt(len / 4 MiB) of
 // them; one GPU: one chunk).  A tile (what one mover claim moves, then one release + flag add) is
-// the stripe, cut to <= 256 KiB: small enough that many movers share one stripe, large enough
-// that the per-tile release fence stays a small share of the copy.
-constexpr uint32_t kBulkTileMax = 256u << 10;
-// a VERIFY job (a receiver's read of its whole copy) is claimed in 1-MiB tiles, independent of the
-// stripe plan: at N = 64 a stripe-sized tile made ~63 claims per copy, and the claim CAS, not the
-// bytes, bounded the mixed-size storm (4.3 s per 2,048-bcast step)
-constexpr uint32_t kVerifyTile = 1u << 20;
+// the stripe, cut to <= 64 KiB: a mover workgroup stores ~20 GB/s into uncached HBM, so a message is
+// fast only when many movers share it; large enough that the per-tile release stays a small share.
+constexpr uint32_t kBulkTileMax = 64u << 10;
+// a VERIFY job (a receiver's read of its whole copy) is cut into 256-KiB tiles, independent of the
+// stripe plan (at N = 64 a stripe-sized tile made ~63 tiles per copy)
+constexpr uint32_t kVerifyTile = 256u << 10;
+// a job is posted as at most kMaxSub sub-jobs of consecutive tiles; a mover draws sub-jobs by ticket
+// (one fetch-add, never retried) and moves all of a sub-job's tiles itself
+constexpr uint32_t kMaxSub = 64;
 struct BulkPlan {
     uint32_t nchunks, stripe, chunk, tile;  // chunk = stripe * (N - 1); stripe, tile multiples of 1 KiB
 };

@@ -583,10 +583,12 @@ __device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o,
     else __hip_atomic_fetch_add(d, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// post a job (one lane): take the next job index of the class, write the slot, then open it for
-// claims (claim word = seq << 32 | next tile).  The ring holds every job that can be unfinished at
-// once (rlo_world.cpp sizes it), so the slot is free at once; the wait is a guard.  The words are
-// BulkJob's, passed as scalars (a struct whose address is taken would live in scratch)
+// post a job (one lane) as nsub <= kMaxSub sub-jobs of consecutive tiles: their indices j0 .. j0 +
+// nsub - 1 in one fetch-add; a slot takes sub-job j once its generation word reads j / J (the ring
+// holds every sub-job that can be unfinished at once -- rlo_world.cpp sizes it -- so that is at once;
+// the wait is a guard).  The bodies land first, then, after one drain, the words with the sequence,
+// which a mover's ticket waits for.  BulkJob's words are passed as scalars (a struct whose address
+// is taken would live in scratch).
 __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t kind, int origin, int lr, uint32_t slot_s,
                                          uint32_t bid, uint32_t len, uint32_t ntiles, int from, uint32_t logidx,
                                          uint32_t q, uint32_t gen) {
@@ -595,25 +597,40 @@ __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t
         bulk_fault(P, 6, (kind << 20) | (len & 0xfffffu));
         return;
     }
-    const uint64_t j = atomicAdd((unsigned long long*)&P.jctl[cls * 16 + kJctlPost], 1ull);
-    const uint32_t slot = (uint32_t)(j & (P.jslots - 1u));
+    const uint32_t per = (ntiles + kMaxSub - 1u) / kMaxSub, nsub = (ntiles + per - 1u) / per;
+    const uint64_t j0 = atomicAdd((unsigned long long*)&P.jctl[cls * 16 + kJctlPost], (unsigned long long)nsub);
     atomicAdd((unsigned long long*)&P.jctl[40 + kind], 1ull);  // diagnostics: posts by kind (41..43)
+    const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
     const uint64_t t0 = now_ticks();
-    while (__hip_atomic_load(&P.jfree[cls * P.jslots + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != j) {
-        __builtin_amdgcn_s_sleep(1);
-        if (now_ticks() - t0 > P.timeout_ticks) {  // cannot happen unless a mover died: stop loudly
-            atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
-            return;
+    for (uint32_t u = 0; u < nsub; u++) {
+        const uint64_t j = j0 + u;
+        while (__hip_atomic_load(&P.jfree[cls * P.jslots + (uint32_t)(j & jm)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+               (j >> lg)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (now_ticks() - t0 > P.timeout_ticks) {  // cannot happen unless a mover died: stop loudly
+                atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                return;
+            }
         }
     }
-    u32x4* dst = reinterpret_cast<u32x4*>(P.jobs + (size_t)cls * P.jslots + slot);
-    st_sys16(dst, u32x4{(uint32_t)(j + 1), kind, (uint32_t)origin, (uint32_t)lr});
-    st_sys16(dst + 1, u32x4{slot_s, bid, len, ntiles});
-    st_sys16(dst + 2, u32x4{0u, 0u, (uint32_t)from, logidx});
-    st_sys16(dst + 3, u32x4{q, gen, 0u, 0u});
+    const uint32_t parent = (uint32_t)(j0 & jm);
+    for (uint32_t u = 0; u < nsub; u++) {
+        u32x4* dst = reinterpret_cast<u32x4*>(P.jobs + (size_t)cls * P.jslots + (uint32_t)((j0 + u) & jm));
+        const uint32_t a = u * per, nt = min(per, ntiles - a);
+        // everything but the 8 bytes holding the sequence (st_sys16 is two 8-B stores, which may
+        // land in either order: the sequence half goes last, after the drain)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + 1, (uint64_t)(uint32_t)origin | ((uint64_t)(uint32_t)lr << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st_sys16(dst + 1, u32x4{slot_s, bid, len, nt});
+        st_sys16(dst + 2, u32x4{a, parent, (uint32_t)from, logidx});
+        st_sys16(dst + 3, u32x4{q, gen, ntiles, (uint32_t)j0});
+    }
     VM_DRAIN();
-    __hip_atomic_store(&P.jclaim[cls * P.jslots + slot], (uint64_t)(j + 1) << 32, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t u = 0; u < nsub; u++) {
+        uint64_t* dst = reinterpret_cast<uint64_t*>(P.jobs + (size_t)cls * P.jslots + (uint32_t)((j0 + u) & jm));
+        __hip_atomic_store(dst, (uint64_t)(uint32_t)(j0 + u + 1u) | ((uint64_t)kind << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // storm payload bytes [off, off + 16) of bcast (origin, bid, len) (off a multiple of 16)
@@ -626,11 +643,11 @@ __device__ __forceinline__ u32x4 storm_granule(uint32_t origin, uint32_t bid, ui
                  mask_bytes((uint32_t)(b >> 32), b0 - 12)};
 }
 
-// A mover workgroup: claims one tile at a time from its class's job stream -- the job at the
-// class head, by a CAS on that job's claim word (seq << 32 | next tile; the seq tells a recycled
-// slot from the job that was read) -- and moves it.  Claims are dynamic, so the work never depends
-// on which movers are busy; a fully claimed job moves the head on.  Exits once every progress
-// workgroup of the part has exited and no job is left.
+// A mover workgroup: draws sub-jobs of its class by ticket (one fetch-add, never retried: the
+// claim rate no longer serialises on one word), waits for the ticket's record, and moves every tile
+// of it.  A slot is freed as soon as its record is read, except a VERIFY job's first slot, whose
+// jdone / jsum accumulate the job until its last sub-job finished.  Exits once every progress
+// workgroup of the part has exited and no sub-job was posted for its ticket.
 template <int W, class SH>
 __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
     BulkSh& S = SS.b;
@@ -640,59 +657,50 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
     const uint32_t cls = mi < na ? JCLS_A : JCLS_B;
     const bool sys = P.sys_scope != 0;
     const int n = P.n;
-    const uint32_t jm = P.jslots - 1u;
+    const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
     uint64_t* posted = &P.jctl[cls * 16 + kJctlPost];
-    uint64_t* head = &P.jctl[cls * 16 + kJctlClaim];
+    uint64_t* ticket = &P.jctl[cls * 16 + kJctlClaim];
     BulkJob* ring = P.jobs + (size_t)cls * P.jslots;
-    uint64_t* jclaim = P.jclaim + (size_t)cls * P.jslots;
     uint64_t acq_key = ~0ull;  // (job, chunk) the last acquire covered
     const uint64_t t_launch = now_ticks();
     for (;;) {
-        // ---- claim one tile
+        // ---- draw a sub-job
         if (tid == 0) {
             uint32_t stop = 0, spins = 0;
-            for (;;) {
-                const uint64_t h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t slot = (uint32_t)(h & jm);
-                const uint64_t c = __hip_atomic_load(&jclaim[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((c >> 32) > h + 1) {  // a later job holds the slot: job h finished and was recycled
-                    atomicCAS((unsigned long long*)head, (unsigned long long)h, (unsigned long long)(h + 1));
-                    continue;
+            const uint64_t j = atomicAdd((unsigned long long*)ticket, 1ull);
+            const uint32_t slot = (uint32_t)(j & jm);
+            const u32x4* js = reinterpret_cast<const u32x4*>(&ring[slot]);
+            u32x4 v0 = __builtin_nontemporal_load(js);
+            while (v0.x != (uint32_t)(j + 1u)) {
+                // not posted (yet): every progress workgroup exited after its last post and the posts
+                // stop short of this ticket -> nothing more will come
+                if (__hip_atomic_load(&P.jctl[kJctlExited], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.n_local &&
+                    __hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j) {
+                    stop = 1;
+                    break;
                 }
-                if ((c >> 32) != h + 1) {  // job h not open yet: idle
-                    if (__hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= h) {
-                        // every progress workgroup exited (after its last post): nothing more will come
-                        if (__hip_atomic_load(&P.jctl[kJctlExited], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.n_local &&
-                            __hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= h) {
-                            stop = 1;
-                            break;
-                        }
-                    }
-                    if (poll32(P.error_flag)) { stop = 1; break; }
-                    __builtin_amdgcn_s_sleep(2);
-                    if ((++spins & 1023u) == 0 && now_ticks() - t_launch > P.deadline_ticks) {
-                        atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
-                        stop = 1;
-                        break;
-                    }
-                    continue;
+                if (poll32(P.error_flag)) { stop = 1; break; }
+                __builtin_amdgcn_s_sleep(2);
+                if ((++spins & 1023u) == 0 && now_ticks() - t_launch > P.deadline_ticks) {
+                    atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                    stop = 1;
+                    break;
                 }
-                const u32x4* js = reinterpret_cast<const u32x4*>(&ring[slot]);
+                v0 = __builtin_nontemporal_load(js);
+            }
+            if (!stop) {
                 u32x4 jv[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) jv[q] = __builtin_nontemporal_load(js + q);
-                if (jv[0].x != (uint32_t)(h + 1)) continue;  // recycled under us: re-read the head
-                const uint32_t T = jv[1].w;                   // BulkJob.ntiles
-                if ((uint32_t)c >= T) {                       // fully claimed: move the head on
-                    atomicCAS((unsigned long long*)head, (unsigned long long)h, (unsigned long long)(h + 1));
-                    continue;
-                }
-                if (atomicCAS((unsigned long long*)&jclaim[slot], (unsigned long long)c, (unsigned long long)(c + 1)) == c) {
-                    u32x4* jd = reinterpret_cast<u32x4*>(&S.mv_job);
+                for (int q = 0; q < 4; q++) jv[q] = __builtin_nontemporal_load(js + q);  // re-read behind the sequence
+                if (jv[0].x != (uint32_t)(j + 1u)) bulk_fault(P, 5, (uint32_t)j);
+                u32x4* jd = reinterpret_cast<u32x4*>(&S.mv_job);
 #pragma unroll
-                    for (int q = 0; q < 4; q++) jd[q] = jv[q];
-                    S.mv_ti = (uint32_t)c;
-                    break;
+                for (int q = 0; q < 4; q++) jd[q] = jv[q];
+                S.mv_ti = slot;
+                if (!(jv[0].y == JOB_VERIFY && jv[2].y == slot)) {  // read: the slot takes sub-job j + J
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&P.jfree[cls * P.jslots + slot], (j >> lg) + 1ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             S.mv_stop = stop;
@@ -700,10 +708,9 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
         BAR();
         if (S.mv_stop) return;
         const BulkJob jb = S.mv_job;  // uniform (LDS broadcast)
-        const uint32_t ti = S.mv_ti;
         if (!(jb.kind >= JOB_SCATTER && jb.kind <= JOB_VERIFY && (uint32_t)jb.origin < (uint32_t)n &&
               (uint32_t)jb.lr < P.n_local && jb.slot < P.bulk_slots && jb.len > 0 && jb.len <= P.bulk_cap &&
-              ti < jb.ntiles)) {
+              jb.ntiles > 0 && jb.ti0 + jb.ntiles <= jb.total && jb.parent <= jm)) {
             if (tid == 0) bulk_fault(P, 4, (jb.kind << 20) | (jb.seq & 0xfffffu));
             return;
         }
@@ -711,164 +718,163 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
         const int o = jb.origin;
         const int me = P.rank_begin + jb.lr;
         const BulkPlan pl = bulk_plan(n, len, P.bulk_cross != 0);
-        const uint32_t jslot = (jb.seq - 1u) & jm;
-
-        if (jb.kind == JOB_SCATTER || jb.kind == JOB_GATHER) {
-            // tile -> (chunk c, stripe k, tile i of that stripe-chunk)
-            uint32_t u = ti, c = 0, k = 0, i = 0;
-            if (jb.kind == JOB_SCATTER) {
-                for (c = 0; c + 1 < pl.nchunks; c++) {
-                    const uint32_t ct = bulk_chunk_tiles(pl, len, c);
-                    if (u < ct) break;
-                    u -= ct;
-                }
-                const uint64_t c0 = (uint64_t)c * pl.chunk;
-                const uint32_t clen = (uint32_t)min((uint64_t)pl.chunk, (uint64_t)len - c0);
-                const uint32_t full = clen / pl.stripe, tf = bulk_tiles_of(pl, pl.stripe);
-                if (u < full * tf) { k = u / tf; i = u - k * tf; }
-                else { k = full; i = u - full * tf; }
-            } else {
-                k = (uint32_t)((me - o - 1 + n) % n);
-                for (c = 0; c + 1 < pl.nchunks; c++) {
-                    const uint32_t ct = bulk_tiles_of(pl, bulk_stripe_len(pl, len, c, k));
-                    if (u < ct) break;
-                    u -= ct;
-                }
-                i = u;
-            }
-            const uint32_t slen = bulk_stripe_len(pl, len, c, k);
-            const uint32_t off0 = c * pl.chunk + k * pl.stripe + i * pl.tile;
-            const uint32_t tlen = min(pl.tile, slen - i * pl.tile);
-            const uint32_t ngr = (tlen + 15u) >> 4;
-            if (jb.kind == JOB_SCATTER) {
-                const int owner = (o + 1 + (int)k) % n;
-                const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, owner, o, s), P.bulk_cap);
-                const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, o, o, s), P.bulk_cap);
-                for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
-                    u32x4 v[4];
-#pragma unroll
-                    for (int uu = 0; uu < 4; uu++) {
-                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                        if (g < ngr) v[uu] = jb.gen ? ld_sc1(rs, off0 + 16u * g) : storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g);
+        for (uint32_t ti = jb.ti0; ti < jb.ti0 + jb.ntiles; ti++) {
+            if (jb.kind == JOB_SCATTER || jb.kind == JOB_GATHER) {
+                // tile -> (chunk c, stripe k, tile i of that stripe-chunk)
+                uint32_t u = ti, c = 0, k = 0, i = 0;
+                if (jb.kind == JOB_SCATTER) {
+                    for (c = 0; c + 1 < pl.nchunks; c++) {
+                        const uint32_t ct = bulk_chunk_tiles(pl, len, c);
+                        if (u < ct) break;
+                        u -= ct;
                     }
-#pragma unroll
-                    for (int uu = 0; uu < 4; uu++) {
-                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                        if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
+                    const uint64_t c0 = (uint64_t)c * pl.chunk;
+                    const uint32_t clen = (uint32_t)min((uint64_t)pl.chunk, (uint64_t)len - c0);
+                    const uint32_t full = clen / pl.stripe, tf = bulk_tiles_of(pl, pl.stripe);
+                    if (u < full * tf) { k = u / tf; i = u - k * tf; }
+                    else { k = full; i = u - full * tf; }
+                } else {
+                    k = (uint32_t)((me - o - 1 + n) % n);
+                    for (c = 0; c + 1 < pl.nchunks; c++) {
+                        const uint32_t ct = bulk_tiles_of(pl, bulk_stripe_len(pl, len, c, k));
+                        if (u < ct) break;
+                        u -= ct;
                     }
+                    i = u;
                 }
-                VM_DRAIN();
-                __syncthreads();
-                if (tid == 0) {
-                    bulk_release(sys);
-                    uint32_t* f = bulk_flags(P, owner, o, s);
-                    bflag_add(f + c, 1u, sys);
-                    bflag_add(f + kBulkTflag, 1u, sys);
-                }
-            } else {
-                // GATHER: my stripe of chunk c must have landed (class-A scatter tiles only)
-                if (tid == 0) {
-                    uint32_t* f = bulk_flags(P, me, o, s);
-                    const uint32_t want = bulk_tiles_of(pl, slen);
-                    uint32_t spins = 0;
-                    if (bflag_ld(f + c, sys) < want) {  // diagnostics: gather tiles waiting now / last wait
-                        atomicAdd((unsigned long long*)&P.jctl[38], 1ull);
-                        P.jctl[46] = ((uint64_t)(uint32_t)o << 48) | ((uint64_t)me << 32) | ((uint64_t)s << 24) | want;
-                    }
-                    while (bflag_ld(f + c, sys) < want) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if ((++spins & 1023u) == 0 && (poll32(P.error_flag) || now_ticks() - t_launch > P.deadline_ticks)) {
-                            atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
-                            break;
+                const uint32_t slen = bulk_stripe_len(pl, len, c, k);
+                const uint32_t off0 = c * pl.chunk + k * pl.stripe + i * pl.tile;
+                const uint32_t tlen = min(pl.tile, slen - i * pl.tile);
+                const uint32_t ngr = (tlen + 15u) >> 4;
+                if (jb.kind == JOB_SCATTER) {
+                    const int owner = (o + 1 + (int)k) % n;
+                    const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, owner, o, s), P.bulk_cap);
+                    const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, o, o, s), P.bulk_cap);
+                    for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
+                        u32x4 v[4];
+    #pragma unroll
+                        for (int uu = 0; uu < 4; uu++) {
+                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                            if (g < ngr) v[uu] = jb.gen ? ld_sc1(rs, off0 + 16u * g) : storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g);
                         }
-                    }
-                    const uint64_t key = ((uint64_t)jb.seq << 8) | c;
-                    if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
-                    atomicAdd((unsigned long long*)&P.jctl[39], 1ull);  // diagnostics: gather waits passed
-                }
-                __syncthreads();
-                const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
-                for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
-                    u32x4 v[4];
-#pragma unroll
-                    for (int uu = 0; uu < 4; uu++) {
-                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                        if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
-                    }
-                    for (int d = 1; d < n; d++) {  // every other non-originator (uniform)
-                        const int dst = (o + d) % n;
-                        if (dst == me) continue;
-                        const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, dst, o, s), P.bulk_cap);
-#pragma unroll
+    #pragma unroll
                         for (int uu = 0; uu < 4; uu++) {
                             const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
                             if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
                         }
                     }
+                    VM_DRAIN();
+                    __syncthreads();
+                    if (tid == 0) {
+                        bulk_release(sys);
+                        uint32_t* f = bulk_flags(P, owner, o, s);
+                        bflag_add(f + c, 1u, sys);
+                        bflag_add(f + kBulkTflag, 1u, sys);
+                    }
+                } else {
+                    // GATHER: my stripe of chunk c must have landed (class-A scatter tiles only)
+                    if (tid == 0) {
+                        uint32_t* f = bulk_flags(P, me, o, s);
+                        const uint32_t want = bulk_tiles_of(pl, slen);
+                        uint32_t spins = 0;
+                        if (bflag_ld(f + c, sys) < want) {  // diagnostics: gather tiles waiting now / last wait
+                            atomicAdd((unsigned long long*)&P.jctl[38], 1ull);
+                            P.jctl[46] = ((uint64_t)(uint32_t)o << 48) | ((uint64_t)me << 32) | ((uint64_t)s << 24) | want;
+                        }
+                        while (bflag_ld(f + c, sys) < want) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if ((++spins & 1023u) == 0 && (poll32(P.error_flag) || now_ticks() - t_launch > P.deadline_ticks)) {
+                                atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                                break;
+                            }
+                        }
+                        const uint64_t key = ((uint64_t)jb.seq << 8) | c;
+                        if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
+                        atomicAdd((unsigned long long*)&P.jctl[39], 1ull);  // diagnostics: gather waits passed
+                    }
+                    __syncthreads();
+                    const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
+                    for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
+                        u32x4 v[4];
+    #pragma unroll
+                        for (int uu = 0; uu < 4; uu++) {
+                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                            if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
+                        }
+                        for (int d = 1; d < n; d++) {  // every other non-originator (uniform)
+                            const int dst = (o + d) % n;
+                            if (dst == me) continue;
+                            const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, dst, o, s), P.bulk_cap);
+    #pragma unroll
+                            for (int uu = 0; uu < 4; uu++) {
+                                const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                                if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
+                            }
+                        }
+                    }
+                    VM_DRAIN();
+                    __syncthreads();
+                    if (tid < 64) {
+                        bulk_release(sys);
+                        // every other receiver got this tile; and so did my own count: my copy may not be
+                        // released (the origin may not reuse it) before my pushes out of it are done
+                        for (int d = 1 + tid; d < n; d += 64) {
+                            const int dst = (o + d) % n;
+                            bflag_add(bulk_flags(P, dst, o, s) + kBulkTflag, 1u, sys);
+                        }
+                    }
                 }
-                VM_DRAIN();
+            } else {  // JOB_VERIFY: checksum my complete copy (the pickup read of every byte)
+                if (tid == 0) {
+                    const uint64_t key = (uint64_t)jb.seq << 8;
+                    if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
+                }
                 __syncthreads();
-                if (tid < 64) {
-                    bulk_release(sys);
-                    // every other receiver got this tile; and so did my own count: my copy may not be
-                    // released (the origin may not reuse it) before my pushes out of it are done
-                    for (int d = 1 + tid; d < n; d += 64) {
-                        const int dst = (o + d) % n;
-                        bflag_add(bulk_flags(P, dst, o, s) + kBulkTflag, 1u, sys);
+                const uint32_t off0 = ti * kVerifyTile;
+                const uint32_t tlen = min(kVerifyTile, len - off0);
+                const uint32_t ngr = (tlen + 15u) >> 4;
+                const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
+                unsigned long long acc = 0;
+                for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
+                    u32x4 v[4];
+    #pragma unroll
+                    for (int uu = 0; uu < 4; uu++) {
+                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                        if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
+                    }
+    #pragma unroll
+                    for (int uu = 0; uu < 4; uu++) {
+                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                        if (g < ngr) {
+                            const uint32_t off = off0 + 16u * g;
+                            const int b0 = (int)len - (int)off;  // the reference's zero-padded tail
+                            const u32x4 w = {mask_bytes(v[uu].x, b0), mask_bytes(v[uu].y, b0 - 4), mask_bytes(v[uu].z, b0 - 8),
+                                             mask_bytes(v[uu].w, b0 - 12)};
+                            acc += chunk_mix(off >> 4, w);
+                        }
                     }
                 }
-            }
-        } else {  // JOB_VERIFY: checksum my complete copy (the pickup read of every byte)
-            if (tid == 0) {
-                const uint64_t key = (uint64_t)jb.seq << 8;
-                if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
-            }
-            __syncthreads();
-            const uint32_t off0 = ti * kVerifyTile;
-            const uint32_t tlen = min(kVerifyTile, len - off0);
-            const uint32_t ngr = (tlen + 15u) >> 4;
-            const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
-            unsigned long long acc = 0;
-            for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
-                u32x4 v[4];
-#pragma unroll
-                for (int uu = 0; uu < 4; uu++) {
-                    const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                    if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
-                }
-#pragma unroll
-                for (int uu = 0; uu < 4; uu++) {
-                    const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                    if (g < ngr) {
-                        const uint32_t off = off0 + 16u * g;
-                        const int b0 = (int)len - (int)off;  // the reference's zero-padded tail
-                        const u32x4 w = {mask_bytes(v[uu].x, b0), mask_bytes(v[uu].y, b0 - 4), mask_bytes(v[uu].z, b0 - 8),
-                                         mask_bytes(v[uu].w, b0 - 12)};
-                        acc += chunk_mix(off >> 4, w);
-                    }
-                }
-            }
-            // workgroup sum -> the job's accumulator (returning add: ordered before the tile count)
-            for (int sh = 32; sh >= 1; sh >>= 1) acc += __shfl_xor(acc, sh);
-            if ((tid & 63) == 0) atomicAdd((unsigned long long*)&S.mv_sum, acc);
-            __syncthreads();
-            if (tid == 0) {
-                (void)__hip_atomic_fetch_add(&P.jsum[cls * P.jslots + jslot], (uint64_t)S.mv_sum, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-                S.mv_sum = 0;
+                // workgroup sum of this tile -> the sub-job's sum (LDS; added to the job's once, below)
+                for (int sh = 32; sh >= 1; sh >>= 1) acc += __shfl_xor(acc, sh);
+                if ((tid & 63) == 0) atomicAdd((unsigned long long*)&S.mv_sum, acc);
             }
         }
-        // ---- tile finished: the last one finishes the job and recycles its slot
-        if (tid == 0) {
-            atomicAdd((unsigned long long*)&P.jctl[36 + cls], 1ull);  // diagnostics: tiles moved per class
-            // this tile's effects (a VERIFY's partial sum) before its count: the finisher reads them
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t old = atomicAdd(&P.jdone[cls * P.jslots + jslot], 1u);
-            if (old + 1u == jb.ntiles) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                if (jb.kind == JOB_VERIFY) {
-                    const uint64_t part = __hip_atomic_load(&P.jsum[cls * P.jslots + jslot], __ATOMIC_RELAXED,
+        // ---- sub-job finished
+        if (tid == 0) atomicAdd((unsigned long long*)&P.jctl[36 + cls], (unsigned long long)jb.ntiles);  // diagnostics
+        if (jb.kind == JOB_VERIFY) {
+            __syncthreads();  // every wave's tile sums are in S.mv_sum
+            if (tid == 0) {
+                const uint32_t ps = jb.parent;
+                (void)__hip_atomic_fetch_add(&P.jsum[cls * P.jslots + ps], (uint64_t)S.mv_sum, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                S.mv_sum = 0;
+                // this sub-job's sum before its count: the finisher reads them
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t old = atomicAdd(&P.jdone[cls * P.jslots + ps], jb.ntiles);
+                if (old + jb.ntiles == jb.total) {  // the job's last tiles: deliver the checksum, release
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const uint64_t part = __hip_atomic_load(&P.jsum[cls * P.jslots + ps], __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
                     const uint64_t tot = part + chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)o, jb.bid, TAG_BCAST, len});
                     atomicAdd((unsigned long long*)&P.stats[jb.lr].bcast_sum, (unsigned long long)tot);
@@ -877,16 +883,16 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                                  u32x4{len, 0xffffffffu, (uint32_t)tot, (uint32_t)(tot >> 32)});
                     const uint32_t nt = n > 2 ? bulk_stripe_tiles(pl, len, (uint32_t)((me - o - 1 + n) % n)) : 0u;
                     bulk_slot_release(P, me, o, s, sys, bulk_total_tiles(pl, len) + nt, jb.bid);
+                    __hip_atomic_store(&P.jdone[cls * P.jslots + ps], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&P.jsum[cls * P.jslots + ps], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&P.jfree[cls * P.jslots + ps], (uint64_t)(jb.pjob >> lg) + 1ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
-                __hip_atomic_store(&P.jdone[cls * P.jslots + jslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&P.jsum[cls * P.jslots + jslot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(&P.jfree[cls * P.jslots + jslot], (uint64_t)(jb.seq - 1u) + P.jslots, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        BAR();  // S.mv_* is rewritten by the next claim
+        BAR();  // S.mv_* is rewritten by the next draw
     }
 }
 

@@ -349,7 +349,6 @@ struct rlo_world {
     std::vector<uint8_t*> ph, pbf;
     DevBuf<uint64_t> d_bheap, d_bflag;
     DevBuf<int32_t> d_part_of, d_part_begin;
-    std::vector<uint64_t> jfree_init;      // [2][jslots] iota: slot i takes job i first
     std::vector<uint32_t> host_bulk_q;     // host mode: next bulk sequence of each local rank
 };
 
@@ -564,7 +563,22 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         if (mv == 0) mv = std::max(16, w->cus - w->nl) & ~1;
         if (mv < 2) { delete w; return RLO_E_OCCUPANCY; }
         w->nmov = (uint32_t)mv;
-        w->jslots = pow2_ceil((uint32_t)w->nl * (uint32_t)(w->L.n + 1) * w->L.bslots + 64u);
+        // every sub-job that can be unfinished at once: per local rank B originations (SCATTER) and
+        // N x B receptions (GATHER + VERIFY), each cut into min(kMaxSub, its tiles) sub-jobs (tile
+        // counts grow with the length: bounded at bulk_max)
+        {
+            const uint32_t bm = (uint32_t)std::min<uint64_t>(w->L.bulk_max, 0xFFF00000ull);
+            const rlo::BulkPlan pl = rlo::bulk_plan(w->L.n, bm, true);
+            const rlo::BulkPlan p1 = rlo::bulk_plan(w->L.n, bm, false);
+            const uint64_t ts = std::max(rlo::bulk_total_tiles(pl, bm), rlo::bulk_total_tiles(p1, bm));
+            const uint64_t tg = std::max(rlo::bulk_stripe_tiles(pl, bm, 0), rlo::bulk_stripe_tiles(p1, bm, 0));
+            const uint64_t tv = (bm + rlo::kVerifyTile - 1) / rlo::kVerifyTile;
+            const uint64_t K = rlo::kMaxSub;
+            const uint64_t nl = (uint64_t)w->nl, B = w->L.bslots, N = (uint64_t)w->L.n;
+            const uint64_t need = nl * B * std::min(K, ts) + nl * N * B * (std::min(K, tg) + std::min(K, tv)) + 64;
+            if (need > (1ull << 26)) { delete w; return RLO_E_INVAL; }
+            w->jslots = pow2_ceil((uint32_t)need);
+        }
     }
     rc = size_lds(w);
     if (rc) { delete w; return rc; }
@@ -583,9 +597,6 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         w->flags = keep;
         if (e) { rlo_world_destroy(w); return RLO_E_HIP; }
         (void)hipMemset(w->bflag, 0, w->L.bflag_bytes[me]);
-        w->jfree_init.resize(2ull * w->jslots);
-        for (uint32_t c = 0; c < 2; c++)
-            for (uint32_t i = 0; i < w->jslots; i++) w->jfree_init[(size_t)c * w->jslots + i] = i;
         w->host_bulk_q.assign(w->nl, 0);
     }
     (void)hipMemset(w->fwd, 0, std::max<uint64_t>(w->L.fwd_bytes[me], 1));
@@ -1262,11 +1273,9 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     // (rlo_device.hpp) and is reloaded, in every launch, not only in a fresh world
     HIPCHK(hipMemsetAsync(w->fwd, 0, w->L.fwd_bytes[w->part], s));
     HIPCHK(hipMemsetAsync(w->d_stats.p, 0, sizeof(rlo::RankStats) * w->nl, s));
-    if (w->L.bulk_max) {  // bulk flags / release counts, job rings (slot i takes job i first)
-        const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);
+    if (w->L.bulk_max) {  // bulk flags / release counts, job rings (generation 0: a slot takes its first sub-job)
         HIPCHK(hipMemsetAsync(w->bflag, 0, w->L.bflag_bytes[w->part], s));
         HIPCHK(hipMemsetAsync(w->jmem, 0, w->jmem_bytes, s));
-        HIPCHK(hipMemcpyAsync(w->jmem + m.jfree, w->jfree_init.data(), w->jfree_init.size() * 8, hipMemcpyHostToDevice, s));
         std::fill(w->host_bulk_q.begin(), w->host_bulk_q.end(), 0u);
     }
     if (w->have_program && (w->P.mode & rlo::MODE_LAT)) {
