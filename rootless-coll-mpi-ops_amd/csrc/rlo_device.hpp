@@ -52,6 +52,7 @@ enum Mode : uint32_t {
     MODE_LAZYPUB = 256u,  // diagnostic: publish counters after the next poll (the pre-eager scheme)
     MODE_NOSPIN = 512u,   // diagnostic: no tight re-poll after an idle iteration
     MODE_NOACQ = 1024u,   // diagnostic (UNSAFE): no agent acquire between iterations (A/B of its cost)
+    MODE_NOFAST = 2048u,  // A/B: every iteration takes the full path (no lone-message fast path)
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };

@@ -1388,11 +1388,92 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
                 if (lat_ok && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
             }
+            // ---- lone-message fast path (wave 0 alone): exactly one candidate, a small ring bcast or
+            // decision, no votes, and room in every out-ring it needs -> load it, deliver it, store it
+            // to its children and drain, here; the other waves see C == 0 and skip to the bookkeeping.
+            // A hop of the latency program or of an IAR decision costs one slot load and one store
+            // drain instead of the storm iteration's seven phases (~17K cycles, tools/lat_anatomy.py)
+            uint32_t fastdone = 0;
+            if (!host && R == 1u && C == 1u && vtot == 0u && !(P.mode & (MODE_PROF | MODE_NOFAST))) {
+                const int g = __builtin_ctzll(__ballot(lane < n_in2 && take > 0u));
+                const uint64_t h0 = rdl64(in_head_r, g);
+                const uint32_t src = (uint32_t)uni((int)t.in_data[g >> 1][g & 1]) + (uint32_t)(h0 & fcap_m) * P.fwd_stride;
+                u32x4 v = {0u, 0u, 0u, 0u};
+                if ((uint32_t)lane < nsmall) v = ld_sc1(rf, src + 16u * (uint32_t)lane);  // header + payload, one trip
+                const uint32_t fw0 = rdl32(v.x, 0), fid = rdl32(v.y, 0), fw2 = rdl32(v.z, 0), ft0 = rdl32(v.w, 0);
+                const int forg = (int)(fw0 & 0xffffu);
+                const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
+                const int ffrom = uni(t.in_src[g >> 1]);
+                bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
+                          (ftag == TAG_BCAST || ftag == TAG_DECISION) &&
+                          !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
+                uint32_t fneed = 0;
+                if (ok) {
+                    fneed = need_of(kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r), forg, sll, sl_r);
+                    const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
+                    ok = __ballot(full) == 0;
+                }
+                if (ok) {
+                    const uint32_t q = (uint32_t)lane;
+                    const int fvote = (int)(int8_t)(fw0 >> 24);
+                    // effects (phase F of the full path)
+                    uint32_t flog = ~0u;
+                    if (ftag == TAG_BCAST) {
+                        if (lane == 0) {
+                            atomicAdd(&S.bcast_delivered, 1ull);
+                            if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
+                            flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
+                                           (uint32_t)now_ticks() - ft0);
+                        }
+                        flog = rdl32(flog, 0);
+                        if (q < fnch)
+                            acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)forg, fid, TAG_BCAST, flen})
+                                              : chunk_mix(q - 1u, v);
+                    } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
+                        PendState* ps = &pend[2 * forg + ((fw2 >> 24) & 1u)];
+                        if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
+                            if (fvote != 0) {
+                                atomicAdd(&S.actions, 1ull);
+                                log_put(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8);
+                            }
+                            ps->valid = PS_NONE;
+                        }
+                        atomicAdd(&S.dec_delivered, 1ull);
+                        if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
+                        log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
+                    }
+                    // forward: the same slot bytes into every needed out-ring (phase G)
+                    for (uint32_t m = fneed; m; m &= m - 1) {
+                        const int oi = __builtin_ctz(m);
+                        const uint64_t slot = rdl64(out_tail_r, oi);
+                        const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
+                        if (q < fnch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+                    }
+                    if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
+                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+                    if (ftag == TAG_BCAST && (P.mode & MODE_LAT) && lane == 0) {  // the round's last pickup
+                        const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[fid], 1u, __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_SYSTEM)
+                                                 : atomicAdd(&P.lat_count[fid], 1u);
+                        if (old + 1u == (uint32_t)(P.n - 1)) {
+                            P.lat_out[fid] = (uint64_t)((uint32_t)now_ticks() - ft0);
+                            if (sys) __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            else __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                    VM_DRAIN();  // wave 0's stores: published in the bookkeeping below
+                    // the bookkeeping sees: in-ring g admitted its one message (rtake_r), these out-rings one each
+                    noi_r = lane < nout ? ((fneed >> lane) & 1u) : 0u;
+                    R = 0;
+                    C = 0;
+                    fastdone = 1;
+                }
+            }
             if (lane == 0) {
                 S.ract = ract;
                 S.vtot = vtot;
                 S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
-                S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = 0;
+                S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = fastdone;
                 S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase; S.nchmax = 0;
                 S.exit_now = done_w0;
                 if (P.mode & MODE_PROF) S.dbg[0] += R;

@@ -1311,6 +1311,9 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool noacq = std::getenv("RLO_NO_ACQUIRE") != nullptr;  // diagnostic A/B, unsafe
     if (noacq) w->P.mode |= rlo::MODE_NOACQ;
     else w->P.mode &= ~rlo::MODE_NOACQ;
+    static const bool nofast = std::getenv("RLO_NO_FAST") != nullptr;  // A/B: no lone-message fast path
+    if (nofast) w->P.mode |= rlo::MODE_NOFAST;
+    else w->P.mode &= ~rlo::MODE_NOFAST;
     hipError_t e = rlo_launch_progress(&w->P, w->nl + (w->L.bulk_max ? (int)w->nmov : 0), w->dyn_lds, s, w->variant);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));
