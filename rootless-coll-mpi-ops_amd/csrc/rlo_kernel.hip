@@ -1388,35 +1388,47 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
                 if (lat_ok && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
             }
-            // ---- lone-message fast path (wave 0 alone): exactly one candidate, a small ring bcast or
-            // decision, no votes, and room in every out-ring it needs -> load it, deliver it, store it
-            // to its children and drain, here; the other waves see C == 0 and skip to the bookkeeping.
-            // A hop of the latency program or of an IAR decision costs one slot load and one store
-            // drain instead of the storm iteration's seven phases (~17K cycles, tools/lat_anatomy.py)
+            // ---- lone-message fast path (wave 0 alone): exactly one candidate, a small ring bcast,
+            // decision or proposal (device judge), no votes, and room in every out-ring it needs ->
+            // load it, apply its effects, store it to its children and drain, here; the other waves
+            // see C == 0 and skip to the bookkeeping.  (My own originations stay on the full path:
+            // built here too, out of line or inline, they tip the kernel over 256 VGPRs -- one wave
+            // per SIMD, and the all-ranks-co-resident check fails.)  A hop of the latency program or of an IAR round costs one slot
+            // load and one store drain instead of the full iteration's seven phases (~17K cycles,
+            // tools/lat_anatomy.py).  Effects restate phase F below line for line.
             uint32_t fastdone = 0;
             if (!host && R == 1u && C == 1u && vtot == 0u && !(P.mode & (MODE_PROF | MODE_NOFAST))) {
-                const int g = __builtin_ctzll(__ballot(lane < n_in2 && take > 0u));
-                const uint64_t h0 = rdl64(in_head_r, g);
-                const uint32_t src = (uint32_t)uni((int)t.in_data[g >> 1][g & 1]) + (uint32_t)(h0 & fcap_m) * P.fwd_stride;
+                const uint32_t q = (uint32_t)lane;
+                const int fg = __builtin_ctzll(__ballot(lane < n_in2 && take > 0u));
+                const uint64_t h0 = rdl64(in_head_r, fg);
+                const uint32_t fsrc = (uint32_t)uni((int)t.in_data[fg >> 1][fg & 1]) + (uint32_t)(h0 & fcap_m) * P.fwd_stride;
                 u32x4 v = {0u, 0u, 0u, 0u};
-                if ((uint32_t)lane < nsmall) v = ld_sc1(rf, src + 16u * (uint32_t)lane);  // header + payload, one trip
+                if (q < nsmall) v = ld_sc1(rf, fsrc + 16u * q);  // header + payload, one trip
+                const int ffrom = uni(t.in_src[fg >> 1]);
                 const uint32_t fw0 = rdl32(v.x, 0), fid = rdl32(v.y, 0), fw2 = rdl32(v.z, 0), ft0 = rdl32(v.w, 0);
                 const int forg = (int)(fw0 & 0xffffu);
                 const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
-                const int ffrom = uni(t.in_src[g >> 1]);
+                const uint32_t fpseq = fw2 >> 24;
+                const int fvote = (int)(int8_t)(fw0 >> 24);
                 bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
-                          (ftag == TAG_BCAST || ftag == TAG_DECISION) &&
-                          !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
-                uint32_t fneed = 0;
+                     (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL) &&
+                     !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
+                int fjudge = 1;
+                uint32_t fkids = 0, fneed = 0;
                 if (ok) {
-                    fneed = need_of(kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r), forg, sll, sl_r);
+                    if (ftag == TAG_PROPOSAL) {  // device judge on the PBuf data (phase D)
+                        uint32_t dl = nsmall > 1 ? rdl32(v.z, 1) : 0u;
+                        if (dl > flen - 16u) dl = flen > 16u ? flen - 16u : 0u;
+                        fjudge = judge_eval(P, rf, me, my_mask, (int32_t)fid, fsrc + kHdr + 16u, dl);
+                        fkids = fjudge == 1 ? kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r) : 0u;
+                    } else {
+                        fkids = kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r);
+                    }
+                    fneed = need_of(fkids, forg, sll, sl_r);
                     const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
                     ok = __ballot(full) == 0;
                 }
                 if (ok) {
-                    const uint32_t q = (uint32_t)lane;
-                    const int fvote = (int)(int8_t)(fw0 >> 24);
-                    // effects (phase F of the full path)
                     uint32_t flog = ~0u;
                     if (ftag == TAG_BCAST) {
                         if (lane == 0) {
@@ -1429,8 +1441,33 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if (q < fnch)
                             acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)forg, fid, TAG_BCAST, flen})
                                               : chunk_mix(q - 1u, v);
+                    } else if (ftag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
+                        if (lane == 0) {
+                            atomicAdd(&S.proposals_recv, 1ull);
+                            if (S.own_state != 0 && (int32_t)fid == S.own_pid) {
+                                set_error(S, P, ERR_PID_COLLISION, fid);  // :690-692
+                            } else {
+                                const uint32_t k = (uint32_t)fg >> 1;
+                                atomicAdd(&S.judge_calls, 1ull);
+                                log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
+                                PendState* ps = &pend[2 * forg + (fpseq & 1u)];
+                                if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
+                                    ps->valid = PS_NONE;
+                                    emit_vote(S, P, me, k, forg, (int32_t)fid, fpseq, 0);
+                                } else {
+                                    const uint32_t nk = (uint32_t)__builtin_popcount(fkids);
+                                    ps->pid = (int32_t)fid;
+                                    ps->word = 0;
+                                    ps->parent_k = (uint16_t)k;
+                                    ps->needed = (uint8_t)nk;
+                                    ps->pseq = fpseq | ((flen - 16u) << 8);
+                                    ps->valid = PS_ACTIVE;
+                                    if (nk == 0) emit_vote(S, P, me, k, forg, (int32_t)fid, fpseq, 1);
+                                }
+                            }
+                        }
                     } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
-                        PendState* ps = &pend[2 * forg + ((fw2 >> 24) & 1u)];
+                        PendState* ps = &pend[2 * forg + (fpseq & 1u)];
                         if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
                             if (fvote != 0) {
                                 atomicAdd(&S.actions, 1ull);
