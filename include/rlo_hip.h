@@ -280,6 +280,13 @@ int rlo_client_bulk_get(rlo_client_t* c, const rlo_log_rec_t* ev, void* dst);
 /* diagnostics, 9 words: posted, forwarded, consumed, tail seen by the kernel, pickups consumed,
  * pickups written, pickup head seen by the kernel, kernel iterations (/4096 beat), state */
 int rlo_client_debug(rlo_client_t* c, uint64_t* out);
+/* diagnostics (kernel launched with RLO_HOST_DIAG set), 8 words valid once the rank stopped serving:
+ * iterations with commands pending, iterations a proposal was held (own proposal active), iterations
+ * blocked on pickup-ring room, host iterations, then commands seen -> drained in < 20 / 100 / 500 /
+ * >= 500 us (counts) */
+int rlo_client_hdiag(rlo_client_t* c, uint64_t* out);
+/* diagnostics: commands the leader's proxy forwarded so far, and when (CLOCK_MONOTONIC ns) */
+int rlo_client_fwd(rlo_client_t* c, uint64_t* fwd, int64_t* fwd_ns);
 
 /* ------------------------------------------------------------------ run */
 int rlo_reset(rlo_world_t* w, void* stream);           /* zero this part's counters (sync) */

@@ -168,6 +168,19 @@ int rlo_client_debug(rlo_client_t* c, uint64_t* out) {
     return RLO_OK;
 }
 
+int rlo_client_fwd(rlo_client_t* c, uint64_t* fwd, int64_t* fwd_ns) {
+    if (!c || !fwd || !fwd_ns) return RLO_E_INVAL;
+    *fwd = ld_acq(&c->box->fwd);
+    *fwd_ns = ld_acq(&c->box->fwd_ns);
+    return RLO_OK;
+}
+
+int rlo_client_hdiag(rlo_client_t* c, uint64_t* out) {
+    if (!c || !out) return RLO_E_INVAL;
+    for (int i = 0; i < 8; i++) out[i] = ld_acq(&c->hctl[rlo::kHctlDiag + i]);
+    return RLO_OK;
+}
+
 int rlo_client_bulk_put(rlo_client_t* c, const void* data, uint64_t len, uint32_t timeout_us, uint32_t* q_out) {
     if (!c || !q_out || len == 0 || !data || len > c->h->bulk_max) return RLO_E_INVAL;
     const auto t0 = std::chrono::steady_clock::now();

@@ -53,6 +53,7 @@ enum Mode : uint32_t {
     MODE_NOSPIN = 512u,   // diagnostic: no tight re-poll after an idle iteration
     MODE_NOACQ = 1024u,   // diagnostic (UNSAFE): no agent acquire between iterations (A/B of its cost)
     MODE_NOFAST = 2048u,  // A/B: every iteration takes the full path (no lone-message fast path)
+    MODE_HDIAG = 4096u,   // diagnostic, host mode: command-wait counters into hctl[kHctlDiag..] at exit
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };
@@ -65,6 +66,8 @@ enum HostCmd : uint32_t { CMD_JUDGE = 16, CMD_OWN_JUDGE = 17, CMD_QUIT = 18, CMD
 constexpr int kHctlWords = 64;
 constexpr int kHctlInjTail = 0, kHctlInjHead = 16, kHctlPkTail = 32, kHctlPkHead = 48;
 constexpr int kHctlState = 40;  // device-written: 1 once the rank's workgroup serves, 2 once it exited
+constexpr int kHctlDiag = 20;  // MODE_HDIAG, 8 words: iterations with commands pending, proposals held (own one
+                               // active), pickup-ring blocks, host iterations, seen -> drained < 20 / 100 / 500 / >= 500 us
 constexpr int kHctlBeat = 41;   // device-written heartbeat: [41] iterations, [42] command tail seen, [43] pickup head seen
 
 enum Judge : uint32_t { JUDGE_APPROVE = 0, JUDGE_MASK = 1, JUDGE_ISP = 2, JUDGE_HASH = 3 };

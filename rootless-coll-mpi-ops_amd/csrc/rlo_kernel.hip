@@ -136,6 +136,7 @@ struct Shared {
     int64_t own_iter, own_n;
     // origination progress
     uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
+    uint64_t hd[8], hd_t0;  // MODE_HDIAG counters (host mode)
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
@@ -959,7 +960,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         for (int i = tid; i < kHistBins; i += kBlock) S.hist[i] = 0;
         for (int i = tid; i < 4 * 64; i += kBlock) { (&S.pubw[0][0])[i] = 0; (&S.snap[0][0])[i] = 0; }
         if (tid < kMaxIn) { S.vout_tail[tid] = 0; S.vout_head[tid] = 0; }
-        if (tid < 8) { S.prof[tid] = 0; S.dbg[tid] = 0; }
+        if (tid < 8) { S.prof[tid] = 0; S.dbg[tid] = 0; S.hd[tid] = 0; }
         if (tid == 0) {
             S.prof_t = __builtin_amdgcn_s_memtime();
             S.own_pid = -1;  // proposal_state_init, :1238
@@ -974,7 +975,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
-            S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0;
+            S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
@@ -1131,6 +1132,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - pk_head);
                 hblock = pk_free < 8u;
                 hlim = hblock ? 0u : (pk_free - 4u) / 2u;
+                if ((P.mode & MODE_HDIAG) && lane == 0) {
+                    S.hd[3]++;
+                    if (hblock) S.hd[2]++;
+                }
             }
             if constexpr (BULK) {
                 // completed bulk receptions: delivered now.  Device programs: counted, logged and
@@ -1281,6 +1286,16 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // behind it becomes candidates in place (a proposal only when no own proposal is
                 // active, and it ends the run)
                 const uint64_t pend_n = rdl64(hpoll, 0) - S.hin_head;
+                if ((P.mode & MODE_HDIAG) && lane == 0) {  // how long seen commands wait here
+                    if (pend_n) {
+                        S.hd[0]++;
+                        if (!S.hd_t0) S.hd_t0 = now_ticks();
+                    } else if (S.hd_t0) {
+                        const uint64_t d = now_ticks() - S.hd_t0;
+                        S.hd[4 + (d < 2000u ? 0 : d < 10000u ? 1 : d < 50000u ? 2 : 3)]++;
+                        S.hd_t0 = 0;
+                    }
+                }
                 const uint32_t np = (uint32_t)min(pend_n, (uint64_t)kPass);
                 if (np) {
                     const uint32_t nit = np * nsmall;
@@ -1331,6 +1346,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (pm) {
                         const uint32_t fp = (uint32_t)__builtin_ctzll(pm);
                         run = (S.own_state == 0 && loc_kind != K_DEC) ? fp + 1u : fp;
+                        if ((P.mode & MODE_HDIAG) && lane == 0 && run == fp) S.hd[1]++;
                     }
                     nh = run;
                     gap_lo = C;
@@ -2358,6 +2374,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         st.t_end = now_ticks();
         st.error = S.error;
         st.error_aux = S.error_aux;
+        if (host && (P.mode & MODE_HDIAG))
+            for (int i = 0; i < 8; i++) pub64_sys(&hctl[kHctlDiag + i], S.hd[i]);
         if (host) pub64_sys(&hctl[kHctlState], 2ull);  // this rank stopped serving
     }
 }

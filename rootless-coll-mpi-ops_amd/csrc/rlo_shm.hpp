@@ -52,6 +52,7 @@ struct ClientBox {
     int64_t rc;                   // RLO_OK / RLO_E_AGAIN (ACQUIRE: slot still busy) / error
     uint64_t q;                   // ACQUIRE: the bulk sequence taken
     uint64_t fwd;                 // leader: commands forwarded into the VRAM ring (diagnostics)
+    int64_t fwd_ns;               // leader: CLOCK_MONOTONIC ns of that forward (diagnostics)
 };
 static_assert(sizeof(ClientBox) == 512, "ClientBox layout");
 

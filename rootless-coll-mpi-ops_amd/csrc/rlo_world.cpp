@@ -320,6 +320,7 @@ struct rlo_world {
     uint8_t* h_cmd = nullptr;       // [nl][cmd_cap][stride]     uncached VRAM, CPU writes through the BAR
     uint64_t* h_ctl = nullptr;      // [nl][kHctlWords]           pinned host: device-written counters
     uint64_t* d_ctl = nullptr;      // [nl][kHctlWords]           uncached VRAM: host-written counters
+    volatile uint32_t* hdp = nullptr;  // the GPU's HDP_MEM_COHERENCY_FLUSH_CNTL register (see hdp_flush)
     rlo::LogRec* h_ev = nullptr;    // [nl][pk_cap]
     uint8_t* h_evp = nullptr;       // [nl][pk_cap][max_payload]
     uint32_t cmd_cap = 0, pk_cap = 0;
@@ -1075,6 +1076,16 @@ static int bar_alloc(void** p, size_t bytes) {
     return RLO_OK;
 }
 
+// CPU stores through the BAR pass the GPU's host data path (HDP), which can hold them for up to ~1 ms
+// before a polling kernel sees them, uncached VRAM or not: drop-in IAR rounds at 8 ranks were
+// bimodal, 110 us or 1.1 ms (profiles/r2_dropin_hdp.txt).  Writing the HDP flush register after a
+// batch of BAR stores pushes them to memory at once (what RCCL's host proxy does for its flags)
+static void hdp_flush(const rlo_world* w) {
+    if (!w->hdp) return;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // the BAR stores (write-combined) before the flush
+    *w->hdp = 1u;
+}
+
 static int host_alloc(void** p, size_t bytes) {
     // coherent (fine-grained) pinned memory: the kernel polls words the CPU writes and vice versa
     hipError_t e = hipHostMalloc(p, std::max<size_t>(bytes, 256), hipHostMallocCoherent | hipHostMallocMapped);
@@ -1154,6 +1165,12 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
         host_free(w);
         return RLO_E_HIP;
     }
+    w->hdp = nullptr;
+    if (!std::getenv("RLO_NO_HDP_FLUSH")) {  // A/B switch; the attribute returns the register's mapped address
+        uint32_t* reg = nullptr;
+        if (hipDeviceGetAttribute(reinterpret_cast<int*>(&reg), hipDeviceAttributeHdpMemFlushCntl, w->device) == hipSuccess)
+            w->hdp = reg;
+    }
     const uint64_t* dev_hctl = nullptr;
     const rlo::LogRec* dev_ev = nullptr;
     const uint8_t* dev_evp = nullptr;
@@ -1208,6 +1225,7 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payl
     __atomic_thread_fence(__ATOMIC_SEQ_CST);  // BAR stores may be write-combined: slot before tail
     __atomic_store_n(&dctl[rlo::kHctlInjTail], tail + 1, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);  // push the tail out now
+    hdp_flush(w);
     return RLO_OK;
 }
 
@@ -1227,6 +1245,7 @@ int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, ui
     w->pk_head[lr] = head + 1;
     __atomic_store_n(&w->d_ctl[(size_t)lr * rlo::kHctlWords + rlo::kHctlPkHead], head + 1, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);  // a write-combined BAR store would otherwise linger
+    hdp_flush(w);
     return 1;
 }
 
@@ -1314,6 +1333,9 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool nofast = std::getenv("RLO_NO_FAST") != nullptr;  // A/B: no lone-message fast path
     if (nofast) w->P.mode |= rlo::MODE_NOFAST;
     else w->P.mode &= ~rlo::MODE_NOFAST;
+    static const bool hdiag = std::getenv("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
+    if (hdiag) w->P.mode |= rlo::MODE_HDIAG;
+    else w->P.mode &= ~rlo::MODE_HDIAG;
     hipError_t e = rlo_launch_progress(&w->P, w->nl + (w->L.bulk_max ? (int)w->nmov : 0), w->dyn_lds, s, w->variant);
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));
@@ -1536,6 +1558,7 @@ int rlo_host_wait_started(rlo_world_t* w, uint32_t timeout_ms) {
 int rlo_host_proxy(rlo_world_t* w) {
     if (!w || !w->shm) return RLO_E_INVAL;
     int acted = 0;
+    bool bar = false;  // BAR stores this pass: one HDP flush after them
     const uint32_t cc = w->cmd_cap, stride = w->L.stride;
     for (int lr = 0; lr < w->nl; lr++) {
         rlo::ClientBox* box = (rlo::ClientBox*)(w->shm + w->SL.cli) + lr;
@@ -1556,10 +1579,13 @@ int rlo_host_proxy(rlo_world_t* w) {
                 std::memcpy(dst + off, src + off, nb);
             }
             w->cmd_tail[lr] = mt;
+            box->fwd_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now().time_since_epoch()).count();
             box->fwd = mt;
             __atomic_thread_fence(__ATOMIC_SEQ_CST);  // BAR stores may be write-combined: slots before tail
             __atomic_store_n(&dctl[rlo::kHctlInjTail], mt, __ATOMIC_RELEASE);
             __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            bar = true;
             acted++;
         }
         const uint64_t pk = __atomic_load_n(&box->mpk, __ATOMIC_ACQUIRE);
@@ -1567,7 +1593,12 @@ int rlo_host_proxy(rlo_world_t* w) {
             w->pk_head[lr] = pk;
             __atomic_store_n(&dctl[rlo::kHctlPkHead], pk, __ATOMIC_RELEASE);
             __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            bar = true;
             acted++;
+        }
+        if (bar) {  // this rank's command / pickup head: visible to its kernel now, not after the pass
+            hdp_flush(w);
+            bar = false;
         }
         const uint64_t rq = __atomic_load_n(&box->req, __ATOMIC_ACQUIRE);
         if (rq == w->cli_req[lr]) continue;

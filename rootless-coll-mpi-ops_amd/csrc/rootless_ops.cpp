@@ -106,6 +106,12 @@ struct progress_engine {
     // RLO_TRACE=1: counters printed at cleanup (diagnostics)
     uint64_t n_progress = 0, n_events = 0, n_pumped = 0, n_judge = 0, n_result = 0;
     int64_t t_submit = 0, sum_prop_ns = 0, max_prop_ns = 0;
+    // RLO_TRACE: my proposal's two legs, as seen here -- submit -> the kernel consumed the command
+    // (the host -> device path), then -> my result event (the device rounds + device -> host path);
+    // histogram buckets < 0.2, 0.5, 1, 2 ms and beyond
+    uint64_t d_sub_idx = 0;
+    int64_t d_cons_ns = 0, d_fwd_ns = 0;
+    uint32_t d_hist[2][5] = {}, d_fh[2][5] = {};  // d_fh: submit -> forwarded by the proxy, forwarded -> consumed
     int64_t t_moved = 0, t_dump = 0;  // RLO_WATCHDOG: last event / last state dump
     progress_engine* next = nullptr;
 };
@@ -247,6 +253,8 @@ void reap_sent(progress_engine* e) {
     }
 }
 
+int leg_bucket(int64_t ns) { return ns < 200000 ? 0 : ns < 500000 ? 1 : ns < 1000000 ? 2 : ns < 2000000 ? 3 : 4; }
+
 void check_alive(progress_engine* e) {
     if (e->failed) return;
     const int st = rlo_client_state(e->cl);
@@ -323,6 +331,11 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             break;
         }
         case RLO_EV_RESULT: {  // my decision went out (:560-563 + _iar_decision_bcast :908-917)
+            if (e->d_cons_ns) {
+                e->d_hist[1][leg_bucket(now_ns() - e->d_cons_ns)]++;
+                e->d_cons_ns = 0;
+            }
+            e->d_sub_idx = 0;
             if (e->t_submit) {
                 const int64_t d = now_ns() - e->t_submit;
                 e->sum_prop_ns += d;
@@ -442,6 +455,24 @@ void progress(progress_engine* e) {
     {
         std::lock_guard<std::mutex> lk(e->mu);
         pump(e);
+        if (e->d_sub_idx && !e->d_cons_ns) {  // RLO_TRACE: has the kernel taken my proposal yet?
+            if (!e->d_fwd_ns) {  // has the leader's proxy forwarded it?
+                uint64_t f = 0;
+                int64_t fns = 0;
+                rlo_client_fwd(e->cl, &f, &fns);
+                if (f >= e->d_sub_idx) {
+                    e->d_fwd_ns = fns;
+                    e->d_fh[0][leg_bucket(fns - e->t_submit)]++;
+                }
+            }
+            uint64_t consumed = 0;
+            rlo_client_cmd_count(e->cl, &consumed, nullptr);
+            if (consumed >= e->d_sub_idx) {
+                e->d_cons_ns = now_ns();
+                e->d_hist[0][leg_bucket(e->d_cons_ns - e->t_submit)]++;
+                if (e->d_fwd_ns) e->d_fh[1][leg_bucket(e->d_cons_ns - e->d_fwd_ns)]++;
+            }
+        }
         while (!e->evq.empty()) {
             const uint32_t k = e->evq.front().ev.kind;
             local.push_back(std::move(e->evq.front()));
@@ -515,7 +546,17 @@ void proxy_loop() {
     unsigned idle = 0;
     uint64_t seen = ~0ull;
     std::vector<rlo_world_t*> mine;
+    // RLO_PROXY_DIAG: the largest gap between two passes (a descheduled proxy stalls every rank)
+    static const bool diag = std::getenv("RLO_PROXY_DIAG") != nullptr;
+    int64_t t_prev = diag ? now_ns() : 0, gap_max = 0, gaps_1ms = 0, passes = 0;
     while (!g_proxy_stop.load(std::memory_order_relaxed)) {
+        if (diag) {
+            const int64_t tn = now_ns();
+            gap_max = std::max(gap_max, tn - t_prev);
+            gaps_1ms += tn - t_prev > 1000000;
+            t_prev = tn;
+            passes++;
+        }
         const uint64_t gen = g_served_gen.load(std::memory_order_acquire);
         if (gen != seen) {
             {
@@ -534,6 +575,9 @@ void proxy_loop() {
         else if (++idle > (1u << 20)) std::this_thread::sleep_for(std::chrono::microseconds(20));  // long idle only
         else __builtin_ia32_pause();
     }
+    if (diag)
+        std::fprintf(stderr, "proxy diag: passes %lld, max gap %.1f us, gaps > 1 ms %lld\n", (long long)passes,
+                     gap_max * 1e-3, (long long)gaps_1ms);
 }
 
 void served_add(rlo_world_t* w) {
@@ -913,6 +957,14 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
                      (unsigned long long)eng->n_events, (unsigned long long)eng->n_pumped, (unsigned long long)eng->n_judge,
                      (unsigned long long)eng->n_result, eng->n_result ? eng->sum_prop_ns / 1e3 / eng->n_result : 0.0,
                      eng->max_prop_ns / 1e3);
+    if (std::getenv("RLO_TRACE"))
+        std::fprintf(stderr, "rlo trace rank %d legs (<0.2/0.5/1/2/>2 ms): submit->consumed %u %u %u %u %u | consumed->result %u %u %u %u %u\n",
+                     eng->rank, eng->d_hist[0][0], eng->d_hist[0][1], eng->d_hist[0][2], eng->d_hist[0][3], eng->d_hist[0][4],
+                     eng->d_hist[1][0], eng->d_hist[1][1], eng->d_hist[1][2], eng->d_hist[1][3], eng->d_hist[1][4]);
+    if (std::getenv("RLO_TRACE"))
+        std::fprintf(stderr, "rlo trace rank %d split: submit->forwarded %u %u %u %u %u | forwarded->consumed %u %u %u %u %u\n",
+                     eng->rank, eng->d_fh[0][0], eng->d_fh[0][1], eng->d_fh[0][2], eng->d_fh[0][3], eng->d_fh[0][4],
+                     eng->d_fh[1][0], eng->d_fh[1][1], eng->d_fh[1][2], eng->d_fh[1][3], eng->d_fh[1][4]);
     // collective quiescence (:1607-1627): every bcast and decision sent anywhere has arrived here
     int sent = (int)eng->sent_bcast, total = 0, done = 0;
     MPI_Request req;
@@ -942,6 +994,14 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
         std::lock_guard<std::mutex> lk(eng->mu);
         pump(eng);
         eng->evq.clear();
+    }
+    if (std::getenv("RLO_HOST_DIAG") && !eng->failed) {
+        uint64_t d[8] = {};
+        rlo_client_hdiag(eng->cl, d);
+        std::fprintf(stderr, "rlo hdiag rank %d: pending iters %llu held %llu pk-blocked %llu host iters %llu | seen->drained "
+                     "<20us %llu <100us %llu <500us %llu >=500us %llu\n", eng->rank, (unsigned long long)d[0],
+                     (unsigned long long)d[1], (unsigned long long)d[2], (unsigned long long)d[3], (unsigned long long)d[4],
+                     (unsigned long long)d[5], (unsigned long long)d[6], (unsigned long long)d[7]);
     }
     MPI_Barrier(eng->group);  // every rank of my GPU's part stopped: the kernel ends
     if (eng->leader) {
@@ -1079,6 +1139,13 @@ int RLO_submit_proposal(RLO_engine_t* eng, char* proposal, size_t prop_size, RLO
     c.id = my_proposal_id;
     c.vote = 1;
     if (post(eng, c, pb.data(), (uint32_t)pb.size(), nullptr)) return -1;
+    static const bool trace = std::getenv("RLO_TRACE") != nullptr;
+    if (trace) {
+        std::lock_guard<std::mutex> lk(eng->mu);
+        if (eng->backlog.empty()) rlo_client_cmd_count(eng->cl, nullptr, &eng->d_sub_idx);
+        eng->d_cons_ns = 0;
+        eng->d_fwd_ns = 0;
+    }
     RLO_make_progress_all();
     return eng->own.state == RLO_COMPLETED ? eng->own.vote : -1;
 }

@@ -106,7 +106,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan",
            "rlo_storm_lengths", "rlo_host_share", "rlo_host_unlink", "rlo_host_proxy", "rlo_host_wait_started",
            "rlo_host_fail", "rlo_client_attach", "rlo_client_detach", "rlo_client_state", "rlo_client_post",
-           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_host_device_judge"]
+           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_client_hdiag", "rlo_client_fwd", "rlo_host_device_judge"]
 
 _lib = None
 
@@ -170,6 +170,8 @@ def load():
     L.rlo_client_bulk_put.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_client_bulk_get.argtypes = [vp, ctypes.POINTER(LogRec), vp]
     L.rlo_client_debug.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.rlo_client_hdiag.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.rlo_client_fwd.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64)]
     L.rlo_bulk_debug.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     L.rlo_device_error.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_strerror.argtypes = [ctypes.c_int]

@@ -138,6 +138,20 @@ static void lat(int rounds, int len) {
     free(l);
 }
 
+/* API_DIAG=1: per-rank loop-gap / round-latency / context-switch counts on stderr (is a slow run
+ * the host descheduling us, or the engine?) */
+static long ctx_switches(const char* key) {
+    FILE* f = fopen("/proc/self/status", "r");
+    char line[256];
+    long v = -1;
+    size_t kl = strlen(key);
+    if (!f) return -1;
+    while (fgets(line, sizeof line, f))
+        if (!strncmp(line, key, kl)) v = atol(line + kl + 1);
+    fclose(f);
+    return v;
+}
+
 static int approve_cb(const void* a, void* c) {
     (void)a;
     (void)c;
@@ -167,15 +181,28 @@ static void iar(int P, int dj) {
     char prop[17] = "0123456789abcdef";
     long expect = (long)P * (g_size - 1), got = 0, approved = 0;
     int done = 0, inflight = 0;
+    const int diag = getenv("API_DIAG") != NULL;
+    double* rl = diag ? calloc((size_t)P + 1, sizeof(double)) : NULL;
+    double gap_max = 0, t_prev = 0, t_sub = 0, t_mine = 0;
+    long gaps_1ms = 0, nvcs0 = diag ? ctx_switches("nonvoluntary_ctxt_switches") : 0;
     MPI_Barrier(MPI_COMM_WORLD);
     double t0 = now_s();
+    t_prev = t0;
     while (got < expect || done < P) {
+        if (diag) {
+            double tn = now_s();
+            if (tn - t_prev > gap_max) gap_max = tn - t_prev;
+            if (tn - t_prev > 1e-3) gaps_1ms++;
+            t_prev = tn;
+        }
         if (!inflight && done < P) {
+            if (diag) t_sub = now_s();
             int ret = RLO_submit_proposal(eng, prop, 16, done * g_size + g_rank);
             inflight = 1;
             if (ret > -1) {
                 approved += RLO_get_vote_my_proposal(eng);
                 inflight = 0;
+                if (diag) rl[done] = now_s() - t_sub;
                 done++;
             }
         }
@@ -183,7 +210,9 @@ static void iar(int P, int dj) {
         if (inflight && RLO_check_proposal_state(eng, 0) == RLO_COMPLETED) {
             approved += RLO_get_vote_my_proposal(eng);
             inflight = 0;
+            if (diag) rl[done] = now_s() - t_sub;
             done++;
+            if (diag && done == P) t_mine = now_s() - t0;
         }
         RLO_user_msg* u = NULL;
         while (RLO_user_pickup_next(eng, &u)) {
@@ -193,6 +222,13 @@ static void iar(int P, int dj) {
     }
     double dt = now_s() - t0, dtmax = 0;
     long app = 0;
+    if (diag) {
+        qsort(rl, (size_t)P, sizeof(double), cmp_d);
+        fprintf(stderr, "diag rank %d: own %.3f s all %.3f s; round us p50 %.1f p99 %.1f max %.1f; loop gap max %.1f us, >1ms %ld; "
+                "nonvoluntary ctx %ld\n", g_rank, t_mine, dt, rl[P / 2] * 1e6, rl[(int)(P * 0.99)] * 1e6, rl[P - 1] * 1e6,
+                gap_max * 1e6, gaps_1ms, ctx_switches("nonvoluntary_ctxt_switches") - nvcs0);
+        free(rl);
+    }
     MPI_Reduce(&dt, &dtmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
     MPI_Reduce(&approved, &app, 1, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
     if (g_rank == 0)
