@@ -1044,8 +1044,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // idle rank is seen one poll round trip later instead of after a whole idle iteration.
             // Bounded, so the idle clock and the deadline still tick.
             for (uint32_t sp = 0;; sp++) {
-                // host mode: the host-written counters live in uncached VRAM (a local poll)
-                if (host && lane < 2) hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
+                // host mode: the host-written counters (pinned host memory: a PCIe read, ~1 us more than
+                // the ring polls) on every 4th re-poll only, so an idle rank still sees a ring message
+                // one VRAM poll after it lands; a command waits at most ~4 re-polls
+                if (host && lane < 2 && (sp & 3u) == 0u) hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);

@@ -19,6 +19,7 @@
 // ring and the pickup head into the VRAM counter the kernel polls, and runs bulk copies between
 // `stage` and the heap on the client's behalf.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 #include "rlo_device.hpp"
@@ -26,7 +27,7 @@
 namespace rlo {
 
 constexpr uint32_t kShmMagic = 0x534f4c52u;  // "RLOS"
-constexpr uint32_t kShmVersion = 1;
+constexpr uint32_t kShmVersion = 2;
 
 enum ShmOp : uint32_t { SHM_OP_NONE = 0, SHM_OP_ACQUIRE = 1, SHM_OP_PUT = 2, SHM_OP_GET = 3 };
 
@@ -41,20 +42,25 @@ struct ShmHdr {
     uint32_t leader_failed, pad;     // the leader gave up (its kernel could not start / ended early)
 };
 
-// one per local rank; the two sides' words on separate 128-byte lines
+// one per local rank; the two sides' words on separate 128-byte lines.  The kernel polls mtail and
+// mpk here directly (its hctl_dev words kHctlInjTail / kHctlPkHead: the box IS that array, one
+// kHctlWords stride per rank), and reads the commands from `cmd` -- no CPU store into VRAM on the
+// command path (see rlo_world.cpp, cmd_host)
 struct ClientBox {
     alignas(128) uint64_t mtail;  // client: commands written into its `cmd` ring
-    alignas(128) uint64_t mpk;    // client: pickup events consumed
     alignas(128) uint64_t req;    // client: bulk request sequence (request fields below valid)
     uint32_t op, arg;             // ShmOp; ACQUIRE -, PUT q, GET origin << 8 | heap slot
     uint64_t off, len;            // byte range of the message this request moves via `stage`
     alignas(128) uint64_t ack;    // leader: last request completed
     int64_t rc;                   // RLO_OK / RLO_E_AGAIN (ACQUIRE: slot still busy) / error
     uint64_t q;                   // ACQUIRE: the bulk sequence taken
-    uint64_t fwd;                 // leader: commands forwarded into the VRAM ring (diagnostics)
-    int64_t fwd_ns;               // leader: CLOCK_MONOTONIC ns of that forward (diagnostics)
+    uint64_t fwd;                 // leader (RLO_BAR_CMDS): commands forwarded into the VRAM ring
+    int64_t fwd_ns;               // leader (RLO_BAR_CMDS): CLOCK_MONOTONIC ns of that forward
+    alignas(128) uint64_t mpk;    // client: pickup events consumed
 };
-static_assert(sizeof(ClientBox) == 512, "ClientBox layout");
+static_assert(sizeof(ClientBox) == kHctlWords * 8, "ClientBox stride = the kernel's host counter stride");
+static_assert(offsetof(ClientBox, mtail) == kHctlInjTail * 8 && offsetof(ClientBox, mpk) == kHctlPkHead * 8,
+              "ClientBox words where the kernel polls its command tail / pickup head");
 
 struct ShmLayout {
     uint64_t hctl, ev, evp, cli, cmd, stage, total;

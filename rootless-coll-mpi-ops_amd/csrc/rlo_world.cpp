@@ -321,6 +321,7 @@ struct rlo_world {
     uint64_t* h_ctl = nullptr;      // [nl][kHctlWords]           pinned host: device-written counters
     uint64_t* d_ctl = nullptr;      // [nl][kHctlWords]           uncached VRAM: host-written counters
     volatile uint32_t* hdp = nullptr;  // the GPU's HDP_MEM_COHERENCY_FLUSH_CNTL register (see hdp_flush)
+    bool cmd_host = false;          // the command ring + host counters in pinned host memory (default)
     rlo::LogRec* h_ev = nullptr;    // [nl][pk_cap]
     uint8_t* h_evp = nullptr;       // [nl][pk_cap][max_payload]
     uint32_t cmd_cap = 0, pk_cap = 0;
@@ -1049,8 +1050,13 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
 }
 
 static void host_free(rlo_world* w) {
-    if (w->h_cmd) (void)hipFree(w->h_cmd);
-    if (w->d_ctl) (void)hipFree(w->d_ctl);
+    if (w->cmd_host) {
+        if (w->h_cmd) (void)hipHostFree(w->h_cmd);
+        if (w->d_ctl) (void)hipHostFree(w->d_ctl);
+    } else {
+        if (w->h_cmd) (void)hipFree(w->h_cmd);
+        if (w->d_ctl) (void)hipFree(w->d_ctl);
+    }
     if (w->shm) {  // h_ctl / h_ev / h_evp point into the segment
         (void)hipHostUnregister(w->shm);
         munmap(w->shm, (size_t)w->shm_bytes);
@@ -1097,7 +1103,8 @@ static int host_alloc(void** p, size_t bytes) {
 // rlo_host_share's segment (rlo_shm.hpp), built by rlo_program_host once the ring sizes are known:
 // created, mapped, registered with HIP (fine-grained: the kernel's counter / event stores reach the
 // clients' polls directly) and described in its header for the clients
-static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec** dev_ev, const uint8_t** dev_evp) {
+static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec** dev_ev, const uint8_t** dev_evp,
+                     uint8_t** dev_cmd, uint64_t** dev_cli) {
     const uint32_t nl = (uint32_t)w->nl;
     const uint64_t stage = w->L.bulk_max ? w->share_stage : 0;
     const rlo::ShmLayout L = rlo::shm_layout(nl, w->cmd_cap, w->pk_cap, w->L.stride, w->max_payload, stage);
@@ -1132,6 +1139,8 @@ static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec*
     *dev_hctl = (const uint64_t*)(db + L.hctl);
     *dev_ev = (const rlo::LogRec*)(db + L.ev);
     *dev_evp = db + L.evp;
+    *dev_cmd = db + L.cmd;
+    *dev_cli = (uint64_t*)(db + L.cli);
     rlo::ShmHdr* h = (rlo::ShmHdr*)b;
     h->version = rlo::kShmVersion;
     h->nl = nl;
@@ -1161,12 +1170,22 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     w->cmd_cap = cc;
     w->pk_cap = pc;
     const size_t nl = (size_t)w->nl;
-    if (bar_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) || bar_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8)) {
+    // Where the host's commands and counters live.  Default: pinned host memory, polled by the
+    // kernel over PCIe (wave 0's poll of them runs beside its ring polls).  RLO_BAR_CMDS=1: uncached
+    // VRAM written by the CPU through the BAR -- a local poll, but in some runs such a store stayed
+    // invisible to the polling kernel for 0.5-2 ms, every round (profiles/r2_dropin_split_legs.txt:
+    // forwarded -> consumed; the kernel itself drained each command within 20 us of seeing it)
+    w->cmd_host = std::getenv("RLO_BAR_CMDS") == nullptr;
+    const int arc = w->cmd_host ? (host_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) ||
+                                   host_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8))
+                                : (bar_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) ||
+                                   bar_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8));
+    if (arc) {
         host_free(w);
         return RLO_E_HIP;
     }
     w->hdp = nullptr;
-    if (!std::getenv("RLO_NO_HDP_FLUSH")) {  // A/B switch; the attribute returns the register's mapped address
+    if (!w->cmd_host && !std::getenv("RLO_NO_HDP_FLUSH")) {  // A/B switch; the attribute returns the register's mapped address
         uint32_t* reg = nullptr;
         if (hipDeviceGetAttribute(reinterpret_cast<int*>(&reg), hipDeviceAttributeHdpMemFlushCntl, w->device) == hipSuccess)
             w->hdp = reg;
@@ -1174,8 +1193,10 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     const uint64_t* dev_hctl = nullptr;
     const rlo::LogRec* dev_ev = nullptr;
     const uint8_t* dev_evp = nullptr;
+    uint8_t* dev_cmd = nullptr;
+    uint64_t* dev_cli = nullptr;
     if (!w->shm_name.empty()) {  // rlo_host_share: the host-side rings in the shared segment
-        int rc = shm_build(w, &dev_hctl, &dev_ev, &dev_evp);
+        int rc = shm_build(w, &dev_hctl, &dev_ev, &dev_evp, &dev_cmd, &dev_cli);
         if (rc) { host_free(w); return rc; }
     } else if (host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
                host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) ||
@@ -1193,10 +1214,13 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     P.log_cap = pc;
     P.log_payload = dev_evp ? const_cast<uint8_t*>(dev_evp) : w->h_evp;
     P.log_stride = w->max_payload;
-    P.hin = w->h_cmd;
+    // shared service, commands in host memory: the kernel reads the clients' own rings and counters in
+    // the segment (the proxy then only serves bulk requests)
+    const bool direct = w->cmd_host && dev_cmd;
+    P.hin = direct ? dev_cmd : w->h_cmd;
     P.hin_cap = cc;
     P.hctl = dev_hctl ? const_cast<uint64_t*>(dev_hctl) : w->h_ctl;
-    P.hctl_dev = w->d_ctl;
+    P.hctl_dev = direct ? dev_cli : w->d_ctl;
     const uint64_t idle = cfg ? cfg->idle_timeout_s : 0;
     P.timeout_ticks = idle ? 100000000ull * idle : ~0ull >> 2;
     P.deadline_ticks = ~0ull >> 2;  // serves until RLO_CMD_QUIT
@@ -1566,9 +1590,9 @@ int rlo_host_proxy(rlo_world_t* w) {
         // commands: the client's shared ring -> the VRAM ring the kernel polls locally.  The client
         // admitted each one only with room in its ring (mtail - device head < cmd_cap), which is
         // room in the VRAM ring too (it holds [device head, copied) of the same sequence)
-        const uint64_t mt = __atomic_load_n(&box->mtail, __ATOMIC_ACQUIRE);
+        const uint64_t mt = w->cmd_host ? 0 : __atomic_load_n(&box->mtail, __ATOMIC_ACQUIRE);
         uint64_t c = w->cmd_tail[lr];
-        if (mt != c) {
+        if (!w->cmd_host && mt != c) {
             const uint8_t* src = w->shm + w->SL.cmd + (size_t)lr * cc * stride;
             uint8_t* dst = w->h_cmd + (size_t)lr * cc * stride;
             for (; c != mt; c++) {
@@ -1588,8 +1612,8 @@ int rlo_host_proxy(rlo_world_t* w) {
             bar = true;
             acted++;
         }
-        const uint64_t pk = __atomic_load_n(&box->mpk, __ATOMIC_ACQUIRE);
-        if (pk != w->pk_head[lr]) {  // pickup events the client consumed: room for the kernel
+        const uint64_t pk = w->cmd_host ? 0 : __atomic_load_n(&box->mpk, __ATOMIC_ACQUIRE);
+        if (!w->cmd_host && pk != w->pk_head[lr]) {  // pickup events the client consumed: room for the kernel
             w->pk_head[lr] = pk;
             __atomic_store_n(&dctl[rlo::kHctlPkHead], pk, __ATOMIC_RELEASE);
             __atomic_thread_fence(__ATOMIC_SEQ_CST);

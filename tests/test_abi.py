@@ -174,7 +174,7 @@ def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
     os.ftruncate(fd, total)
     m = mmap.mmap(fd, total)
     os.close(fd)
-    hdr = struct.pack("<10I9Q2I", 0, 1, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
+    hdr = struct.pack("<10I9Q2I", 0, 2, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
                       off["cli"], off["cmd"], off["stage"], total, 0, 0)
     m[:len(hdr)] = hdr
     m[0:4] = struct.pack("<I", 0x534F4C52)  # magic last
@@ -234,7 +234,8 @@ def test_shared_service_client_protocol_without_gpu():
             assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 1
             assert (got.origin, buf.raw[:4]) == (i, b"ev%02d" % i)
         assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0
-        assert struct.unpack_from("<Q", m, box + 128)[0] == 2  # mpk: the proxy hands it to the kernel
+        # mpk: the kernel polls it here, at its pickup-head word (kHctlPkHead = 48)
+        assert struct.unpack_from("<Q", m, box + 48 * 8)[0] == 2
         assert lib.rlo_client_detach(c) == 0
     finally:
         m.close()
