@@ -127,7 +127,7 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
     legs = [("storm", ["storm", "20000", "64"]), ("lat", ["lat", "500", "64"]), ("iar", ["iar", "2000"])]
     # iardj: the same consensus loop with the approve-all judge registered on the device
     # (RLO_progress_engine_new_dj, an extension; the reference judges with its callback only)
-    legs_ours = legs + [("iardj", ["iardj", "2000"])]
+    legs_ours = legs + [("iardj", ["iardj", "2000"]), ("iarpool", ["iarpool", "8000"])]
     for nr in ranks:
         rec = {"ranks": nr, "ours": {}, "reference_host_mpi": {}, "cores": nr}
         for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
@@ -137,8 +137,10 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
             for leg, args in (legs_ours if name == "ours" else legs):
                 note("api n=%d %s %s" % (nr, name, leg))
                 try:
+                    # iarpool: the proposal pool extension, 16 own proposals in flight per rank
+                    env = dict(os.environ, RLO_PROPOSAL_POOL="16") if leg == "iarpool" else None
                     r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(nr), exe] + args,
-                                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20)
+                                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20, env=env)
                     lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
                     rec[name][leg] = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
                 except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
@@ -149,6 +151,7 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
                 "bcast_per_s": round(o["storm"]["bcast_per_s"] / f["storm"]["bcast_per_s"], 2),
                 "decisions_per_s": round(o["iar"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
                 "decisions_per_s_device_judge": round(o["iardj"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
+                "decisions_per_s_pool16": round(o["iarpool"]["decisions_per_s"] / f["iar"]["decisions_per_s"], 2),
                 "p50_latency": round(o["lat"]["p50_us"] / f["lat"]["p50_us"], 2)}
         except Exception:  # noqa: BLE001
             pass
@@ -361,6 +364,19 @@ def small_n_legs(rlo, local, stream, sizes=(4, 8), rounds=2000, p=512):
             rec["decisions_per_s_kernel"] = round(n * p / (ms * 1e-3), 1)
             rec["decision_us"] = round(ms * 1e3 / p, 2)  # one proposal round trip per rank, back to back
             rec["verified"] = bool(rc == 0 and (st["error"] == 0).all() and int(st["own_decided"].sum()) == n * p)
+        # the proposal pool (rootless_ops.c:30, unfinished in the reference): 16 own proposals in flight
+        # per rank instead of one (:241)
+        with rlo.World(n, max_payload=32, device=local, proposal_pool=16) as w:
+            pp = 4 * p
+            w.program_iar([(r, it * n + r, b"0123456789abcdef") for it in range(pp) for r in range(n)], pool=16)
+            _step(w, stream, None)
+            t = time.perf_counter()
+            rc, ms = _step(w, stream, None)
+            dt = time.perf_counter() - t
+            st = w.stats()
+            rec["pool16_decisions_per_s"] = round(n * pp / dt, 1)
+            rec["pool16_decisions_per_s_kernel"] = round(n * pp / (ms * 1e-3), 1)
+            rec["verified"] &= bool(rc == 0 and (st["error"] == 0).all() and int(st["own_decided"].sum()) == n * pp)
         out["n%d" % n] = rec
     return out
 
@@ -577,6 +593,20 @@ def main():
         ok &= rc == 0 and int(sum_over_ranks(float(ist["own_decided"].sum()))) == R * p * copies
         ok &= bool((ist["error"] == 0).all())
     w.close()
+    if not args.no_extras and world == 1:
+        # the proposal pool at the C4 shape: every rank keeps 16 own proposals in flight (its own world:
+        # the pending table is N x 16 entries of LDS, sized at creation)
+        p = 4 * args.iar_p
+        with rlo.World(R, max_payload=32, device=local, proposal_pool=16) as wp:
+            wp.program_iar([(r, it * R + r, b"0123456789abcdef") for it in range(p) for r in range(R)], pool=16)
+            _step(wp, stream, None)
+            t1 = time.perf_counter()
+            rc, ims = _step(wp, stream, None)
+            idt = time.perf_counter() - t1
+            ist = wp.stats()
+        extras["pool16_decisions_per_s"] = round(R * p / idt, 1)
+        extras["pool16_decisions_kernel_ms"] = round(ims, 3)
+        ok &= rc == 0 and int(ist["own_decided"].sum()) == R * p and bool((ist["error"] == 0).all())
     if not args.no_extras and world == 1:
         # SURVEY 8(d) C2's payload sizes: the same storm at 256 B .. 4 KiB (roofline per size)
         if rank == 0:

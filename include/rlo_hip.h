@@ -70,6 +70,11 @@ typedef struct {
     uint64_t bulk_max;
     uint32_t bulk_slots;  /* heap slots per origin (power of two <= 8, N * slots <= 256); 0 = 2 */
     uint32_t movers;      /* mover workgroups of the part (>= 2, half scatter, half gather); 0 = auto */
+    /* proposal pool (PROPOSAL_POOL_SIZE, rootless_ops.c:30): pending-proposal entries per origin
+     * in every rank's table (power of two <= 16; LDS N x pool x 16 B per rank); 0 = 2.  An iar
+     * program keeps up to rlo_iar_cfg_t.pool <= this many own proposals in flight per rank */
+    uint32_t proposal_pool;
+    uint32_t pad;
 } rlo_world_cfg_t;
 
 typedef struct {
@@ -83,6 +88,7 @@ typedef struct {
                                                     iteration) or 4 (256), chosen at creation     */
     uint32_t bulk_slots, movers;                 /* bulk: heap slots per origin, mover workgroups   */
     uint64_t bulk_max, heap_bytes;               /* bulk: largest message, this part's heap bytes   */
+    uint32_t proposal_pool, pad2;                /* pending entries per origin (own proposals in flight) */
 } rlo_world_info_t;
 
 /* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522
@@ -105,6 +111,7 @@ typedef struct {
     uint32_t flags;            /* RLO_PART_*                                                */
     uint64_t bulk_max;         /* as rlo_world_cfg_t (the same on every part)               */
     uint32_t bulk_slots, movers;
+    uint32_t proposal_pool, pad; /* as rlo_world_cfg_t (the same on every part)             */
 } rlo_part_cfg_t;
 int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out);
 int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap); /* returns RLO_PART_BLOB_BYTES */
@@ -152,10 +159,14 @@ typedef struct {
     const uint8_t* judge_mask; /* [N] for RLO_JUDGE_MASK                                   */
     const char* judge_isp;     /* N NUL-terminated strings, concatenated (RLO_JUDGE_ISP)    */
     uint32_t flags, log_cap;
+    uint32_t pool;             /* own proposals in flight per rank (<= the world's proposal_pool);
+                                  0 = 1: one own proposal per engine (rootless_ops.c:241)     */
+    uint32_t pad;
 } rlo_iar_cfg_t;
 /* proposals in per-origin submission order: origin[i] submits pid[i] with
- * data[data_off[i] .. +data_len[i]); a rank submits its next proposal when its
- * previous decision has been broadcast (one own proposal per engine, rootless_ops.c:241). */
+ * data[data_off[i] .. +data_len[i]); a rank keeps up to cfg->pool of its proposals in flight
+ * (the proposal pool, rootless_ops.c:30, :1251-1366) and submits the next one as soon as a pool
+ * slot's decision has been broadcast; pool 1 = the reference's one own proposal (:241). */
 int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, const int32_t* origin, const int32_t* pid,
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len);
 
@@ -183,6 +194,10 @@ typedef struct {
     uint32_t idle_timeout_s; /* kernel stops (RLO_DERR_TIMEOUT) after this long without any
                                 progress; 0 = never                                          */
     uint32_t flags;
+    uint32_t pool;           /* own proposals a rank may keep in flight (<= the world's proposal_pool):
+                                the proposal pool (rootless_ops.c:30); 0 = 1 (my_own_proposal, :241).
+                                A proposal command beyond it waits in the command ring              */
+    uint32_t pad;
 } rlo_host_cfg_t;
 int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg);
 
@@ -190,7 +205,8 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg);
 #define RLO_CMD_BCAST 0u      /* payload = user bytes; id = caller's sequence number           */
 #define RLO_CMD_PROPOSAL 2u   /* payload = serialized PBuf (pid, vote, data_len, data) :1369   */
 #define RLO_CMD_JUDGE 16u     /* verdict for an RLO_EV_JUDGE event: origin, pid, pseq, vote     */
-#define RLO_CMD_OWN_JUDGE 17u /* verdict of the originator's final judge(NULL) (:773): vote      */
+#define RLO_CMD_OWN_JUDGE 17u /* verdict of the originator's final judge(NULL) (:773): id = pid,
+                                 pseq = the RLO_EV_OWN_JUDGE event's aux (pool slot), vote       */
 #define RLO_CMD_QUIT 18u      /* stop this rank's progress (after everything before it)          */
 #define RLO_CMD_BULK 10u      /* bulk origination: payload = {u32 len, u32 q}; use rlo_host_bulk_send */
 #define RLO_CMD_BULK_RELEASE 19u /* a bulk delivery was copied out: origin, pseq = heap slot        */
@@ -214,7 +230,8 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* cmd, const void* pa
 #define RLO_EV_RESULT 4u    /* my own proposal decided: id = pid, vote = decision                */
 #define RLO_EV_JUDGE 6u     /* call judge(data): origin, from, id = pid, aux = pseq,
                                payload = the proposal's PBuf (len bytes)                        */
-#define RLO_EV_OWN_JUDGE 7u /* call judge(NULL) for my proposal id (all votes were 1)          */
+#define RLO_EV_OWN_JUDGE 7u /* call judge(NULL) for my proposal id (all votes were 1); aux = its
+                               proposal-pool slot (echo it in RLO_CMD_OWN_JUDGE.pseq)          */
 #define RLO_EV_JUDGED 8u    /* device judge (rlo_host_device_judge): origin, from, id = pid, vote =
                                verdict, aux = pseq, payload = PBuf -- informational, no reply        */
 /* next event of local rank `rank`: 1 = got one (payload copied, up to cap bytes), 0 = none */

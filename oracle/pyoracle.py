@@ -77,6 +77,11 @@ def lib():
         L.orc_judge_hash.restype = ctypes.c_uint32
         L.orc_iar.argtypes = [ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_char_p, i32p, i32p, ctypes.POINTER(JudgeCfg),
                               i32p, ctypes.c_int]
+        L.orc_iar_pool.argtypes = [ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_char_p, i32p, i32p,
+                                   ctypes.POINTER(JudgeCfg), ctypes.c_int, i32p, ctypes.c_int]
+        L.orc_iar_pool.restype = ctypes.c_int
+        L.orc_iar_rounds_pool.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, i32p, ctypes.c_int]
+        L.orc_iar_rounds_pool.restype = ctypes.c_int
         L.orc_iar_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(JudgeCfg), i64p, i64p, i64p]
         L.orc_iar_bench.restype = ctypes.c_int64
         _lib = L
@@ -185,27 +190,34 @@ def judge_cfg(kind=ORC_JUDGE_APPROVE, decline=None, isp=None, seed=0, ppm=0):
     return cfg, keep
 
 
-def iar(n, proposals, cfg, cap=1 << 16):
-    """proposals: list of (origin, pid, data bytes).  Returns list of event tuples."""
+def iar(n, proposals, cfg, cap=1 << 16, pool=0):
+    """proposals: list of (origin, pid, data bytes).  Returns list of event tuples.  pool 0: all
+    submitted up front (orc_iar, the reference's one my_own_proposal); pool >= 1: the proposal pool
+    (orc_iar_pool, every origin keeps up to `pool` in flight, list order)."""
     origin = np.array([p[0] for p in proposals], dtype=np.int32)
     pid = np.array([p[1] for p in proposals], dtype=np.int32)
     blob = b"".join(p[2] for p in proposals)
     off = np.cumsum([0] + [len(p[2]) for p in proposals[:-1]]).astype(np.int32)
     dl = np.array([len(p[2]) for p in proposals], dtype=np.int32)
     ev = np.zeros(6 * cap, dtype=np.int32)
-    k = lib().orc_iar(n, len(proposals), _p(origin, ctypes.c_int32), _p(pid, ctypes.c_int32), blob, _p(off, ctypes.c_int32),
-                      _p(dl, ctypes.c_int32), ctypes.byref(cfg), _p(ev, ctypes.c_int32), cap)
+    if pool:
+        k = lib().orc_iar_pool(n, len(proposals), _p(origin, ctypes.c_int32), _p(pid, ctypes.c_int32), blob,
+                               _p(off, ctypes.c_int32), _p(dl, ctypes.c_int32), ctypes.byref(cfg), pool,
+                               _p(ev, ctypes.c_int32), cap)
+    else:
+        k = lib().orc_iar(n, len(proposals), _p(origin, ctypes.c_int32), _p(pid, ctypes.c_int32), blob,
+                          _p(off, ctypes.c_int32), _p(dl, ctypes.c_int32), ctypes.byref(cfg), _p(ev, ctypes.c_int32), cap)
     if k < 0:
         raise RuntimeError("oracle iar failed")
     return [tuple(int(x) for x in ev[6 * i:6 * i + 6]) for i in range(k)]
 
 
-def iar_rounds(n, p, cfg, cap=None):
-    """orc_iar_rounds: iar_bench's workload (one outstanding proposal per rank, pid = it * n + r) with
-    every event: list of (ev, rank, pid, a, b, c)"""
+def iar_rounds(n, p, cfg, cap=None, pool=1):
+    """orc_iar_rounds_pool: iar_bench's workload (`pool` outstanding proposals per rank, pid = it * n + r)
+    with every event: list of (ev, rank, pid, a, b, c)"""
     cap = cap or 4 * n * n * p + 1024
     ev = np.zeros(6 * cap, dtype=np.int32)
-    k = lib().orc_iar_rounds(n, p, ctypes.byref(cfg), _p(ev, ctypes.c_int32), cap)
+    k = lib().orc_iar_rounds_pool(n, p, pool, ctypes.byref(cfg), _p(ev, ctypes.c_int32), cap)
     if k < 0:
         raise RuntimeError("oracle iar_rounds failed")
     return [tuple(int(x) for x in r) for r in ev[:6 * k].reshape(k, 6)]

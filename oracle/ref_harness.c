@@ -281,6 +281,48 @@ static void mode_iar(int origin, unsigned mask) {
     RLO_progress_engine_cleanup(eng);
 }
 
+#ifdef RLO_HAVE_PROPOSAL_POOL
+/* the proposal pool (drop-in extension; the reference keeps one own proposal, rootless_ops.c:241):
+ * every rank submits `per` proposals (pid 1000 + i * N + rank, data "p<i>-r<rank>") keeping up to
+ * RLO_proposal_pool_depth in flight; judge = the decline mask (judge_mask_cb logs every call) */
+static void mode_pool(int per, unsigned mask) {
+    MaskCtx ctx = {mask, g_rank};
+    RLO_engine_t* eng = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &judge_mask_cb, &ctx, &action_log_cb);
+    const int depth = RLO_proposal_pool_depth(eng);
+    int fl[16], nfl = 0, sub = 0, done = 0;
+    long got = 0, expect = (long)per * (g_size - 1);
+    MPI_Barrier(MPI_COMM_WORLD);
+    while (done < per || got < expect) {
+        while (nfl < depth && sub < per) {
+            char prop[64];
+            snprintf(prop, sizeof prop, "p%d-r%d", sub, g_rank);
+            const int pid = 1000 + sub * g_size + g_rank;
+            RLO_submit_proposal(eng, prop, strlen(prop), pid);
+            fl[nfl++] = pid;
+            sub++;
+        }
+        RLO_make_progress_all();
+        for (int i = 0; i < nfl;) {
+            if (RLO_check_proposal_state(eng, fl[i]) != RLO_COMPLETED) { i++; continue; }
+            emit("{\"ev\":\"result\",\"rank\":%d,\"pid\":%d,\"vote\":%d}", g_rank, fl[i], RLO_get_vote_proposal(eng, fl[i]));
+            done++;
+            fl[i] = fl[--nfl];
+        }
+        RLO_user_msg* u = NULL;
+        while (RLO_user_pickup_next(eng, &u)) {
+            if (u->type == RLO_IAR_DECISION) {
+                emit("{\"ev\":\"decision\",\"rank\":%d,\"pid\":%d,\"vote\":%d,\"origin\":%d}", g_rank, u->pid, u->vote,
+                     *(int*)u->buf);
+                got++;
+            }
+            RLO_user_msg_recycle(eng, u);
+        }
+    }
+    emit("{\"ev\":\"depth\",\"rank\":%d,\"depth\":%d}", g_rank, depth);
+    RLO_progress_engine_cleanup(eng);
+}
+#endif
+
 /* ---------------------------------------------------------------- multi */
 static int judge_isp_log_cb(const void* arg, void* ctx) {
     int r = is_proposal_approved_cb(arg, ctx);
@@ -562,6 +604,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(mode, "multi")) mode_multi(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
 #ifdef RLO_HAVE_DEVICE_JUDGE
     else if (!strcmp(mode, "multi_dj")) mode_multi_dj(atoi(argv[3]), atoi(argv[4]), atoi(argv[5]));
+#endif
+#ifdef RLO_HAVE_PROPOSAL_POOL
+    else if (!strcmp(mode, "pool")) mode_pool(atoi(argv[3]), (unsigned)strtoul(argv[4], 0, 0));
 #endif
     else if (!strcmp(mode, "tests")) mode_tests();
     else if (!strcmp(mode, "tests_safe")) mode_tests_safe();

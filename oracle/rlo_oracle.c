@@ -609,7 +609,9 @@ typedef struct {
     int n;
     topo_t* t;
     ofifo* inbox;
-    own_t* own;
+    own_t* own;  /* [n][pool]: the proposal pool (PROPOSAL_POOL_SIZE, rootless_ops.c:30); pool 1 =
+                    my_own_proposal (:241) */
+    int pool;
     pending_t** pend; /* per rank dynamic array */
     int* npend;
     int* cappend;
@@ -643,9 +645,18 @@ static void bcast_from(iar_sim* s, int r, omsg* m) {
     for (int i = 0; i < kk; i++) post(s->inbox, kids[i], r, m);
 }
 
-/* RLO_submit_proposal, rootless_ops.c:876-906 */
+/* a free pool slot of rank r (proposalPool_proposal_add :1253-1279 "first available"), or NULL */
+static own_t* own_free(iar_sim* s, int r) {
+    for (int k = 0; k < s->pool; k++)
+        if (s->own[r * s->pool + k].state == 0) return &s->own[r * s->pool + k];
+    return NULL;
+}
+
+/* RLO_submit_proposal, rootless_ops.c:876-906 (pool 1: it overwrites my_own_proposal, as the
+ * reference does; larger pools take a free slot, the caller checks there is one) */
 static void submit(iar_sim* s, int r, int32_t pid, const char* data, uint32_t dl) {
-    own_t* o = &s->own[r];
+    own_t* o = own_free(s, r);
+    if (!o) o = &s->own[r * s->pool];
     o->pid = pid;
     o->vote = 1;
     o->needed = s->t[r].sll;
@@ -663,15 +674,23 @@ static void vote_to(iar_sim* s, int r, int parent, int32_t pid, int32_t vote) { 
 }
 
 /* _iar_decision_bcast :908-917: PBuf(pid, decision, 7, "IAR_DEC") in a 64-byte buffer */
-static void decision_bcast(iar_sim* s, int r, int32_t pid, int32_t d) {
+static void decision_bcast(iar_sim* s, int r, own_t* o, int32_t pid, int32_t d) {
     omsg m = {ORC_DECISION, r, -1, pid, d, 64, pbuf_make(pid, d, 7, "IAR_DEC", 64), 0};
     bcast_from(s, r, &m);
     free(m.data);
     s->decisions++;
     if (d) s->approved++;
     ev_put(s, ORC_EV_RESULT, r, pid, d, 0, 0);
-    s->own[r].state = 0;
-    s->own[r].vote = d;
+    o->state = 0;
+    o->vote = d;
+}
+
+/* the pool slot holding own proposal pid (any state: the reference keeps my_own_proposal.pid after
+ * the decision until RLO_proposal_reset), or NULL */
+static own_t* own_find(iar_sim* s, int r, int32_t pid) {
+    for (int k = 0; k < s->pool; k++)
+        if (s->own[r * s->pool + k].pid == pid) return &s->own[r * s->pool + k];
+    return NULL;
 }
 
 static pending_t* find_pending(iar_sim* s, int r, int32_t pid, int* idx) { /* _find_proposal_msg :1036-1053 */
@@ -694,7 +713,7 @@ static void handle(iar_sim* s, int r, omsg* in) {
             int32_t pid = in->id;
             uint64_t dl;
             memcpy(&dl, in->data + 8, 8);
-            if (pid == s->own[r].pid) { ev_put(s, ORC_EV_ERROR, r, pid, 1, in->origin, 0); break; } /* :690-692 */
+            if (own_find(s, r, pid)) { ev_put(s, ORC_EV_ERROR, r, pid, 1, in->origin, 0); break; } /* :690-692 */
             char* arg = calloc(1, dl + 1);
             memcpy(arg, in->data + 16, dl);
             int jr = judge_eval(&s->j, r, pid, arg);
@@ -717,8 +736,8 @@ static void handle(iar_sim* s, int r, omsg* in) {
             break;
         }
         case ORC_VOTE: { /* _iar_vote_handler :743-812 */
-            own_t* o = &s->own[r];
-            if (in->id == o->pid) {
+            own_t* o = own_find(s, r, in->id);  /* proposalPool_vote_merge :1286-1305 */
+            if (o) {
                 o->recvd++;
                 o->vote &= in->vote;
                 if (o->recvd == o->needed) {
@@ -728,7 +747,7 @@ static void handle(iar_sim* s, int r, omsg* in) {
                         ev_put(s, ORC_EV_JUDGE, r, o->pid, 1, jr, r);
                         o->vote = jr;
                     }
-                    decision_bcast(s, r, o->pid, o->vote);
+                    decision_bcast(s, r, o, o->pid, o->vote);
                 }
                 break;
             }
@@ -766,12 +785,13 @@ static void handle(iar_sim* s, int r, omsg* in) {
     }
 }
 
-static void sim_init(iar_sim* s, int n, const orc_judge_cfg* judge) {
+static void sim_init(iar_sim* s, int n, const orc_judge_cfg* judge, int pool) {
     memset(s, 0, sizeof *s);
     s->n = n;
+    s->pool = pool < 1 ? 1 : pool;
     s->t = malloc(n * sizeof(topo_t));
     s->inbox = calloc(n, sizeof(ofifo));
-    s->own = calloc(n, sizeof(own_t));
+    s->own = calloc((size_t)n * s->pool, sizeof(own_t));
     s->pend = calloc(n, sizeof(pending_t*));
     s->npend = calloc(n, sizeof(int));
     s->cappend = calloc(n, sizeof(int));
@@ -783,7 +803,7 @@ static void sim_init(iar_sim* s, int n, const orc_judge_cfg* judge) {
     }
     for (int r = 0; r < n; r++) {
         topo_init(n, r, &s->t[r]);
-        s->own[r].pid = -1; /* proposal_state_init :1238 */
+        for (int k = 0; k < s->pool; k++) s->own[r * s->pool + k].pid = -1; /* proposal_state_init :1238 */
     }
 }
 
@@ -813,7 +833,7 @@ int orc_iar(int n, int nprop, const int32_t* origin, const int32_t* pid, const c
             const int32_t* data_len, const orc_judge_cfg* judge, int32_t* events, int cap) {
     if (n < 2) return -1;
     iar_sim s;
-    sim_init(&s, n, judge);
+    sim_init(&s, n, judge, 1);
     s.ev = events;
     s.cap = cap;
     s.record = 1;
@@ -824,14 +844,52 @@ int orc_iar(int n, int nprop, const int32_t* origin, const int32_t* pid, const c
     return nev;
 }
 
-/* every rank keeps one outstanding proposal (pid = iter * n + rank, 16-byte body) for p iterations;
- * the next is submitted once RLO_get_vote_my_proposal saw the previous one decided (testcases.c
- * :401-486 drive loop, at scale).  events != NULL records them (orc_iar's format). */
-static int64_t iar_rounds(int n, int p, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls,
+/* the proposal pool (PROPOSAL_POOL_SIZE, rootless_ops.c:30, :159-165, :1251-1366 -- declared but
+ * never wired into the reference's handlers): every origin submits its proposals in list order,
+ * keeping up to `pool` of them in flight; a slot is free again once its decision went out.  Votes
+ * and collisions are matched by pid over the pool's slots; everything else is orc_iar's. */
+int orc_iar_pool(int n, int nprop, const int32_t* origin, const int32_t* pid, const char* data, const int32_t* data_off,
+                 const int32_t* data_len, const orc_judge_cfg* judge, int pool, int32_t* events, int cap) {
+    if (n < 2 || pool < 1) return -1;
+    iar_sim s;
+    sim_init(&s, n, judge, pool);
+    s.ev = events;
+    s.cap = cap;
+    s.record = 1;
+    int* next = calloc(n, sizeof(int));  /* per origin: index into the list of its next proposal */
+    int busy = 1;
+    while (busy) {
+        busy = 0;
+        for (int r = 0; r < n; r++) {
+            for (;;) {
+                while (next[r] < nprop && origin[next[r]] != r) next[r]++;
+                if (next[r] >= nprop || !own_free(&s, r)) break;
+                const int i = next[r]++;
+                submit(&s, r, pid[i], data + data_off[i], (uint32_t)data_len[i]);
+                busy = 1;
+            }
+        }
+        busy |= sim_step_all(&s);
+        for (int r = 0; r < n && !busy; r++) {
+            while (next[r] < nprop && origin[next[r]] != r) next[r]++;
+            busy |= next[r] < nprop;
+        }
+    }
+    int nev = s.overflow ? -1 : s.nev;
+    free(next);
+    sim_free(&s);
+    return nev;
+}
+
+/* every rank keeps `pool` outstanding proposals (pid = iter * n + rank, 16-byte body) for p
+ * iterations; the next is submitted once a slot's decision went out (pool 1: once
+ * RLO_get_vote_my_proposal saw the previous one decided, testcases.c :401-486 drive loop, at
+ * scale).  events != NULL records them (orc_iar's format). */
+static int64_t iar_rounds(int n, int p, int pool, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls,
                           int64_t* actions, int32_t* events, int cap, int* nev) {
     if (n < 2) return -1;
     iar_sim s;
-    sim_init(&s, n, judge);
+    sim_init(&s, n, judge, pool);
     if (events) {
         s.ev = events;
         s.cap = cap;
@@ -843,14 +901,17 @@ static int64_t iar_rounds(int n, int p, const orc_judge_cfg* judge, int64_t* app
     while (busy) {
         busy = 0;
         for (int r = 0; r < n; r++) {
-            if (s.own[r].state == 0 && iter[r] < p) {
+            while (own_free(&s, r) && iter[r] < p) {
                 submit(&s, r, iter[r] * n + r, body, 16);
                 iter[r]++;
                 busy = 1;
             }
         }
         busy |= sim_step_all(&s);
-        for (int r = 0; r < n && !busy; r++) busy |= (s.own[r].state != 0 || iter[r] < p);
+        for (int r = 0; r < n && !busy; r++) {
+            busy |= iter[r] < p;
+            for (int k = 0; k < s.pool; k++) busy |= s.own[r * s.pool + k].state != 0;
+        }
     }
     if (approved) *approved = s.approved;
     if (judge_calls) *judge_calls = s.judge_calls;
@@ -863,11 +924,15 @@ static int64_t iar_rounds(int n, int p, const orc_judge_cfg* judge, int64_t* app
 }
 
 int64_t orc_iar_bench(int n, int p, const orc_judge_cfg* judge, int64_t* approved, int64_t* judge_calls, int64_t* actions) {
-    return iar_rounds(n, p, judge, approved, judge_calls, actions, NULL, 0, NULL);
+    return iar_rounds(n, p, 1, judge, approved, judge_calls, actions, NULL, 0, NULL);
 }
 
 int orc_iar_rounds(int n, int p, const orc_judge_cfg* judge, int32_t* events, int cap) {
+    return orc_iar_rounds_pool(n, p, 1, judge, events, cap);
+}
+
+int orc_iar_rounds_pool(int n, int p, int pool, const orc_judge_cfg* judge, int32_t* events, int cap) {
     int nev = 0;
-    if (iar_rounds(n, p, judge, NULL, NULL, NULL, events, cap, &nev) < 0) return -1;
+    if (pool < 1 || iar_rounds(n, p, pool, judge, NULL, NULL, NULL, events, cap, &nev) < 0) return -1;
     return nev;
 }

@@ -99,6 +99,14 @@ int64_t orc_iar_bench(int n, int p, const orc_judge_cfg* judge, int64_t* approve
 /* the same workload with every event recorded (orc_iar's format); returns #events or -1 */
 int orc_iar_rounds(int n, int p, const orc_judge_cfg* judge, int32_t* events, int cap);
 
+/* the proposal pool (PROPOSAL_POOL_SIZE, rootless_ops.c:30, :1251-1366): every rank keeps up to
+ * `pool` own proposals in flight.  orc_iar_pool: each origin submits its proposals (list order)
+ * whenever a pool slot is free; orc_iar_rounds_pool: orc_iar_rounds with `pool` outstanding per
+ * rank.  Same event format; returns #events or -1.                                             */
+int orc_iar_pool(int n, int nprop, const int32_t* origin, const int32_t* pid, const char* data, const int32_t* data_off,
+                 const int32_t* data_len, const orc_judge_cfg* judge, int pool, int32_t* events, int cap);
+int orc_iar_rounds_pool(int n, int p, int pool, const orc_judge_cfg* judge, int32_t* events, int cap);
+
 #ifdef __cplusplus
 }
 #endif

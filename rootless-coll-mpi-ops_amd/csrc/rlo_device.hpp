@@ -30,6 +30,7 @@ constexpr int kMaxCand = 256;     // messages handled per rank per progress iter
 constexpr int kStagePasses = 4;  // 4 x 64 messages per progress iteration
 constexpr int kHistBins = 128;    // latency histogram: 4 sub-bins per octave of 10 ns ticks
 constexpr int kMaxParts = 64;     // parts (processes x GPUs) of one world
+constexpr int kPoolMax = 16;      // own proposals in flight per rank (PROPOSAL_POOL_SIZE, rootless_ops.c:30)
 constexpr int kCtrlHdrWords = 16; // per-part control words before the rank blocks: [0] error flag
 // latency program of a world split over parts: the round word and the per-round delivery counts are
 // one world-wide copy in part 0's control region (peer-mapped like the ring counters), after its rank
@@ -84,8 +85,9 @@ enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_
 // Slot header, 16 bytes:
 //   w0 = origin (16 b) | tag (8 b) << 16 | vote (8 b) << 24
 //   w1 = id   (bcast id / proposal pid)
-//   w2 = len (16 b, payload bytes) | mark 0xA5 (8 b) << 16 | pseq (8 b) << 24 (pseq: per-origin
-//        proposal sequence; the mark, set at origination, tells a written slot from zeroed ring memory)
+//   w2 = len (16 b, payload bytes) | mark 0xA5 (8 b) << 16 | pseq (8 b) << 24 (pseq: the origin's
+//        proposal-pool slot of a proposal / its decision, which names the receivers' pending entry
+//        (origin, pseq); the mark, set at origination, tells a written slot from zeroed ring memory)
 //   w3 = t0   (low 32 bits of s_memrealtime at origination, 100 MHz)
 // Vote slot, 16 bytes: w0 = origin | vote << 24, w1 = pid, w2 = pseq, w3 = voter
 
@@ -173,6 +175,11 @@ struct Params {
     const uint32_t* prop_data_len;
     const uint8_t* prop_data;
     const int64_t* expect_dec;    // [n_local] decisions each rank picks up
+    // proposal pool: pend_slots entries per origin in every rank's pending table (a power of two
+    // <= kPoolMax, fixed at world creation: the table is dynamic LDS [N x pend_slots] x 16 B); an
+    // originator keeps up to own_pool <= pend_slots own proposals in flight, in slots it takes
+    // round-robin, and reuses a slot only after that slot's decision went out
+    uint32_t pend_slots, own_pool;
     // outputs
     RankStats* stats;             // [n_local]
     LogRec* log;                  // [n_local * log_cap]
@@ -182,7 +189,7 @@ struct Params {
     uint64_t timeout_ticks;       // no progress for this long -> ERR_TIMEOUT (100 MHz ticks)
     uint64_t deadline_ticks;      // hard cap on one launch (every spin is bounded)
     uint32_t* error_flag;         // this part's error word (polled every iteration)
-    // dynamic LDS carve-out: [pend: 2N x 16 B][olist: nout_max x 256 x 2 B]
+    // dynamic LDS carve-out: [pend: N x pend_slots x 16 B][olist: nout_max x 256 x 2 B]
     //                        [stage: 256 x nsmall x 16 B][stage2: stage2_bytes]
     uint32_t nsmall;              // slot chunks staged per message on the small path (<= 8)
     uint32_t stage2_bytes;        // LDS staging for large messages (multiple of 1 KiB, >= 1 KiB)

@@ -130,10 +130,19 @@ struct Shared {
     // wave 0: last published counter per lane (in-ring heads, out-ring tails, vote-in heads, vote-out
     // tails) and the last poll per lane (in tails, vote-in tails, out heads, vote-out heads)
     uint64_t pubw[4][64], snap[4][64];
-    // own proposal (my_own_proposal, :241)
-    int32_t own_pid;
-    uint32_t own_word, own_needed, own_state, own_decision, own_pseq;
-    int64_t own_iter, own_n;
+    // own proposals: the proposal pool (PROPOSAL_POOL_SIZE 16, rootless_ops.c:30, :159-165,
+    // :1251-1366; my_own_proposal :241 when the pool depth is 1).  Slot k is named by the pseq byte
+    // of the proposal, its votes and its decision; state 0 free, 1 voting, 2 decided (decision to
+    // originate), 3 waiting for the host's final judge(NULL)
+    int32_t own_pid[kPoolMax];
+    uint32_t own_word[kPoolMax], own_state[kPoolMax], own_decision[kPoolMax];
+    uint32_t own_needed, own_rr;
+    unsigned long long own_iter;
+    int64_t own_n;
+    // local IAR originations of this iteration: candidates [R, R + loc_nd) decisions, then
+    // [R + loc_nd, R + loc_n) proposals (prop_idx + i), each with its pool slot
+    uint32_t loc_nd, loc_n;
+    uint8_t loc_slot[2 * kPoolMax];
     // origination progress
     uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
     uint64_t hd[8], hd_t0;  // MODE_HDIAG counters (host mode)
@@ -400,6 +409,15 @@ __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint
     st_sys16(dst, u32x4{r.kind, (uint32_t)r.origin, (uint32_t)r.from, r.id});
     st_sys16(dst + 1, u32x4{r.len, (uint32_t)r.vote, r.aux, r.payload_idx});
     return want_rec ? i : r.payload_idx;
+}
+
+// a received proposal carries one of my own in-flight pids (the reference checks its one
+// my_own_proposal, :690-692; here every slot of the pool)
+template <class SH>
+__device__ __forceinline__ bool own_has(const SH& S, const Params& P, int32_t pid) {
+    bool hit = false;
+    for (uint32_t k = 0; k < P.pend_slots; k++) hit |= S.own_state[k] != 0u && S.own_pid[k] == pid;
+    return hit;
 }
 
 // vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741)
@@ -915,13 +933,16 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     }
     const uint32_t nsmall = P.nsmall;  // chunks per staged message
     const uint32_t nmagic = nsmall > 1 ? 0xFFFFFFFFu / nsmall + 1u : 0u;
-    PendState* pend = reinterpret_cast<PendState*>(dyn_lds);                        // [2 * n]
-    uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + 32u * (uint32_t)P.n);  // [oi][256]
-    uint8_t* stage = dyn_lds + 32u * (uint32_t)P.n + P.nout_max * (2u * kMaxCand);  // [message][q] x 16 B
+    const uint32_t pend_bytes = 16u * (uint32_t)P.n * P.pend_slots;
+    PendState* pend = reinterpret_cast<PendState*>(dyn_lds);                   // [n][pend_slots]
+    uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + pend_bytes);       // [oi][256]
+    uint8_t* stage = dyn_lds + pend_bytes + P.nout_max * (2u * kMaxCand);      // [message][q] x 16 B
     uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
     const uint32_t s2_blocks = P.stage2_bytes / 1024u;
 #define STG(c, q) (stage + (((uint32_t)(c) * nsmall + (uint32_t)(q)) << 4))
 #define OL(oi, r) olist[(uint32_t)(oi) * (uint32_t)kMaxCand + (uint32_t)(r)]
+    // the pending entry of (origin, pool slot) (rlo_device.hpp Params.pend_slots)
+#define PEND(o, q) pend[(uint32_t)(o) * P.pend_slots + ((uint32_t)(q) & (P.pend_slots - 1u))]
 
     const int lr = blockIdx.x;
     const int me = P.rank_begin + lr;
@@ -953,7 +974,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&P.topo[lr]);
         uint32_t* dst = reinterpret_cast<uint32_t*>(&S.t);
         for (int i = tid; i < (int)(sizeof(RankTopo) / 4); i += kBlock) dst[i] = src[i];
-        for (int i = tid; i < 2 * P.n; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
+        for (int i = tid; i < P.n * (int)P.pend_slots; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
         if constexpr (BULK) {
             for (int i = tid; i < P.n * (int)P.bulk_slots; i += kBlock) bpend[i] = BulkPend{0u, 0u, 0u, -1, 0u, 0u, 0u, 0u};
         }
@@ -963,8 +984,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (tid < 8) { S.prof[tid] = 0; S.dbg[tid] = 0; S.hd[tid] = 0; }
         if (tid == 0) {
             S.prof_t = __builtin_amdgcn_s_memtime();
-            S.own_pid = -1;  // proposal_state_init, :1238
-            S.own_word = 0; S.own_needed = 0; S.own_state = 0; S.own_decision = 0; S.own_pseq = 0;
+            for (int k = 0; k < kPoolMax; k++) {  // proposalPools_reset, :1351-1362
+                S.own_pid[k] = -1;
+                S.own_word[k] = 0; S.own_state[k] = 0; S.own_decision[k] = 0;
+            }
+            S.own_needed = 0; S.own_rr = 0; S.loc_nd = 0; S.loc_n = 0;
             S.own_iter = 0;
             S.own_n = ((P.mode & MODE_IAR) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
             S.lat_pos = 0;
@@ -1124,7 +1148,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             PSX(1);
             // host mode: publish the command head / pickup tail of the previous iteration; the pickup
             // ring bounds this iteration's events: a ring message makes <= 2 (action + decision), plus
-            // <= 2 of the own proposal (final-judge request, result)
+            // <= 2 per own proposal in flight (final-judge request, result)
             bool hblock = false;
             uint32_t hlim = kMaxCand;
             if (host) {
@@ -1132,8 +1156,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if (lane == 1) pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
                 const uint64_t pk_head = rdl64(hpoll, 1);
                 const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - pk_head);
-                hblock = pk_free < 8u;
-                hlim = hblock ? 0u : (pk_free - 4u) / 2u;
+                const uint32_t own_ev = 2u * P.own_pool + 2u;
+                hblock = pk_free < own_ev + 4u;
+                hlim = hblock ? 0u : (pk_free - own_ev) / 2u;
                 if ((P.mode & MODE_HDIAG) && lane == 0) {
                     S.hd[3]++;
                     if (hblock) S.hd[2]++;
@@ -1231,7 +1256,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             vin_head_r += vtake;  // merged by wave 1 before the next publish
             // in-rings: fair per-ring quotas
             const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)kMaxCand) : 0u;
-            const uint32_t reserve = host ? kPass + 1u : ((P.mode & MODE_IAR) ? 2u : 0u);  // host: stage block + decision
+            const uint32_t reserve = host ? kPass + P.pend_slots : ((P.mode & MODE_IAR) ? P.pend_slots + 1u : 0u);  // host: stage block; the pool's originations
             const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
             // max-min fair (water-filling) quotas: a ring's share that a short ring leaves unused goes
@@ -1276,9 +1301,38 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // local originations
             uint32_t C = R, loc_kind = 0, nstorm = 0, storm_base = 0, lat_id = 0xffffffffu;
             int64_t prop_idx = -1;
+            bool hprop_ok = false;  // host mode: a pool slot is free for one host proposal this iteration
             if ((P.mode & MODE_IAR) && !hblock) {
-                if (S.own_state == 2) { loc_kind = K_DEC; C++; }
-                else if (S.own_state == 0 && S.own_iter < S.own_n) { loc_kind = K_PROP; prop_idx = P.prop_off[lr] + S.own_iter; C++; }
+                // the proposal pool: every decided slot originates its decision (:560-563, :908-917),
+                // then free slots (round-robin from own_rr) take the next proposals of my list, up to
+                // own_pool in flight (:876-906).  Lane k holds slot k
+                const uint32_t ps_ = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
+                const uint64_t dm = __ballot(ps_ == 2u);
+                const uint64_t busy = __ballot(ps_ != 0u);
+                uint32_t nd = 0, np = 0;
+                if (lane == 0) {
+                    for (uint64_t m = dm; m; m &= m - 1) S.loc_slot[nd++] = (uint8_t)__builtin_ctzll(m);
+                    const int64_t left = S.own_n - (int64_t)S.own_iter;
+                    const uint32_t room = P.own_pool > (uint32_t)__popcll(busy) ? P.own_pool - (uint32_t)__popcll(busy) : 0u;
+                    uint32_t want = left < (int64_t)room ? (uint32_t)(left > 0 ? left : 0) : room;
+                    uint32_t k = S.own_rr;
+                    for (uint32_t i = 0; i < P.pend_slots && np < want; i++, k = (k + 1u) & (P.pend_slots - 1u))
+                        if (!((busy >> k) & 1ull)) S.loc_slot[nd + np++] = (uint8_t)k;
+                    if (host) {  // the slot a host proposal would take (np == 0: host ranks have no list)
+                        for (uint32_t i = 0; i < P.pend_slots && ((busy >> k) & 1ull); i++) k = (k + 1u) & (P.pend_slots - 1u);
+                        S.loc_slot[2 * kPoolMax - 1] = (uint8_t)k;
+                    }
+                    S.own_rr = k;
+                }
+                hprop_ok = (uint32_t)__popcll(busy) < P.own_pool;
+                nd = rdl32(nd, 0);
+                np = rdl32(np, 0);
+                if (nd + np) {
+                    loc_kind = nd ? K_DEC : K_PROP;
+                    if (np) prop_idx = P.prop_off[lr] + (int64_t)S.own_iter;
+                    C += nd + np;
+                }
+                if (lane == 0) { S.loc_nd = nd; S.loc_n = nd + np; }
             }
             uint32_t hbase = C, nh = 0, gap_lo = C;
             if (host && !hblock) {
@@ -1321,11 +1375,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const int vo = (int)(int8_t)(hd.x >> 24);
                         if (htag == CMD_JUDGE) {  // verdict of judge(data) for a held proposal (:698)
                             const int og = (int)(hd.x & 0xffffu);
-                            PendState* ps = &pend[2 * (og < P.n ? og : 0) + ((hd.z >> 24) & 1u)];
+                            PendState* ps = &PEND(og < P.n ? og : 0, hd.z >> 24);
                             if (og < P.n && ps->valid == PS_JREQ && ps->pid == (int32_t)hd.y) ps->valid = vo ? PS_JYES : PS_JNO;
                             else set_error(S, P, ERR_HOST_CMD, hd.x);
                         } else if (htag == CMD_OWN_JUDGE) {  // final judge(NULL) of my proposal (:770-775)
-                            if (S.own_state == 3) { S.own_decision = vo ? 1u : 0u; S.own_state = 2; }
+                            const uint32_t k = (hd.z >> 24) & (P.pend_slots - 1u);
+                            if (S.own_state[k] == 3 && S.own_pid[k] == (int32_t)hd.y) { S.own_decision[k] = vo ? 1u : 0u; S.own_state[k] = 2; }
                             else set_error(S, P, ERR_HOST_CMD, hd.x);
                         } else if (htag == CMD_QUIT) {
                             S.quit = 1;
@@ -1347,7 +1402,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                                          (run >= 64 ? ~0ull : ((1ull << run) - 1ull));
                     if (pm) {
                         const uint32_t fp = (uint32_t)__builtin_ctzll(pm);
-                        run = (S.own_state == 0 && loc_kind != K_DEC) ? fp + 1u : fp;
+                        run = hprop_ok ? fp + 1u : fp;
                         if ((P.mode & MODE_HDIAG) && lane == 0 && run == fp) S.hd[1]++;
                     }
                     nh = run;
@@ -1444,7 +1499,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                     fneed = need_of(fkids, forg, sll, sl_r);
                     const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
-                    ok = __ballot(full) == 0;
+                    // a proposal whose pending entry still holds an earlier proposal of that pool slot
+                    // goes the full path (held there until that one's decision was applied)
+                    const bool held = ftag == TAG_PROPOSAL && PEND(forg, fpseq).valid != PS_NONE;
+                    ok = __ballot(full) == 0 && !held;
                 }
                 if (ok) {
                     uint32_t flog = ~0u;
@@ -1462,13 +1520,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     } else if (ftag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
                         if (lane == 0) {
                             atomicAdd(&S.proposals_recv, 1ull);
-                            if (S.own_state != 0 && (int32_t)fid == S.own_pid) {
+                            if (own_has(S, P, (int32_t)fid)) {
                                 set_error(S, P, ERR_PID_COLLISION, fid);  // :690-692
                             } else {
                                 const uint32_t k = (uint32_t)fg >> 1;
                                 atomicAdd(&S.judge_calls, 1ull);
                                 log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
-                                PendState* ps = &pend[2 * forg + (fpseq & 1u)];
+                                PendState* ps = &PEND(forg, fpseq);
                                 if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                                     ps->valid = PS_NONE;
                                     emit_vote(S, P, me, k, forg, (int32_t)fid, fpseq, 0);
@@ -1485,7 +1543,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             }
                         }
                     } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
-                        PendState* ps = &pend[2 * forg + (fpseq & 1u)];
+                        PendState* ps = &PEND(forg, fpseq);
                         if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
                             if (fvote != 0) {
                                 atomicAdd(&S.actions, 1ull);
@@ -1624,27 +1682,28 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (origin >= P.n) {
                         set_error(S, P, ERR_BAD_SLOT, v.x);
                     } else if (origin == me) {  // a vote for my own proposal (:756-783)
-                        if (S.own_state != 1 || pid != S.own_pid) {
+                        const uint32_t k = pseq & (P.pend_slots - 1u);  // the pool slot (proposalPool_vote_merge :1286)
+                        if (S.own_state[k] != 1 || pid != S.own_pid[k]) {
                             set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
                         } else {
-                            const uint32_t nw = atomicAdd(&S.own_word, inc) + inc;
+                            const uint32_t nw = atomicAdd(&S.own_word[k], inc) + inc;
                             if ((nw & 0xffffu) == S.own_needed) {
                                 const int d = (nw >> 16) == 0 ? 1 : 0;
                                 if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback
-                                    log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, 1);
-                                    S.own_state = 3;
+                                    log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
+                                    S.own_state[k] = 3;
                                 } else {
                                     if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
                                         atomicAdd(&S.judge_calls, 1ull);
                                         if (!host) log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
                                     }
-                                    S.own_decision = (uint32_t)d;
-                                    S.own_state = 2;
+                                    S.own_decision[k] = (uint32_t)d;
+                                    S.own_state[k] = 2;
                                 }
                             }
                         }
                     } else {  // _vote_merge (:1056-1070)
-                        PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                        PendState* ps = &PEND(origin, pseq);
                         if (ps->valid != PS_ACTIVE || ps->pid != pid) {
                             set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
                         } else {
@@ -1689,15 +1748,19 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     // PBuf [pid][vote][data_len u64][data] at slot + 16 (rootless_ops.c:1402-1410)
                     const uint32_t plen = w2 & 0xffffu;
                     if (hjudge) {  // the host judges: hold the proposal at the head of its ring until the verdict
-                        PendState* ps = &pend[2 * origin + ((w2 >> 24) & 1u)];
+                        PendState* ps = &PEND(origin, w2 >> 24);
                         const uint8_t pv = ps->valid;
                         if ((pv == PS_JYES || pv == PS_JNO) && ps->pid == (int32_t)id) {
                             judge = pv == PS_JYES ? 1 : 0;
                         } else {
                             judge = -1;
-                            if (S.own_state != 0 && (int32_t)id == S.own_pid) set_error(S, P, ERR_PID_COLLISION, id);  // :690-692
-                            else want_jreq = !(pv == PS_JREQ && ps->pid == (int32_t)id);
+                            if (own_has(S, P, (int32_t)id)) set_error(S, P, ERR_PID_COLLISION, id);  // :690-692
+                            // ask once; an entry still held by an earlier proposal of the same pool slot
+                            // (its decision is ahead in this ring, applied this iteration) waits
+                            else want_jreq = pv == PS_NONE;
                         }
+                    } else if (PEND(origin, w2 >> 24).valid != PS_NONE) {
+                        judge = -1;  // held one iteration: the entry's previous proposal is decided in this batch
                     } else {
                         uint32_t dl = nsmall > 1 ? reinterpret_cast<const u32x4*>(STG(c, 1))->z : 0u;
                         if (dl > plen - 16u) dl = plen > 16u ? plen - 16u : 0u;
@@ -1735,7 +1798,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     id = h.y;
                     if (((h.x >> 16) & 0xffu) == TAG_PROPOSAL) {  // RLO_submit_proposal :876-906 (payload = PBuf)
                         w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
-                        w2 = (h.z & 0xffffu) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                        w2 = (h.z & 0xffffu) | ((uint32_t)S.loc_slot[2 * kPoolMax - 1] << 24);  // its pool slot
                     } else if (BULK && ((h.x >> 16) & 0xffu) == TAG_BULK) {  // payload = descriptor {len, q}
                         w0 = (uint32_t)me | (TAG_BULK << 16) | (0xffu << 24);
                         w2 = 16u;
@@ -1748,20 +1811,23 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         kind = K_BAD;
                         kids = 0;
                     }
-                } else if (loc_kind == K_DEC && c == R) {
-                    kind = K_DEC;
-                    group = kGroupLocal + K_DEC;
-                    id = (uint32_t)S.own_pid;
-                    w0 = (uint32_t)me | (TAG_DECISION << 16) | ((S.own_decision & 0xffu) << 24);
-                    w2 = 23u | (S.own_pseq << 24);
-                } else if (loc_kind == K_PROP && c == R) {
-                    const int64_t pi = S.prop_idx;
-                    kind = K_PROP;
-                    group = kGroupLocal + K_PROP;
-                    src = (uint32_t)pi;
-                    id = (uint32_t)P.prop_pid[pi];
-                    w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
-                    w2 = (16u + P.prop_data_len[pi]) | ((uint32_t)(S.own_iter & 0xff) << 24);
+                } else if (loc_kind && c >= R && c < R + S.loc_n) {  // the pool's decisions, then proposals
+                    const uint32_t i = c - R, k = S.loc_slot[i];
+                    if (i < S.loc_nd) {  // _iar_decision_bcast :908-917
+                        kind = K_DEC;
+                        group = kGroupLocal + K_DEC;
+                        id = (uint32_t)S.own_pid[k];
+                        w0 = (uint32_t)me | (TAG_DECISION << 16) | ((S.own_decision[k] & 0xffu) << 24);
+                        w2 = 23u | (k << 24);
+                    } else {  // RLO_submit_proposal :876-906
+                        const int64_t pi = S.prop_idx + (int64_t)(i - S.loc_nd);
+                        kind = K_PROP;
+                        group = kGroupLocal + K_PROP;
+                        src = (uint32_t)pi;
+                        id = (uint32_t)P.prop_pid[pi];
+                        w0 = (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24);
+                        w2 = (16u + P.prop_data_len[pi]) | (k << 24);
+                    }
                 } else {
                     kind = K_LAT;
                     group = kGroupLocal + K_LAT;
@@ -1799,7 +1865,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t plen = lw2 & 0xffffu;
                 uint32_t slot = 0;
                 if (lane == 0) {
-                    PendState* ps = &pend[2 * lorg + ((lw2 >> 24) & 1u)];
+                    PendState* ps = &PEND(lorg, lw2 >> 24);
                     ps->pid = (int32_t)lid;
                     ps->valid = PS_JREQ;
                     slot = log_put(S, P, lr, LOG_JREQ, lorg, lfrom, lid, plen, -1, lw2 >> 24);
@@ -1913,7 +1979,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const int32_t pid = (int32_t)id;
                         const int k = (int)(group >> 1);
                         atomicAdd(&S.proposals_recv, 1ull);
-                        if (S.own_state != 0 && pid == S.own_pid) {
+                        if (own_has(S, P, pid)) {
                             set_error(S, P, ERR_PID_COLLISION, (uint32_t)pid);  // :690-692 (the reference never votes)
                         } else {
                             atomicAdd(&S.judge_calls, 1ull);
@@ -1926,7 +1992,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 for (uint32_t q = 0; 16u * q < len && 16u * q < P.log_stride; q++)
                                     st_sys16(dst + 16u * q, ld_sc1(rf, src + kHdr + 16u * q));
                             }
-                            PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                            PendState* ps = &PEND(origin, pseq);
                             if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                                 ps->valid = PS_NONE;
                                 emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 0);
@@ -1942,7 +2008,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             }
                         }
                     } else if (tag == TAG_DECISION) {  // :603-615, _iar_decision_handler :814-859
-                        PendState* ps = &pend[2 * origin + (pseq & 1u)];
+                        PendState* ps = &PEND(origin, pseq);
                         if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)id) {
                             if (vote != 0) {
                                 atomicAdd(&S.actions, 1ull);
@@ -1995,18 +2061,20 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                       }
                     }
                 } else if (kind == K_PROP || (kind == K_HOST && tag == TAG_PROPOSAL)) {
-                    S.own_pid = (int32_t)id;
-                    S.own_word = 0;
+                    // proposalPool_proposal_add (:1253-1279): slot pseq takes the proposal
+                    const uint32_t k = pseq & (P.pend_slots - 1u);
+                    S.own_pid[k] = (int32_t)id;
+                    S.own_word[k] = 0;
                     S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
-                    S.own_pseq = pseq;
-                    S.own_state = 1;
+                    S.own_state[k] = 1;
+                    if (kind == K_PROP) atomicAdd(&S.own_iter, 1ull);  // admitted proposals are a prefix of the list
                 } else if (kind == K_DEC) {
+                    const uint32_t k = pseq & (P.pend_slots - 1u);
                     atomicAdd(&S.own_decided, 1ull);
                     if (vote) atomicAdd(&S.own_approved, 1ull);
-                    log_put(S, P, lr, LOG_RESULT, me, -1, id, 0, vote, 0);
-                    S.own_state = 0;
-                    S.own_pid = -1;  // RLO_proposal_reset via RLO_get_vote_my_proposal (:1649-1673)
-                    S.own_iter++;
+                    log_put(S, P, lr, LOG_RESULT, me, -1, id, 0, vote, k);
+                    S.own_state[k] = 0;
+                    S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
                 } else if (kind == K_LAT) {
                     const uint32_t np = S.lat_pos + 1u;
                     S.lat_pos = np;
@@ -2301,8 +2369,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if (P.mode & MODE_STORM) done &= sched_next == sched_n;
                 if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == expect_bcast;
                 if (P.mode & MODE_LAT) done &= S.lat_pos >= S.lat_pos_n;
-                if ((P.mode & MODE_IAR) && !host)
-                    done &= S.own_iter == S.own_n && S.own_state == 0 && (int64_t)S.dec_delivered == S.expect_dec;
+                if ((P.mode & MODE_IAR) && !host) {
+                    bool idle = true;
+                    for (uint32_t k = 0; k < P.pend_slots; k++) idle &= S.own_state[k] == 0u;
+                    done &= (int64_t)S.own_iter == S.own_n && idle && (int64_t)S.dec_delivered == S.expect_dec;
+                }
                 if (host) done = S.quit != 0;
                 if (S.error == ERR_TIMEOUT) done = true;
                 if (peer_failed) done = true;  // another rank failed: stop everyone

@@ -154,6 +154,7 @@ struct Layout {
     uint64_t bulk_max = 0;
     uint32_t bslots = 0, bcap = 0;
     std::vector<uint64_t> heap_bytes, bflag_bytes;            // per part
+    uint32_t pend_slots = 2;  // proposal pool: pending entries per origin (rlo_device.hpp Params.pend_slots)
 };
 
 int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uint32_t ring_slots, uint64_t bulk_max,
@@ -399,8 +400,8 @@ int size_lds_variant(rlo_world* w, int variant) {
     int api = 0;
     bool ok = false;
     for (uint32_t ns = std::min<uint32_t>(8u, L.stride / 16u); ns >= 1 && !ok; ns--) {
-        // [pending proposals 2N x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
-        const size_t fixed = stat + (size_t)32 * L.n + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
+        // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
+        const size_t fixed = stat + (size_t)16 * L.n * L.pend_slots + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
         if (per_block < fixed + 1024 + 512) continue;
         size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
         for (;;) {
@@ -549,6 +550,11 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, cfg->bulk_max,
                           cfg->bulk_slots, w->L);
     if (rc) { delete w; return rc; }
+    {
+        const uint32_t pp = cfg->proposal_pool ? cfg->proposal_pool : 2u;
+        if ((pp & (pp - 1u)) || pp > (uint32_t)rlo::kPoolMax) { delete w; return RLO_E_INVAL; }
+        w->L.pend_slots = pp;
+    }
     w->part = cfg->part;
     w->rb = w->L.pb[w->part];
     w->nl = w->L.pb[w->part + 1] - w->rb;
@@ -740,6 +746,7 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
     pc.bulk_max = cfg->bulk_max;
     pc.bulk_slots = cfg->bulk_slots;
     pc.movers = cfg->movers;
+    pc.proposal_pool = cfg->proposal_pool;
     rlo_world* w = nullptr;
     int rc = rlo_part_create(&pc, &w);
     if (rc) return rc;
@@ -802,6 +809,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->movers = w->nmov;
     o->bulk_max = w->L.bulk_max;
     o->heap_bytes = w->L.heap_bytes[w->part];
+    o->proposal_pool = w->L.pend_slots;
     return RLO_OK;
 }
 
@@ -833,6 +841,8 @@ static void base_params(rlo_world* w) {
     P.window = 32;
     P.n_local = (uint32_t)w->nl;
     P.ring_cap = w->L.stride - rlo::kHdr;
+    P.pend_slots = w->L.pend_slots;
+    P.own_pool = 1;  // one own proposal per engine (rootless_ops.c:241) unless a program asks for more
     if (w->L.bulk_max) {
         const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);
         P.bulk_slots = w->L.bslots;
@@ -1003,8 +1013,11 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
                     const uint8_t* data, const uint32_t* data_off, const uint32_t* data_len) {
     if (!w || !cfg || nprop < 0 || (nprop && (!origin || !pid || !data_off || !data_len))) return RLO_E_INVAL;
     if (!w->connected) return RLO_E_NOTCONNECTED;
+    const uint32_t pool = cfg->pool ? cfg->pool : 1u;
+    if (pool > w->L.pend_slots) return RLO_E_INVAL;  // the world's proposal_pool bounds it
     base_params(w);
     rlo::Params& P = w->P;
+    P.own_pool = pool;
     const int n = w->L.n, nl = w->nl, rb = w->rb;
     std::vector<int64_t> off(nl + 1, 0), expect(nl, 0), per(n, 0);
     for (int64_t i = 0; i < nprop; i++) {
@@ -1165,6 +1178,8 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     const uint32_t cc = cfg && cfg->cmd_slots ? pow2_ceil(cfg->cmd_slots) : 256u;
     const uint32_t pc = cfg && cfg->pickup_slots ? pow2_ceil(cfg->pickup_slots) : 1024u;
     if (pc < 64 || cc < 4 || (uint64_t)cc * w->L.stride > 0xFFFF0000ull) return RLO_E_INVAL;
+    const uint32_t pool = cfg && cfg->pool ? cfg->pool : 1u;
+    if (pool > w->L.pend_slots) return RLO_E_INVAL;
     HIPCHK(hipSetDevice(w->device));
     host_free(w);
     w->cmd_cap = cc;
@@ -1209,6 +1224,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     base_params(w);
     rlo::Params& P = w->P;
     P.mode = rlo::MODE_HOST | rlo::MODE_IAR;
+    P.own_pool = pool;
     P.host_judge = 1;  // judge(data) / judge(NULL) are the host's callbacks (rlo_host_device_judge: the device's)
     P.log = dev_ev ? const_cast<rlo::LogRec*>(dev_ev) : w->h_ev;
     P.log_cap = pc;

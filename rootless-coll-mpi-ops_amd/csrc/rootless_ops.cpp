@@ -91,7 +91,9 @@ struct progress_engine {
     std::deque<Cmd> backlog;         // commands the ring had no room for yet
     std::deque<RLO_msg_t*> wait;     // my bcasts until the device took them (queue_wait, :1594)
     uint64_t bcast_seq = 0;
-    RLO_proposal_state own{};        // my_own_proposal (:241)
+    RLO_proposal_state own{};        // my_own_proposal (:241): the most recently submitted one
+    int pool_depth = 1;              // extension: own proposals in flight (RLO_PROPOSAL_POOL)
+    std::map<int, RLO_proposal_state> props;  // pool_depth > 1: every own proposal by pid
     std::map<std::pair<int, int>, std::vector<char>> approved;  // (origin, pid) -> PBuf (queue_iar_pending)
     long sent_bcast = 0, recved_bcast = 0;  // :1600, :586
     bool failed = false;
@@ -331,6 +333,21 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             break;
         }
         case RLO_EV_RESULT: {  // my decision went out (:560-563 + _iar_decision_bcast :908-917)
+            if (e->pool_depth > 1) {
+                auto it = e->props.find((int)ev.id);
+                if (it != e->props.end()) {
+                    it->second.vote = ev.vote;
+                    it->second.votes_recved = it->second.votes_needed;
+                    it->second.state = RLO_COMPLETED;
+                }
+                e->n_result++;
+                e->sent_bcast++;  // a decision counts as a sent bcast (:1600)
+                if ((int)ev.id != e->own.pid) break;  // own mirrors the most recent submission
+                e->own.vote = ev.vote;
+                e->own.votes_recved = e->own.votes_needed;
+                e->own.state = RLO_COMPLETED;
+                break;
+            }
             if (e->d_cons_ns) {
                 e->d_hist[1][leg_bucket(now_ns() - e->d_cons_ns)]++;
                 e->d_cons_ns = 0;
@@ -387,6 +404,7 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             std::memset(&c, 0, sizeof c);
             c.kind = RLO_CMD_OWN_JUDGE;
             c.id = (int32_t)ev.id;
+            c.pseq = ev.aux;  // the proposal's pool slot
             c.vote = v;
             post(e, c, nullptr, 0, nullptr);
             break;
@@ -805,6 +823,12 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     bool multi = false;
     for (int d : devs) multi |= d != devs[0];
 
+    {  // extension: the proposal pool depth, the largest any rank asks for (RLO_PROPOSAL_POOL)
+        int mine = 1, depth = 1;
+        if (const char* pp = std::getenv("RLO_PROPOSAL_POOL")) mine = std::max(1, std::min(16, std::atoi(pp)));
+        MPI_Allreduce(&mine, &depth, 1, MPI_INT, MPI_MAX, e->comm);
+        e->pool_depth = depth;
+    }
     e->bulk_max = 64ull << 20;  // extension: bcasts beyond the data area up to RLO_BULK_MAX bytes (0: off)
     if (const char* bm = std::getenv("RLO_BULK_MAX")) e->bulk_max = std::strtoull(bm, nullptr, 10);
     int rc = RLO_OK;
@@ -832,6 +856,8 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
         pc.flags = multi ? RLO_PART_UNCACHED : 0u;
         pc.bulk_max = e->bulk_max;
         pc.bulk_slots = 2;
+        pc.proposal_pool = 2;  // pending entries per origin: a power of two >= the pool depth
+        while (pc.proposal_pool < (uint32_t)e->pool_depth) pc.proposal_pool *= 2;
         pc.movers = 4;  // RLO_BULK_MOVERS: mover workgroups of the part
         if (const char* mv = std::getenv("RLO_BULK_MOVERS")) pc.movers = (uint32_t)std::strtoul(mv, nullptr, 10);
         rc = rlo_part_create(&pc, &e->w);
@@ -852,6 +878,7 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
             rlo_host_cfg_t hc;
             std::memset(&hc, 0, sizeof hc);
             hc.pickup_slots = 512;
+            hc.pool = (uint32_t)e->pool_depth;
             rc = rlo_program_host(e->w, &hc);
         }
         if (rc == RLO_OK && dj) {  // extension: the device judges (every local rank's string for ISP)
@@ -1133,6 +1160,7 @@ int RLO_submit_proposal(RLO_engine_t* eng, char* proposal, size_t prop_size, RLO
     pbuf_put(pb.data(), my_proposal_id, 1, prop_size, proposal);
     eng->t_submit = now_ns();
     eng->own.state = RLO_IN_PROGRESS;
+    if (eng->pool_depth > 1) eng->props[my_proposal_id] = eng->own;  // application thread only
     rlo_cmd_t c;
     std::memset(&c, 0, sizeof c);
     c.kind = RLO_CMD_PROPOSAL;
@@ -1151,9 +1179,25 @@ int RLO_submit_proposal(RLO_engine_t* eng, char* proposal, size_t prop_size, RLO
 }
 
 int RLO_check_proposal_state(RLO_engine_t* eng, int pid) {
-    (void)pid;  // ignored, as in the reference (:869-872)
     RLO_make_progress_all();
-    return eng->own.state;
+    if (eng->pool_depth > 1) {  // extension: the proposal pool reports the pid asked for
+        auto it = eng->props.find(pid);
+        return it == eng->props.end() ? RLO_INVALID : it->second.state;
+    }
+    return eng->own.state;  // pid ignored, as in the reference (:869-872)
+}
+
+int RLO_proposal_pool_depth(RLO_engine_t* eng) { return eng ? eng->pool_depth : 0; }
+
+int RLO_get_vote_proposal(RLO_engine_t* eng, RLO_ID pid) {
+    assert(eng);
+    if (eng->pool_depth <= 1) return eng->own.pid == pid ? RLO_get_vote_my_proposal(eng) : -1;
+    auto it = eng->props.find(pid);
+    if (it == eng->props.end() || it->second.state != RLO_COMPLETED) return -1;
+    const int ret = it->second.vote;
+    eng->props.erase(it);
+    if (eng->own.pid == pid) RLO_proposal_reset(&eng->own);
+    return ret;
 }
 
 int RLO_get_vote_my_proposal(RLO_engine_t* eng) {

@@ -33,7 +33,7 @@ RLO_EV_ACTION, RLO_EV_RESULT, RLO_EV_JUDGE, RLO_EV_OWN_JUDGE, RLO_EV_JUDGED = 3,
 class WorldCfg(ctypes.Structure):
     _fields_ = [("n_ranks", ctypes.c_int32), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("bulk_max", ctypes.c_uint64), ("bulk_slots", ctypes.c_uint32),
-                ("movers", ctypes.c_uint32)]
+                ("movers", ctypes.c_uint32), ("proposal_pool", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class WorldInfo(ctypes.Structure):
@@ -44,14 +44,16 @@ class WorldInfo(ctypes.Structure):
                 ("blocks_per_cu", ctypes.c_int32), ("part", ctypes.c_int32), ("n_parts", ctypes.c_int32),
                 ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),
                 ("waves", ctypes.c_int32), ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32),
-                ("bulk_max", ctypes.c_uint64), ("heap_bytes", ctypes.c_uint64)]
+                ("bulk_max", ctypes.c_uint64), ("heap_bytes", ctypes.c_uint64), ("proposal_pool", ctypes.c_uint32),
+                ("pad2", ctypes.c_uint32)]
 
 
 class PartCfg(ctypes.Structure):
     _fields_ = [("n_ranks", ctypes.c_int32), ("n_parts", ctypes.c_int32), ("part", ctypes.c_int32),
                 ("part_begin", ctypes.c_void_p), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("flags", ctypes.c_uint32), ("bulk_max", ctypes.c_uint64),
-                ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32)]
+                ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32), ("proposal_pool", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
 
 
 class StormCfg(ctypes.Structure):
@@ -63,12 +65,12 @@ class StormCfg(ctypes.Structure):
 class IarCfg(ctypes.Structure):
     _fields_ = [("judge_kind", ctypes.c_uint32), ("judge_ppm", ctypes.c_uint32), ("judge_seed", ctypes.c_uint64),
                 ("judge_mask", ctypes.c_void_p), ("judge_isp", ctypes.c_char_p), ("flags", ctypes.c_uint32),
-                ("log_cap", ctypes.c_uint32)]
+                ("log_cap", ctypes.c_uint32), ("pool", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class HostCfg(ctypes.Structure):
     _fields_ = [("cmd_slots", ctypes.c_uint32), ("pickup_slots", ctypes.c_uint32), ("idle_timeout_s", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("pool", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class Cmd(ctypes.Structure):

@@ -9,7 +9,7 @@ processes on one box cannot (64 / 256 ranks).
     for ev in hw.poll(rank): ...      # RLO_make_progress_all (:538): deliveries, judge requests,
                                       # actions, own results
     hw.judge(rank, ev, vote)          # verdict of judge(data) (:698) for an RLO_EV_JUDGE event
-    hw.own_judge(rank, pid, vote)     # verdict of judge(NULL) (:773)
+    hw.own_judge(rank, ev, vote)      # verdict of judge(NULL) (:773) for an RLO_EV_OWN_JUDGE event
     hw.close()                        # RLO_CMD_QUIT to every rank, wait for the kernel
 """
 import ctypes
@@ -26,13 +26,14 @@ def pbuf(pid, vote, data):
 
 
 class HostWorld:
-    def __init__(self, n, max_payload=256, device=-1, cmd_slots=0, pickup_slots=0, idle_timeout_s=60):
-        self.world = World(n, max_payload=max_payload, device=device)
+    def __init__(self, n, max_payload=256, device=-1, cmd_slots=0, pickup_slots=0, idle_timeout_s=60, pool=1):
+        """pool: own proposals a rank may keep in flight (the proposal pool; 1 = my_own_proposal)"""
+        self.world = World(n, max_payload=max_payload, device=device, proposal_pool=max(2, 1 << (pool - 1).bit_length()))
         self.lib = self.world.lib
         self.h = self.world.h
         self.n = n
         self.max_payload = self.world.info["slot_stride"] - 16
-        cfg = L.HostCfg(cmd_slots, pickup_slots, idle_timeout_s, 0)
+        cfg = L.HostCfg(cmd_slots, pickup_slots, idle_timeout_s, 0, pool, 0)
         check(self.lib.rlo_program_host(self.h, ctypes.byref(cfg)), "rlo_program_host")
         self.stream = ctypes.c_void_p()
         dev = device if device >= 0 else 0
@@ -71,8 +72,9 @@ class HostWorld:
     def judge(self, rank, ev, vote):
         return self._post(rank, L.Cmd(L.RLO_CMD_JUDGE, ev["origin"], ev["id"], ev["aux"], int(vote), 0))
 
-    def own_judge(self, rank, pid, vote):
-        return self._post(rank, L.Cmd(L.RLO_CMD_OWN_JUDGE, 0, pid, 0, int(vote), 0))
+    def own_judge(self, rank, ev, vote):
+        """verdict of judge(NULL) for an RLO_EV_OWN_JUDGE event (its pid and pool slot)"""
+        return self._post(rank, L.Cmd(L.RLO_CMD_OWN_JUDGE, 0, ev["id"], ev["aux"], int(vote), 0))
 
     # ---------------------------------------------------------------- events
     def poll(self, rank, limit=1 << 16):

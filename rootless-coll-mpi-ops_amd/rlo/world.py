@@ -21,14 +21,16 @@ class World:
     """A world of n ranks.  World(n) hosts all of them on one GPU; World.part(...) creates one
     part of a sharded world (export() -> exchange blobs -> connect(blobs))."""
 
-    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None, bulk_max=0, bulk_slots=0, movers=0):
+    def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None, bulk_max=0, bulk_slots=0, movers=0,
+                 proposal_pool=0):
         """bulk_max > 0: messages longer than max_payload (up to bulk_max bytes) are bulk messages --
         announced through the rings, moved by `movers` mover workgroups (0 = auto) between per-rank
-        heaps of bulk_slots slots per origin (rlo_hip.h)."""
+        heaps of bulk_slots slots per origin (rlo_hip.h).  proposal_pool: pending entries per origin
+        = the most own proposals a rank can keep in flight (power of two <= 16; 0 = 2)."""
         self.lib = L.load()
         h = ctypes.c_void_p()
         if _part is None:
-            cfg = L.WorldCfg(n, max_payload, ring_slots, device, bulk_max, bulk_slots, movers)
+            cfg = L.WorldCfg(n, max_payload, ring_slots, device, bulk_max, bulk_slots, movers, proposal_pool)
             check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
         else:
             n_parts, part, begin, flags = _part
@@ -37,7 +39,8 @@ class World:
             if begin is not None:
                 self._pb = (ctypes.c_int32 * (n_parts + 1))(*begin)
                 pb = ctypes.cast(self._pb, ctypes.c_void_p)
-            cfg = L.PartCfg(n, n_parts, part, pb, max_payload, ring_slots, device, flags, bulk_max, bulk_slots, movers)
+            cfg = L.PartCfg(n, n_parts, part, pb, max_payload, ring_slots, device, flags, bulk_max, bulk_slots, movers,
+                            proposal_pool)
             check(self.lib.rlo_part_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_part_create")
         self.h = h
         self.n = n
@@ -46,10 +49,10 @@ class World:
 
     @classmethod
     def part(cls, n, n_parts, part, part_begin=None, max_payload=4096, ring_slots=0, device=-1, uncached=False,
-             bulk_max=0, bulk_slots=0, movers=0):
+             bulk_max=0, bulk_slots=0, movers=0, proposal_pool=0):
         return cls(n, max_payload, ring_slots, device,
                    _part=(n_parts, part, part_begin, L.RLO_PART_UNCACHED if uncached else 0), bulk_max=bulk_max,
-                   bulk_slots=bulk_slots, movers=movers)
+                   bulk_slots=bulk_slots, movers=movers, proposal_pool=proposal_pool)
 
     def _query(self):
         info = L.WorldInfo()
@@ -103,8 +106,9 @@ class World:
         self._lat_rounds = rounds
 
     def program_iar(self, proposals, judge=L.RLO_JUDGE_APPROVE, mask=None, isp=None, seed=0, ppm=0, log=False,
-                    log_cap=0, prof=False):
-        """proposals: list of (origin, pid, data bytes) in per-origin submission order."""
+                    log_cap=0, prof=False, pool=1):
+        """proposals: list of (origin, pid, data bytes) in per-origin submission order; every rank keeps
+        up to `pool` of its own in flight (the proposal pool, <= the world's proposal_pool)."""
         origin = np.array([p[0] for p in proposals], dtype=np.int32)
         pid = np.array([p[1] for p in proposals], dtype=np.int32)
         blob = np.frombuffer(b"".join(p[2] for p in proposals) or b"\0", dtype=np.uint8).copy()
@@ -124,6 +128,7 @@ class World:
             self._keep.append(cfg.judge_isp)
         cfg.flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_PROF if prof else 0)
         cfg.log_cap = log_cap
+        cfg.pool = pool
         self._keep.append(cfg)
         d = lambda a: a.ctypes.data
         check(self.lib.rlo_program_iar(self.h, ctypes.byref(cfg), len(proposals), d(origin), d(pid), d(blob), d(doff),

@@ -102,6 +102,39 @@ def test_iar_matches_reference(harness, case):
         assert got[k] == case[k], k
 
 
+@pytest.mark.parametrize("n,per,mask,depth", [(4, 12, 0, 4), (5, 10, 0b00100, 16), (8, 6, 0b10010000, 16),
+                                              (8, 4, 0, 1)])
+def test_proposal_pool_matches_oracle(harness, n, per, mask, depth):
+    """extension: the proposal pool (RLO_PROPOSAL_POOL=depth; the reference's PROPOSAL_POOL_SIZE,
+    rootless_ops.c:30, never wired in): every rank keeps up to `depth` own proposals in flight through
+    RLO_submit_proposal / RLO_check_proposal_state(pid) / RLO_get_vote_proposal(pid).  Judge calls
+    (rank, NULL?, proposal), actions, every decision pickup and every result equal the pool oracle's
+    (orc_iar_pool, whose one-proposal case is pinned to the reference's fixtures)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    import pyoracle as orc
+
+    env = dict(os.environ, RLO_PROPOSAL_POOL=str(depth))
+    recs = capture.run(harness, n, "pool", per, mask, timeout=80, env=env)
+    assert {r["depth"] for r in recs if r["ev"] == "depth"} == {depth}
+    props = [(o, 1000 + i * n + o, ("p%d-r%d" % (i, o)).encode()) for i in range(per) for o in range(n)]
+    pid_of = {d.decode(): pid for (_, pid, d) in props}
+    cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=[(mask >> r) & 1 for r in range(n)])
+    ev = orc.iar(n, props, cfg, cap=1 << 20, pool=depth)
+    assert not [e for e in ev if e[0] == orc.ORC_EV_ERROR]
+    want_j = sorted((e[1], e[3], e[2] if not e[3] else -1) for e in ev if e[0] == orc.ORC_EV_JUDGE)
+    want_a = sorted((e[1], e[2]) for e in ev if e[0] == orc.ORC_EV_ACTION)
+    want_d = sorted((e[1], e[2], e[3], e[4]) for e in ev if e[0] == orc.ORC_EV_PICKUP)
+    want_r = sorted((e[1], e[2], e[3]) for e in ev if e[0] == orc.ORC_EV_RESULT)
+    got_j = sorted((r["rank"], r["null"], pid_of[r["arg"]] if not r["null"] else -1) for r in recs if r["ev"] == "judge")
+    got_a = sorted((r["rank"], r["pid"]) for r in recs if r["ev"] == "action")
+    got_d = sorted((r["rank"], r["pid"], r["vote"], r["origin"]) for r in recs if r["ev"] == "decision")
+    got_r = sorted((r["rank"], r["pid"], r["vote"]) for r in recs if r["ev"] == "result")
+    assert got_j == want_j
+    assert got_a == want_a
+    assert got_d == want_d
+    assert got_r == want_r
+
+
 @pytest.mark.parametrize("case", [c for c in load("multi.json")["cases"] if c["n"] <= MAXN],
                          ids=lambda c: "n%d-a%d-m%d-g%d" % (c["n"], c["active_1"], c["mod"], c["agree"]))
 def test_multi_proposal_matches_reference(harness, case):

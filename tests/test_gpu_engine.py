@@ -212,24 +212,29 @@ def test_iar_concurrent_all_ranks(rlo, n, p, ppm):
     assert (st["dec_delivered"] == (n - 1) * p).all()
 
 
-@pytest.mark.parametrize("n,p,ppm", [(64, 8, 814), (256, 4, 201), (64, 4, 50000)])
-def test_iar_concurrent_exact_sets(rlo, n, p, ppm):
-    """C4 at scale, exactly: every rank keeps one outstanding proposal (pid = it * n + r); seeded
-    declines sized so ~5% of proposals are declined (ppm 814 at N = 64, 201 at N = 256; 50,000 =
-    nearly all declined).  Per (origin, pid) against the oracle (orc_iar_rounds): the judge-call set
-    (rank, origin, pid, NULL arg, verdict), the action set, every decision pickup with its decision,
-    and every originator's result."""
-    kind = rlo.abi.RLO_JUDGE_HASH
+@pytest.mark.parametrize("n,p,ppm,pool", [(64, 8, 814, 1), (256, 4, 201, 1), (64, 4, 50000, 1),
+                                          (8, 64, 20000, 16), (64, 32, 814, 16), (256, 16, 201, 16),
+                                          (64, 16, 50000, 4), (5, 48, 0, 8)])
+def test_iar_concurrent_exact_sets(rlo, n, p, ppm, pool):
+    """C4 at scale, exactly: every rank runs p proposals (pid = it * n + r) keeping `pool` of them in
+    flight (pool 1: the reference's one own proposal, rootless_ops.c:241; up to 16: the proposal pool,
+    :30, :1251-1366); seeded declines sized so ~5% of proposals are declined (ppm 814 at N = 64, 201
+    at N = 256; 50,000 = nearly all declined).  Per (origin, pid) against the oracle (orc_iar_rounds_pool,
+    the same pool depth): the judge-call set (rank, origin,
+    pid, NULL arg, verdict), the action set, every decision pickup with its decision, and every
+    originator's result."""
+    kind = rlo.abi.RLO_JUDGE_HASH if ppm else rlo.abi.RLO_JUDGE_APPROVE
     props = [(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)]
     cap = 3 * n * p + 64
-    with rlo.World(n) as w:
-        w.program_iar(props, judge=kind, seed=99, ppm=ppm, log=True, log_cap=cap)
+    with rlo.World(n, max_payload=32, proposal_pool=max(2, pool)) as w:
+        assert w.info["proposal_pool"] == max(2, pool)
+        w.program_iar(props, judge=kind, seed=99, ppm=ppm, log=True, log_cap=cap, pool=pool)
         w.run()
         st = w.stats()
         logs = [w.log(r, cap=cap) for r in range(n)]
     assert (st["error"] == 0).all(), st["error"]
     cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_HASH, seed=99, ppm=ppm)
-    ev = orc.iar_rounds(n, p, cfg)
+    ev = orc.iar_rounds(n, p, cfg, pool=pool)
     want = {"judge": set(), "action": set(), "pickup": set(), "result": set()}
     for e, rank, pid, a, b, c in ev:
         if e == orc.ORC_EV_JUDGE:
@@ -257,7 +262,7 @@ def test_iar_concurrent_exact_sets(rlo, n, p, ppm):
         assert got[k] == want[k], (k, len(got[k]), len(want[k]), sorted(got[k] ^ want[k])[:6])
     declined = sum(1 for (_, _, d) in want["result"] if d == 0)
     assert len(want["result"]) == n * p
-    if ppm < 10000:
+    if 0 < ppm < 10000:
         assert 0 < declined < n * p and want["action"], declined  # both outcomes exercised
 
 

@@ -70,8 +70,10 @@ def test_host_bcast_matches_oracle(rlo, n, k, ln, maxp):
     assert (st["originated"] == k).all()
 
 
-def _run_iar(rlo, n, proposals, decline):
-    """proposals: (origin, pid, data); at most one per origin (one own proposal per engine)."""
+def _run_iar(rlo, n, proposals, decline, pool=1):
+    """proposals: (origin, pid, data); at most `pool` per origin (pool 1: one own proposal per engine,
+    rootless_ops.c:241; more: the proposal pool, :30 -- all submitted at once, the kernel keeps up
+    to `pool` in flight and holds the rest in the command ring)."""
     from rlo import abi
 
     judge, actions, pickups, results = [], [], [], []
@@ -90,7 +92,7 @@ def _run_iar(rlo, n, proposals, decline):
             hw.judge(r, ev, v)
         elif k == abi.RLO_EV_OWN_JUDGE:
             judge.append((r, ev["id"], 1, 1, r))
-            hw.own_judge(r, ev["id"], 1)
+            hw.own_judge(r, ev, 1)
         elif k == abi.RLO_EV_ACTION:
             data = approved.pop((r, ev["origin"], ev["id"]))
             actions.append((r, ev["id"], 1, len(data), ev["origin"]))
@@ -101,7 +103,7 @@ def _run_iar(rlo, n, proposals, decline):
         else:
             raise AssertionError(ev)
 
-    with rlo.HostWorld(n, max_payload=256) as hw:
+    with rlo.HostWorld(n, max_payload=256, pool=pool) as hw:
         hw_ref.append(hw)
         for o, pid, data in proposals:
             hw.propose(o, pid, data)
@@ -113,15 +115,19 @@ def _run_iar(rlo, n, proposals, decline):
     return judge, actions, pickups, results
 
 
-@pytest.mark.parametrize("n,origins,mask_ranks", [(8, [1], [4]), (8, [0, 3, 5, 6], []), (16, [0, 5, 9, 15], [6, 12]),
-                                                  (64, list(range(0, 64, 5)), [7, 33]), (256, [0, 77, 128, 255], [3])])
-def test_host_iar_matches_oracle(rlo, n, origins, mask_ranks):
+@pytest.mark.parametrize("n,origins,mask_ranks,per,pool", [(8, [1], [4], 1, 1), (8, [0, 3, 5, 6], [], 1, 1),
+                                                           (16, [0, 5, 9, 15], [6, 12], 1, 1),
+                                                           (64, list(range(0, 64, 5)), [7, 33], 1, 1),
+                                                           (256, [0, 77, 128, 255], [3], 1, 1),
+                                                           (8, [0, 3, 5, 6], [], 12, 4), (16, [0, 5, 9, 15], [6, 12], 20, 16),
+                                                           (64, list(range(0, 64, 7)), [7, 33], 6, 8)])
+def test_host_iar_matches_oracle(rlo, n, origins, mask_ranks, per, pool):
     decline = np.zeros(n, dtype=np.uint8)
     decline[mask_ranks] = 1
-    props = [(o, 1000 + o, ("proposal-from-%d" % o).encode()) for o in origins]
-    judge, actions, pickups, results = _run_iar(rlo, n, props, decline)
+    props = [(o, 1000 + i * n + o, ("proposal-%d-from-%d" % (i, o)).encode()) for i in range(per) for o in origins]
+    judge, actions, pickups, results = _run_iar(rlo, n, props, decline, pool=pool)
     cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=decline)
-    ev = orc.iar(n, props, cfg)
+    ev = orc.iar(n, props, cfg, pool=pool if per > 1 else 0)
     assert not [e for e in ev if e[0] == orc.ORC_EV_ERROR]
     want_j = sorted((e[1], e[2], e[3], e[4], e[5]) for e in ev if e[0] == orc.ORC_EV_JUDGE)
     want_a = sorted((e[1], e[2], e[3], e[4], e[5]) for e in ev if e[0] == orc.ORC_EV_ACTION)

@@ -96,6 +96,28 @@ def test_iar_rounds_events_agree_with_totals(n, p, ppm):
     assert sorted(e[2] for e in res) == sorted(it * n + r for it in range(p) for r in range(n))
 
 
+@pytest.mark.parametrize("n,p,ppm,pool", [(8, 12, 0, 4), (16, 6, 50000, 16), (64, 3, 814, 8), (5, 20, 20000, 16)])
+def test_iar_pool_outcomes_equal_single_proposal_rounds(n, p, ppm, pool):
+    """the proposal pool (rootless_ops.c:30, :1251-1366) changes when a proposal runs, not what happens
+    to it: orc_iar_rounds_pool's per-(origin, pid) judge calls, actions, decision pickups and results
+    equal orc_iar_rounds' (pool 1, the reference's one my_own_proposal, which the golden IAR cases pin)"""
+    kind = orc.ORC_JUDGE_HASH if ppm else orc.ORC_JUDGE_APPROVE
+    cfg, keep = orc.judge_cfg(kind, seed=7, ppm=ppm)
+    one = orc.iar_rounds(n, p, cfg)
+    many = orc.iar_rounds(n, p, cfg, pool=pool)
+    assert len(many) == len(one) and set(many) == set(one)
+    assert not [e for e in many if e[0] == orc.ORC_EV_ERROR]
+
+
+def test_iar_pool_one_per_origin_equals_reference_model(golden):
+    """with at most one proposal per origin the pool oracle is orc_iar, case for case (iar.json)"""
+    for case in golden("iar.json")["cases"]:
+        n, o, mask = case["n"], case["origin"], case["mask"]
+        cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=[(mask >> r) & 1 for r in range(n)])
+        props = [(o, 100 + o, ("proposal-from-%d" % o).encode())]
+        assert orc.iar(n, props, cfg, pool=4) == orc.iar(n, props, cfg)
+
+
 def _iar_events(n, origin, mask):
     cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=[(mask >> r) & 1 for r in range(n)])
     prop = ("proposal-from-%d" % origin).encode()

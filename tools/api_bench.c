@@ -9,6 +9,7 @@
  *                                           progress + pickup until all (N-1)K arrived
  *   mpiexec -n N api_bench lat ROUNDS LEN   one random originator per round, barrier between
  *   mpiexec -n N api_bench iar P            every rank keeps one proposal outstanding, P each
+ *   RLO_PROPOSAL_POOL=d mpiexec -n N api_bench iarpool P   d in flight per rank (extension)
  * Rank 0 prints one JSON line.  Payload bytes are checked at every receiver.
  */
 #include <stdint.h>
@@ -237,6 +238,54 @@ static void iar(int P, int dj) {
     RLO_progress_engine_cleanup(eng);
 }
 
+#ifdef RLO_HAVE_PROPOSAL_POOL
+/* the proposal pool (extension; RLO_PROPOSAL_POOL=d at engine creation): every rank keeps d of its
+ * P proposals in flight, device judge approving all (the reference allows one, rootless_ops.c:241) */
+static void iarpool(int P) {
+    RLO_device_judge j = {RLO_DJUDGE_APPROVE, NULL, 0, 0};
+    RLO_engine_t* eng = RLO_progress_engine_new_dj(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &j, NULL, &action_cb);
+    if (!eng) {
+        if (g_rank == 0) fprintf(g_out, "{\"mode\":\"iarpool\",\"error\":\"no engine\"}\n");
+        return;
+    }
+    const int D = RLO_proposal_pool_depth(eng);
+    char prop[17] = "0123456789abcdef";
+    long expect = (long)P * (g_size - 1), got = 0, approved = 0;
+    int sub = 0, done = 0, fl[16], nfl = 0;
+    MPI_Barrier(MPI_COMM_WORLD);
+    double t0 = now_s();
+    while (got < expect || done < P) {
+        while (nfl < D && sub < P) {
+            const int pid = sub * g_size + g_rank;
+            RLO_submit_proposal(eng, prop, 16, pid);
+            fl[nfl++] = pid;
+            sub++;
+        }
+        RLO_make_progress_all();
+        for (int i = 0; i < nfl;) {
+            const int v = RLO_get_vote_proposal(eng, fl[i]);
+            if (v < 0) { i++; continue; }
+            approved += v;
+            done++;
+            fl[i] = fl[--nfl];
+        }
+        RLO_user_msg* u = NULL;
+        while (RLO_user_pickup_next(eng, &u)) {
+            if (u->type == RLO_IAR_DECISION) got++;
+            RLO_user_msg_recycle(eng, u);
+        }
+    }
+    double dt = now_s() - t0, dtmax = 0;
+    long app = 0;
+    MPI_Reduce(&dt, &dtmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+    MPI_Reduce(&approved, &app, 1, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
+    if (g_rank == 0)
+        fprintf(g_out, "{\"mode\":\"iarpool\",\"ranks\":%d,\"P\":%d,\"pool\":%d,\"seconds\":%.6f,\"decisions_per_s\":%.1f,\"approved\":%ld}\n",
+               g_size, P, D, dtmax, g_size * (double)P / dtmax, app);
+    RLO_progress_engine_cleanup(eng);
+}
+#endif
+
 int main(int argc, char** argv) {
     MPI_Init(&argc, &argv);
     MPI_Comm_rank(MPI_COMM_WORLD, &g_rank);
@@ -244,7 +293,7 @@ int main(int argc, char** argv) {
     g_out = fdopen(dup(1), "w");
     if (!g_out || !freopen("/dev/null", "w", stdout)) return 3;
     if (argc < 3) {
-        if (g_rank == 0) fprintf(stderr, "usage: api_bench storm K LEN | lat ROUNDS LEN | iar P | iardj P\n");
+        if (g_rank == 0) fprintf(stderr, "usage: api_bench storm K LEN | lat ROUNDS LEN | iar P | iardj P | iarpool P\n");
         MPI_Finalize();
         return 2;
     }
@@ -253,6 +302,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[1], "iar")) iar(atoi(argv[2]), 0);
 #ifdef RLO_HAVE_DEVICE_JUDGE
     else if (!strcmp(argv[1], "iardj")) iar(atoi(argv[2]), 1);
+#endif
+#ifdef RLO_HAVE_PROPOSAL_POOL
+    else if (!strcmp(argv[1], "iarpool")) iarpool(atoi(argv[2]));
 #endif
     fflush(g_out);
     MPI_Finalize();

@@ -35,7 +35,7 @@ def main():
                     if k == abi.RLO_EV_JUDGE:
                         hw.judge(r, ev, 1)
                     elif k == abi.RLO_EV_OWN_JUDGE:
-                        hw.own_judge(r, ev["id"], 1)
+                        hw.own_judge(r, ev, 1)
                     elif k == abi.RLO_EV_RESULT:
                         done[r] += 1
                         if done[r] < P:
