@@ -207,7 +207,8 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
     if (max_rings * cap * L.stride > limit) cap = pow2_floor(limit / (max_rings * L.stride));
     if (cap < 16) return RLO_E_INVAL;
     L.cap = cap;
-    L.vote_cap = std::max<uint32_t>(64u, pow2_ceil(2u * (uint32_t)n));
+    // a vote slot is taken per proposal in flight through the edge: N origins x pool slots each
+    L.vote_cap = std::max<uint32_t>(64u, pow2_ceil(L.pend_slots * (uint32_t)n));
 
     const uint64_t ring_bytes = (uint64_t)cap * L.stride;
     L.fwd_bytes.assign(nparts, 0);
@@ -547,14 +548,14 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     // not invalidated by another XCD's write-through stores, and a consumer on that XCD read the
     // zeros (seen as unmarked slot headers that never became visible).  RLO_CACHED_RINGS=1: A/B only
     if (!std::getenv("RLO_CACHED_RINGS")) w->flags |= RLO_PART_UNCACHED;
-    int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, cfg->bulk_max,
-                          cfg->bulk_slots, w->L);
-    if (rc) { delete w; return rc; }
     {
         const uint32_t pp = cfg->proposal_pool ? cfg->proposal_pool : 2u;
         if ((pp & (pp - 1u)) || pp > (uint32_t)rlo::kPoolMax) { delete w; return RLO_E_INVAL; }
-        w->L.pend_slots = pp;
+        w->L.pend_slots = pp;  // before the layout: it sizes the vote rings
     }
+    int rc = build_layout(cfg->n_ranks, cfg->n_parts, cfg->part_begin, w->max_payload, cfg->ring_slots, cfg->bulk_max,
+                          cfg->bulk_slots, w->L);
+    if (rc) { delete w; return rc; }
     w->part = cfg->part;
     w->rb = w->L.pb[w->part];
     w->nl = w->L.pb[w->part + 1] - w->rb;
