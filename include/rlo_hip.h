@@ -196,7 +196,10 @@ typedef struct {
     uint32_t flags;
     uint32_t pool;           /* own proposals a rank may keep in flight (<= the world's proposal_pool):
                                 the proposal pool (rootless_ops.c:30); 0 = 1 (my_own_proposal, :241).
-                                A proposal command beyond it waits in the command ring              */
+                                A proposal command beyond it waits at the head of the command ring
+                                and holds up every command behind it (judge verdicts too): keep
+                                extra proposals on the host until an RLO_EV_RESULT frees a slot
+                                (librootless_ops.so and rlo/host.py do)                           */
     uint32_t pad;
 } rlo_host_cfg_t;
 int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg);

@@ -94,6 +94,8 @@ struct progress_engine {
     RLO_proposal_state own{};        // my_own_proposal (:241): the most recently submitted one
     int pool_depth = 1;              // extension: own proposals in flight (RLO_PROPOSAL_POOL)
     std::map<int, RLO_proposal_state> props;  // pool_depth > 1: every own proposal by pid
+    int own_inflight = 0;            // own proposals posted whose result has not arrived
+    std::deque<std::pair<int, std::vector<char>>> held_props;  // submitted beyond the pool: (pid, PBuf)
     std::map<std::pair<int, int>, std::vector<char>> approved;  // (origin, pid) -> PBuf (queue_iar_pending)
     long sent_bcast = 0, recved_bcast = 0;  // :1600, :586
     bool failed = false;
@@ -218,6 +220,18 @@ int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t l
     return 0;
 }
 
+// RLO_CMD_PROPOSAL with the serialized PBuf (:876-906); counts it in flight until its result
+int post_proposal(progress_engine* e, int pid, const std::vector<char>& pb) {
+    rlo_cmd_t c;
+    std::memset(&c, 0, sizeof c);
+    c.kind = RLO_CMD_PROPOSAL;
+    c.id = pid;
+    c.vote = 1;
+    if (post(e, c, pb.data(), (uint32_t)pb.size(), nullptr)) return -1;
+    e->own_inflight++;
+    return 0;
+}
+
 // [e->mu held]
 void flush_backlog(progress_engine* e) {
     while (!e->backlog.empty()) {
@@ -333,6 +347,12 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
             break;
         }
         case RLO_EV_RESULT: {  // my decision went out (:560-563 + _iar_decision_bcast :908-917)
+            if (e->own_inflight > 0) e->own_inflight--;
+            if (!e->held_props.empty() && e->own_inflight < e->pool_depth) {  // its pool slot is free again
+                auto hp = std::move(e->held_props.front());
+                e->held_props.pop_front();
+                if (post_proposal(e, hp.first, hp.second)) e->failed = true;
+            }
             if (e->pool_depth > 1) {
                 auto it = e->props.find((int)ev.id);
                 if (it != e->props.end()) {
@@ -1161,12 +1181,13 @@ int RLO_submit_proposal(RLO_engine_t* eng, char* proposal, size_t prop_size, RLO
     eng->t_submit = now_ns();
     eng->own.state = RLO_IN_PROGRESS;
     if (eng->pool_depth > 1) eng->props[my_proposal_id] = eng->own;  // application thread only
-    rlo_cmd_t c;
-    std::memset(&c, 0, sizeof c);
-    c.kind = RLO_CMD_PROPOSAL;
-    c.id = my_proposal_id;
-    c.vote = 1;
-    if (post(eng, c, pb.data(), (uint32_t)pb.size(), nullptr)) return -1;
+    // a proposal beyond the pool waits HERE, not in the command ring: there it would hold up the
+    // judge verdicts behind it, which other ranks' proposals -- and so my own -- wait for
+    if (eng->own_inflight >= eng->pool_depth) {
+        eng->held_props.emplace_back(my_proposal_id, std::move(pb));
+        return -1;
+    }
+    if (post_proposal(eng, my_proposal_id, pb)) return -1;
     static const bool trace = std::getenv("RLO_TRACE") != nullptr;
     if (trace) {
         std::lock_guard<std::mutex> lk(eng->mu);

@@ -40,6 +40,9 @@ class HostWorld:
         check(self.lib.rlo_stream_create(dev, ctypes.byref(self.stream)), "rlo_stream_create")
         check(self.lib.rlo_launch_ex(self.h, self.stream, 0), "rlo_launch_ex")
         self.backlog = [[] for _ in range(n)]
+        self.pool = pool
+        self.inflight = [0] * n    # own proposals posted whose result has not arrived
+        self.held = [[] for _ in range(n)]  # proposals beyond the pool, posted as results free slots
         self._rec = L.LogRec()
         self._buf = ctypes.create_string_buffer(self.max_payload + 16)
         self.closed = False
@@ -67,6 +70,12 @@ class HostWorld:
         return self._post(rank, L.Cmd(L.RLO_CMD_BCAST, 0, seq, 0, 0, 0), bytes(payload))
 
     def propose(self, rank, pid, data):
+        """RLO_submit_proposal; beyond `pool` in flight the proposal waits here (as librootless_ops.so
+        does), not in the command ring, where it would hold up the judge verdicts behind it"""
+        if self.inflight[rank] >= self.pool:
+            self.held[rank].append((pid, bytes(data)))
+            return True
+        self.inflight[rank] += 1
         return self._post(rank, L.Cmd(L.RLO_CMD_PROPOSAL, 0, pid, 0, 1, 0), pbuf(pid, 1, bytes(data)))
 
     def judge(self, rank, ev, vote):
@@ -90,6 +99,10 @@ class HostWorld:
             if r.payload_idx != 0xFFFFFFFF:
                 ev["payload"] = buf.raw[:min(r.len, len(buf))]
             out.append(ev)
+            if r.kind == L.RLO_EV_RESULT:  # a pool slot is free again
+                self.inflight[rank] -= 1
+                if self.held[rank]:
+                    self.propose(rank, *self.held[rank].pop(0))
         return out
 
     def running(self):
