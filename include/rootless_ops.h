@@ -159,8 +159,9 @@ RLO_engine_t* RLO_progress_engine_new_dj(MPI_Comm mpi_comm, size_t msg_size_max,
  * RLO_progress_engine_new, a rank may call RLO_submit_proposal again while earlier own proposals are
  * still in flight: up to d run at once (further ones wait, in submission order, for a slot), each
  * decided independently.  RLO_check_proposal_state(eng, pid) then reports the state of THAT pid (the
- * reference ignores pid), RLO_get_vote_proposal(eng, pid) returns its vote (-1 while not completed)
- * and forgets it; RLO_get_vote_my_proposal keeps meaning the most recently submitted proposal.
+ * reference ignores pid; an unknown pid still reports the most recent proposal), RLO_get_vote_proposal
+ * (eng, pid) returns its vote (-1 while not completed) and forgets it; RLO_get_vote_my_proposal keeps
+ * meaning the most recently submitted proposal.
  * d = 1 (the default) is the reference's behaviour. */
 #define RLO_HAVE_PROPOSAL_POOL 1
 int RLO_proposal_pool_depth(RLO_engine_t* eng);

@@ -1203,9 +1203,9 @@ int RLO_check_proposal_state(RLO_engine_t* eng, int pid) {
     RLO_make_progress_all();
     if (eng->pool_depth > 1) {  // extension: the proposal pool reports the pid asked for
         auto it = eng->props.find(pid);
-        return it == eng->props.end() ? RLO_INVALID : it->second.state;
+        if (it != eng->props.end()) return it->second.state;
     }
-    return eng->own.state;  // pid ignored, as in the reference (:869-872)
+    return eng->own.state;  // pid ignored (or unknown), as in the reference (:869-872)
 }
 
 int RLO_proposal_pool_depth(RLO_engine_t* eng) { return eng ? eng->pool_depth : 0; }
@@ -1224,6 +1224,7 @@ int RLO_get_vote_proposal(RLO_engine_t* eng, RLO_ID pid) {
 int RLO_get_vote_my_proposal(RLO_engine_t* eng) {
     if (eng->own.state != RLO_COMPLETED) return -1;
     int ret = eng->own.vote;
+    if (eng->pool_depth > 1) eng->props.erase(eng->own.pid);
     RLO_proposal_reset(&eng->own);
     return ret;
 }
