@@ -8,7 +8,4 @@ python3 -c "
 import json; d=json.load(open('gpurun_out/bench_quick.json'))
 print('value', d['value'], 'frac', d['roofline']['frac'], 'dec', d.get('decisions_per_s'), 'pool16', d.get('pool16_decisions_per_s'))
 print(json.dumps(d.get('small_worlds')))"
-# the drop-in's proposal pool at 8 rank processes (16 in flight per rank) beside the one-proposal loop
-for m in iardj iarpool; do
-  RLO_PROPOSAL_POOL=16 timeout -k 5 120 /opt/conda/bin/mpiexec -n 8 rootless-coll-mpi-ops_amd/lib/rlo_api_bench $m 4000 2>/dev/null | grep mode || { echo "api $m failed"; exit 1; }
-done
+bash tools/gpu_api_pool.sh
