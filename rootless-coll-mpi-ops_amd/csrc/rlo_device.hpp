@@ -108,6 +108,8 @@ struct RankTopo {
     uint64_t vout_ring[kMaxIn];            // vote ring to the parent of in-edge k, in the parent's part
     uint64_t vout_tail[kMaxIn];            // its tail word, in the parent's ctrl
     uint64_t vin_head[kMaxFanout];         // head word of the vote ring from child j, in the child's ctrl
+    uint64_t in_base[kMaxIn];              // forward region of in-edge k's producer part (pulled payloads)
+    uint32_t orig_data, orig_pad;          // pull worlds: my relay ring (byte offset in my part)
 };
 
 struct RankStats {
@@ -180,6 +182,14 @@ struct Params {
     // originator keeps up to own_pool <= pend_slots own proposals in flight, in slots it takes
     // round-robin, and reuses a slot only after that slot's decision went out
     uint32_t pend_slots, own_pool;
+    // pulled payloads (slots beyond the small copy path, no bulk): a large bcast travels each edge as
+    // its header (mark kRefMark) + a reference chunk {byte offset of the sender's copy in the sender's
+    // part}.  The sender's copy sits in its RELAY ring (one per rank, fwd_cap slots): an originator or
+    // a forwarding rank writes the message there once, its children load the payload from there (and
+    // write it into their own relay ring if they forward it on), and a relay slot is reused only after
+    // every child consumed the references written up to it (a release queue on the out-ring heads).
+    // A wall rank then stores header + reference per child instead of the whole payload per child.
+    uint32_t pull, pull_pad;
     // outputs
     RankStats* stats;             // [n_local]
     LogRec* log;                  // [n_local * log_cap]

@@ -43,6 +43,7 @@ static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
 static constexpr uint32_t kIdleSpin = 256;  // tight re-polls after an idle iteration (~0.1 ms at most)
+static constexpr int kRelQ = 4;  // pull worlds: relay-ring release records (coalesced when full)
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -66,6 +67,7 @@ struct CandL {          // one message of this iteration, kept for the copy phas
     uint32_t need;      // admitted out-ring bits (2j + vc); 0 when not admitted
     uint32_t logidx;    // log record of this delivery (payload capture) or ~0u
     uint32_t kind, group;
+    uint32_t relay;     // pull worlds: byte offset of this message's slot in my relay ring, ~0u = none
 };
 
 // bulk-message state (the BULK instantiation only)
@@ -146,6 +148,12 @@ struct Shared {
     // origination progress
     uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
     uint64_t hd[8], hd_t0;  // MODE_HDIAG counters (host mode)
+    // pull worlds: my relay ring (slots taken / released), this iteration's allocations, and the release
+    // records: relay count rq_relay[e] is released once every out-ring's consumer passed rq_out[e][oi]
+    uint64_t relay_tail, relay_rel;
+    uint32_t relay_n, ref_any, rq_n, rq_h;
+    uint64_t rq_relay[kRelQ];
+    uint64_t rq_out[kRelQ][kMaxOut];
     // counters
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
@@ -293,6 +301,10 @@ __device__ __forceinline__ uint32_t chunk_mix(uint32_t q, u32x4 w) {
 // slot mark (w2 bits 16..23 of every slot header, rlo_device.hpp): rings are zeroed at creation,
 // so a staged header without the mark is a slot whose bytes were not visible yet
 static constexpr uint32_t kSlotMark = 0xA5u;
+// pull worlds (Params.pull): a large bcast's header carries kRefMark instead, and its first payload
+// chunk is the reference {byte offset of the sender's relay slot in the sender's part, ~offset, kRefMagic, 0}
+static constexpr uint32_t kRefMark = 0x5Au;
+static constexpr uint32_t kRefMagic = 0x52454631u;  // "REF1": reference chunk = {off, ~off, magic, 0}
 
 __device__ __forceinline__ uint32_t mask_bytes(uint32_t w, int keep) {  // keep the low `keep` bytes
     return keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
@@ -1000,6 +1012,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0;
+            S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
@@ -1146,6 +1159,22 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             peer_failed = __builtin_amdgcn_readfirstlane(errf) != 0;
             PSX(1);
+            // pull worlds: relay slots whose references every child consumed are free again (the
+            // records are in order; out_head_r = the children's consumption counts just polled)
+            uint32_t relay_free = kMaxCand;
+            if (P.pull) {
+                const uint32_t nq = S.rq_n;
+                uint32_t nrel = 0, e = S.rq_h;
+                uint64_t rel = S.relay_rel;
+                for (; nrel < nq; nrel++, e = (e + 1u) % (uint32_t)kRelQ) {
+                    const bool ok = lane >= nout || out_head_r >= S.rq_out[e][lane];
+                    if (__ballot(!ok)) break;
+                    rel = S.rq_relay[e];
+                }
+                if (lane == 0 && nrel) { S.rq_h = e; S.rq_n = nq - nrel; S.relay_rel = rel; }
+                const uint64_t used = S.relay_tail - rel;
+                relay_free = used >= P.fwd_cap ? 0u : P.fwd_cap - (uint32_t)used;
+            }
             // host mode: publish the command head / pickup tail of the previous iteration; the pickup
             // ring bounds this iteration's events: a ring message makes <= 2 (action + decision), plus
             // <= 2 per own proposal in flight (final-judge request, result)
@@ -1263,7 +1292,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // to the long rings, so a rank fed mostly by one hot parent (a wall rank) drains it in big
             // batches instead of 256/nact per iteration (the per-iteration cost hardly depends on the
             // batch size)
-            const uint32_t budget = min(kMaxCand - reserve, hlim);
+            // (pull worlds: every candidate may need a relay slot)
+            const uint32_t budget = min(min(kMaxCand - reserve, hlim), relay_free);
             const uint32_t want = hblock ? 0u : min(ra, win_r);
             uint32_t take = want;
             {
@@ -1406,6 +1436,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if ((P.mode & MODE_HDIAG) && lane == 0 && run == fp) S.hd[1]++;
                     }
                     nh = run;
+                    if (P.pull && nh > (relay_free > C ? relay_free - C : 0u)) nh = relay_free > C ? relay_free - C : 0u;
                     gap_lo = C;
                     hbase = kHostBase + ncp;
                     if ((uint32_t)lane >= ncp && (uint32_t)lane < ncp + nh) {
@@ -1425,6 +1456,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const int64_t rem = sched_n - sched_next;
                     uint32_t ww = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
                     if (ww > kMaxCand - C) ww = kMaxCand - C;
+                    if (P.pull && ww > (relay_free > C ? relay_free - C : 0u)) ww = relay_free > C ? relay_free - C : 0u;
                     if constexpr (BULK) {
                         // per-bcast lengths; a bulk one needs its heap slot back from every receiver
                         // of the previous use (done(me, s)); the window ends before one that does not
@@ -1459,6 +1491,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         lat_ok = S.b.sdone[q & (bsl - 1u)] >= (uint64_t)(q / bsl) * (uint64_t)(P.n - 1);
                     }
                 }
+                if (P.pull && C >= relay_free) lat_ok = false;  // no relay slot for it yet
                 if (lat_ok && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
             }
             // ---- lone-message fast path (wave 0 alone): exactly one candidate, a small ring bcast,
@@ -1732,7 +1765,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 kind = K_RING;
                 const int origin = (int)(w0 & 0xffffu);
                 const uint32_t tag = (w0 >> 16) & 0xffu;
-                if (((w2 >> 16) & 0xffu) != kSlotMark) {
+                const uint32_t mk = (w2 >> 16) & 0xffu;
+                if (mk != kSlotMark && !(P.pull && mk == kRefMark && tag == TAG_BCAST && ((kHdr + (w2 & 0xffffu) + 15u) >> 4) > nsmall)) {
                     // a slot whose bytes were not visible behind its published tail: every header
                     // carries the mark from its origination, so this is a protocol violation -- stop
                     // loudly instead of forwarding zeros (rings are uncached, rlo_world.cpp)
@@ -2095,10 +2129,26 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                              kind == K_HOST ? 1u : 0u);
                 }
             }
+            // pull worlds: a large bcast this rank sends on gets a slot of its relay ring -- the copy its
+            // children load (RelQ records free it once they consumed the references)
+            uint32_t relay = ~0u;
+            if (P.pull) {
+                const bool rl = isbig && an != 0u && tag == TAG_BCAST;
+                const uint64_t bm = __ballot(rl);
+                if (bm) {
+                    uint32_t rb = 0;
+                    if (lane == 0) {
+                        rb = atomicAdd(&S.relay_n, (uint32_t)__popcll(bm));
+                        S.ref_any = 1;
+                    }
+                    rb = rdl32(rb, 0) + (uint32_t)__popcll(bm & lt_mask);
+                    if (rl) relay = t.orig_data + (uint32_t)((S.relay_tail + rb) & fcap_m) * P.fwd_stride;
+                }
+            }
             if (active) {
                 CandL& cl = S.cand[c];
                 cl.w0 = w0; cl.id = id; cl.w2 = w2; cl.t0 = t0;
-                cl.src = src; cl.need = an; cl.logidx = logidx; cl.kind = kind;
+                cl.src = src; cl.need = an; cl.logidx = logidx; cl.kind = kind; cl.relay = relay;
             }
             {  // wave-aggregated counters (one LDS op per wave instead of 64 same-address atomics)
                 const uint64_t bdel = __ballot(admitted && kind == K_RING && tag == TAG_BCAST);
@@ -2168,7 +2218,24 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const uint32_t nch = (kHdr + (cl.w2 & 0xffffu) + 15u) >> 4;
                     uint8_t* dst = stage2 + (b << 10);
                     if (cl.kind == K_RING) {
-                        if (q < nch) dma16(rf, dst, cl.src + 16u * q);
+                        if (P.pull && ((cl.w2 >> 16) & 0xffu) == kRefMark) {
+                            // pulled: the payload from the sender's relay slot (the reference staged as
+                            // chunk 1 in phase D0), the header as classified
+                            const u32x4 ref = *reinterpret_cast<const u32x4*>(STG(cc, 1));
+                            const uint32_t roff = (uint32_t)uni((int)ref.x);
+                            // a reference that is not one (unwritten / torn chunk): stop loudly, load nothing
+                            const bool rok = uni((int)ref.y) == (int)~roff && (uint32_t)uni((int)ref.z) == kRefMagic;
+                            if (!rok && lane == 0) set_error(S, P, ERR_BAD_SLOT, 0x5EF0000u | (q & 0xffffu));
+                            const __amdgpu_buffer_rsrc_t rr =
+                                mk_rsrc(reinterpret_cast<void*>(uni64(t.in_base[cl.group >> 1]) + roff), rok ? nch * 16u : 0u);
+                            if (rok && q < nch && q != 0) {
+                                if (sys) __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * q, 0, 0, kAuxSc1 | 1);
+                                else __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * q, 0, 0, kAuxSc1);
+                            }
+                            if (q == 0) *reinterpret_cast<u32x4*>(dst) = u32x4{cl.w0, cl.id, cl.w2, cl.t0};
+                        } else if (q < nch) {
+                            dma16(rf, dst, cl.src + 16u * q);
+                        }
                     } else if (cl.kind == K_HOST) {  // payload from the command slot, header as classified
                         if (q < nch && q != 0)
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(dst), 16, cl.src + 16u * q, 0, 0, kAuxSc1 | 1);
@@ -2253,11 +2320,25 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const CandL& cl = S.cand[cc];
                         const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
                         const u32x4 v = *reinterpret_cast<const u32x4*>(stage2 + (b << 10) + 16u * lane);
-                        for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
-                            const int oi = __builtin_ctz(a2);
-                            const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
-                            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
-                            if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+                        const uint32_t rly = cl.relay;
+                        if (P.pull && rly != ~0u) {
+                            // pulled on: each child gets header (kRefMark) + reference to my relay copy
+                            const u32x4 hv = q == 0 ? u32x4{v.x, v.y, (v.z & 0xff00ffffu) | (kRefMark << 16), v.w}
+                                                    : u32x4{rly, ~rly, kRefMagic, 0u};
+                            for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
+                                const int oi = __builtin_ctz(a2);
+                                const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
+                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
+                                if (q <= 1u) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, hv, sys);
+                            }
+                            if (q < nch && q != 0) st_ring(rf, rly + 16u * q, v, sys);  // the relay copy
+                        } else {
+                            for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
+                                const int oi = __builtin_ctz(a2);
+                                const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
+                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
+                                if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+                            }
                         }
                         if (q < nch && cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
                             acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})
@@ -2313,6 +2394,24 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             if (lane < nout) {
                 out_tail_r += noi_r;
+                // pull worlds: this iteration's relay slots are released once the children consumed up
+                // to these tails (coalesced into the newest record when all kRelQ are pending)
+                if (P.pull && S.ref_any) {
+                    const uint32_t qn = S.rq_n;
+                    const uint32_t e = (S.rq_h + (qn == (uint32_t)kRelQ ? qn - 1u : qn)) % (uint32_t)kRelQ;
+                    S.rq_out[e][lane] = out_tail_r;
+                }
+            }
+            if (P.pull && lane == 0 && S.ref_any) {
+                const uint32_t qn = S.rq_n;
+                const uint32_t e = (S.rq_h + (qn == (uint32_t)kRelQ ? qn - 1u : qn)) % (uint32_t)kRelQ;
+                S.relay_tail += S.relay_n;
+                S.rq_relay[e] = S.relay_tail;
+                if (qn < (uint32_t)kRelQ) S.rq_n = qn + 1u;
+                S.relay_n = 0;
+                S.ref_any = 0;
+            }
+            if (lane < nout) {
                 // this iteration's stores are drained (see above): publish now, not after the next
                 // poll -- one poll round trip less per hop
                 if (eager && out_tail_r != PUB_OUT) { PUB_OUT = out_tail_r; pub64(OTPTR, out_tail_r, sys); }

@@ -155,6 +155,11 @@ struct Layout {
     uint32_t bslots = 0, bcap = 0;
     std::vector<uint64_t> heap_bytes, bflag_bytes;            // per part
     uint32_t pend_slots = 2;  // proposal pool: pending entries per origin (rlo_device.hpp Params.pend_slots)
+    // pulled payloads (rlo_device.hpp Params.pull): a large bcast crosses an edge as header +
+    // reference, the receiver loads the payload from the sender's relay ring; every rank has one
+    // (cap slots, after the forward rings of its part) holding the large bcasts it sends on
+    bool pull = false;
+    std::vector<uint64_t> orig_off;  // [n] byte offset of rank r's relay ring in its part's region
 };
 
 int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uint32_t ring_slots, uint64_t bulk_max,
@@ -198,6 +203,15 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         rings[L.part_of[e.dst]] += 2;
         vrings[L.part_of[e.src]] += 1;
     }
+    // pulled payloads for slots beyond the small copy path (8 chunks), not in bulk worlds (their ring
+    // messages stay pushed); RLO_PULL=0 / 1 forces it off / on (A/B)
+    {
+        const char* pe = std::getenv("RLO_PULL");
+        L.pull = pe ? std::atoi(pe) != 0 : (L.stride > 8u * 16u && !bulk_max);
+        if (bulk_max) L.pull = false;
+    }
+    if (L.pull)
+        for (int r = 0; r < n; r++) rings[L.part_of[r]] += 1;  // the relay ring
     const uint64_t max_rings = *std::max_element(rings.begin(), rings.end());
     // default depth (tools/sweep.py, profiles/r1s5_sweep64.log): small slots (the 8-wave path,
     // payload <= 112 B) keep the wall ranks' hot rings from refusing: 64 B storm at 256 ranks
@@ -222,6 +236,12 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         L.vote_off[e] = L.vote_bytes[ps];
         L.vote_bytes[ps] += (uint64_t)L.vote_cap * rlo::kVoteSlot;
     }
+    L.orig_off.assign(n, 0);
+    if (L.pull)
+        for (int r = 0; r < n; r++) {
+            L.orig_off[r] = L.fwd_bytes[L.part_of[r]];
+            L.fwd_bytes[L.part_of[r]] += ring_bytes;
+        }
     if (*std::max_element(L.vote_bytes.begin(), L.vote_bytes.end()) > limit) return RLO_E_INVAL;
 
     // control words: per part a header (word 0 = error flag), then per rank an inbox block
@@ -455,6 +475,7 @@ void build_topo(rlo_world* w) {
         t.n_inbox = 2 * t.n_in + t.sll;
         t.outbox_ctrl = L.outbox[r];
         t.n_outbox = 2 * t.sll + t.n_in;
+        t.orig_data = (uint32_t)L.orig_off[r];
     }
     for (size_t e = 0; e < L.E.size(); e++) {
         const Edge& ed = L.E[e];
@@ -475,6 +496,7 @@ void build_topo(rlo_world* w) {
                 t.in_head[ed.k][vc] = (uint64_t)(uintptr_t)(w->pc[ps] + L.outbox[ed.src] + 2 * ed.j + vc);
             }
             t.in_src[ed.k] = ed.src;
+            t.in_base[ed.k] = (uint64_t)(uintptr_t)w->pf[ps];  // the producer's slots (pulled payloads)
             t.vout_ring[ed.k] = (uint64_t)(uintptr_t)(w->pv[ps] + L.vote_off[e]);
             t.vout_tail[ed.k] = (uint64_t)(uintptr_t)(w->pc[ps] + L.inbox[ed.src] + 2 * L.in_edges[ed.src].size() + ed.j);
         }
@@ -843,6 +865,7 @@ static void base_params(rlo_world* w) {
     P.n_local = (uint32_t)w->nl;
     P.ring_cap = w->L.stride - rlo::kHdr;
     P.pend_slots = w->L.pend_slots;
+    P.pull = w->L.pull && w->nsmall >= 2 ? 1u : 0u;  // the reference chunk is staged as chunk 1
     P.own_pool = 1;  // one own proposal per engine (rootless_ops.c:241) unless a program asks for more
     if (w->L.bulk_max) {
         const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);

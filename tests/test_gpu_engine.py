@@ -132,6 +132,22 @@ def test_storm_small_rings_backpressure(rlo):
     assert int(st["stalls"].sum()) > 0
 
 
+@pytest.mark.parametrize("n,ln,slots", [(64, 1000, 16), (37, 3000, 32)])
+def test_storm_pulled_payloads_small_rings(rlo, n, ln, slots):
+    """pull worlds (slots beyond the small copy path): large bcasts cross every edge as header +
+    reference into the sender's relay ring; with 16/32-slot rings (and relay rings) the relay-slot
+    release records and the ring credits are under constant pressure.  Every rank's delivery count and
+    checksum of the payload bytes it loaded equal the oracle's."""
+    with rlo.World(n, max_payload=ln, ring_slots=slots) as w:
+        w.program_storm(6000, ln, seed=13, window=64)
+        w.run()
+        st = w.stats()
+    exp = orc.storm_expected(n, 13, 6000, ln)
+    assert (st["error"] == 0).all()
+    assert np.array_equal(st["bcast_delivered"].astype(np.int64), exp["count"])
+    assert np.array_equal(st["bcast_sum"], exp["sum"])
+
+
 def _iar_device(rlo, n, proposals, judge, mask=None, isp=None):
     with rlo.World(n) as w:
         w.program_iar(proposals, judge=judge, mask=mask, isp=isp, log=True, log_cap=4096)
