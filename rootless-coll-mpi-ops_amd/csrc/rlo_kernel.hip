@@ -151,7 +151,7 @@ struct Shared {
     // pull worlds: my relay ring (slots taken / released), this iteration's allocations, and the release
     // records: relay count rq_relay[e] is released once every out-ring's consumer passed rq_out[e][oi]
     uint64_t relay_tail, relay_rel;
-    uint32_t relay_n, ref_any, rq_n, rq_h;
+    uint32_t relay_n, ref_any, rq_n, rq_h, relay_free;
     uint64_t rq_relay[kRelQ];
     uint64_t rq_out[kRelQ][kMaxOut];
     // counters
@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0;
-            S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0;
+            S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
@@ -1174,6 +1174,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if (lane == 0 && nrel) { S.rq_h = e; S.rq_n = nq - nrel; S.relay_rel = rel; }
                 const uint64_t used = S.relay_tail - rel;
                 relay_free = used >= P.fwd_cap ? 0u : P.fwd_cap - (uint32_t)used;
+                if (lane == 0) S.relay_free = relay_free;
             }
             // host mode: publish the command head / pickup tail of the previous iteration; the pickup
             // ring bounds this iteration's events: a ring message makes <= 2 (action + decision), plus
@@ -1292,8 +1293,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // to the long rings, so a rank fed mostly by one hot parent (a wall rank) drains it in big
             // batches instead of 256/nact per iteration (the per-iteration cost hardly depends on the
             // batch size)
-            // (pull worlds: every candidate may need a relay slot)
-            const uint32_t budget = min(min(kMaxCand - reserve, hlim), relay_free);
+            const uint32_t budget = min(kMaxCand - reserve, hlim);
             const uint32_t want = hblock ? 0u : min(ra, win_r);
             uint32_t take = want;
             {
@@ -1436,7 +1436,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if ((P.mode & MODE_HDIAG) && lane == 0 && run == fp) S.hd[1]++;
                     }
                     nh = run;
-                    if (P.pull && nh > (relay_free > C ? relay_free - C : 0u)) nh = relay_free > C ? relay_free - C : 0u;
                     gap_lo = C;
                     hbase = kHostBase + ncp;
                     if ((uint32_t)lane >= ncp && (uint32_t)lane < ncp + nh) {
@@ -1456,7 +1455,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const int64_t rem = sched_n - sched_next;
                     uint32_t ww = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
                     if (ww > kMaxCand - C) ww = kMaxCand - C;
-                    if (P.pull && ww > (relay_free > C ? relay_free - C : 0u)) ww = relay_free > C ? relay_free - C : 0u;
                     if constexpr (BULK) {
                         // per-bcast lengths; a bulk one needs its heap slot back from every receiver
                         // of the previous use (done(me, s)); the window ends before one that does not
@@ -1491,7 +1489,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         lat_ok = S.b.sdone[q & (bsl - 1u)] >= (uint64_t)(q / bsl) * (uint64_t)(P.n - 1);
                     }
                 }
-                if (P.pull && C >= relay_free) lat_ok = false;  // no relay slot for it yet
                 if (lat_ok && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next) { lat_id = S.lat_own_next; C++; }
             }
             // ---- lone-message fast path (wave 0 alone): exactly one candidate, a small ring bcast,
@@ -2130,19 +2127,21 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
             }
             // pull worlds: a large bcast this rank sends on gets a slot of its relay ring -- the copy its
-            // children load (RelQ records free it once they consumed the references)
+            // children load (RelQ records free it once they consumed the references).  With the relay
+            // ring full it is pushed whole instead, as in small-slot worlds: the relay ring is one
+            // resource shared by every tree through this rank, so waiting for a slot could close a cycle
+            // of waits around the skip ring -- pushing never waits for it
             uint32_t relay = ~0u;
             if (P.pull) {
                 const bool rl = isbig && an != 0u && tag == TAG_BCAST;
                 const uint64_t bm = __ballot(rl);
                 if (bm) {
-                    uint32_t rb = 0;
-                    if (lane == 0) {
-                        rb = atomicAdd(&S.relay_n, (uint32_t)__popcll(bm));
-                        S.ref_any = 1;
-                    }
-                    rb = rdl32(rb, 0) + (uint32_t)__popcll(bm & lt_mask);
-                    if (rl) relay = t.orig_data + (uint32_t)((S.relay_tail + rb) & fcap_m) * P.fwd_stride;
+                    uint32_t rb0 = 0;
+                    if (lane == 0) rb0 = atomicAdd(&S.relay_n, (uint32_t)__popcll(bm));
+                    rb0 = rdl32(rb0, 0);
+                    const uint32_t rb = rb0 + (uint32_t)__popcll(bm & lt_mask), rfree = S.relay_free;
+                    if (rl && rb < rfree) relay = t.orig_data + (uint32_t)((S.relay_tail + rb) & fcap_m) * P.fwd_stride;
+                    if (lane == 0 && rb0 < rfree) S.ref_any = 1;
                 }
             }
             if (active) {
@@ -2232,7 +2231,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 if (sys) __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * q, 0, 0, kAuxSc1 | 1);
                                 else __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * q, 0, 0, kAuxSc1);
                             }
-                            if (q == 0) *reinterpret_cast<u32x4*>(dst) = u32x4{cl.w0, cl.id, cl.w2, cl.t0};
+                            // (the header with the ordinary mark: sent on pushed, if no relay slot is free)
+                            if (q == 0) *reinterpret_cast<u32x4*>(dst) = u32x4{cl.w0, cl.id, (cl.w2 & 0xff00ffffu) | (kSlotMark << 16), cl.t0};
                         } else if (q < nch) {
                             dma16(rf, dst, cl.src + 16u * q);
                         }
@@ -2402,12 +2402,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     S.rq_out[e][lane] = out_tail_r;
                 }
             }
-            if (P.pull && lane == 0 && S.ref_any) {
-                const uint32_t qn = S.rq_n;
-                const uint32_t e = (S.rq_h + (qn == (uint32_t)kRelQ ? qn - 1u : qn)) % (uint32_t)kRelQ;
-                S.relay_tail += S.relay_n;
-                S.rq_relay[e] = S.relay_tail;
-                if (qn < (uint32_t)kRelQ) S.rq_n = qn + 1u;
+            if (P.pull && lane == 0) {
+                if (S.ref_any) {
+                    const uint32_t qn = S.rq_n;
+                    const uint32_t e = (S.rq_h + (qn == (uint32_t)kRelQ ? qn - 1u : qn)) % (uint32_t)kRelQ;
+                    S.relay_tail += min(S.relay_n, S.relay_free);  // the requests beyond the free slots were pushed
+                    S.rq_relay[e] = S.relay_tail;
+                    if (qn < (uint32_t)kRelQ) S.rq_n = qn + 1u;
+                }
                 S.relay_n = 0;
                 S.ref_any = 0;
             }
