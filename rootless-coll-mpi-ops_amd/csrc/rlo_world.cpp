@@ -203,12 +203,12 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         rings[L.part_of[e.dst]] += 2;
         vrings[L.part_of[e.src]] += 1;
     }
-    // pulled payloads for slots beyond the small copy path (8 chunks), not in bulk worlds (their ring
-    // messages stay pushed); RLO_PULL=0 / 1 forces it off / on (A/B)
+    // pulled payloads (RLO_PULL=1, slots beyond the small copy path, not in bulk worlds): measured no
+    // faster than pushing (256 B -9 %, 4 KiB +3 %, profiles/r2s2_pull_waves_ab.txt: the large-message
+    // path is bound by its staging rounds, not by the wall ranks' store volume), so opt-in
     {
         const char* pe = std::getenv("RLO_PULL");
-        L.pull = pe ? std::atoi(pe) != 0 : (L.stride > 8u * 16u && !bulk_max);
-        if (bulk_max) L.pull = false;
+        L.pull = pe && std::atoi(pe) != 0 && L.stride > 8u * 16u && !bulk_max;
     }
     if (L.pull)
         for (int r = 0; r < n; r++) rings[L.part_of[r]] += 1;  // the relay ring

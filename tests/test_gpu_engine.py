@@ -137,11 +137,21 @@ def test_storm_pulled_payloads_small_rings(rlo, n, ln, slots):
     """pull worlds (slots beyond the small copy path): large bcasts cross every edge as header +
     reference into the sender's relay ring; with 16/32-slot rings (and relay rings) the relay-slot
     release records and the ring credits are under constant pressure.  Every rank's delivery count and
-    checksum of the payload bytes it loaded equal the oracle's."""
-    with rlo.World(n, max_payload=ln, ring_slots=slots) as w:
-        w.program_storm(6000, ln, seed=13, window=64)
+    checksum of the payload bytes it loaded equal the oracle's (RLO_PULL=1: opt-in, read at creation)."""
+    import os
+
+    os.environ["RLO_PULL"] = "1"
+    try:
+        w = rlo.World(n, max_payload=ln, ring_slots=slots)
+    finally:
+        del os.environ["RLO_PULL"]
+    with w:
+        w.program_storm(6000, ln, seed=13, window=64, log=True, log_cap=6008)
         w.run()
         st = w.stats()
+        rows, payload = w.log(5, cap=6008, payload=True)
+    for row in rows:  # rank 5's delivered bytes, exactly
+        assert bytes(payload[row[8]][:ln]) == orc.payload(row[2], row[4], ln)
     exp = orc.storm_expected(n, 13, 6000, ln)
     assert (st["error"] == 0).all()
     assert np.array_equal(st["bcast_delivered"].astype(np.int64), exp["count"])

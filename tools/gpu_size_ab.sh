@@ -1,0 +1,25 @@
+# A/B sweep of the payload-size storms (256 ranks, 65,536 bcasts): pulled payloads x waves x ring slots
+set -o pipefail
+run() {  # env... -- len
+  env "$@" timeout -k 10 120 python3 - <<'PY' || exit 1
+import sys, os
+sys.path.insert(0, "rootless-coll-mpi-ops_amd"); sys.path.insert(0, "oracle")
+import rlo, pyoracle as orc, numpy as np
+L = int(os.environ["LEN"]); n, k = 256, 1 << 16
+with rlo.World(n, max_payload=max(64, L), ring_slots=int(os.environ.get("SLOTS", "0"))) as w:
+    w.program_storm(k, L, seed=0x5EED)
+    w.run(); w.run()
+    ms = w.kernel_ms(); st = w.stats(); wv = w.info["waves"]
+exp = orc.storm_expected(n, 0x5EED, k, L)
+ok = bool((st["error"] == 0).all() and np.array_equal(st["bcast_sum"], exp["sum"]))
+alg = 2 * (n - 1) * (L + 16) * k / (ms * 1e-3) / 1e9
+print("len=%d pull=%s waves=%d slots=%s kernel_ms=%.3f bcast/s=%.0f frac=%.4f ok=%s" % (L, os.environ.get("RLO_PULL", "-"), wv, os.environ.get("SLOTS", "0"), ms, k / (ms * 1e-3), alg / 8000, ok), flush=True)
+PY
+}
+for L in 256 4096; do
+  run LEN=$L RLO_PULL=0
+  run LEN=$L RLO_PULL=1
+  run LEN=$L RLO_PULL=0 RLO_WAVES=8
+  run LEN=$L RLO_PULL=1 RLO_WAVES=8
+  run LEN=$L RLO_PULL=1 SLOTS=1024
+done
