@@ -249,7 +249,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return ((uint64_t)(uint32_t)uni((int)(v >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)v);
 }
 
-// i / d for the small d = nsmall (<= 8) and i < 2^16: multiply-high by ceil(2^32 / d)
+// i / d for the small d = nsmall (<= 24) and i < 2^16: multiply-high by ceil(2^32 / d)
 __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { return magic ? __umulhi(i, magic) : i; }
 
 // MODE_PROF: thread 0 charges the shader cycles since the last stamp to phase `ph`
@@ -1676,22 +1676,26 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         S.cand[cc].group = (uint32_t)g;
                     }
                 }
-                // item i = (candidate i / nsmall, chunk i % nsmall); nsmall <= 8, so <= 8 loads per lane
+                // item i = (candidate i / nsmall, chunk i % nsmall), in batches of 8 loads per lane: one
+                // round trip when nsmall <= 8, ceil(nsmall / 8) for the medium slots (<= 24 chunks) that
+                // take the small copy path too
                 const uint32_t nit = (c_hi - c_lo) * nsmall;
-                u32x4 sv[8];
+                for (uint32_t i0 = 0; i0 < nit; i0 += 512u) {
+                    u32x4 sv[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    if ((uint32_t)u * 64u < nit) {  // uniform: every lane takes part in the shuffle
-                        const uint32_t i = (uint32_t)u * 64u + (uint32_t)lane;
-                        const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
-                        const uint32_t so = (uint32_t)__shfl((int)src, (int)(mi & 63u));
-                        if (i < nit) sv[u] = ld_sc1(rf, so + 16u * q);
+                    for (int u = 0; u < 8; u++) {
+                        if (i0 + (uint32_t)u * 64u < nit) {  // uniform: every lane takes part in the shuffle
+                            const uint32_t i = i0 + (uint32_t)u * 64u + (uint32_t)lane;
+                            const uint32_t mi = div_small(i, nmagic), q = i - mi * nsmall;
+                            const uint32_t so = (uint32_t)__shfl((int)src, (int)(mi & 63u));
+                            if (i < nit) sv[u] = ld_sc1(rf, so + 16u * q);
+                        }
                     }
-                }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const uint32_t i = (uint32_t)u * 64u + (uint32_t)lane;
-                    if (i < nit) *reinterpret_cast<u32x4*>(STG(c_lo, 0) + (i << 4)) = sv[u];
+                    for (int u = 0; u < 8; u++) {
+                        const uint32_t i = i0 + (uint32_t)u * 64u + (uint32_t)lane;
+                        if (i < nit) *reinterpret_cast<u32x4*>(STG(c_lo, 0) + (i << 4)) = sv[u];
+                    }
                 }
             }
             VM_DRAIN();  // wave 1: its vote loads
@@ -1978,7 +1982,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint64_t b = __ballot(bit);
                 if (bit) {
                     const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
-                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 9)));  // c < 512: 9 bits
+                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 9)));  // c < 512: 9 bits; nch <= 63: 6 bits
                     if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
                 }
             }
@@ -2288,8 +2292,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (qb >= nq) { qb -= nq; rb++; }
                     const uint32_t ea = OL(oi, r);
                     const uint32_t eb = i + 64u < b ? (uint32_t)OL(oi, rb) : (uint32_t)kBigFlag;
-                    const bool va = !(ea & kBigFlag) && q < ((ea >> 9) & 0xfu);
-                    const bool vb = !(eb & kBigFlag) && qb < ((eb >> 9) & 0xfu);
+                    const bool va = !(ea & kBigFlag) && q < ((ea >> 9) & 0x3fu);
+                    const bool vb = !(eb & kBigFlag) && qb < ((eb >> 9) & 0x3fu);
                     u32x4 xa = {0u, 0u, 0u, 0u}, xb = {0u, 0u, 0u, 0u};
                     if (va) xa = *reinterpret_cast<const u32x4*>(stage + __umul24(ea & 0x1ffu, stg_msg) + (q << 4));
                     if (vb) xb = *reinterpret_cast<const u32x4*>(stage + __umul24(eb & 0x1ffu, stg_msg) + (qb << 4));

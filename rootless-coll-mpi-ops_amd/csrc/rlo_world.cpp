@@ -406,7 +406,7 @@ JobMem job_mem(uint32_t J, uint32_t nl) {
 }
 
 // co-residency of the part's workgroups (rank-workgroups, plus the mover workgroups of a bulk
-// world): largest small-path stage (nsmall chunks per message, <= 8) and then the largest stage2
+// world): largest small-path stage (nsmall chunks per message, <= 24) and then the largest stage2
 // (<= 64 KiB) at which the occupancy calculator (LDS allocation granularity, registers, waves)
 // still co-schedules them
 int size_lds_variant(rlo_world* w, int variant) {
@@ -420,7 +420,11 @@ int size_lds_variant(rlo_world* w, int variant) {
     const size_t bpend = variant == 5 ? (size_t)L.n * L.bslots * 32 : 0;  // pending bulk receptions
     int api = 0;
     bool ok = false;
-    for (uint32_t ns = std::min<uint32_t>(8u, L.stride / 16u); ns >= 1 && !ok; ns--) {
+    // every message of a medium slot (<= 24 chunks: payload <= 368 B) takes the small copy path when the
+    // stage fits (packed (message, chunk) copies; the large-message path moves one message per 1-KiB
+    // block: 256 B storm 2.0M bcast/s, profiles/r2s2_diag_sizes.log); larger slots stage 8 chunks
+    const uint32_t ns0 = L.stride / 16u <= 24u ? L.stride / 16u : 8u;
+    for (uint32_t ns = ns0; ns >= 1 && !ok; ns--) {
         // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
         const size_t fixed = stat + (size_t)16 * L.n * L.pend_slots + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
         if (per_block < fixed + 1024 + 512) continue;

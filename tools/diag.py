@@ -42,8 +42,11 @@ def report(name, w, ms, deliveries):
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=256)
 ap.add_argument("--k", type=int, default=1 << 18)
+ap.add_argument("--lens", default="64,4096", help="storm payload sizes")
+ap.add_argument("--storm-only", action="store_true")
 args = ap.parse_args()
-for ln, win in ((64, 64), (4096, 32)):
+for ln in [int(x) for x in args.lens.split(",")]:
+    win = 64 if ln <= 1024 else 32
     w = rlo.World(args.n, max_payload=max(64, ln))
     k = args.k if ln <= 1024 else args.k // 8
     w.program_storm(k, ln, window=win)
@@ -52,6 +55,8 @@ for ln, win in ((64, 64), (4096, 32)):
     ms = w.run()
     report("storm len=%d win=%d (%.0f/s)" % (ln, win, k / ms0 * 1e3), w, ms, k * (args.n - 1))
     w.close()
+if args.storm_only:
+    sys.exit(0)
 w = rlo.World(args.n)
 p = 32
 props = [(r, it * args.n + r, b"0123456789abcdef") for it in range(p) for r in range(args.n)]
