@@ -43,7 +43,7 @@ static constexpr uint32_t kGolden32 = 0x9E3779B9u;
 static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
 static constexpr uint32_t kIdleSpin = 256;  // tight re-polls after an idle iteration (~0.1 ms at most)
-static constexpr int kRelQ = 4;  // pull worlds: relay-ring release records (coalesced when full)
+static constexpr int kRelQ = 16;  // pull worlds: relay-ring release records (coalesced when full)
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -1173,7 +1173,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
                 if (lane == 0 && nrel) { S.rq_h = e; S.rq_n = nq - nrel; S.relay_rel = rel; }
                 const uint64_t used = S.relay_tail - rel;
-                relay_free = used >= P.fwd_cap ? 0u : P.fwd_cap - (uint32_t)used;
+                relay_free = used >= P.relay_cap ? 0u : P.relay_cap - (uint32_t)used;
                 if (lane == 0) S.relay_free = relay_free;
             }
             // host mode: publish the command head / pickup tail of the previous iteration; the pickup
@@ -2144,8 +2144,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (lane == 0) rb0 = atomicAdd(&S.relay_n, (uint32_t)__popcll(bm));
                     rb0 = rdl32(rb0, 0);
                     const uint32_t rb = rb0 + (uint32_t)__popcll(bm & lt_mask), rfree = S.relay_free;
-                    if (rl && rb < rfree) relay = t.orig_data + (uint32_t)((S.relay_tail + rb) & fcap_m) * P.fwd_stride;
+                    if (rl && rb < rfree) relay = t.orig_data + (uint32_t)((S.relay_tail + rb) & (P.relay_cap - 1u)) * P.fwd_stride;
                     if (lane == 0 && rb0 < rfree) S.ref_any = 1;
+                    if ((P.mode & MODE_PROF) && lane == 0 && rb0 + (uint32_t)__popcll(bm) > rfree)  // pushed: relay full
+                        atomicAdd((unsigned long long*)&S.dbg[4], (unsigned long long)(rb0 + (uint32_t)__popcll(bm) - max(rb0, rfree)));
                 }
             }
             if (active) {

@@ -159,6 +159,7 @@ struct Layout {
     // reference, the receiver loads the payload from the sender's relay ring; every rank has one
     // (cap slots, after the forward rings of its part) holding the large bcasts it sends on
     bool pull = false;
+    uint32_t relay_cap = 0;
     std::vector<uint64_t> orig_off;  // [n] byte offset of rank r's relay ring in its part's region
 };
 
@@ -237,11 +238,23 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         L.vote_bytes[ps] += (uint64_t)L.vote_cap * rlo::kVoteSlot;
     }
     L.orig_off.assign(n, 0);
-    if (L.pull)
+    if (L.pull) {
+        // relay rings: 4x the ring depth where the part's region stays one buffer resource (a relay slot
+        // is released only once every child consumed it, which lags the ring credits)
+        L.relay_cap = cap;
+        for (uint32_t f = 4; f > 1; f /= 2) {
+            bool fits = true;
+            for (int p = 0; p < nparts; p++) {
+                const uint64_t nlp = (uint64_t)(L.pb[p + 1] - L.pb[p]);
+                fits &= L.fwd_bytes[p] + nlp * f * ring_bytes <= limit;
+            }
+            if (fits) { L.relay_cap = f * cap; break; }
+        }
         for (int r = 0; r < n; r++) {
             L.orig_off[r] = L.fwd_bytes[L.part_of[r]];
-            L.fwd_bytes[L.part_of[r]] += ring_bytes;
+            L.fwd_bytes[L.part_of[r]] += (uint64_t)L.relay_cap * L.stride;
         }
+    }
     if (*std::max_element(L.vote_bytes.begin(), L.vote_bytes.end()) > limit) return RLO_E_INVAL;
 
     // control words: per part a header (word 0 = error flag), then per rank an inbox block
@@ -870,6 +883,7 @@ static void base_params(rlo_world* w) {
     P.ring_cap = w->L.stride - rlo::kHdr;
     P.pend_slots = w->L.pend_slots;
     P.pull = w->L.pull && w->nsmall >= 2 ? 1u : 0u;  // the reference chunk is staged as chunk 1
+    P.relay_cap = w->L.relay_cap;
     P.own_pool = 1;  // one own proposal per engine (rootless_ops.c:241) unless a program asks for more
     if (w->L.bulk_max) {
         const JobMem m = job_mem(w->jslots, (uint32_t)w->nl);
