@@ -166,8 +166,10 @@ def size_legs(rlo, R, device, stream, sizes=(256, 1024, 4096), k=1 << 16, steps=
     import numpy as np
 
     out = []
-    with rlo.World(R, max_payload=max(sizes), device=device) as w:
-        for s in sizes:
+    for s in sizes:
+        # the slot is the workload's payload size, as an application sizes its engine (slots of <= 24
+        # chunks take the small copy path, larger ones the large-message path)
+        with rlo.World(R, max_payload=s, device=device) as w:
             w.program_storm(k, s, seed=0x5EED)
             sums, kms, ok = [], [], True
             t0 = 0.0
@@ -675,6 +677,23 @@ def main():
             line["roofline"]["traffic_error"] = why
     if api_leg is not None:
         line["dropin_api"] = api_leg
+        # C4 at the reference's own world sizes: the device engine (one GPU) beside
+        # the compiled reference under host MPI on the box's cores, same N
+        sw = line.get("small_worlds") or {}
+        c4 = {}
+        for key, rec in sw.items():
+            ref = ((api_leg.get(key) or {}).get("reference_host_mpi") or {})
+            r_lat, r_dec = (ref.get("lat") or {}).get("p50_us"), (ref.get("iar") or {}).get("decisions_per_s")
+            c4[key] = {"device_p50_us": rec.get("p50_us"), "reference_p50_us": r_lat,
+                       "device_decisions_per_s": rec.get("decisions_per_s"),
+                       "device_pool16_decisions_per_s": rec.get("pool16_decisions_per_s"),
+                       "reference_decisions_per_s": r_dec}
+            if r_dec:
+                c4[key]["decisions_x_reference"] = round(rec["decisions_per_s"] / r_dec, 2)
+                if rec.get("pool16_decisions_per_s"):
+                    c4[key]["pool16_decisions_x_reference"] = round(rec["pool16_decisions_per_s"] / r_dec, 2)
+        if c4:
+            line["c4_vs_reference"] = c4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         note("cpu baseline")
         line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds)

@@ -931,6 +931,9 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
 
 template <int W, bool BULK>
 __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
+    // pulled payloads (Params.pull) exist only in the 4-wave kernel without bulk messages (slots beyond
+    // the small copy path); compiled out of the others
+#define PULL_ON (W == 4 && !BULK && P.pull != 0u)
     constexpr int kWaves = W, kBlock = 64 * W, kMaxCand = 64 * W;
     constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at the last 64 candidates
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
@@ -1162,7 +1165,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // pull worlds: relay slots whose references every child consumed are free again (the
             // records are in order; out_head_r = the children's consumption counts just polled)
             uint32_t relay_free = kMaxCand;
-            if (P.pull) {
+            if (PULL_ON) {
                 const uint32_t nq = S.rq_n;
                 uint32_t nrel = 0, e = S.rq_h;
                 uint64_t rel = S.relay_rel;
@@ -1680,7 +1683,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // round trip when nsmall <= 8, ceil(nsmall / 8) for the medium slots (<= 24 chunks) that
                 // take the small copy path too
                 const uint32_t nit = (c_hi - c_lo) * nsmall;
-                for (uint32_t i0 = 0; i0 < nit; i0 += 512u) {
+                // (8 waves: slots <= 8 chunks, one batch -- the loop is compiled out)
+                for (uint32_t i0 = 0; i0 < (W == 8 ? 1u : nit); i0 += 512u) {
                     u32x4 sv[8];
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
@@ -1767,7 +1771,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const int origin = (int)(w0 & 0xffffu);
                 const uint32_t tag = (w0 >> 16) & 0xffu;
                 const uint32_t mk = (w2 >> 16) & 0xffu;
-                if (mk != kSlotMark && !(P.pull && mk == kRefMark && tag == TAG_BCAST && ((kHdr + (w2 & 0xffffu) + 15u) >> 4) > nsmall)) {
+                if (mk != kSlotMark && !(PULL_ON && mk == kRefMark && tag == TAG_BCAST && ((kHdr + (w2 & 0xffffu) + 15u) >> 4) > nsmall)) {
                     // a slot whose bytes were not visible behind its published tail: every header
                     // carries the mark from its origination, so this is a protocol violation -- stop
                     // loudly instead of forwarding zeros (rings are uncached, rlo_world.cpp)
@@ -2136,7 +2140,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // resource shared by every tree through this rank, so waiting for a slot could close a cycle
             // of waits around the skip ring -- pushing never waits for it
             uint32_t relay = ~0u;
-            if (P.pull) {
+            if (PULL_ON) {
                 const bool rl = isbig && an != 0u && tag == TAG_BCAST;
                 const uint64_t bm = __ballot(rl);
                 if (bm) {
@@ -2223,7 +2227,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const uint32_t nch = (kHdr + (cl.w2 & 0xffffu) + 15u) >> 4;
                     uint8_t* dst = stage2 + (b << 10);
                     if (cl.kind == K_RING) {
-                        if (P.pull && ((cl.w2 >> 16) & 0xffu) == kRefMark) {
+                        if (PULL_ON && ((cl.w2 >> 16) & 0xffu) == kRefMark) {
                             // pulled: the payload from the sender's relay slot (the reference staged as
                             // chunk 1 in phase D0), the header as classified
                             const u32x4 ref = *reinterpret_cast<const u32x4*>(STG(cc, 1));
@@ -2327,7 +2331,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
                         const u32x4 v = *reinterpret_cast<const u32x4*>(stage2 + (b << 10) + 16u * lane);
                         const uint32_t rly = cl.relay;
-                        if (P.pull && rly != ~0u) {
+                        if (PULL_ON && rly != ~0u) {
                             // pulled on: each child gets header (kRefMark) + reference to my relay copy
                             const u32x4 hv = q == 0 ? u32x4{v.x, v.y, (v.z & 0xff00ffffu) | (kRefMark << 16), v.w}
                                                     : u32x4{rly, ~rly, kRefMagic, 0u};
@@ -2402,13 +2406,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 out_tail_r += noi_r;
                 // pull worlds: this iteration's relay slots are released once the children consumed up
                 // to these tails (coalesced into the newest record when all kRelQ are pending)
-                if (P.pull && S.ref_any) {
+                if (PULL_ON && S.ref_any) {
                     const uint32_t qn = S.rq_n;
                     const uint32_t e = (S.rq_h + (qn == (uint32_t)kRelQ ? qn - 1u : qn)) % (uint32_t)kRelQ;
                     S.rq_out[e][lane] = out_tail_r;
                 }
             }
-            if (P.pull && lane == 0) {
+            if (PULL_ON && lane == 0) {
                 if (S.ref_any) {
                     const uint32_t qn = S.rq_n;
                     const uint32_t e = (S.rq_h + (qn == (uint32_t)kRelQ ? qn - 1u : qn)) % (uint32_t)kRelQ;

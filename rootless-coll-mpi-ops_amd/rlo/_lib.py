@@ -8,7 +8,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
+LIB_PATH = os.environ.get("RLO_LIB_AB") or os.path.join(PKG_DIR, "lib", "librlo_hip.so")  # RLO_LIB_AB: A/B builds only
 
 RLO_OK = 0
 RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6

@@ -13,13 +13,17 @@ with rlo.World(n, max_payload=max(64, L), ring_slots=int(os.environ.get("SLOTS",
 exp = orc.storm_expected(n, 0x5EED, k, L)
 ok = bool((st["error"] == 0).all() and np.array_equal(st["bcast_sum"], exp["sum"]))
 alg = 2 * (n - 1) * (L + 16) * k / (ms * 1e-3) / 1e9
-print("len=%d pull=%s waves=%d slots=%s kernel_ms=%.3f bcast/s=%.0f frac=%.4f ok=%s" % (L, os.environ.get("RLO_PULL", "-"), wv, os.environ.get("SLOTS", "0"), ms, k / (ms * 1e-3), alg / 8000, ok), flush=True)
+print("len=%d cached=%s pull=%s waves=%d slots=%s kernel_ms=%.3f bcast/s=%.0f frac=%.4f ok=%s" % (L, os.environ.get("RLO_CACHED_RINGS", "-"), os.environ.get("RLO_PULL", "-"), wv, os.environ.get("SLOTS", "0"), ms, k / (ms * 1e-3), alg / 8000, ok), flush=True)
 PY
 }
-for L in 256 4096; do
-  run LEN=$L RLO_PULL=0
-  run LEN=$L RLO_PULL=1
-  run LEN=$L RLO_PULL=0 RLO_WAVES=8
-  run LEN=$L RLO_PULL=1 RLO_WAVES=8
-  run LEN=$L RLO_PULL=1 SLOTS=1024
+# VARIANTS: one environment assignment list per line
+VARIANTS=${VARIANTS:-"RLO_PULL=0
+RLO_PULL=1
+RLO_PULL=0 RLO_WAVES=8
+RLO_PULL=1 RLO_WAVES=8
+RLO_PULL=1 SLOTS=1024"}
+for L in ${LENS:-256 4096}; do
+  while read -r v; do
+    [ -n "$v" ] && { run LEN=$L $v || exit 1; }
+  done <<< "$VARIANTS"
 done
