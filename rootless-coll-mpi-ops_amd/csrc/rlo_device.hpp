@@ -202,7 +202,7 @@ struct Params {
     // dynamic LDS carve-out: [pend: N x pend_slots x 16 B][olist: nout_max x 256 x 2 B]
     //                        [stage: 256 x nsmall x 16 B][stage2: stage2_bytes]
     uint32_t nsmall;              // slot chunks staged per message on the small path (<= 24)
-    uint32_t stage2_bytes;        // LDS staging for large messages (multiple of 1 KiB, >= 1 KiB)
+    uint32_t stage2_bytes;        // LDS staging for large messages (multiple of 1 KiB, 1 KiB .. 128 KiB)
     uint32_t nout_max;            // 2 x max send_list_len over the ranks of this launch
     // host-service mode (MODE_HOST): all in pinned host memory.  Pickup records / payloads use
     // log / log_payload above as per-rank rings of log_cap slots.

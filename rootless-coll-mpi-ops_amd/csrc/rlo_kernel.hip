@@ -126,7 +126,8 @@ struct Shared {
     uint16_t pos[kMaxCand][kMaxFanout];  // large messages: slot in out-ring (j, vc) relative to tail0
     uint16_t big[kMaxCand];              // admitted messages too large for the stage path
     uint32_t nbig, bm, bq0, nblk;
-    uint32_t blk_c[64], blk_q0[64];      // large-message blocks staged in stage2
+    uint32_t blk_c[128], blk_q0[128];    // large-message blocks staged in stage2 (two halves when pipelined)
+    uint32_t nblk2[2];                   // blocks planned into each half
     // vote rings towards my parents (LDS atomics from every wave)
     uint64_t vout_tail[kMaxIn], vout_head[kMaxIn];
     // wave 0: last published counter per lane (in-ring heads, out-ring tails, vote-in heads, vote-out
@@ -2186,10 +2187,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
             // ---------------- G1: stage the first group of large messages (before any store)
             const uint32_t nbig = S.nbig;
-            auto plan_big = [&]() {  // wave 0: next (message, 64-chunk block) pairs for stage2, lane-parallel
+            // stage2 in two halves of hb blocks: round r+1's loads are in flight while round r is stored
+            // (one wait covers both), instead of load -> store -> wait for the stores -> load
+            const bool pipe = s2_blocks >= 2u;
+            const uint32_t hb = pipe ? min(s2_blocks / 2u, 64u) : min(s2_blocks, 64u);
+            auto plan_big = [&](uint32_t h) {  // wave 0: next (message, 64-chunk block) pairs for half h, lane-parallel
                 if (w == 0) {
                     const uint32_t bm = S.bm, bq0 = S.bq0;
-                    const uint32_t lim = min(s2_blocks, 64u);
+                    const uint32_t lim = hb, hoff = h * hb;
                     const uint32_t mi = bm + (uint32_t)lane;
                     uint32_t nb = 0, cc = 0, q0 = 0;
                     if (mi < nbig) {
@@ -2201,8 +2206,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     uint32_t tot;
                     const uint32_t st = wave_excl_scan(nb, &tot);
                     for (uint32_t k = 0; k < nb && st + k < lim; k++) {
-                        S.blk_c[st + k] = cc;
-                        S.blk_q0[st + k] = q0 + 64u * k;
+                        S.blk_c[hoff + st + k] = cc;
+                        S.blk_q0[hoff + st + k] = q0 + 64u * k;
                     }
                     const uint64_t cut = __ballot(nb != 0 && st + nb > lim);  // the first cut message is the cursor
                     uint32_t nbm, nbq0, nblk;
@@ -2216,12 +2221,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         nbq0 = 0;
                         nblk = tot;
                     }
-                    if (lane == 0) { S.bm = nbm; S.bq0 = nbq0; S.nblk = nblk; }
+                    if (lane == 0) { S.bm = nbm; S.bq0 = nbq0; S.nblk2[h] = nblk; }
                 }
             };
-            auto stage_big = [&]() {  // wave w stages (and later stores) blocks b = w, w + 4, ...
-                const uint32_t nblk = S.nblk;
-                for (uint32_t b = (uint32_t)w; b < nblk; b += kWaves) {
+            // wave w issues the loads of (and later stores) the blocks b = w, w + 4, ... of half h; the
+            // caller waits (VM_DRAIN) before they are read
+            auto issue_big = [&](uint32_t h) {
+                const uint32_t nblk = S.nblk2[h];
+                for (uint32_t b0 = (uint32_t)w; b0 < nblk; b0 += kWaves) {
+                    const uint32_t b = h * hb + b0;
                     const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
                     const CandL& cl = S.cand[cc];
                     const uint32_t nch = (kHdr + (cl.w2 & 0xffffu) + 15u) >> 4;
@@ -2256,18 +2264,18 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                    : gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), q);
                     }
                 }
-                VM_DRAIN();
-                // agent acquire (without the leading vmcnt(0) of the fence builtin: drained above):
-                // these LDS-DMA loads may leave lines in L1 that straddle into the next, maybe
-                // unwritten, slot, and the next iteration must not read them from there.  It completes
-                // under the stores, and phase A's VM_DRAIN (or the eager drain) waits for it
-                ACQ_NEXT();
             };
+            // agent acquire after a drain (without the leading vmcnt(0) of the fence builtin): these
+            // LDS-DMA loads may leave lines in L1 that straddle into the next, maybe unwritten, slot, and
+            // the next iteration must not read them from there.  It completes under the stores, and
+            // phase A's VM_DRAIN (or the eager drain) waits for it
             if (nbig) {
                 if (tid == 0) { S.bm = 0; S.bq0 = 0; }
-                plan_big();
+                plan_big(0u);
                 BAR();
-                stage_big();
+                issue_big(0u);
+                VM_DRAIN();
+                ACQ_NEXT();
             }
 
             // ---------------- G2: small messages.  Out-ring oi (oi = w, w + 4, ...) receives its
@@ -2323,9 +2331,18 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
             // ---------------- G3: large messages, 64 x 16 B per wave store instruction
             if (nbig) {
+                uint32_t cur = 0;  // the half staged for this round
                 for (;;) {
-                    const uint32_t nblk = S.nblk;
-                    for (uint32_t b = (uint32_t)w; b < nblk; b += kWaves) {
+                    const bool more = S.bm < nbig;  // uniform: S.bm was last written before a barrier
+                    if (more && pipe) {
+                        BAR();  // every wave is done with the other half's blocks (stage2 and blk_*)
+                        plan_big(cur ^ 1u);
+                        BAR();
+                        issue_big(cur ^ 1u);  // in flight while this round's half is stored
+                    }
+                    const uint32_t nblk = S.nblk2[cur];
+                    for (uint32_t b0 = (uint32_t)w; b0 < nblk; b0 += kWaves) {
+                        const uint32_t b = cur * hb + b0;
                         const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
                         const CandL& cl = S.cand[cc];
                         const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
@@ -2357,11 +2374,17 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 st_sys16(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride + 16u * (q - 1), v);
                         }
                     }
-                    if (S.bm >= nbig) break;  // S.bm is rewritten only after the next barrier
-                    BAR();                    // every wave is done with stage2 and blk_*
-                    plan_big();
-                    BAR();
-                    stage_big();  // loads behind this iteration's stores drain in order (only when > stage2)
+                    if (!more) break;
+                    if (pipe) {
+                        cur ^= 1u;
+                    } else {  // one stage2 block: load -> store -> wait, round by round
+                        BAR();
+                        plan_big(cur);
+                        BAR();
+                        issue_big(cur);
+                    }
+                    VM_DRAIN();  // the next half's loads (and this round's stores: vmcnt is in order)
+                    ACQ_NEXT();
                 }
             }
             if (lat_deliv) {  // latency program: the last of N-1 pickups completes the round

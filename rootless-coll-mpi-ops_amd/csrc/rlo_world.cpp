@@ -441,7 +441,7 @@ int size_lds_variant(rlo_world* w, int variant) {
         // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
         const size_t fixed = stat + (size_t)16 * L.n * L.pend_slots + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
         if (per_block < fixed + 1024 + 512) continue;
-        size_t s2 = std::min<size_t>(64 * 1024, (per_block - fixed - 512) & ~(size_t)1023);
+        size_t s2 = std::min<size_t>(128 * 1024, (per_block - fixed - 512) & ~(size_t)1023);  // two halves of <= 64 blocks
         for (;;) {
             w->dyn_lds = fixed - stat + s2;
             if (rlo_occupancy(&api, w->dyn_lds, variant) != hipSuccess) api = 0;
