@@ -240,3 +240,31 @@ def test_shared_service_client_protocol_without_gpu():
     finally:
         m.close()
         os.unlink("/dev/shm" + name)
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """every rlo_hip.h struct the Python mirror declares has the C compiler's size and field offsets
+    (a field added on one side only would make the library read past the caller's struct)"""
+    import subprocess
+
+    from rlo import _lib as L
+
+    pairs = {"rlo_world_cfg_t": L.WorldCfg, "rlo_world_info_t": L.WorldInfo, "rlo_part_cfg_t": L.PartCfg,
+             "rlo_storm_cfg_t": L.StormCfg, "rlo_iar_cfg_t": L.IarCfg, "rlo_host_cfg_t": L.HostCfg,
+             "rlo_cmd_t": L.Cmd, "rlo_log_rec_t": L.LogRec}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rlo_hip.h"', 'int main(void) {']
+    for cname, py in pairs.items():
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for fname, _ in py._fields_:
+            cf = {"from_": "from"}.get(fname, fname)
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, fname, cname, cf))
+    lines += ['return 0;', '}']
+    src = tmp_path / "sizes.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", "-I", INCLUDE, str(src), "-o", str(exe)], check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines())
+    for cname, py in pairs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got["%s.%s" % (cname, fname)]) == getattr(py, fname).offset, (cname, fname)
