@@ -2329,8 +2329,18 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
             }
 
-            // ---------------- G3: large messages, 64 x 16 B per wave store instruction
+            // ---------------- G3: large messages, 64 x 16 B per wave store instruction.  The out-rings'
+            // bases and start tails lane-distributed (lane oi), a message's slot positions read with one
+            // LDS load per block (lane j): the per-(block, out-ring) work is register-only -- it was a
+            // chain of dependent LDS loads, ~400 cycles per out-ring per block with one wave per SIMD
             if (nbig) {
+                // (4 waves: the large-slot kernel; the 8-wave kernel, where large messages are rare, keeps
+                // the LDS reads -- it has no registers to spare)
+                constexpr bool kRegs = W == 4;
+                const uint32_t ot0_r = kRegs && lane < nout ? (uint32_t)S.out_tail0[lane] : 0u;  // mod fwd_cap (pow2)
+                const uint64_t oring_r = kRegs && lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;
+#define G3_SLOT(oi) (kRegs ? rdl32(ot0_r, oi) + rdl32(posr, (oi) >> 1) : (uint32_t)S.out_tail0[oi] + S.pos[cc][(oi) >> 1])
+#define G3_RING(oi) (kRegs ? rdl64(oring_r, oi) : ORING(oi))
                 uint32_t cur = 0;  // the half staged for this round
                 for (;;) {
                     const bool more = S.bm < nbig;  // uniform: S.bm was last written before a barrier
@@ -2348,23 +2358,24 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
                         const u32x4 v = *reinterpret_cast<const u32x4*>(stage2 + (b << 10) + 16u * lane);
                         const uint32_t rly = cl.relay;
+                        const uint32_t posr = kRegs && lane < sll ? (uint32_t)S.pos[cc][lane] : 0u;  // slot in out-ring (j, vc)
                         if (PULL_ON && rly != ~0u) {
                             // pulled on: each child gets header (kRefMark) + reference to my relay copy
                             const u32x4 hv = q == 0 ? u32x4{v.x, v.y, (v.z & 0xff00ffffu) | (kRefMark << 16), v.w}
                                                     : u32x4{rly, ~rly, kRefMagic, 0u};
                             for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
                                 const int oi = __builtin_ctz(a2);
-                                const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
-                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
-                                if (q <= 1u) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, hv, sys);
+                                const uint32_t slot = G3_SLOT(oi);
+                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
+                                if (q <= 1u) st_ring(ro, (slot & fcap_m) * P.fwd_stride + 16u * q, hv, sys);
                             }
                             if (q < nch && q != 0) st_ring(rf, rly + 16u * q, v, sys);  // the relay copy
                         } else {
                             for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
                                 const int oi = __builtin_ctz(a2);
-                                const uint64_t slot = S.out_tail0[oi] + S.pos[cc][oi >> 1];
-                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
-                                if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+                                const uint32_t slot = G3_SLOT(oi);
+                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
+                                if (q < nch) st_ring(ro, (slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
                             }
                         }
                         if (q < nch && cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
@@ -2386,6 +2397,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     VM_DRAIN();  // the next half's loads (and this round's stores: vmcnt is in order)
                     ACQ_NEXT();
                 }
+#undef G3_SLOT
+#undef G3_RING
             }
             if (lat_deliv) {  // latency program: the last of N-1 pickups completes the round
                 const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
