@@ -954,7 +954,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + pend_bytes);       // [oi][256]
     uint8_t* stage = dyn_lds + pend_bytes + P.nout_max * (2u * kMaxCand);      // [message][q] x 16 B
     uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
-    const uint32_t s2_blocks = P.stage2_bytes / 1024u;
+    // large-message blocks: kBlkCh chunks (kSub per lane) -- 128 (2 KiB) in the 4-wave large-slot kernel,
+    // so a 1-KiB payload is one block, not 64 chunks + a 1-chunk block; 64 where registers are short
+    constexpr uint32_t kSub = W == 4 ? 2u : 1u, kBlkCh = 64u * kSub, kBlkBytes = 16u * kBlkCh;
+    const uint32_t s2_blocks = P.stage2_bytes / kBlkBytes;
 #define STG(c, q) (stage + (((uint32_t)(c) * nsmall + (uint32_t)(q)) << 4))
 #define OL(oi, r) olist[(uint32_t)(oi) * (uint32_t)kMaxCand + (uint32_t)(r)]
     // the pending entry of (origin, pool slot) (rlo_device.hpp Params.pend_slots)
@@ -2201,20 +2204,20 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         cc = S.big[mi];
                         const uint32_t nch = (kHdr + (S.cand[cc].w2 & 0xffffu) + 15u) >> 4;
                         q0 = lane == 0 ? bq0 : 0u;
-                        nb = (nch - q0 + 63u) >> 6;
+                        nb = (nch - q0 + kBlkCh - 1u) / kBlkCh;
                     }
                     uint32_t tot;
                     const uint32_t st = wave_excl_scan(nb, &tot);
                     for (uint32_t k = 0; k < nb && st + k < lim; k++) {
                         S.blk_c[hoff + st + k] = cc;
-                        S.blk_q0[hoff + st + k] = q0 + 64u * k;
+                        S.blk_q0[hoff + st + k] = q0 + kBlkCh * k;
                     }
                     const uint64_t cut = __ballot(nb != 0 && st + nb > lim);  // the first cut message is the cursor
                     uint32_t nbm, nbq0, nblk;
                     if (cut) {
                         const int l = __builtin_ctzll(cut);
                         nbm = bm + (uint32_t)l;
-                        nbq0 = rdl32(q0, l) + 64u * (lim - rdl32(st, l));
+                        nbq0 = rdl32(q0, l) + kBlkCh * (lim - rdl32(st, l));
                         nblk = lim;
                     } else {
                         nbm = min(bm + 64u, nbig);
@@ -2230,10 +2233,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t nblk = S.nblk2[h];
                 for (uint32_t b0 = (uint32_t)w; b0 < nblk; b0 += kWaves) {
                     const uint32_t b = h * hb + b0;
-                    const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
+                    const uint32_t cc = S.blk_c[b], q0b = S.blk_q0[b];
                     const CandL& cl = S.cand[cc];
                     const uint32_t nch = (kHdr + (cl.w2 & 0xffffu) + 15u) >> 4;
-                    uint8_t* dst = stage2 + (b << 10);
+#pragma unroll 1
+                    for (uint32_t u = 0; u < kSub; u++) {  // chunks q0 + lane + 64 u land at block + 1 KiB u + 16 lane
+                    const uint32_t q = q0b + lane + 64u * u;
+                    uint8_t* dst = stage2 + b * kBlkBytes + 1024u * u;
                     if (cl.kind == K_RING) {
                         if (PULL_ON && ((cl.w2 >> 16) & 0xffu) == kRefMark) {
                             // pulled: the payload from the sender's relay slot (the reference staged as
@@ -2262,6 +2268,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         *reinterpret_cast<u32x4*>(dst + 16u * lane) =
                             q == 0 ? u32x4{cl.w0, cl.id, cl.w2, cl.t0}
                                    : gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), q);
+                    }
                     }
                 }
             };
@@ -2353,36 +2360,53 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const uint32_t nblk = S.nblk2[cur];
                     for (uint32_t b0 = (uint32_t)w; b0 < nblk; b0 += kWaves) {
                         const uint32_t b = cur * hb + b0;
-                        const uint32_t cc = S.blk_c[b], q = S.blk_q0[b] + lane;
+                        const uint32_t cc = S.blk_c[b], q0b = S.blk_q0[b];
                         const CandL& cl = S.cand[cc];
                         const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
-                        const u32x4 v = *reinterpret_cast<const u32x4*>(stage2 + (b << 10) + 16u * lane);
+                        u32x4 vv[kSub];  // chunk q0 + lane + 64 u
+#pragma unroll
+                        for (uint32_t u = 0; u < kSub; u++)
+                            vv[u] = *reinterpret_cast<const u32x4*>(stage2 + b * kBlkBytes + 1024u * u + 16u * lane);
                         const uint32_t rly = cl.relay;
                         const uint32_t posr = kRegs && lane < sll ? (uint32_t)S.pos[cc][lane] : 0u;  // slot in out-ring (j, vc)
+                        const uint32_t q = q0b + lane;
                         if (PULL_ON && rly != ~0u) {
-                            // pulled on: each child gets header (kRefMark) + reference to my relay copy
+                            // pulled on: each child gets header (kRefMark) + reference to my relay copy (only a
+                            // message's first block holds chunks 0 and 1)
+                            const u32x4 v = vv[0];
                             const u32x4 hv = q == 0 ? u32x4{v.x, v.y, (v.z & 0xff00ffffu) | (kRefMark << 16), v.w}
                                                     : u32x4{rly, ~rly, kRefMagic, 0u};
-                            for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
+                            for (uint32_t a2 = q0b == 0u ? (uint32_t)uni((int)cl.need) : 0u; a2; a2 &= a2 - 1) {
                                 const int oi = __builtin_ctz(a2);
                                 const uint32_t slot = G3_SLOT(oi);
                                 const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
                                 if (q <= 1u) st_ring(ro, (slot & fcap_m) * P.fwd_stride + 16u * q, hv, sys);
                             }
-                            if (q < nch && q != 0) st_ring(rf, rly + 16u * q, v, sys);  // the relay copy
+#pragma unroll
+                            for (uint32_t u = 0; u < kSub; u++)  // the relay copy
+                                if (q + 64u * u < nch && q + 64u * u != 0) st_ring(rf, rly + 16u * (q + 64u * u), vv[u], sys);
                         } else {
                             for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
                                 const int oi = __builtin_ctz(a2);
                                 const uint32_t slot = G3_SLOT(oi);
                                 const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
-                                if (q < nch) st_ring(ro, (slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+                                const uint32_t so = (slot & fcap_m) * P.fwd_stride + 16u * q;
+#pragma unroll
+                                for (uint32_t u = 0; u < kSub; u++)
+                                    if (q + 64u * u < nch) st_ring(ro, so + 1024u * u, vv[u], sys);
                             }
                         }
-                        if (q < nch && cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
-                            acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})
-                                              : chunk_mix(q - 1u, v);
-                            if (q > 0 && cl.logidx != ~0u && 16u * q <= P.log_stride)
-                                st_sys16(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride + 16u * (q - 1), v);
+                        if (cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
+#pragma unroll
+                            for (uint32_t u = 0; u < kSub; u++) {
+                                const uint32_t qq = q + 64u * u;
+                                if (qq < nch) {
+                                    acc_sum += qq == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})
+                                                       : chunk_mix(qq - 1u, vv[u]);
+                                    if (qq > 0 && cl.logidx != ~0u && 16u * qq <= P.log_stride)
+                                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride + 16u * (qq - 1), vv[u]);
+                                }
+                            }
                         }
                     }
                     if (!more) break;
