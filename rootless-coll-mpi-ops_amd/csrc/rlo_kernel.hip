@@ -1507,7 +1507,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // load and one store drain instead of the full iteration's seven phases (~17K cycles,
             // tools/lat_anatomy.py).  Effects restate phase F below line for line.
             uint32_t fastdone = 0;
-            if (!host && R == 1u && C == 1u && vtot == 0u && !(P.mode & (MODE_PROF | MODE_NOFAST))) {
+            // (host-service mode too, for bcasts and decisions -- its proposals take the full path for
+            // the host-judge hold and the JUDGED events -- when the pickup ring has room for their events)
+            if ((!host || hlim >= 2u) && R == 1u && C == 1u && vtot == 0u && !(P.mode & (MODE_PROF | MODE_NOFAST))) {
                 const uint32_t q = (uint32_t)lane;
                 const int fg = __builtin_ctzll(__ballot(lane < n_in2 && take > 0u));
                 const uint64_t h0 = rdl64(in_head_r, fg);
@@ -1521,7 +1523,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t fpseq = fw2 >> 24;
                 const int fvote = (int)(int8_t)(fw0 >> 24);
                 bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
-                     (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL) &&
+                     (ftag == TAG_BCAST || ftag == TAG_DECISION || (!host && ftag == TAG_PROPOSAL)) &&
                      !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
                 int fjudge = 1;
                 uint32_t fkids = 0, fneed = 0;
