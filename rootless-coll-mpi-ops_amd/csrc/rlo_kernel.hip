@@ -148,6 +148,7 @@ struct Shared {
     uint8_t loc_slot[2 * kPoolMax];
     // origination progress
     uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
+    uint32_t hwait;  // host mode: judge verdicts the host owes this rank (its command ring is polled every spin then)
     uint64_t hd[8], hd_t0;  // MODE_HDIAG counters (host mode)
     // pull worlds: my relay ring (slots taken / released), this iteration's allocations, and the release
     // records: relay count rq_relay[e] is released once every out-ring's consumer passed rq_out[e][oi]
@@ -1018,7 +1019,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
-            S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0;
+            S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0; S.hwait = 0;
             S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
@@ -1091,7 +1092,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // host mode: the host-written counters (pinned host memory: a PCIe read, ~1 us more than
                 // the ring polls) on every 4th re-poll only, so an idle rank still sees a ring message
                 // one VRAM poll after it lands; a command waits at most ~4 re-polls
-                if (host && lane < 2 && (sp & 3u) == 0u) hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
+                // (every spin while a judge verdict is owed: the host answers within a few microseconds)
+                if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u))
+                    hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
@@ -1413,12 +1416,21 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if (htag == CMD_JUDGE) {  // verdict of judge(data) for a held proposal (:698)
                             const int og = (int)(hd.x & 0xffffu);
                             PendState* ps = &PEND(og < P.n ? og : 0, hd.z >> 24);
-                            if (og < P.n && ps->valid == PS_JREQ && ps->pid == (int32_t)hd.y) ps->valid = vo ? PS_JYES : PS_JNO;
-                            else set_error(S, P, ERR_HOST_CMD, hd.x);
+                            if (og < P.n && ps->valid == PS_JREQ && ps->pid == (int32_t)hd.y) {
+                                ps->valid = vo ? PS_JYES : PS_JNO;
+                                atomicSub(&S.hwait, 1u);
+                            } else {
+                                set_error(S, P, ERR_HOST_CMD, hd.x);
+                            }
                         } else if (htag == CMD_OWN_JUDGE) {  // final judge(NULL) of my proposal (:770-775)
                             const uint32_t k = (hd.z >> 24) & (P.pend_slots - 1u);
-                            if (S.own_state[k] == 3 && S.own_pid[k] == (int32_t)hd.y) { S.own_decision[k] = vo ? 1u : 0u; S.own_state[k] = 2; }
-                            else set_error(S, P, ERR_HOST_CMD, hd.x);
+                            if (S.own_state[k] == 3 && S.own_pid[k] == (int32_t)hd.y) {
+                                S.own_decision[k] = vo ? 1u : 0u;
+                                S.own_state[k] = 2;
+                                atomicSub(&S.hwait, 1u);
+                            } else {
+                                set_error(S, P, ERR_HOST_CMD, hd.x);
+                            }
                         } else if (htag == CMD_QUIT) {
                             S.quit = 1;
                         } else if (BULK && htag == CMD_BULK_RELEASE) {  // the host copied a bulk delivery out
@@ -1735,6 +1747,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 const int d = (nw >> 16) == 0 ? 1 : 0;
                                 if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback
                                     log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
+                                    atomicAdd(&S.hwait, 1u);
                                     S.own_state[k] = 3;
                                 } else {
                                     if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
@@ -1914,6 +1927,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     ps->pid = (int32_t)lid;
                     ps->valid = PS_JREQ;
                     slot = log_put(S, P, lr, LOG_JREQ, lorg, lfrom, lid, plen, -1, lw2 >> 24);
+                    atomicAdd(&S.hwait, 1u);  // (lane 0 of several waves)
                 }
                 slot = rdl32(slot, 0);
                 uint8_t* dst = P.log_payload + ((size_t)lr * P.log_cap + slot) * P.log_stride;
