@@ -55,6 +55,7 @@ enum Mode : uint32_t {
     MODE_NOACQ = 1024u,   // diagnostic (UNSAFE): no agent acquire between iterations (A/B of its cost)
     MODE_NOFAST = 2048u,  // A/B: every iteration takes the full path (no lone-message fast path)
     MODE_HDIAG = 4096u,   // diagnostic, host mode: command-wait counters into hctl[kHctlDiag..] at exit
+    MODE_PIPE = 8192u,    // A/B: large-message staging rounds pipelined over two halves of stage2
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };

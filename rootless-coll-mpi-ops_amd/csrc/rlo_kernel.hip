@@ -2206,9 +2206,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
             // ---------------- G1: stage the first group of large messages (before any store)
             const uint32_t nbig = S.nbig;
-            // stage2 in two halves of hb blocks: round r+1's loads are in flight while round r is stored
-            // (one wait covers both), instead of load -> store -> wait for the stores -> load
-            const bool pipe = s2_blocks >= 2u;
+            // staging rounds of all of stage2: load -> store -> wait.  (MODE_PIPE, A/B: two halves, round r+1's
+            // loads in flight while round r is stored -- measured slower, the rounds halve)
+            const bool pipe = s2_blocks >= 2u && (P.mode & MODE_PIPE);
             const uint32_t hb = pipe ? min(s2_blocks / 2u, 64u) : min(s2_blocks, 64u);
             auto plan_big = [&](uint32_t h) {  // wave 0: next (message, 64-chunk block) pairs for half h, lane-parallel
                 if (w == 0) {
