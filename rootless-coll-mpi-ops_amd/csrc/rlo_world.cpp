@@ -434,9 +434,14 @@ int size_lds_variant(rlo_world* w, int variant) {
     int api = 0;
     bool ok = false;
     // every message of a medium slot (<= 24 chunks: payload <= 368 B) takes the small copy path when the
-    // stage fits (packed (message, chunk) copies; the large-message path moves one message per 1-KiB
-    // block: 256 B storm 2.0M bcast/s, profiles/r2s2_diag_sizes.log); larger slots stage 8 chunks
-    const uint32_t ns0 = L.stride / 16u <= 24u ? L.stride / 16u : 8u;
+    // stage fits (packed (message, chunk) copies; the large-message path moves one message per LDS
+    // block: 256 B storm 2.0M bcast/s, profiles/r2s2_diag_sizes.log)
+    // (large slots stage 5 chunks -- header + 64 B, so a 64-B message or a proposal still takes the small
+    // path -- and leave the LDS to the large-message rounds: 4 KiB storm 109 -> 104 ms, 1 KiB 40.4 -> 38.4,
+    // profiles/r2s4_nsmall_ab.txt)
+    uint32_t ns0 = L.stride / 16u <= 24u ? L.stride / 16u : 5u;
+    if (const char* e = std::getenv("RLO_NSMALL"))  // A/B: staged chunks per candidate in large-slot worlds
+        if (L.stride / 16u > 24u) ns0 = std::max(2u, std::min(8u, (uint32_t)std::atoi(e)));
     for (uint32_t ns = ns0; ns >= 1 && !ok; ns--) {
         // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
         const size_t fixed = stat + (size_t)16 * L.n * L.pend_slots + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
