@@ -214,10 +214,22 @@ def _world(rlo, dist, R, world, rank, local, **kw):
         return rlo.World(R, device=local, **kw)
     if os.environ.get("RLO_BENCH_DEVICE") and kw.get("bulk_max") and not kw.get("movers"):
         kw["movers"] = 16
-    w = rlo.World.part(R, world, rank, device=local, uncached=True, **kw)
+    # every part learns whether every other part was made: a part that failed alone would otherwise
+    # leave its peers waiting in this exchange while it moves on to the next leg's (the ranks desync)
+    w, err = None, None
+    try:
+        w = rlo.World.part(R, world, rank, device=local, uncached=True, **kw)
+        mine = w.export()
+    except Exception as e:  # noqa: BLE001 - re-raised below, on every rank
+        err, mine = "rank %d: %r" % (rank, e), None
     blobs = [None] * world
-    dist.all_gather_object(blobs, w.export())
-    w.connect(blobs)
+    dist.all_gather_object(blobs, (mine, err))
+    errs = [e for _, e in blobs if e]
+    if errs:
+        if w is not None:
+            w.close()
+        raise RuntimeError("world part creation failed: " + "; ".join(errs))
+    w.connect([b for b, _ in blobs])
     return w
 
 
@@ -627,12 +639,14 @@ def main():
             extras["bulk"] = bulk_leg(rlo, dist, world, rank, local, stream, red)
         except Exception as e:  # noqa: BLE001 - reported, never fails the headline line
             extras["bulk"] = {"error": repr(e)[:300]}
+            note("rank %d: bulk leg failed: %r" % (rank, e))
         if rank == 0:
             note("mixed-size leg (C5)")
         try:
             extras["c5_mixed"] = c5_leg(rlo, dist, world, rank, local, stream, red)
         except Exception as e:  # noqa: BLE001
             extras["c5_mixed"] = {"error": repr(e)[:300]}
+            note("rank %d: C5 leg failed: %r" % (rank, e))
     lib.rlo_stream_destroy(stream)
     ok = bool(sum_over_ranks(0.0 if ok else 1.0) == 0.0)
 

@@ -2292,12 +2292,24 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // LDS-DMA loads may leave lines in L1 that straddle into the next, maybe unwritten, slot, and
             // the next iteration must not read them from there.  It completes under the stores, and
             // phase A's VM_DRAIN (or the eager drain) waits for it
+            // MODE_PROF: wave 0's cycles waiting for a round's loads (and stores) in dbg[3], the rounds in
+            // dbg[4] (push worlds: pull worlds count relay-full pushes there)
+            auto big_drain = [&]() {
+                if ((P.mode & MODE_PROF) && tid == 0) {
+                    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+                    VM_DRAIN();
+                    S.dbg[3] += __builtin_amdgcn_s_memtime() - c0;
+                    if (!PULL_ON) S.dbg[4]++;
+                } else {
+                    VM_DRAIN();
+                }
+            };
             if (nbig) {
                 if (tid == 0) { S.bm = 0; S.bq0 = 0; }
                 plan_big(0u);
                 BAR();
                 issue_big(0u);
-                VM_DRAIN();
+                big_drain();
                 ACQ_NEXT();
             }
 
@@ -2434,7 +2446,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         BAR();
                         issue_big(cur);
                     }
-                    VM_DRAIN();  // the next half's loads (and this round's stores: vmcnt is in order)
+                    big_drain();  // the next half's loads (and this round's stores: vmcnt is in order)
                     ACQ_NEXT();
                 }
 #undef G3_SLOT

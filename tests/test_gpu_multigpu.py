@@ -11,8 +11,10 @@ N-part path is exercised here the way it runs there.
 import json
 import os
 import re
+import signal
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -76,9 +78,27 @@ def test_bench_two_parts_under_torchrun():
            "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
            "--warmup", "1", "--ranks", "64", "--k", "16384", "--lat-rounds", "200", "--no-api", "--no-pmc",
            "--no-cpu-baseline"]
-    r = subprocess.run(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=240)
-    lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
-    assert r.returncode == 0 and lines, r.stderr.decode()[-3000:]
+    # Bounded below the suite's per-test limit, output to files (torchrun's workers outlive a killed
+    # agent's pipes), so a stall fails with the bench's own progress lines instead of a bare timeout
+    with tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
+        p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=fo, stderr=fe, start_new_session=True)
+        try:
+            p.wait(timeout=100)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGTERM)  # the agent stops its workers
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+            fe.seek(0)
+            ps = subprocess.run(["ps", "-eo", "pid,ppid,etime,stat,args"], stdout=subprocess.PIPE).stdout.decode()
+            pytest.fail("two-part bench stalled after 100 s; stderr tail:\n" + fe.read().decode()[-4000:] +
+                        "\nprocesses:\n" + ps[-4000:])
+        fo.seek(0)
+        fe.seek(0)
+        out, err = fo.read(), fe.read()
+    lines = [ln for ln in out.decode().splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, err.decode()[-3000:]
     line = json.loads(lines[-1])
     assert line["n_gpus"] == 2 and line["mode"] == "sharded" and line["verified"], line
     assert line["world_ranks"] == 128 and line["value"] > 0

@@ -27,9 +27,11 @@ def report(name, w, ms, deliveries):
     dbg = st["dbg"].astype(np.float64)
     for r in sorted(set([0, 1, 2, 128, 255, int(np.argmax(st["stalls"]))])):
         d = dbg[r]
-        print("   rank %3d: iters %d busy %d | ring cands %.0f admitted %.0f | storm-allowed iters %.0f offered %.0f | "
-              "pull: relay-full pushes (dbg4) %.0f | backlog %.0f | child copies %.0f | max out fill %.0f"
-              % (r, st["iterations"][r], st["busy_iterations"][r], d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]))
+        print("   rank %3d: iters %d busy %d | ring cands %.0f admitted %.0f | storm-allowed iters %.0f | "
+              "large rounds: drain cycles %.0f, rounds (push) / relay-full pushes (pull) %.0f (%.0f cycles/round) | "
+              "backlog %.0f | child copies %.0f | max out fill %.0f"
+              % (r, st["iterations"][r], st["busy_iterations"][r], d[0], d[1], d[2], d[3], d[4], d[3] / max(d[4], 1),
+                 d[5], d[6], d[7]))
         h = st["hist"][r].astype(np.float64)
         it_r = max(1, st["iterations"][r])
         print("            per out-ring (oi: misfits/iter, admitted/iter, free@start/iter): " + " ".join(
