@@ -190,7 +190,8 @@ def size_legs(rlo, R, device, stream, sizes=(256, 1024, 4096), k=1 << 16, steps=
             gbs = k * 2.0 * (R - 1) * (s + 16) / (kernel_ms * 1e-3) / 1e9
             out.append({"payload_bytes": s, "bcasts": k, "bcast_per_s": round(k / dt, 1),
                         "deliveries_per_s": round(k * (R - 1) / dt, 1), "kernel_ms": round(kernel_ms, 3),
-                        "alg_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "verified": ok})
+                        "alg_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "payloads": "pulled" if w.info["pull"] else "pushed", "verified": ok})
     return out
 
 

@@ -88,7 +88,9 @@ typedef struct {
                                                     iteration) or 4 (256), chosen at creation     */
     uint32_t bulk_slots, movers;                 /* bulk: heap slots per origin, mover workgroups   */
     uint64_t bulk_max, heap_bytes;               /* bulk: largest message, this part's heap bytes   */
-    uint32_t proposal_pool, pad2;                /* pending entries per origin (own proposals in flight) */
+    uint32_t proposal_pool;                      /* pending entries per origin (own proposals in flight) */
+    uint32_t pull;                               /* 1: large bcasts cross edges as header + reference into
+                                                    the sender's relay ring (pulled payloads)           */
 } rlo_world_info_t;
 
 /* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522

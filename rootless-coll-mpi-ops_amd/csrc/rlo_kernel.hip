@@ -955,10 +955,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + pend_bytes);       // [oi][256]
     uint8_t* stage = dyn_lds + pend_bytes + P.nout_max * (2u * kMaxCand);      // [message][q] x 16 B
     uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
-    // large-message blocks: kBlkCh chunks (kSub per lane) -- 128 (2 KiB) in the 4-wave large-slot kernel,
-    // so a 1-KiB payload is one block, not 64 chunks + a 1-chunk block; 64 where registers are short
-    constexpr uint32_t kSub = W == 4 ? 2u : 1u, kBlkCh = 64u * kSub, kBlkBytes = 16u * kBlkCh;
-    const uint32_t s2_blocks = P.stage2_bytes / kBlkBytes;
+    // large messages move in groups of up to kSubMax 1-KiB units (64 payload chunks, one per lane) of
+    // one message, packed into stage2: a 4-KiB payload is one group of four units, a 1-KiB payload one
+    // group of one unit.  The per-group work (LDS metadata, out-ring walk) is what a staging round
+    // costs, so the fewer groups per byte the better; one unit where registers are short (8 waves)
+    constexpr uint32_t kSubMax = W == 4 ? 4u : 1u;
+    constexpr uint32_t kPair = W == 4 ? 2u : 1u;  // units in registers at once
+    const uint32_t s2_units = P.stage2_bytes >> 10;
 #define STG(c, q) (stage + (((uint32_t)(c) * nsmall + (uint32_t)(q)) << 4))
 #define OL(oi, r) olist[(uint32_t)(oi) * (uint32_t)kMaxCand + (uint32_t)(r)]
     // the pending entry of (origin, pool slot) (rlo_device.hpp Params.pend_slots)
@@ -2208,37 +2211,47 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             const uint32_t nbig = S.nbig;
             // staging rounds of all of stage2: load -> store -> wait.  (MODE_PIPE, A/B: two halves, round r+1's
             // loads in flight while round r is stored -- measured slower, the rounds halve)
-            const bool pipe = s2_blocks >= 2u && (P.mode & MODE_PIPE);
-            const uint32_t hb = pipe ? min(s2_blocks / 2u, 64u) : min(s2_blocks, 64u);
-            auto plan_big = [&](uint32_t h) {  // wave 0: next (message, 64-chunk block) pairs for half h, lane-parallel
+            const bool pipe = s2_units >= 2u * kSubMax && (P.mode & MODE_PIPE);
+            const uint32_t hu = pipe ? min(s2_units / 2u, 64u) : min(s2_units, 128u);  // units per round
+            const uint32_t hg = pipe ? 64u : 128u;                                     // groups per round
+            const uint32_t gsub = min(kSubMax, hu), gspan = 64u * gsub;                 // a group's units, chunks
+            // groups hold PAYLOAD chunks (payload chunk p is slot chunk p + 1): the header is known from
+            // classification and is stored from registers.  blk_q0[g] = first payload chunk | first unit << 16
+            auto plan_big = [&](uint32_t h) {  // wave 0: the next (message, group) pairs for half h, lane-parallel
                 if (w == 0) {
                     const uint32_t bm = S.bm, bq0 = S.bq0;
-                    const uint32_t lim = hb, hoff = h * hb;
+                    const uint32_t goff = h * hg, uoff = h * hu;
                     const uint32_t mi = bm + (uint32_t)lane;
-                    uint32_t nb = 0, cc = 0, q0 = 0;
+                    uint32_t ng = 0, nu = 0, cc = 0, q0 = 0;
                     if (mi < nbig) {
                         cc = S.big[mi];
-                        const uint32_t nch = (kHdr + (S.cand[cc].w2 & 0xffffu) + 15u) >> 4;
+                        const uint32_t pch = ((S.cand[cc].w2 & 0xffffu) + 15u) >> 4;  // payload chunks
                         q0 = lane == 0 ? bq0 : 0u;
-                        nb = (nch - q0 + kBlkCh - 1u) / kBlkCh;
+                        ng = (pch - q0 + gspan - 1u) / gspan;
+                        nu = (pch - q0 + 63u) >> 6;
                     }
-                    uint32_t tot;
-                    const uint32_t st = wave_excl_scan(nb, &tot);
-                    for (uint32_t k = 0; k < nb && st + k < lim; k++) {
-                        S.blk_c[hoff + st + k] = cc;
-                        S.blk_q0[hoff + st + k] = q0 + kBlkCh * k;
+                    uint32_t totg, totu;
+                    const uint32_t sg = wave_excl_scan(ng, &totg), su = wave_excl_scan(nu, &totu);
+                    // the first message that does not fit whole is the cursor: its whole groups that fit go
+                    // now (every lane before it fits, so sg <= hg and su <= hu there)
+                    const uint64_t cut = __ballot(ng != 0 && (sg + ng > hg || su + nu > hu));
+                    const uint32_t l = cut ? (uint32_t)__builtin_ctzll(cut) : 64u;
+                    const uint32_t fitg = (uint32_t)lane == l ? min(hg - sg, (hu - su) / gsub) : 0u;
+                    const uint32_t nw = (uint32_t)lane < l ? ng : fitg;
+                    for (uint32_t k = 0; k < nw; k++) {
+                        S.blk_c[goff + sg + k] = cc;
+                        S.blk_q0[goff + sg + k] = (q0 + gspan * k) | ((uoff + su + gsub * k) << 16);
                     }
-                    const uint64_t cut = __ballot(nb != 0 && st + nb > lim);  // the first cut message is the cursor
                     uint32_t nbm, nbq0, nblk;
                     if (cut) {
-                        const int l = __builtin_ctzll(cut);
-                        nbm = bm + (uint32_t)l;
-                        nbq0 = rdl32(q0, l) + kBlkCh * (lim - rdl32(st, l));
-                        nblk = lim;
+                        const uint32_t f = rdl32(fitg, (int)l);
+                        nbm = bm + l;
+                        nbq0 = rdl32(q0, (int)l) + gspan * f;
+                        nblk = rdl32(sg, (int)l) + f;
                     } else {
                         nbm = min(bm + 64u, nbig);
                         nbq0 = 0;
-                        nblk = tot;
+                        nblk = totg;
                     }
                     if (lane == 0) { S.bm = nbm; S.bq0 = nbq0; S.nblk2[h] = nblk; }
                 }
@@ -2248,42 +2261,39 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             auto issue_big = [&](uint32_t h) {
                 const uint32_t nblk = S.nblk2[h];
                 for (uint32_t b0 = (uint32_t)w; b0 < nblk; b0 += kWaves) {
-                    const uint32_t b = h * hb + b0;
-                    const uint32_t cc = S.blk_c[b], q0b = S.blk_q0[b];
+                    const uint32_t b = h * hg + b0;
+                    const uint32_t cc = S.blk_c[b], qw = S.blk_q0[b], q0b = qw & 0xffffu;
                     const CandL& cl = S.cand[cc];
-                    const uint32_t nch = (kHdr + (cl.w2 & 0xffffu) + 15u) >> 4;
+                    const uint32_t pch = ((cl.w2 & 0xffffu) + 15u) >> 4;  // payload chunks
+                    const uint32_t nsub = min(gsub, (pch - q0b + 63u) >> 6);
 #pragma unroll 1
-                    for (uint32_t u = 0; u < kSub; u++) {  // chunks q0 + lane + 64 u land at block + 1 KiB u + 16 lane
-                    const uint32_t q = q0b + lane + 64u * u;
-                    uint8_t* dst = stage2 + b * kBlkBytes + 1024u * u;
+                    for (uint32_t u = 0; u < nsub; u++) {  // payload chunk q0 + lane + 64 u lands at unit + u, 16 lane
+                    const uint32_t pq = q0b + lane + 64u * u;
+                    uint8_t* dst = stage2 + ((qw >> 16) + u) * 1024u;
                     if (cl.kind == K_RING) {
                         if (PULL_ON && ((cl.w2 >> 16) & 0xffu) == kRefMark) {
                             // pulled: the payload from the sender's relay slot (the reference staged as
-                            // chunk 1 in phase D0), the header as classified
+                            // chunk 1 in phase D0)
                             const u32x4 ref = *reinterpret_cast<const u32x4*>(STG(cc, 1));
                             const uint32_t roff = (uint32_t)uni((int)ref.x);
                             // a reference that is not one (unwritten / torn chunk): stop loudly, load nothing
                             const bool rok = uni((int)ref.y) == (int)~roff && (uint32_t)uni((int)ref.z) == kRefMagic;
-                            if (!rok && lane == 0) set_error(S, P, ERR_BAD_SLOT, 0x5EF0000u | (q & 0xffffu));
+                            if (!rok && lane == 0) set_error(S, P, ERR_BAD_SLOT, 0x5EF0000u | (pq & 0xffffu));
                             const __amdgpu_buffer_rsrc_t rr =
-                                mk_rsrc(reinterpret_cast<void*>(uni64(t.in_base[cl.group >> 1]) + roff), rok ? nch * 16u : 0u);
-                            if (rok && q < nch && q != 0) {
-                                if (sys) __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * q, 0, 0, kAuxSc1 | 1);
-                                else __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * q, 0, 0, kAuxSc1);
+                                mk_rsrc(reinterpret_cast<void*>(uni64(t.in_base[cl.group >> 1]) + roff), rok ? (pch + 1u) * 16u : 0u);
+                            if (rok && pq < pch) {
+                                if (sys) __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * (pq + 1u), 0, 0, kAuxSc1 | 1);
+                                else __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * (pq + 1u), 0, 0, kAuxSc1);
                             }
-                            // (the header with the ordinary mark: sent on pushed, if no relay slot is free)
-                            if (q == 0) *reinterpret_cast<u32x4*>(dst) = u32x4{cl.w0, cl.id, (cl.w2 & 0xff00ffffu) | (kSlotMark << 16), cl.t0};
-                        } else if (q < nch) {
-                            dma16(rf, dst, cl.src + 16u * q);
+                        } else if (pq < pch) {
+                            dma16(rf, dst, cl.src + 16u * (pq + 1u));
                         }
-                    } else if (cl.kind == K_HOST) {  // payload from the command slot, header as classified
-                        if (q < nch && q != 0)
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(dst), 16, cl.src + 16u * q, 0, 0, kAuxSc1 | 1);
-                        if (q == 0) *reinterpret_cast<u32x4*>(dst) = u32x4{cl.w0, cl.id, cl.w2, cl.t0};
-                    } else if (q < nch) {
+                    } else if (cl.kind == K_HOST) {  // payload from the command slot
+                        if (pq < pch)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, lds_ptr(dst), 16, cl.src + 16u * (pq + 1u), 0, 0, kAuxSc1 | 1);
+                    } else if (pq < pch) {
                         *reinterpret_cast<u32x4*>(dst + 16u * lane) =
-                            q == 0 ? u32x4{cl.w0, cl.id, cl.w2, cl.t0}
-                                   : gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), q);
+                            gen_chunk(P, cl.kind, me, cl.id, cl.w2 & 0xffffu, cl.src, (int)(int8_t)(cl.w0 >> 24), pq + 1u);
                     }
                     }
                 }
@@ -2387,52 +2397,62 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                     const uint32_t nblk = S.nblk2[cur];
                     for (uint32_t b0 = (uint32_t)w; b0 < nblk; b0 += kWaves) {
-                        const uint32_t b = cur * hb + b0;
-                        const uint32_t cc = S.blk_c[b], q0b = S.blk_q0[b];
+                        const uint32_t b = cur * hg + b0;
+                        const uint32_t cc = S.blk_c[b], qw = S.blk_q0[b], q0b = qw & 0xffffu;
                         const CandL& cl = S.cand[cc];
-                        const uint32_t blen = cl.w2 & 0xffffu, nch = (kHdr + blen + 15u) >> 4;
-                        u32x4 vv[kSub];  // chunk q0 + lane + 64 u
-#pragma unroll
-                        for (uint32_t u = 0; u < kSub; u++)
-                            vv[u] = *reinterpret_cast<const u32x4*>(stage2 + b * kBlkBytes + 1024u * u + 16u * lane);
+                        const uint32_t blen = cl.w2 & 0xffffu, pch = (blen + 15u) >> 4;  // payload chunks
+                        const uint32_t nsub = min(gsub, (pch - q0b + 63u) >> 6);     // uniform
                         const uint32_t rly = cl.relay;
                         const uint32_t posr = kRegs && lane < sll ? (uint32_t)S.pos[cc][lane] : 0u;  // slot in out-ring (j, vc)
-                        const uint32_t q = q0b + lane;
-                        if (PULL_ON && rly != ~0u) {
-                            // pulled on: each child gets header (kRefMark) + reference to my relay copy (only a
-                            // message's first block holds chunks 0 and 1)
-                            const u32x4 v = vv[0];
-                            const u32x4 hv = q == 0 ? u32x4{v.x, v.y, (v.z & 0xff00ffffu) | (kRefMark << 16), v.w}
-                                                    : u32x4{rly, ~rly, kRefMagic, 0u};
-                            for (uint32_t a2 = q0b == 0u ? (uint32_t)uni((int)cl.need) : 0u; a2; a2 &= a2 - 1) {
+                        // the header (slot chunk 0) from registers, by lane 0 of the message's first group
+                        const bool hdr = q0b == 0u && lane == 0;
+                        const uint32_t hw2 = cl.w2 & 0xff00ffffu;
+                        const bool bc = cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST;
+                        if (bc && hdr) acc_sum += chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen});
+                        if (PULL_ON && rly != ~0u && q0b == 0u) {
+                            // pulled on: each child gets header (kRefMark) + reference to my relay copy
+                            const u32x4 hv = lane == 0 ? u32x4{cl.w0, cl.id, hw2 | (kRefMark << 16), cl.t0}
+                                                       : u32x4{rly, ~rly, kRefMagic, 0u};
+                            for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {
                                 const int oi = __builtin_ctz(a2);
                                 const uint32_t slot = G3_SLOT(oi);
                                 const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
-                                if (q <= 1u) st_ring(ro, (slot & fcap_m) * P.fwd_stride + 16u * q, hv, sys);
-                            }
-#pragma unroll
-                            for (uint32_t u = 0; u < kSub; u++)  // the relay copy
-                                if (q + 64u * u < nch && q + 64u * u != 0) st_ring(rf, rly + 16u * (q + 64u * u), vv[u], sys);
-                        } else {
-                            for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
-                                const int oi = __builtin_ctz(a2);
-                                const uint32_t slot = G3_SLOT(oi);
-                                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
-                                const uint32_t so = (slot & fcap_m) * P.fwd_stride + 16u * q;
-#pragma unroll
-                                for (uint32_t u = 0; u < kSub; u++)
-                                    if (q + 64u * u < nch) st_ring(ro, so + 1024u * u, vv[u], sys);
+                                if (lane <= 1) st_ring(ro, (slot & fcap_m) * P.fwd_stride + 16u * lane, hv, sys);
                             }
                         }
-                        if (cl.kind == K_RING && ((cl.w0 >> 16) & 0xffu) == TAG_BCAST) {
+                        // the group's units two at a time (registers: 4 x 16 B live across the out-ring walk)
+                        for (uint32_t u0 = 0; u0 < nsub; u0 += kPair) {  // uniform
+                            u32x4 vv[kPair];  // payload chunk q0 + lane + 64 (u0 + u)
 #pragma unroll
-                            for (uint32_t u = 0; u < kSub; u++) {
-                                const uint32_t qq = q + 64u * u;
-                                if (qq < nch) {
-                                    acc_sum += qq == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{cl.w0 & 0xffffu, cl.id, TAG_BCAST, blen})
-                                                       : chunk_mix(qq - 1u, vv[u]);
-                                    if (qq > 0 && cl.logidx != ~0u && 16u * qq <= P.log_stride)
-                                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride + 16u * (qq - 1), vv[u]);
+                            for (uint32_t u = 0; u < kPair; u++)
+                                if (u0 + u < nsub) vv[u] = *reinterpret_cast<const u32x4*>(stage2 + ((qw >> 16) + u0 + u) * 1024u + 16u * lane);
+                            const uint32_t pq = q0b + lane + 64u * u0;
+                            if (PULL_ON && rly != ~0u) {
+#pragma unroll
+                                for (uint32_t u = 0; u < kPair; u++)  // the relay copy (slot chunks 1 ..)
+                                    if (u0 + u < nsub && pq + 64u * u < pch) st_ring(rf, rly + 16u * (pq + 64u * u + 1u), vv[u], sys);
+                            } else {
+                                const u32x4 hv = u32x4{cl.w0, cl.id, hw2 | (kSlotMark << 16), cl.t0};
+                                for (uint32_t a2 = (uint32_t)uni((int)cl.need); a2; a2 &= a2 - 1) {  // uniform loop
+                                    const int oi = __builtin_ctz(a2);
+                                    const uint32_t slot = G3_SLOT(oi);
+                                    const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(G3_RING(oi)), oring_bytes);
+                                    const uint32_t s0 = (slot & fcap_m) * P.fwd_stride;
+#pragma unroll
+                                    for (uint32_t u = 0; u < kPair; u++)
+                                        if (u0 + u < nsub && pq + 64u * u < pch) st_ring(ro, s0 + 16u * (pq + 1u) + 1024u * u, vv[u], sys);
+                                    if (hdr && u0 == 0u) st_ring(ro, s0, hv, sys);
+                                }
+                            }
+                            if (bc) {
+#pragma unroll
+                                for (uint32_t u = 0; u < kPair; u++) {
+                                    const uint32_t pp = pq + 64u * u;
+                                    if (u0 + u < nsub && pp < pch) {
+                                        acc_sum += chunk_mix(pp, vv[u]);
+                                        if (cl.logidx != ~0u && 16u * (pp + 1u) <= P.log_stride)
+                                            st_sys16(P.log_payload + ((size_t)lr * P.log_cap + cl.logidx) * P.log_stride + 16u * pp, vv[u]);
+                                    }
                                 }
                             }
                         }

@@ -204,12 +204,14 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         rings[L.part_of[e.dst]] += 2;
         vrings[L.part_of[e.src]] += 1;
     }
-    // pulled payloads (RLO_PULL=1, slots beyond the small copy path, not in bulk worlds): measured no
-    // faster than pushing (256 B -9 %, 4 KiB +3 %, profiles/r2s2_pull_waves_ab.txt: the large-message
-    // path is bound by its staging rounds, not by the wall ranks' store volume), so opt-in
+    // pulled payloads (not in bulk worlds): the default where slots hold messages beyond the small
+    // copy path (> 24 chunks); RLO_PULL=0 pushes, RLO_PULL=1 also pulls in medium-slot worlds.  Since
+    // the large-message rounds move whole messages per group, pulling is faster than pushing (1 KiB
+    // storm 37.6 -> 35.8 ms, 4 KiB 86.8 -> 79.3 ms, profiles/r2s5_sizes_groups_ab.txt)
     {
         const char* pe = std::getenv("RLO_PULL");
-        L.pull = pe && std::atoi(pe) != 0 && L.stride > 8u * 16u && !bulk_max;
+        const bool want = pe ? std::atoi(pe) != 0 : L.stride / 16u > 24u;
+        L.pull = want && L.stride > 8u * 16u && !bulk_max;
     }
     if (L.pull)
         for (int r = 0; r < n; r++) rings[L.part_of[r]] += 1;  // the relay ring
@@ -855,6 +857,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->bulk_max = w->L.bulk_max;
     o->heap_bytes = w->L.heap_bytes[w->part];
     o->proposal_pool = w->L.pend_slots;
+    o->pull = w->L.pull && w->nsmall >= 2 ? 1u : 0u;  // as Params.pull
     return RLO_OK;
 }
 

@@ -49,7 +49,7 @@ class WorldInfo(ctypes.Structure):
                 ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),
                 ("waves", ctypes.c_int32), ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32),
                 ("bulk_max", ctypes.c_uint64), ("heap_bytes", ctypes.c_uint64), ("proposal_pool", ctypes.c_uint32),
-                ("pad2", ctypes.c_uint32)]
+                ("pull", ctypes.c_uint32)]
 
 
 class PartCfg(ctypes.Structure):

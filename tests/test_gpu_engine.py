@@ -132,19 +132,22 @@ def test_storm_small_rings_backpressure(rlo):
     assert int(st["stalls"].sum()) > 0
 
 
+@pytest.mark.parametrize("pull", ["1", "0"])
 @pytest.mark.parametrize("n,ln,slots", [(64, 1000, 16), (37, 3000, 32)])
-def test_storm_pulled_payloads_small_rings(rlo, n, ln, slots):
-    """pull worlds (slots beyond the small copy path): large bcasts cross every edge as header +
-    reference into the sender's relay ring; with 16/32-slot rings (and relay rings) the relay-slot
-    release records and the ring credits are under constant pressure.  Every rank's delivery count and
-    checksum of the payload bytes it loaded equal the oracle's (RLO_PULL=1: opt-in, read at creation)."""
+def test_storm_pulled_payloads_small_rings(rlo, n, ln, slots, pull):
+    """pull worlds (the default for slots beyond the small copy path): large bcasts cross every edge
+    as header + reference into the sender's relay ring; with 16/32-slot rings (and relay rings) the
+    relay-slot release records and the ring credits are under constant pressure.  RLO_PULL=0 (read at
+    creation) pushes the payloads instead.  Every rank's delivery count and checksum of the payload
+    bytes it loaded equal the oracle's, either way."""
     import os
 
-    os.environ["RLO_PULL"] = "1"
+    os.environ["RLO_PULL"] = pull
     try:
         w = rlo.World(n, max_payload=ln, ring_slots=slots)
     finally:
         del os.environ["RLO_PULL"]
+    assert w.info["pull"] == int(pull)
     with w:
         w.program_storm(6000, ln, seed=13, window=64, log=True, log_cap=6008)
         w.run()
