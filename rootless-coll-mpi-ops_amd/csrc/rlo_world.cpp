@@ -1425,7 +1425,10 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     else w->P.mode &= ~rlo::MODE_NOFAST;
     // A/B: large-message staging rounds pipelined over two halves of stage2 (measured slower than whole
     // rounds: 4 KiB storm 122 vs 109 ms, profiles/r2s4_pipe_ab.txt)
-    static const bool pipe = std::getenv("RLO_BIG_PIPE") != nullptr;
+    static const bool pipe = [] {
+        const char* e = std::getenv("RLO_BIG_PIPE");
+        return e && std::atoi(e) != 0;
+    }();
     if (pipe) w->P.mode |= rlo::MODE_PIPE;
     else w->P.mode &= ~rlo::MODE_PIPE;
     static const bool hdiag = std::getenv("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
