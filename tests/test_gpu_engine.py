@@ -111,6 +111,31 @@ def test_storm_full_size_checksums(rlo, n, k, ln):
     assert int(st["originated"].sum()) == k
 
 
+@pytest.mark.parametrize("pull", ["1", "0"])
+@pytest.mark.parametrize("n,k,ln,slot", [(300, 4000, 4000, 4096), (64, 20000, 1100, 4096), (17, 3000, 2500, 2500)])
+def test_storm_large_groups(rlo, n, k, ln, slot, pull):
+    """the large-message rounds' group planner: payloads whose last 1-KiB unit is partial (1,100 B:
+    two units; 2,500 B: three; 4,000 B: four), messages cut between rounds, shorter payloads than the
+    slot, and a world of more ranks than CUs (two rank-workgroups per CU, so a smaller stage2), pulled
+    and pushed; delivery counts and payload checksums equal the oracle's (mixed sizes in one world are
+    the bulk worlds' C5 program, tests/test_gpu_bulk.py)"""
+    import os
+
+    os.environ["RLO_PULL"] = pull
+    try:
+        w = rlo.World(n, max_payload=slot)
+    finally:
+        del os.environ["RLO_PULL"]
+    with w:
+        w.program_storm(k, ln, seed=0x6A)
+        w.run()
+        st = w.stats()
+    exp = orc.storm_expected(n, 0x6A, k, ln)
+    assert (st["error"] == 0).all()
+    assert np.array_equal(st["bcast_delivered"].astype(np.int64), exp["count"])
+    assert np.array_equal(st["bcast_sum"], exp["sum"])
+
+
 def test_storm_repeatable_across_launches(rlo):
     with rlo.World(64) as w:
         w.program_storm(5000, 64, seed=3)
