@@ -2207,7 +2207,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             BAR();  // olist / cand / n_oi / big complete
             PST(4, 7);
 
-            // ---------------- G1: stage the first group of large messages (before any store)
+            // ---------------- G1: stage the first round of large-message groups (before any store)
             const uint32_t nbig = S.nbig;
             // staging rounds of all of stage2: load -> store -> wait.  (MODE_PIPE, A/B: two halves, round r+1's
             // loads in flight while round r is stored -- measured slower, the rounds halve)
