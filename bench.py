@@ -47,6 +47,30 @@ def percentile(a, p):
     return float(np.percentile(np.asarray(a, dtype=np.float64), p)) if len(a) else 0.0
 
 
+_DUMP = {"dir": "", "recs": {}}
+_DUMP_FIELDS = ("bcast_delivered", "bcast_sum", "originated", "own_decided", "own_approved", "actions", "judge_calls",
+                "dec_delivered", "error")
+
+
+def dump_leg(name, w, st, **extra):
+    """--dump: this part's per-rank statistics of one leg (the world ranks it holds), for the test that
+    compares the multi-part runs with the oracle (the bench itself never imports the oracle)"""
+    if not _DUMP["dir"]:
+        return
+    rec = {"rank_begin": int(w.rank_begin), "n_local": int(w.n_local)}
+    rec.update({f: [int(x) for x in st[f]] for f in _DUMP_FIELDS})
+    rec.update(extra)
+    _DUMP["recs"][name] = rec
+
+
+def dump_write(rank):
+    if not _DUMP["dir"]:
+        return
+    os.makedirs(_DUMP["dir"], exist_ok=True)
+    with open(os.path.join(_DUMP["dir"], "rank%d.json" % rank), "w") as f:
+        json.dump(_DUMP["recs"], f)
+
+
 def cpu_baseline(n, length, seed, target_s):
     """The oracle's clean-room CPU restatement ("port") on the box's host cores: the same storm (n
     virtual ranks, length-byte payloads, random originators) with every tree edge copying the bytes,
@@ -128,8 +152,13 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
     # iardj: the same consensus loop with the approve-all judge registered on the device
     # (RLO_progress_engine_new_dj, an extension; the reference judges with its callback only)
     legs_ours = legs + [("iardj", ["iardj", "2000"]), ("iarpool", ["iarpool", "8000"])]
+    avail = len(os.sched_getaffinity(0))
     for nr in ranks:
-        rec = {"ranks": nr, "ours": {}, "reference_host_mpi": {}, "cores": nr}
+        # the reference: one rank per core, pinned (BASELINE.md CPU-baseline plan); ours unpinned, since a
+        # GPU leader process runs the application thread beside its pump and proxy threads
+        rec = {"ranks": nr, "ours": {}, "reference_host_mpi": {}, "cores": nr, "cores_available": avail,
+               "pinning": {"reference_host_mpi": "mpiexec -bind-to core: one core per rank (%d cores)" % nr,
+                           "ours": "none (%d cores available; the GPU does the engine's work)" % avail}}
         for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
             if not os.path.exists(exe):
                 rec[name] = {"error": "not built"}
@@ -139,7 +168,8 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150):
                 try:
                     # iarpool: the proposal pool extension, 16 own proposals in flight per rank
                     env = dict(os.environ, RLO_PROPOSAL_POOL="16") if leg == "iarpool" else None
-                    r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec, "-n", str(nr), exe] + args,
+                    bind = ["-bind-to", "core"] if name == "reference_host_mpi" else []
+                    r = subprocess.run(["timeout", "-k", "5", str(timeout_s), mpiexec] + bind + ["-n", str(nr), exe] + args,
                                        stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20, env=env)
                     lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
                     rec[name][leg] = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
@@ -196,15 +226,43 @@ def size_legs(rlo, R, device, stream, sizes=(256, 1024, 4096), k=1 << 16, steps=
 
 
 def _step(w, stream, dist):
-    """one launch of the loaded program; every part reset before any part launches"""
-    w.reset(stream)
+    """one launch of the loaded program; every part reset before any part launches.  Never raises
+    between its two barriers: a part whose reset / launch / wait fails still joins both (its peers'
+    kernels then stop at their no-progress timeout), so the parts stay in step -- an exception here
+    once left one part in the next leg's collectives while its peer waited in this one's"""
+    err = None
+    try:
+        w.reset(stream)
+    except Exception as e:  # noqa: BLE001 - reported, the parts stay in step
+        err = e
     if dist is not None:
         dist.barrier()
-    w.launch(stream, no_reset=True)
-    rc = w.wait(raise_on_device_error=False)
+    rc = -99
+    if err is None:
+        try:
+            w.launch(stream, no_reset=True)
+            rc = w.wait(raise_on_device_error=False)
+        except Exception as e:  # noqa: BLE001
+            err = e
     if dist is not None:
         dist.barrier()  # no peer still stores into this part's rings / heaps
+    if err is not None:
+        note("part %d: step failed: %r" % (w.info.get("part", -1), err))
+        return rc, 0.0
     return rc, w.kernel_ms()
+
+
+def _agree(dist, world, err):
+    """every part learns every part's error (None = fine); raises on all of them if any failed"""
+    if world == 1:
+        if err:
+            raise RuntimeError(err)
+        return
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    bad = [e for e in errs if e]
+    if bad:
+        raise RuntimeError("; ".join(bad))
 
 
 def _world(rlo, dist, R, world, rank, local, **kw):
@@ -215,14 +273,14 @@ def _world(rlo, dist, R, world, rank, local, **kw):
         return rlo.World(R, device=local, **kw)
     if os.environ.get("RLO_BENCH_DEVICE") and kw.get("bulk_max") and not kw.get("movers"):
         kw["movers"] = 16
-    # every part learns whether every other part was made: a part that failed alone would otherwise
-    # leave its peers waiting in this exchange while it moves on to the next leg's (the ranks desync)
+    # every part learns whether every other part was made and connected: a part that failed alone would
+    # otherwise leave its peers waiting in this exchange while it moves on to the next leg's (the ranks desync)
     w, err = None, None
     try:
         w = rlo.World.part(R, world, rank, device=local, uncached=True, **kw)
         mine = w.export()
     except Exception as e:  # noqa: BLE001 - re-raised below, on every rank
-        err, mine = "rank %d: %r" % (rank, e), None
+        err, mine = "rank %d: create/export: %r" % (rank, e), None
     blobs = [None] * world
     dist.all_gather_object(blobs, (mine, err))
     errs = [e for _, e in blobs if e]
@@ -230,7 +288,15 @@ def _world(rlo, dist, R, world, rank, local, **kw):
         if w is not None:
             w.close()
         raise RuntimeError("world part creation failed: " + "; ".join(errs))
-    w.connect([b for b, _ in blobs])
+    try:
+        w.connect([b for b, _ in blobs])
+    except Exception as e:  # noqa: BLE001
+        err = "rank %d: connect: %r" % (rank, e)
+    try:
+        _agree(dist, world, err)
+    except Exception:
+        w.close()
+        raise
     return w
 
 
@@ -263,6 +329,7 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
                 sums.append(st["bcast_sum"].copy())
                 kms.append(ms)
             ok &= bool(np.array_equal(sums[0], sums[1]))
+            dump_leg("bulk_%dMiB" % mib, w, st, seed=0xB0 + mib, rounds=rounds, len=nbytes)
             rt = 0.0
             if w.rank_begin == 0:  # world rank 0's clock saw every round complete
                 obs = w.round_ticks().astype(np.float64)
@@ -336,6 +403,7 @@ def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3, 
             if i:
                 kms.append(ms)
         dt = red((time.perf_counter() - t0) / steps, "max")
+        dump_leg("c5", w, st, seed=seed, k=k, lo=lo, hi=hi, order=1, world_ranks=R)
         ok &= int(red(float(st["originated"].sum()), "sum")) == k
         ok &= int(red(float(st["bcast_delivered"].sum()), "sum")) == k * (R - 1)
         ok &= all(np.array_equal(sums[0], x) for x in sums[1:])
@@ -406,11 +474,12 @@ def reference_datapoint(length, ranks=8):
     try:
         with tempfile.TemporaryDirectory() as td:
             out = os.path.join(td, "o.jsonl")
-            subprocess.run(["timeout", "-k", "5", "100", mpiexec, "-n", str(ranks), exe, out, "bench", "2000",
-                            str(length)], cwd=td, timeout=120, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           check=True)
+            subprocess.run(["timeout", "-k", "5", "100", mpiexec, "-bind-to", "core", "-n", str(ranks), exe, out, "bench",
+                            "2000", str(length)], cwd=td, timeout=120, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL, check=True)
             rec = json.loads(open(out).read().splitlines()[0])
             rec["cores"] = ranks
+            rec["pinning"] = "mpiexec -bind-to core: one core per rank"
             rec["kind"] = "reference"
             return rec
     except Exception as e:  # noqa: BLE001 - informative only
@@ -433,7 +502,10 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
     ap.add_argument("--no-api", action="store_true", help="skip the drop-in rootless_ops.h API leg")
     ap.add_argument("--no-bulk", action="store_true", help="skip the large-message leg (vs RCCL at N > 1)")
+    ap.add_argument("--dump", default="", help="directory: every rank writes its ranks' per-leg statistics there "
+                                                "(tests/test_gpu_multigpu.py checks them against the oracle)")
     args = ap.parse_args()
+    _DUMP["dir"] = args.dump
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -538,6 +610,7 @@ def main():
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     st = w.stats()
+    dump_leg("storm", w, st, seed=seed, k=k, len=length, world_ranks=R)
     ok &= bool((st["error"] == 0).all())
     copies = world if mode == "replicas" else 1  # independent worlds each run the whole storm
     ok &= int(sum_over_ranks(float(st["originated"].sum()))) == k * copies
@@ -567,6 +640,7 @@ def main():
         # picked up round i
         w.program_latency(args.lat_rounds, length, seed=17)
         step()
+        dump_leg("latency", w, w.stats(), seed=17, rounds=args.lat_rounds, len=length)
         if world == 1 or mode == "replicas":
             # one-way: origination -> last pickup, both on this GPU's clock
             lat_us = w.latencies_ticks().astype(np.float64) * 0.01
@@ -603,6 +677,7 @@ def main():
         barrier()
         idt = max_over_ranks(time.perf_counter() - t1)
         ist = w.stats()
+        dump_leg("iar", w, ist, p=p)
         extras["decisions_per_s"] = round(R * p * copies / idt, 1)
         extras["decisions_kernel_ms"] = round(max_over_ranks(ims), 3)
         ok &= rc == 0 and int(sum_over_ranks(float(ist["own_decided"].sum()))) == R * p * copies
@@ -712,6 +787,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         note("cpu baseline")
         line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds)
+    dump_write(rank)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

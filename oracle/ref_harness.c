@@ -23,6 +23,7 @@
  *   bench  K LEN                 storm throughput: every rank originates K bcasts
  *   lat    ROUNDS LEN SEED       unloaded latency: one random originator per round
  *   iarbench P                   every rank keeps one outstanding proposal, approve-all
+ *   setupfail LEN, twice O D     drop-in only: engine setup failure, a second submission (see below)
  */
 #include "rootless_ops.h"
 #include "rlo_testvec.h"
@@ -323,6 +324,56 @@ static void mode_pool(int per, unsigned mask) {
 }
 #endif
 
+#ifdef RLO_DROPIN
+/* drop-in robustness (no reference counterpart).
+ * setupfail LEN: the first engine's setup fails after its kernels were launched (RLO_FAULT_ATTACH names
+ * the rank whose attach fails): every rank must get NULL back, promptly (the leaders stop their kernels);
+ * then the process builds a second engine and runs mode_parents on it. */
+static void mode_parents(int len);
+static void mode_setupfail(int len) {
+    RLO_engine_t* e = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, NULL, NULL, NULL);
+    emit("{\"ev\":\"first\",\"rank\":%d,\"ok\":%d}", g_rank, e != NULL);
+    if (e) RLO_progress_engine_cleanup(e);
+    unsetenv("RLO_FAULT_ATTACH");
+    MPI_Barrier(MPI_COMM_WORLD);
+    mode_parents(len);
+}
+
+/* twice ORIGIN DECLINER: with one own proposal per engine (no pool), ORIGIN submits "first" and, before
+ * it is decided, "second", which DECLINER declines.  my_own_proposal is then the second one
+ * (rootless_ops.c:878-883, votes count only for its pid, :756): the result ORIGIN reads must be the
+ * second proposal's (0), never the first's (1). */
+static int judge_second_cb(const void* arg, void* ctx) {
+    MaskCtx* c = (MaskCtx*)ctx;
+    return (arg && !strcmp((const char*)arg, "second") && ((c->mask >> c->rank) & 1u)) ? 0 : 1;
+}
+static void mode_twice(int origin, int decliner) {
+    MaskCtx ctx = {1u << decliner, g_rank};
+    RLO_engine_t* eng = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, &judge_second_cb, &ctx, NULL);
+    MPI_Barrier(MPI_COMM_WORLD);
+    if (g_rank == origin) {
+        RLO_submit_proposal(eng, "first", 5, 501);
+        RLO_submit_proposal(eng, "second", 6, 502);
+        while (RLO_check_proposal_state(eng, 502) != RLO_COMPLETED) RLO_make_progress_all();
+        emit("{\"ev\":\"result\",\"rank\":%d,\"vote\":%d}", g_rank, RLO_get_vote_my_proposal(eng));
+    } else {
+        int done = 0;
+        while (!done) {
+            RLO_make_progress_all();
+            RLO_user_msg* u = NULL;
+            while (RLO_user_pickup_next(eng, &u)) {
+                if (u->type == RLO_IAR_DECISION) {
+                    emit("{\"ev\":\"decision\",\"rank\":%d,\"pid\":%d,\"vote\":%d}", g_rank, u->pid, u->vote);
+                    if (u->pid == 502) done = 1;
+                }
+                RLO_user_msg_recycle(eng, u);
+            }
+        }
+    }
+    RLO_progress_engine_cleanup(eng);
+}
+#endif
+
 /* ---------------------------------------------------------------- multi */
 static int judge_isp_log_cb(const void* arg, void* ctx) {
     int r = is_proposal_approved_cb(arg, ctx);
@@ -607,6 +658,10 @@ int main(int argc, char** argv) {
 #endif
 #ifdef RLO_HAVE_PROPOSAL_POOL
     else if (!strcmp(mode, "pool")) mode_pool(atoi(argv[3]), (unsigned)strtoul(argv[4], 0, 0));
+#endif
+#ifdef RLO_DROPIN
+    else if (!strcmp(mode, "setupfail")) mode_setupfail(atoi(argv[3]));
+    else if (!strcmp(mode, "twice")) mode_twice(atoi(argv[3]), atoi(argv[4]));
 #endif
     else if (!strcmp(mode, "tests")) mode_tests();
     else if (!strcmp(mode, "tests_safe")) mode_tests_safe();

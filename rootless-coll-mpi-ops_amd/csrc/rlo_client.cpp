@@ -195,8 +195,10 @@ int rlo_client_bulk_put(rlo_client_t* c, const void* data, uint64_t len, uint32_
         const uint64_t n = len - off < win ? len - off : win;
         std::memcpy(c->stage, (const uint8_t*)data + off, n);
         rc = request(c, rlo::SHM_OP_PUT, (uint32_t)q, off, n, nullptr);
-        if (rc != RLO_OK) return rc;
+        if (rc != RLO_OK) return rc;  // q stays free: the next attempt acquires it again
     }
+    rc = request(c, rlo::SHM_OP_COMMIT, (uint32_t)q, 0, 0, nullptr);
+    if (rc != RLO_OK) return rc;
     *q_out = (uint32_t)q;
     return RLO_OK;
 }

@@ -231,7 +231,6 @@ struct Params {
     uint64_t* jfree;                // [2][jslots] generation: slot j % J takes sub-job j once jfree == j / J
     uint32_t* jdone;                // [2][jslots] finished tiles of the slot's job
     uint64_t* jsum;                 // [2][jslots] VERIFY checksum accumulator
-    uint32_t* bshadow;              // [n_local][kMaxPend][8] global copies of the pending-reception records
     uint32_t storm_order;           // RLO_ORDER_SLOTS: bcast b originates at b mod N
     uint32_t host_judge;            // host mode: 1 = judges are the host's callbacks, 0 = the device registry
 };
@@ -279,8 +278,15 @@ struct BulkJob {         // 64 B, one slot of a part's job ring: one SUB-job (co
 static_assert(sizeof(BulkJob) == 64, "job slot");
 
 // part-local job-ring control words (each on its own 128-B line): [cls*16 + 0] jobs posted,
-// [cls*16 + 8] head (first job not fully claimed), [32] exited progress workgroups
-constexpr int kJctlPost = 0, kJctlClaim = 8, kJctlExited = 32, kJctlWords = 48;
+// [cls*16 + 8] head (first job not fully claimed), [32] exited progress workgroups; then diagnostics
+// (rlo_bulk_debug): tiles finished per class, gather tiles that waited / passed their wait, the sink
+// line an out-of-range flag index is redirected to (posts by job kind follow it), slot releases,
+// bulk originations that waited for a slot, the last gather wait, and the first fault record (the
+// bulk guards' site-specific detail, written once)
+constexpr int kJctlPost = 0, kJctlClaim = 8, kJctlExited = 32;
+constexpr int kJctlTilesDone = 36, kJctlGatherWaited = 38, kJctlGatherPassed = 39, kJctlSink = 40,
+              kJctlPostsByKind = 40, kJctlReleases = 44, kJctlSlotWaits = 45, kJctlLastGather = 46,
+              kJctlFault = 47, kJctlWords = 48;
 
 // stripe / chunk / tile plan of a bulk message: a pure function of (N, len, cross-GPU), so every
 // rank derives the same one (cross: parts span GPUs -> pipelined chunks, ~sqrt(len / 4 MiB) of

@@ -561,14 +561,14 @@ __device__ __forceinline__ uint8_t* bulk_heap(const Params& P, int r, int o, uin
     return reinterpret_cast<uint8_t*>(P.bheap[p]) + ((lr * (uint64_t)P.n + (uint64_t)o) * P.bulk_slots + s) * P.bulk_cap;
 }
 __device__ __forceinline__ uint32_t* bulk_flags(const Params& P, int r, int o, uint32_t s) {
-    if (!bulk_ok(P, r, o, s, 2)) return reinterpret_cast<uint32_t*>(P.jctl + 40);
+    if (!bulk_ok(P, r, o, s, 2)) return reinterpret_cast<uint32_t*>(P.jctl + kJctlSink);
     const int p = P.part_of[r];
     const uint64_t lr = (uint64_t)(r - P.part_begin[p]);
     return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(P.bflag[p]) +
                                        ((lr * (uint64_t)P.n + (uint64_t)o) * P.bulk_slots + s) * kBulkLine);
 }
 __device__ __forceinline__ uint64_t* bulk_done(const Params& P, int o, uint32_t s) {
-    if (!bulk_ok(P, o, o, s, 3)) return P.jctl + 40;
+    if (!bulk_ok(P, o, o, s, 3)) return P.jctl + kJctlSink;
     const int p = P.part_of[o];
     const uint64_t lr = (uint64_t)(o - P.part_begin[p]), nlp = (uint64_t)(P.part_begin[p + 1] - P.part_begin[p]);
     return reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(P.bflag[p]) +
@@ -599,11 +599,11 @@ __device__ __forceinline__ void bulk_acquire(bool sys) {
 // every receiver did this): RLO_user_msg_recycle of a bulk delivery (rootless_ops.c:981-992)
 __device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o, uint32_t s, bool sys,
                                                   uint32_t want = 0u, uint32_t bid = 0u) {
-    atomicAdd((unsigned long long*)&P.jctl[44], 1ull);  // diagnostics: releases
+    atomicAdd((unsigned long long*)&P.jctl[kJctlReleases], 1ull);  // diagnostics: releases
     uint32_t* f = bulk_flags(P, r, o, s);
     if (want) {  // the reception must be complete here: a release mid-reception would lose it
         const uint32_t tf = bflag_ld(f + kBulkTflag, sys);
-        if (tf < want && atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+        if (tf < want && atomicCAS((unsigned long long*)&P.jctl[kJctlFault], 0ull,
                                    (0xEEull << 56) | ((uint64_t)(r & 0xff) << 48) | ((uint64_t)(o & 0xff) << 40) |
                                        ((uint64_t)(s & 0xf) << 36) | ((uint64_t)(bid & 0xfff) << 24) | ((tf & 0xfffu) << 12) |
                                        (want & 0xfffu)) == 0ull)
@@ -632,7 +632,7 @@ __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t
     }
     const uint32_t per = (ntiles + kMaxSub - 1u) / kMaxSub, nsub = (ntiles + per - 1u) / per;
     const uint64_t j0 = atomicAdd((unsigned long long*)&P.jctl[cls * 16 + kJctlPost], (unsigned long long)nsub);
-    atomicAdd((unsigned long long*)&P.jctl[40 + kind], 1ull);  // diagnostics: posts by kind (41..43)
+    atomicAdd((unsigned long long*)&P.jctl[kJctlPostsByKind + kind], 1ull);  // diagnostics: posts by kind (41..43)
     const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
     const uint64_t t0 = now_ticks();
     for (uint32_t u = 0; u < nsub; u++) {
@@ -811,8 +811,8 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                         const uint32_t want = bulk_tiles_of(pl, slen);
                         uint32_t spins = 0;
                         if (bflag_ld(f + c, sys) < want) {  // diagnostics: gather tiles waiting now / last wait
-                            atomicAdd((unsigned long long*)&P.jctl[38], 1ull);
-                            P.jctl[46] = ((uint64_t)(uint32_t)o << 48) | ((uint64_t)me << 32) | ((uint64_t)s << 24) | want;
+                            atomicAdd((unsigned long long*)&P.jctl[kJctlGatherWaited], 1ull);
+                            P.jctl[kJctlLastGather] = ((uint64_t)(uint32_t)o << 48) | ((uint64_t)me << 32) | ((uint64_t)s << 24) | want;
                         }
                         while (bflag_ld(f + c, sys) < want) {
                             __builtin_amdgcn_s_sleep(1);
@@ -823,7 +823,7 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                         }
                         const uint64_t key = ((uint64_t)jb.seq << 8) | c;
                         if (key != acq_key) { bulk_acquire(sys); acq_key = key; }
-                        atomicAdd((unsigned long long*)&P.jctl[39], 1ull);  // diagnostics: gather waits passed
+                        atomicAdd((unsigned long long*)&P.jctl[kJctlGatherPassed], 1ull);  // diagnostics: gather waits passed
                     }
                     __syncthreads();
                     const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
@@ -893,7 +893,7 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
             }
         }
         // ---- sub-job finished
-        if (tid == 0) atomicAdd((unsigned long long*)&P.jctl[36 + cls], (unsigned long long)jb.ntiles);  // diagnostics
+        if (tid == 0) atomicAdd((unsigned long long*)&P.jctl[kJctlTilesDone + cls], (unsigned long long)jb.ntiles);  // diagnostics
         if (jb.kind == JOB_VERIFY) {
             __syncthreads();  // every wave's tile sums are in S.mv_sum
             if (tid == 0) {
@@ -1233,18 +1233,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             const int o = (int)(e / bsl);
                             const uint32_t sl = e % bsl;
                             const BulkPend pe = bpend[e];
-                            {  // the LDS record must still be what registration wrote
-                                const u32x4* sh = reinterpret_cast<const u32x4*>(P.bshadow + ((size_t)lr * kMaxPend + e) * 8u);
-                                const u32x4 a = sh[0], b = sh[1];
-                                const uint32_t bad = (a.x != pe.bid) | ((a.y != pe.len) << 1) | ((a.z != pe.ntiles) << 2) |
-                                                     ((a.w != (uint32_t)pe.from) << 3) | ((b.x != pe.t0) << 4) | ((b.y != pe.q) << 5) |
-                                                     ((b.z != pe.pad0) << 6);
-                                if (bad && atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
-                                                     (0xDDull << 56) | ((uint64_t)(me & 0xff) << 48) | ((uint64_t)(e & 0xff) << 40) |
-                                                         ((uint64_t)(bad & 0x7f) << 32) | ((uint64_t)(a.x & 0xffff) << 16) |
-                                                         (pe.bid & 0xffff)) == 0ull)
-                                    bulk_fault(P, 14, (e << 8) | bad);
-                            }
                             const uint32_t ob = atomicAnd(&S.b.bonw[e >> 5], ~(1u << (e & 31u)));
                             if (!((ob >> (e & 31u)) & 1u) || pe.pad0 != (0x5A000000u | ((uint32_t)o << 8) | sl))
                                 bulk_fault(P, 11, (e << 8) | (pe.pad0 & 0xffu));
@@ -1490,7 +1478,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const bool ok = !isb || S.b.sdone[q & (bsl - 1u)] >= (uint64_t)(q / bsl) * (uint64_t)(P.n - 1);
                         const uint64_t bad = __ballot((uint32_t)lane < ww && !ok);
                         if (bad) ww = (uint32_t)__builtin_ctzll(bad);
-                        if (bad && lane == 0) atomicAdd((unsigned long long*)&P.jctl[45], 1ull);  // diagnostics: slot waits
+                        if (bad && lane == 0) atomicAdd((unsigned long long*)&P.jctl[kJctlSlotWaits], 1ull);  // diagnostics: slot waits
                         if ((uint32_t)lane < ww) {
                             S.b.bq[lane] = isb ? q : ~0u;
                             S.b.blen[lane] = ln;
@@ -2096,7 +2084,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         {  // the same message announced here twice (it must arrive exactly once)
                             const BulkPend pv = bpend[e];
                             if (pv.pad0 == (0x5A000000u | ((uint32_t)origin << 8) | sl) && pv.bid == id &&
-                                atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+                                atomicCAS((unsigned long long*)&P.jctl[kJctlFault], 0ull,
                                           ((uint64_t)me << 56) | ((uint64_t)(e & 0xffu) << 48) | ((uint64_t)(id & 0xffffu) << 32) |
                                               ((uint64_t)(from & 0xffff) << 16) | (pv.from & 0xffff)) == 0ull)
                                 bulk_fault(P, 12, (e << 12) | (id & 0xfffu));
@@ -2105,7 +2093,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if ((ob >> (e & 31u)) & 1u) {  // still live: which message was, which one came
                             const BulkPend od = bpend[e];
                             const uint32_t tf = bflag_ld(bulk_flags(P, me, origin, sl) + kBulkTflag, sys);
-                            if (atomicCAS((unsigned long long*)&P.jctl[47], 0ull,
+                            if (atomicCAS((unsigned long long*)&P.jctl[kJctlFault], 0ull,
                                           ((uint64_t)me << 56) | ((uint64_t)(e & 0xffu) << 48) | ((uint64_t)(od.bid & 0xffffu) << 32) |
                                               ((uint64_t)(id & 0xffffu) << 16) | ((tf & 0xffu) << 8) | (od.ntiles & 0xffu)) == 0ull)
                                 bulk_fault(P, 10, (e << 12) | (id & 0xfffu));
@@ -2113,11 +2101,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const BulkPend np_ = BulkPend{id, dsc.x, bulk_total_tiles(pl, dsc.x) + nt, from, t0, dsc.y,
                                                       0x5A000000u | ((uint32_t)origin << 8) | sl, 0u};
                         bpend[e] = np_;
-                        {  // the guard's global copy (compared at completion)
-                            u32x4* sh = reinterpret_cast<u32x4*>(P.bshadow + ((size_t)lr * kMaxPend + e) * 8u);
-                            sh[0] = u32x4{np_.bid, np_.len, np_.ntiles, (uint32_t)np_.from};
-                            sh[1] = u32x4{np_.t0, np_.q, np_.pad0, np_.pad1};
-                        }
                         S.b.bact[atomicAdd(&S.b.nbact, 1u)] = e;
                         if (nt) post_job(P, JCLS_B, JOB_GATHER, origin, lr, sl, id, dsc.x, nt, from, ~0u, dsc.y, 0u);
                       }

@@ -27,9 +27,12 @@
 namespace rlo {
 
 constexpr uint32_t kShmMagic = 0x534f4c52u;  // "RLOS"
-constexpr uint32_t kShmVersion = 2;
+constexpr uint32_t kShmVersion = 3;
 
-enum ShmOp : uint32_t { SHM_OP_NONE = 0, SHM_OP_ACQUIRE = 1, SHM_OP_PUT = 2, SHM_OP_GET = 3 };
+// a bulk origination: ACQUIRE (the next bulk sequence q, once its heap slot is free; q is not taken
+// yet), PUT the bytes window by window, COMMIT q (taken: the announcement carries it).  A failed PUT
+// leaves q free for the next attempt, so no heap slot is ever lost to a half-staged message
+enum ShmOp : uint32_t { SHM_OP_NONE = 0, SHM_OP_ACQUIRE = 1, SHM_OP_PUT = 2, SHM_OP_GET = 3, SHM_OP_COMMIT = 4 };
 
 struct ShmHdr {
     uint32_t magic, version;
@@ -49,7 +52,7 @@ struct ShmHdr {
 struct ClientBox {
     alignas(128) uint64_t mtail;  // client: commands written into its `cmd` ring
     alignas(128) uint64_t req;    // client: bulk request sequence (request fields below valid)
-    uint32_t op, arg;             // ShmOp; ACQUIRE -, PUT q, GET origin << 8 | heap slot
+    uint32_t op, arg;             // ShmOp; ACQUIRE -, PUT q, GET origin << 8 | heap slot, COMMIT q
     uint64_t off, len;            // byte range of the message this request moves via `stage`
     alignas(128) uint64_t ack;    // leader: last request completed
     int64_t rc;                   // RLO_OK / RLO_E_AGAIN (ACQUIRE: slot still busy) / error

@@ -35,6 +35,20 @@ namespace {
 
 thread_local int g_last_hip = 0;
 
+// A/B and diagnostic switches from the environment (RLO_WAVES, RLO_NSMALL, RLO_CACHED_RINGS, RLO_LAZY_PUB,
+// RLO_NO_IDLE_SPIN, RLO_NO_ACQUIRE, RLO_NO_FAST, RLO_BIG_PIPE, RLO_HOST_DIAG, RLO_BAR_CMDS,
+// RLO_NO_HDP_FLUSH) exist only in the diagnostics build (make DIAG=1 -> lib_diag/, -DRLO_DIAG): some of
+// them are unsafe by design (RLO_NO_ACQUIRE drops an acquire, RLO_CACHED_RINGS brings back rings that
+// failed rarely), so the product library reads none of them
+const char* diag_env(const char* name) {
+#ifdef RLO_DIAG
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 #define HIPCHK(x)                                  \
     do {                                           \
         hipError_t e_ = (x);                       \
@@ -404,10 +418,10 @@ int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
 
 // job-ring memory of a part (uncached, part-local): [jobs 2J x 64 B][jctl][jclaim 2J][jfree 2J][jdone 2J][jsum 2J]
 struct JobMem {
-    uint64_t jobs, jctl, jclaim, jfree, jdone, jsum, shadow, bytes;
+    uint64_t jobs, jctl, jclaim, jfree, jdone, jsum, bytes;
 };
-// + shadow: [nl][kMaxPend] copies of the pending-reception records (a guard against LDS corruption)
 JobMem job_mem(uint32_t J, uint32_t nl) {
+    (void)nl;
     JobMem m;
     m.jobs = 0;
     m.jctl = m.jobs + 2ull * J * sizeof(rlo::BulkJob);
@@ -415,8 +429,7 @@ JobMem job_mem(uint32_t J, uint32_t nl) {
     m.jfree = m.jclaim + 2ull * J * 8;
     m.jdone = m.jfree + 2ull * J * 8;
     m.jsum = (m.jdone + 2ull * J * 4 + 127) & ~127ull;
-    m.shadow = m.jsum + 2ull * J * 8;
-    m.bytes = m.shadow + (uint64_t)nl * rlo::kMaxPend * 32;
+    m.bytes = m.jsum + 2ull * J * 8;
     return m;
 }
 
@@ -442,7 +455,7 @@ int size_lds_variant(rlo_world* w, int variant) {
     // path -- and leave the LDS to the large-message rounds: 4 KiB storm 109 -> 104 ms, 1 KiB 40.4 -> 38.4,
     // profiles/r2s4_nsmall_ab.txt)
     uint32_t ns0 = L.stride / 16u <= 24u ? L.stride / 16u : 5u;
-    if (const char* e = std::getenv("RLO_NSMALL"))  // A/B: staged chunks per candidate in large-slot worlds
+    if (const char* e = diag_env("RLO_NSMALL"))  // A/B: staged chunks per candidate in large-slot worlds
         if (L.stride / 16u > 24u) ns0 = std::max(2u, std::min(8u, (uint32_t)std::atoi(e)));
     for (uint32_t ns = ns0; ns >= 1 && !ok; ns--) {
         // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
@@ -474,7 +487,7 @@ int size_lds_variant(rlo_world* w, int variant) {
 // bcast/s with 8 waves, but 256 B .. 4 KiB 30-40 % slower).  RLO_WAVES=4 / 8 forces one (A/B)
 int size_lds(rlo_world* w) {
     if (w->L.bulk_max) return size_lds_variant(w, 5);  // bulk worlds: the 4-wave kernel with movers
-    const char* env = std::getenv("RLO_WAVES");
+    const char* env = diag_env("RLO_WAVES");
     const int force = env ? std::atoi(env) : 0;
     const bool small = w->L.stride <= 8u * 16u;
     if (force != 4 && (small || force == 8) && w->nl <= w->cus && size_lds_variant(w, 8) == RLO_OK) return RLO_OK;
@@ -593,7 +606,7 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     // line of ring memory left in some XCD's L2 by an earlier kernel (the creation / reset fill) is
     // not invalidated by another XCD's write-through stores, and a consumer on that XCD read the
     // zeros (seen as unmarked slot headers that never became visible).  RLO_CACHED_RINGS=1: A/B only
-    if (!std::getenv("RLO_CACHED_RINGS")) w->flags |= RLO_PART_UNCACHED;
+    if (!diag_env("RLO_CACHED_RINGS")) w->flags |= RLO_PART_UNCACHED;
     {
         const uint32_t pp = cfg->proposal_pool ? cfg->proposal_pool : 2u;
         if ((pp & (pp - 1u)) || pp > (uint32_t)rlo::kPoolMax) { delete w; return RLO_E_INVAL; }
@@ -911,7 +924,6 @@ static void base_params(rlo_world* w) {
         P.jfree = reinterpret_cast<uint64_t*>(w->jmem + m.jfree);
         P.jdone = reinterpret_cast<uint32_t*>(w->jmem + m.jdone);
         P.jsum = reinterpret_cast<uint64_t*>(w->jmem + m.jsum);
-        P.bshadow = reinterpret_cast<uint32_t*>(w->jmem + m.shadow);
     }
 }
 
@@ -1240,7 +1252,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     // VRAM written by the CPU through the BAR -- a local poll, but in some runs such a store stayed
     // invisible to the polling kernel for 0.5-2 ms, every round (profiles/r2_dropin_split_legs.txt:
     // forwarded -> consumed; the kernel itself drained each command within 20 us of seeing it)
-    w->cmd_host = std::getenv("RLO_BAR_CMDS") == nullptr;
+    w->cmd_host = diag_env("RLO_BAR_CMDS") == nullptr;
     const int arc = w->cmd_host ? (host_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) ||
                                    host_alloc((void**)&w->d_ctl, nl * rlo::kHctlWords * 8))
                                 : (bar_alloc((void**)&w->h_cmd, nl * cc * w->L.stride) ||
@@ -1250,7 +1262,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
         return RLO_E_HIP;
     }
     w->hdp = nullptr;
-    if (!w->cmd_host && !std::getenv("RLO_NO_HDP_FLUSH")) {  // A/B switch; the attribute returns the register's mapped address
+    if (!w->cmd_host && !diag_env("RLO_NO_HDP_FLUSH")) {  // A/B switch; the attribute returns the register's mapped address
         uint32_t* reg = nullptr;
         if (hipDeviceGetAttribute(reinterpret_cast<int*>(&reg), hipDeviceAttributeHdpMemFlushCntl, w->device) == hipSuccess)
             w->hdp = reg;
@@ -1300,10 +1312,15 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payl
     const int lr = rank - w->rb;
     uint64_t* ctl = w->h_ctl + (size_t)lr * rlo::kHctlWords;
     uint64_t* dctl = w->d_ctl + (size_t)lr * rlo::kHctlWords;
-    const uint64_t tail = w->cmd_tail[lr];
+    // shared service with commands in host memory (rlo_program_host "direct"): the kernel reads the
+    // rank's own command ring and counter in the segment, so a command the leader posts itself (the
+    // QUIT of a failed engine setup) goes there, behind whatever the rank's client posted
+    const bool direct = w->shm && w->cmd_host;
+    rlo::ClientBox* box = direct ? (rlo::ClientBox*)(w->shm + w->SL.cli) + lr : nullptr;
+    const uint64_t tail = direct ? __atomic_load_n(&box->mtail, __ATOMIC_ACQUIRE) : w->cmd_tail[lr];
     const uint64_t head = __atomic_load_n(&ctl[rlo::kHctlInjHead], __ATOMIC_ACQUIRE);
     if (tail - head >= w->cmd_cap) return RLO_E_AGAIN;
-    uint8_t* slot = w->h_cmd + ((size_t)lr * w->cmd_cap + (tail & (w->cmd_cap - 1))) * w->L.stride;
+    uint8_t* slot = (direct ? w->shm + w->SL.cmd : w->h_cmd) + ((size_t)lr * w->cmd_cap + (tail & (w->cmd_cap - 1))) * w->L.stride;
     uint32_t hdr[4];
     hdr[0] = (uint32_t)(c->origin & 0xffff) | ((c->kind & 0xffu) << 16) | ((uint32_t)(c->vote & 0xff) << 24);
     hdr[1] = (uint32_t)c->id;
@@ -1311,6 +1328,10 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payl
     hdr[3] = 0;
     std::memcpy(slot, hdr, sizeof hdr);
     if (len) std::memcpy(slot + rlo::kHdr, payload, len);
+    if (direct) {
+        __atomic_store_n(&box->mtail, tail + 1, __ATOMIC_RELEASE);
+        return RLO_OK;
+    }
     w->cmd_tail[lr] = tail + 1;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);  // BAR stores may be write-combined: slot before tail
     __atomic_store_n(&dctl[rlo::kHctlInjTail], tail + 1, __ATOMIC_RELEASE);
@@ -1333,6 +1354,10 @@ int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, ui
         std::memcpy(payload, w->h_evp + ((size_t)lr * w->pk_cap + i) * w->max_payload, n);
     }
     w->pk_head[lr] = head + 1;
+    if (w->shm && w->cmd_host) {  // direct mode: the kernel polls the pickup head in the rank's ClientBox
+        __atomic_store_n(&((rlo::ClientBox*)(w->shm + w->SL.cli) + lr)->mpk, head + 1, __ATOMIC_RELEASE);
+        return 1;
+    }
     __atomic_store_n(&w->d_ctl[(size_t)lr * rlo::kHctlWords + rlo::kHctlPkHead], head + 1, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);  // a write-combined BAR store would otherwise linger
     hdp_flush(w);
@@ -1411,27 +1436,27 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     HIPCHK(hipEventRecord(w->ev0, s));
     // diagnostic A/B switch: publish producer counters after the next poll instead of at the end
     // of the iteration that drained the stores
-    static const bool lazy = std::getenv("RLO_LAZY_PUB") != nullptr;
+    static const bool lazy = diag_env("RLO_LAZY_PUB") != nullptr;
     if (lazy) w->P.mode |= rlo::MODE_LAZYPUB;
     else w->P.mode &= ~rlo::MODE_LAZYPUB;
-    static const bool nospin = std::getenv("RLO_NO_IDLE_SPIN") != nullptr;  // diagnostic
+    static const bool nospin = diag_env("RLO_NO_IDLE_SPIN") != nullptr;  // diagnostic
     if (nospin) w->P.mode |= rlo::MODE_NOSPIN;
     else w->P.mode &= ~rlo::MODE_NOSPIN;
-    static const bool noacq = std::getenv("RLO_NO_ACQUIRE") != nullptr;  // diagnostic A/B, unsafe
+    static const bool noacq = diag_env("RLO_NO_ACQUIRE") != nullptr;  // diagnostic A/B, unsafe
     if (noacq) w->P.mode |= rlo::MODE_NOACQ;
     else w->P.mode &= ~rlo::MODE_NOACQ;
-    static const bool nofast = std::getenv("RLO_NO_FAST") != nullptr;  // A/B: no lone-message fast path
+    static const bool nofast = diag_env("RLO_NO_FAST") != nullptr;  // A/B: no lone-message fast path
     if (nofast) w->P.mode |= rlo::MODE_NOFAST;
     else w->P.mode &= ~rlo::MODE_NOFAST;
     // A/B: large-message staging rounds pipelined over two halves of stage2 (measured slower than whole
     // rounds: 4 KiB storm 122 vs 109 ms, profiles/r2s4_pipe_ab.txt)
     static const bool pipe = [] {
-        const char* e = std::getenv("RLO_BIG_PIPE");
+        const char* e = diag_env("RLO_BIG_PIPE");
         return e && std::atoi(e) != 0;
     }();
     if (pipe) w->P.mode |= rlo::MODE_PIPE;
     else w->P.mode &= ~rlo::MODE_PIPE;
-    static const bool hdiag = std::getenv("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
+    static const bool hdiag = diag_env("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
     if (hdiag) w->P.mode |= rlo::MODE_HDIAG;
     else w->P.mode &= ~rlo::MODE_HDIAG;
     hipError_t e = rlo_launch_progress(&w->P, w->nl + (w->L.bulk_max ? (int)w->nmov : 0), w->dyn_lds, s, w->variant);
@@ -1712,12 +1737,11 @@ int rlo_host_proxy(rlo_world_t* w) {
             const uint64_t need = (uint64_t)(q / B) * (uint64_t)(w->L.n - 1);
             const volatile uint64_t* done = reinterpret_cast<const volatile uint64_t*>(
                 w->bflag + ((uint64_t)w->nl * w->L.n * B + (uint64_t)lr * B + s) * rlo::kBulkLine);
-            if (*done >= need) {
-                w->host_bulk_q[lr] = q + 1;
-                box->q = q;
-            } else {
-                rc = RLO_E_AGAIN;  // receivers still hold the slot's previous message
-            }
+            if (*done >= need) box->q = q;  // taken only by COMMIT, once the bytes are staged
+            else rc = RLO_E_AGAIN;          // receivers still hold the slot's previous message
+        } else if (box->op == rlo::SHM_OP_COMMIT) {
+            if (box->arg == w->host_bulk_q[lr]) w->host_bulk_q[lr]++;
+            else rc = RLO_E_INVAL;
         } else if (box->op == rlo::SHM_OP_PUT || box->op == rlo::SHM_OP_GET) {
             const bool put = box->op == rlo::SHM_OP_PUT;
             const uint32_t origin = put ? (uint32_t)rank : box->arg >> 8;

@@ -379,10 +379,13 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
                 e->max_prop_ns = std::max(e->max_prop_ns, d);
             }
             e->n_result++;
+            e->sent_bcast++;  // a decision counts as a sent bcast (:1600)
+            // only the result of the proposal my_own_proposal holds: a second submission while the first
+            // is in flight overwrote it (:878-883), and the reference counts votes only for that pid (:756)
+            if ((int)ev.id != e->own.pid) break;
             e->own.vote = ev.vote;
             e->own.votes_recved = e->own.votes_needed;
             e->own.state = RLO_COMPLETED;
-            e->sent_bcast++;  // a decision counts as a sent bcast (:1600)
             break;
         }
         case RLO_EV_JUDGE: {  // judge(proposal data, ctx) (:698); data is zero-padded like the
@@ -797,14 +800,28 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
         if (const char* sd = std::getenv("RLO_DEVICE")) return std::atoi(sd) % ndev;
         return e->size <= ndev ? r : (int)((int64_t)r * ndev / e->size);
     };
-    e->device = dev_of(e->rank);
-    std::vector<int> part_begin;  // contiguous blocks of ranks per GPU
-    for (int r = 0; r < e->size; r++)
-        if (r == 0 || dev_of(r) != dev_of(r - 1)) part_begin.push_back(r);
+    // RLO_PARTS=k: deal the ranks into k contiguous parts (k leaders, k persistent kernels, ring
+    // mappings exchanged between the leaders) even where they share a GPU -- the multi-part engine an
+    // 8-GPU node runs, exercised on one GPU.  Every rank must see the same k (the largest is taken)
+    int kparts = 0;
+    {
+        int mine = 0;
+        if (const char* sp = std::getenv("RLO_PARTS")) mine = std::max(0, std::atoi(sp));
+        MPI_Allreduce(&mine, &kparts, 1, MPI_INT, MPI_MAX, e->comm);
+        kparts = std::min(kparts, e->size);
+    }
+    std::vector<int> part_begin;  // contiguous blocks of ranks: one per GPU, or RLO_PARTS of them
+    if (kparts > 0) {
+        for (int p = 0; p < kparts; p++) part_begin.push_back((int)((int64_t)e->size * p / kparts));
+    } else {
+        for (int r = 0; r < e->size; r++)
+            if (r == 0 || dev_of(r) != dev_of(r - 1)) part_begin.push_back(r);
+    }
     const int n_parts = (int)part_begin.size();
     part_begin.push_back(e->size);
     int part = 0;
     while (part_begin[part + 1] <= e->rank) part++;
+    e->device = dev_of(part_begin[part]);  // a part's ranks share its leader's GPU
     e->leader = e->rank == part_begin[part];
     MPI_Comm_split(e->comm, part, e->rank, &e->group);
     MPI_Comm leaders;
@@ -937,6 +954,10 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     setup_trace(e->rank, "launched+started");
     if (ok) {  // members map their ranks through the leader's segment
         MPI_Bcast(shm_name, (int)sizeof shm_name, MPI_CHAR, 0, e->group);
+        // RLO_FAULT_ATTACH=r (fault injection for tests): rank r's attach fails, after every kernel was
+        // launched -- the path on which the leaders must stop their serving kernels cleanly
+        const char* fa = std::getenv("RLO_FAULT_ATTACH");
+        if (fa && std::atoi(fa) == e->rank) shm_name[1] = '!';
         rc = rlo_client_attach(shm_name, e->rank, &e->cl);
         ok = agree(rc == RLO_OK);
         if (e->leader) rlo_host_unlink(e->w);  // every client attached (or gave up): drop the name
@@ -1116,13 +1137,18 @@ int RLO_bcast_gen(RLO_engine_t* eng, RLO_msg_t* msg_in, enum RLO_COMM_TAGS tag) 
     if (msg_in->ext) {  // extension: a bulk bcast -- its bytes into my heap slot once the slot is free
         uint32_t q = 0;
         int rc;
+        // my heap slot is free once every receiver released its previous message; they do so while they
+        // make progress, which they may be waiting on me for (a bounded wait, then the engine fails)
+        const int64_t t0 = now_ns();
         while ((rc = rlo_client_bulk_put(eng->cl, msg_in->ext, msg_in->ext_len, 0, &q)) == RLO_E_AGAIN) {
             RLO_make_progress_all();
             if (eng->failed) return -1;
+            if (now_ns() - t0 > 60ll * 1000000000ll) { rc = RLO_E_TIMEOUT; break; }
         }
         if (rc != RLO_OK) {
             std::fprintf(stderr, "rlo: rank %d: bulk bcast of %zu bytes failed: %s\n", eng->rank, msg_in->ext_len,
                          rlo_strerror(rc));
+            if (rc != RLO_E_INVAL) eng->failed = true;  // the service itself failed (a bad argument leaves it usable)
             return -1;
         }
         const uint32_t desc[4] = {(uint32_t)msg_in->ext_len, q, 0u, 0u};

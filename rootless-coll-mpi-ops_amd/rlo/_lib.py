@@ -9,10 +9,10 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
-# RLO_LIB_AB (tools/gpu_lib_ab.sh): an A/B build of an earlier commit, honoured only under tools/ab_libs/
-_AB = os.environ.get("RLO_LIB_AB")
-if _AB and os.path.realpath(_AB).startswith(os.path.join(os.path.dirname(PKG_DIR), "tools", "ab_libs") + os.sep):
-    LIB_PATH = os.path.realpath(_AB)
+# RLO_DIAG_LIB=1: the diagnostics build (make DIAG=1 -> lib_diag/), whose library honours the A/B
+# environment switches the product library ignores (rlo_world.cpp diag_env)
+if os.environ.get("RLO_DIAG_LIB") == "1":
+    LIB_PATH = os.path.join(PKG_DIR, "lib_diag", "librlo_hip.so")
 
 RLO_OK = 0
 RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6

@@ -6,7 +6,7 @@ run_processes(): one spawned process per part; blobs are exchanged through a que
                  regions are mapped with hipIpc (dmabuf), launches start after a barrier
                  that follows every part's reset.
 A program spec is a dict: {"kind": "storm", "k", "len", "seed", "window", "log", "len_max", "order"} or
-{"kind": "iar", "props": [(origin, pid, bytes)], "judge", "mask", "isp", "seed", "ppm", "log"} or
+{"kind": "iar", "props": [(origin, pid, bytes)], "judge", "mask", "isp", "seed", "ppm", "log", "pool"} or
 {"kind": "lat", "rounds", "len", "seed"} (the round word lives in part 0; st["round_ticks"] is world
 rank 0's clock at each round's completion).
 """
@@ -29,7 +29,7 @@ def _program(w, spec):
         from . import _lib as L
         w.program_iar(spec["props"], judge=spec.get("judge", L.RLO_JUDGE_APPROVE), mask=spec.get("mask"),
                       isp=spec.get("isp"), seed=spec.get("seed", 0), ppm=spec.get("ppm", 0),
-                      log=spec.get("log", False), log_cap=spec.get("log_cap", 0))
+                      log=spec.get("log", False), log_cap=spec.get("log_cap", 0), pool=spec.get("pool", 1))
     elif spec["kind"] == "lat":
         w.program_latency(spec["rounds"], spec["len"], seed=spec.get("seed", 0x5EED))
     else:

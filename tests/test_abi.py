@@ -174,7 +174,7 @@ def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
     os.ftruncate(fd, total)
     m = mmap.mmap(fd, total)
     os.close(fd)
-    hdr = struct.pack("<10I9Q2I", 0, 2, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
+    hdr = struct.pack("<10I9Q2I", 0, 3, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
                       off["cli"], off["cmd"], off["stage"], total, 0, 0)
     m[:len(hdr)] = hdr
     m[0:4] = struct.pack("<I", 0x534F4C52)  # magic last

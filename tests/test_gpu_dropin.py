@@ -198,3 +198,110 @@ def test_reference_testcases_pass_8_ranks(harness):
     """the same self-checking wrappers at 8 ranks"""
     got, text = capture.run(harness, 8, "tests_safe", timeout=80, want_stdout=True)
     check_results(got, text, 8, [dict(r, ret=1) for r in load("testcases.json")["results"]])
+
+
+# ---- one engine in several parts (RLO_PARTS=k): k leaders, k persistent kernels, ring mappings exchanged
+# between the leaders with MPI_Allgather (rootless_ops.cpp engine_new) -- the form every engine of an
+# 8-GPU node takes, exercised on one GPU.  One communicator is one engine (rootless_ops.c:1454-1468)
+# whatever its parts; every result must equal the reference's fixtures as in one part.
+def _parts_env(k):
+    return dict(os.environ, RLO_PARTS=str(k))
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_multi_part_engine_stream(harness, k):
+    for case in load("stream.json")["cases"]:
+        if case["n"] > MAXN or case["n"] < k:
+            continue
+        n = case["n"]
+        recs = capture.run(harness, n, "stream", case["seed"], case["k"], case["len"], timeout=80, env=_parts_env(k))
+        assert capture.stream(recs, n) == case["deliveries"], (k, n, case["seed"])
+
+
+@pytest.mark.parametrize("n", [5, 8])
+def test_multi_part_engine_parents(harness, n):
+    fx = load("parents.json")
+    got = capture.parents(capture.run(harness, n, "parents", fx["len"], timeout=80, env=_parts_env(2)), n)
+    assert got["parent"] == fx["by_n"][str(n)]["parent"]
+    assert got["hash"] == fx["by_n"][str(n)]["hash"]
+
+
+@pytest.mark.parametrize("case", [c for c in load("iar.json")["cases"] if c["n"] == 8][:6],
+                         ids=lambda c: "n%d-o%d-m%d" % (c["n"], c["origin"], c["mask"]))
+def test_multi_part_engine_iar(harness, case):
+    """proposal down the tree, votes back up, decision down again -- across the part boundary"""
+    got = capture.iar(capture.run(harness, case["n"], "iar", case["origin"], case["mask"], timeout=80,
+                                  env=_parts_env(2)))
+    for key in ("judge", "actions", "pickups", "decision"):
+        assert got[key] == case[key], key
+
+
+def test_multi_part_engine_tests2(harness):
+    """testcases.c's two-engines-per-process IAR tests, each engine in two parts"""
+    fx = load("testcases2.json")
+    got, text = capture.run(harness, fx["n"], "tests2", timeout=80, want_stdout=True, env=_parts_env(2))
+    check_results(got, text, fx["n"], fx["results"])
+
+
+def test_multi_part_engine_pool(harness):
+    """the proposal pool (16 in flight per rank) over three parts, against the pool oracle"""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    import pyoracle as orc
+
+    n, per, mask, depth = 8, 6, 0b10010000, 16
+    env = dict(_parts_env(3), RLO_PROPOSAL_POOL=str(depth))
+    recs = capture.run(harness, n, "pool", per, mask, timeout=80, env=env)
+    props = [(o, 1000 + i * n + o, ("p%d-r%d" % (i, o)).encode()) for i in range(per) for o in range(n)]
+    pid_of = {d.decode(): pid for (_, pid, d) in props}
+    cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=[(mask >> r) & 1 for r in range(n)])
+    ev = orc.iar(n, props, cfg, cap=1 << 20, pool=depth)
+    assert sorted((e[1], e[3], e[2] if not e[3] else -1) for e in ev if e[0] == orc.ORC_EV_JUDGE) == \
+        sorted((r["rank"], r["null"], pid_of[r["arg"]] if not r["null"] else -1) for r in recs if r["ev"] == "judge")
+    assert sorted((e[1], e[2], e[3], e[4]) for e in ev if e[0] == orc.ORC_EV_PICKUP) == \
+        sorted((r["rank"], r["pid"], r["vote"], r["origin"]) for r in recs if r["ev"] == "decision")
+    assert sorted((e[1], e[2], e[3]) for e in ev if e[0] == orc.ORC_EV_RESULT) == \
+        sorted((r["rank"], r["pid"], r["vote"]) for r in recs if r["ev"] == "result")
+
+
+def test_multi_part_engine_bulk(harness):
+    """bulk bcasts (beyond the 32,764-B data area) through a two-part drop-in engine"""
+    import pyoracle as orc
+
+    n, k, seed, lo, hi = 8, 24, 21, 64, 1 << 20
+    recs = capture.run(harness, n, "bulkstream", seed, k, lo, hi, timeout=120, env=_parts_env(2))
+    par = orc.storm(n, seed, k, lo, want_parent=True, len_max=hi, order=1)["parent"]
+    want = []
+    for b in range(k):
+        o, ln = b % n, orc.len_of(seed, b, lo, hi)
+        data = orc.payload(o, b, ln)
+        dl, h = (ln, orc.fnv1a(data)) if ln > 32764 else (0, orc.region_hash(data))
+        want += [(r, b, o, int(par[b, r]), dl, "%016x" % h) for r in range(n) if r != o]
+    got = [(x["rank"], x["bid"], x["origin"], x["parent"], x["len"], x["hash"]) for x in recs]
+    assert sorted(got) == sorted(want)
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_engine_setup_failure_is_clean(harness, k):
+    """a rank's attach fails after the leaders launched their kernels (RLO_FAULT_ATTACH): every rank gets
+    NULL back and the leaders stop their serving kernels through the ranks' own command rings (the
+    shared segment the kernel reads) -- then the same processes build a working engine"""
+    n = 5
+    env = dict(_parts_env(k), RLO_FAULT_ATTACH="3")
+    recs = capture.run(harness, n, "setupfail", 64, timeout=60, env=env)
+    first = [r for r in recs if r.get("ev") == "first"]
+    assert sorted(r["rank"] for r in first) == list(range(n)) and not any(r["ok"] for r in first), first
+    fx = load("parents.json")
+    got = capture.parents([r for r in recs if "ev" not in r], n)
+    assert got["parent"] == fx["by_n"][str(n)]["parent"]
+
+
+def test_second_submission_takes_over_own_proposal(harness):
+    """one own proposal per engine (no pool): a second RLO_submit_proposal while the first is in flight
+    becomes my_own_proposal; the result the originator reads is the second proposal's (declined here),
+    never the first one's (the pool-1 result path checks the pid)"""
+    n, origin, decliner = 4, 1, 3
+    recs = capture.run(harness, n, "twice", origin, decliner, timeout=60)
+    res = [r for r in recs if r["ev"] == "result"]
+    assert res == [{"ev": "result", "rank": origin, "vote": 0}], res
+    dec = {(r["rank"], r["pid"]): r["vote"] for r in recs if r["ev"] == "decision"}
+    assert all(dec.get((r, 502)) == 0 for r in range(n) if r != origin), dec

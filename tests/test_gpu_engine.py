@@ -277,47 +277,18 @@ def test_iar_concurrent_exact_sets(rlo, n, p, ppm, pool):
     the same pool depth): the judge-call set (rank, origin,
     pid, NULL arg, verdict), the action set, every decision pickup with its decision, and every
     originator's result."""
+    import iar_sets
+
     kind = rlo.abi.RLO_JUDGE_HASH if ppm else rlo.abi.RLO_JUDGE_APPROVE
-    props = [(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)]
     cap = 3 * n * p + 64
     with rlo.World(n, max_payload=32, proposal_pool=max(2, pool)) as w:
         assert w.info["proposal_pool"] == max(2, pool)
-        w.program_iar(props, judge=kind, seed=99, ppm=ppm, log=True, log_cap=cap, pool=pool)
+        w.program_iar(iar_sets.props(n, p), judge=kind, seed=99, ppm=ppm, log=True, log_cap=cap, pool=pool)
         w.run()
         st = w.stats()
-        logs = [w.log(r, cap=cap) for r in range(n)]
+        logs = {r: w.log(r, cap=cap) for r in range(n)}
     assert (st["error"] == 0).all(), st["error"]
-    cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_HASH, seed=99, ppm=ppm)
-    ev = orc.iar_rounds(n, p, cfg, pool=pool)
-    want = {"judge": set(), "action": set(), "pickup": set(), "result": set()}
-    for e, rank, pid, a, b, c in ev:
-        if e == orc.ORC_EV_JUDGE:
-            want["judge"].add((rank, c, pid, a, b))
-        elif e == orc.ORC_EV_ACTION:
-            want["action"].add((rank, c, pid))
-        elif e == orc.ORC_EV_PICKUP:
-            want["pickup"].add((rank, b, pid, a))
-        elif e == orc.ORC_EV_RESULT:
-            want["result"].add((rank, pid, a))
-    got = {"judge": set(), "action": set(), "pickup": set(), "result": set()}
-    counts = {k: 0 for k in got}
-    for r in range(n):
-        for kind_, tag, origin, frm, pid, ln, vote, aux, _ in logs[r]:
-            if kind_ == LOG_JUDGE:
-                got["judge"].add((r, origin, pid, aux, vote)); counts["judge"] += 1
-            elif kind_ == LOG_ACTION:
-                got["action"].add((r, origin, pid)); counts["action"] += 1
-            elif kind_ == LOG_DELIVER and tag == 4:
-                got["pickup"].add((r, origin, pid, vote)); counts["pickup"] += 1
-            elif kind_ == LOG_RESULT:
-                got["result"].add((r, pid, vote)); counts["result"] += 1
-    for k in want:
-        assert counts[k] == len(got[k]), (k, "duplicate records")
-        assert got[k] == want[k], (k, len(got[k]), len(want[k]), sorted(got[k] ^ want[k])[:6])
-    declined = sum(1 for (_, _, d) in want["result"] if d == 0)
-    assert len(want["result"]) == n * p
-    if 0 < ppm < 10000:
-        assert 0 < declined < n * p and want["action"], declined  # both outcomes exercised
+    iar_sets.check(logs, n, p, ppm, pool)
 
 
 def test_latency_program(rlo):

@@ -2,21 +2,26 @@
 N-part path is exercised here the way it runs there.
 
   * a part whose peer sits on another GPU (its exported blob names another PCI bus) switches to
-    system scope, and a cached part refuses to join such a world (rings and heaps that peers store
-    into over xGMI must be uncached);
+    system scope (rings and heaps are uncached in every world, so peers may store into them over xGMI);
   * bench.py --gpus 2 under torch.distributed.run (gloo control plane, both ranks on this GPU via
-    RLO_BENCH_DEVICE): one 128-rank world in two parts, the storm, latency, decisions, rootless bulk
-    and mixed-size legs, each verified.
+    RLO_BENCH_DEVICE): one 128-rank world in two parts -- the storm, latency, decisions, rootless bulk
+    and mixed-size legs of the driver's multi-GPU run, each part's per-rank statistics (bench.py
+    --dump) compared with the oracle: delivery counts and checksums per world rank, bulk checksums per
+    round, decision totals.
 """
 import json
 import os
+import shutil
 import re
 import signal
 import subprocess
 import sys
 import tempfile
 
+import numpy as np
 import pytest
+
+import pyoracle as orc
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -54,56 +59,105 @@ def test_cross_gpu_peer_switches_to_system_scope(rlo):
         w1.close()
 
 
-def test_cached_part_refuses_a_world_spanning_gpus(rlo):
-    """rings are uncached by default; the diagnostic RLO_CACHED_RINGS makes cached ones, which may
-    not join a world whose parts span GPUs"""
-    n = 8
-    os.environ["RLO_CACHED_RINGS"] = "1"
-    try:
-        c0 = rlo.World.part(n, 2, 0, max_payload=64)
-        c1 = rlo.World.part(n, 2, 1, max_payload=64)
-    finally:
-        del os.environ["RLO_CACHED_RINGS"]
-    try:
-        with pytest.raises(rlo.RloError):
-            c0.connect([c0.export(), _forge_bus(c1.export())])
-    finally:
-        c0.close()
-        c1.close()
+def _merged(recs, name):
+    """one leg's per-rank statistics of every part, by world rank"""
+    parts = sorted((r[name] for r in recs), key=lambda x: x["rank_begin"])
+    out = {"meta": parts[0]}
+    for f in ("bcast_delivered", "bcast_sum", "originated", "own_decided", "own_approved", "actions", "judge_calls",
+              "dec_delivered", "error"):
+        out[f] = np.array([v for p in parts for v in p[f]], dtype=np.uint64)
+    return out
+
+
+def _check_dump(d, parts):
+    recs = [json.load(open(os.path.join(d, "rank%d.json" % r))) for r in range(parts)]
+    # the storm: per world rank, deliveries and the checksum of every byte picked up
+    s = _merged(recs, "storm")
+    m = s["meta"]
+    exp = orc.storm_expected(m["world_ranks"], m["seed"], m["k"], m["len"])
+    assert (s["error"] == 0).all()
+    assert np.array_equal(s["bcast_delivered"].astype(np.int64), exp["count"])
+    assert np.array_equal(s["bcast_sum"], exp["sum"])
+    assert int(s["originated"].sum()) == m["k"]
+    # the latency program: one bcast per round from origin_of(seed, i), the storm's payloads
+    lt = _merged(recs, "latency")
+    m = lt["meta"]
+    exp = orc.storm_expected(len(lt["bcast_sum"]), m["seed"], m["rounds"], m["len"])
+    assert np.array_equal(lt["bcast_delivered"].astype(np.int64), exp["count"])
+    assert np.array_equal(lt["bcast_sum"], exp["sum"])
+    # decisions: one outstanding proposal per rank, approve-all (oracle totals)
+    ia = _merged(recs, "iar")
+    n = len(ia["own_decided"])
+    cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_APPROVE)
+    ref = orc.iar_bench(n, ia["meta"]["p"], cfg)
+    assert int(ia["own_decided"].sum()) == ref["decisions"] and int(ia["own_approved"].sum()) == ref["approved"]
+    assert int(ia["actions"].sum()) == ref["actions"] and int(ia["judge_calls"].sum()) == ref["judge_calls"]
+    assert (ia["dec_delivered"] == ia["meta"]["p"] * (n - 1)).all()
+    # rootless bulk rounds (one rank per part): every receiver's checksum of every round's bytes
+    bulk = [k for k in recs[0] if k.startswith("bulk_")]
+    assert bulk, recs[0].keys()
+    for name in bulk:
+        b = _merged(recs, name)
+        m = b["meta"]
+        g = len(b["bcast_sum"])
+        want, cnt = np.zeros(g, dtype=np.uint64), np.zeros(g, dtype=np.int64)
+        for i in range(m["rounds"]):
+            o = orc.origin_of(m["seed"], i, g)
+            cs = np.uint64(orc.msg_checksum(o, i, 0, orc.payload(o, i, m["len"])))
+            for r in range(g):
+                if r != o:
+                    want[r] += cs
+                    cnt[r] += 1
+        assert (b["error"] == 0).all(), name
+        assert np.array_equal(b["bcast_delivered"].astype(np.int64), cnt), name
+        assert np.array_equal(b["bcast_sum"], want), name
+    # C5: mixed 64 B .. 1 MiB, every rank originating in every slot
+    c5 = _merged(recs, "c5")
+    m = c5["meta"]
+    exp = orc.storm_expected(m["world_ranks"], m["seed"], m["k"], m["lo"], len_max=m["hi"], order=m["order"])
+    assert (c5["error"] == 0).all()
+    assert np.array_equal(c5["bcast_delivered"].astype(np.int64), exp["count"])
+    assert np.array_equal(c5["bcast_sum"], exp["sum"])
 
 
 def test_bench_two_parts_under_torchrun():
     env = dict(os.environ, RLO_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    dump = tempfile.mkdtemp(prefix="rlo_dump")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
            "--warmup", "1", "--ranks", "64", "--k", "16384", "--lat-rounds", "200", "--no-api", "--no-pmc",
-           "--no-cpu-baseline"]
+           "--no-cpu-baseline", "--dump", dump]
     # Bounded below the suite's per-test limit, output to files (torchrun's workers outlive a killed
     # agent's pipes), so a stall fails with the bench's own progress lines instead of a bare timeout
-    with tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
-        p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=fo, stderr=fe, start_new_session=True)
-        try:
-            p.wait(timeout=100)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGTERM)  # the agent stops its workers
+    try:
+        with tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
+            p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=fo, stderr=fe, start_new_session=True)
             try:
-                p.wait(timeout=20)
+                p.wait(timeout=100)
             except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
+                os.killpg(p.pid, signal.SIGTERM)  # the agent stops its workers
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                fe.seek(0)
+                ps = subprocess.run(["ps", "-eo", "pid,ppid,etime,stat,args"], stdout=subprocess.PIPE).stdout.decode()
+                pytest.fail("two-part bench stalled after 100 s; stderr tail:\n" + fe.read().decode()[-4000:] +
+                            "\nprocesses:\n" + ps[-4000:])
+            fo.seek(0)
             fe.seek(0)
-            ps = subprocess.run(["ps", "-eo", "pid,ppid,etime,stat,args"], stdout=subprocess.PIPE).stdout.decode()
-            pytest.fail("two-part bench stalled after 100 s; stderr tail:\n" + fe.read().decode()[-4000:] +
-                        "\nprocesses:\n" + ps[-4000:])
-        fo.seek(0)
-        fe.seek(0)
-        out, err = fo.read(), fe.read()
-    lines = [ln for ln in out.decode().splitlines() if ln.startswith("{")]
-    assert p.returncode == 0 and lines, err.decode()[-3000:]
-    line = json.loads(lines[-1])
-    assert line["n_gpus"] == 2 and line["mode"] == "sharded" and line["verified"], line
-    assert line["world_ranks"] == 128 and line["value"] > 0
-    assert "round_p50_us" in line and line["decisions_per_s"] > 0
-    bulk = line["bulk"]
-    assert "error" not in bulk and all(s["verified"] for s in bulk["sizes"]), bulk
-    c5 = line["c5_mixed"]
-    assert "error" not in c5 and c5["verified"], c5
+            out, err = fo.read(), fe.read()
+        lines = [ln for ln in out.decode().splitlines() if ln.startswith("{")]
+        assert p.returncode == 0 and lines, err.decode()[-3000:]
+        assert b"leg failed" not in err and b"step failed" not in err, err.decode()[-3000:]  # on either part
+        line = json.loads(lines[-1])
+        assert line["n_gpus"] == 2 and line["mode"] == "sharded" and line["verified"], line
+        assert line["world_ranks"] == 128 and line["value"] > 0
+        assert "round_p50_us" in line and line["decisions_per_s"] > 0
+        bulk = line["bulk"]
+        assert "error" not in bulk and all(s["verified"] for s in bulk["sizes"]), bulk
+        c5 = line["c5_mixed"]
+        assert "error" not in c5 and c5["verified"], c5
+        _check_dump(dump, 2)  # against the oracle, not only step-to-step repeatability
+    finally:
+        shutil.rmtree(dump, ignore_errors=True)

@@ -99,6 +99,42 @@ def test_iar_sharded_inprocess(rlo):
     assert (st["dec_delivered"] == (n - 1) * p).all()
 
 
+# C4 in the form an 8-GPU world takes: the parts of one world each run their own kernel, and proposals,
+# votes and decisions cross the part boundaries.  Exact sets per (origin, pid) against the pool oracle
+# (tests/iar_sets.py), not sums: a pid swap between two proposals fails.  ~5 % of proposals declined
+# (ppm per judge call sized for the world: 814 at 64 ranks, 3,400 at 16, 201 at 256)
+@pytest.mark.parametrize("n,bounds,p,ppm,pool", [(64, [0, 20, 64], 8, 814, 1), (64, [0, 32, 64], 24, 814, 16),
+                                                 (16, [0, 3, 16], 16, 50000, 4)])
+def test_iar_sharded_inprocess_exact_sets(rlo, n, bounds, p, ppm, pool):
+    import iar_sets
+    from rlo import sharded
+
+    cap = 3 * n * p + 64
+    spec = {"kind": "iar", "props": iar_sets.props(n, p), "judge": rlo.abi.RLO_JUDGE_HASH, "seed": 99, "ppm": ppm,
+            "log": True, "log_cap": cap, "pool": pool}
+    (st, logs, _), rcs = sharded.run_inprocess(n, bounds, spec, max_payload=32, proposal_pool=max(2, pool))
+    assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
+    assert (st["error"] == 0).all()
+    iar_sets.check(logs, n, p, ppm, pool)
+
+
+@pytest.mark.parametrize("n,bounds,p,ppm,pool", [(16, [0, 5, 11, 16], 12, 3400, 1), (16, [0, 8, 16], 32, 3400, 16),
+                                                 (256, [0, 64, 128, 192, 256], 4, 201, 4)])
+def test_iar_sharded_processes_exact_sets(rlo, n, bounds, p, ppm, pool):
+    """one process per part, rings and vote rings mapped across processes with hipIpc"""
+    import iar_sets
+    from rlo import sharded
+
+    cap = 3 * n * p + 64
+    spec = {"kind": "iar", "props": iar_sets.props(n, p), "judge": rlo.abi.RLO_JUDGE_HASH, "seed": 99, "ppm": ppm,
+            "log": True, "log_cap": cap, "pool": pool}
+    (st, logs, _), rcs = sharded.run_processes(n, bounds, spec, max_payload=32, uncached=True,
+                                               proposal_pool=max(2, pool))
+    assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
+    assert (st["error"] == 0).all()
+    iar_sets.check(logs, n, p, ppm, pool)
+
+
 @pytest.mark.parametrize("n,bounds,ln", [(16, [0, 8, 16], 64), (13, [0, 5, 9, 13], 200), (64, [0, 1, 32, 63, 64], 64),
                                          (256, [0, 64, 128, 192, 256], 64)])
 def test_storm_sharded_processes(rlo, n, bounds, ln):
