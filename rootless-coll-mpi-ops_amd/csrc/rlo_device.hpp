@@ -56,6 +56,7 @@ enum Mode : uint32_t {
     MODE_NOFAST = 2048u,  // A/B: every iteration takes the full path (no lone-message fast path)
     MODE_HDIAG = 4096u,   // diagnostic, host mode: command-wait counters into hctl[kHctlDiag..] at exit
     MODE_PIPE = 8192u,    // A/B: large-message staging rounds pipelined over two halves of stage2
+    MODE_LL = 16384u,     // doorbells (below): lone messages and originations hop without a counter round trip
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };
@@ -111,7 +112,28 @@ struct RankTopo {
     uint64_t vin_head[kMaxFanout];         // head word of the vote ring from child j, in the child's ctrl
     uint64_t in_base[kMaxIn];              // forward region of in-edge k's producer part (pulled payloads)
     uint32_t orig_data, orig_pad;          // pull worlds: my relay ring (byte offset in my part)
+    // doorbells (MODE_LL, below): word indices of my forward bells (in-edge k at + kBellWords k) and my
+    // vote bells (child j at + 2 j) in my part's ctrl region; the remote bells I ring, as addresses
+    uint32_t in_bell, vin_bell;
+    uint64_t out_bell[kMaxFanout];         // child j's forward bell for the edge (me -> child j)
+    uint64_t vout_bell[kMaxIn];            // the parent of in-edge k: its vote bell for me
 };
+
+// Doorbells (MODE_LL: the latency / IAR / host programs of worlds without bulk messages).  A message a
+// rank forwards on its own -- a lone ring message, a local origination -- is also written, data-tagged,
+// into the child's DOORBELL for the edge: one per directed edge (both virtual channels), kBellChunks
+// 16-B chunks (header + 112 B) as 32-B pairs of LL granules {d0, T, d1, T}, {d2, T, d3, T} where
+// T = (ring sequence + 1) | vc << 31.  Every 8-byte half carries T, so a reader that finds T in all of
+// them holds the message, whatever order the halves landed in (MI355X_MICROARCH.md handoff-1to1: the
+// data is the flag).  The consumer polls the bell beside its ring counters: a bell tagged with the
+// sequence at its ring head IS the head message -- no counter poll, no slot load, no producer drain on
+// the hop.  The ring slot and the counter are still written (a bell is overwritten by the next message
+// on the edge; whatever the consumer does not take from a bell it takes through the counter), so the
+// batched path is unchanged.  A vote bell (child -> parent) is one granule pair {origin | pseq << 16 |
+// vote << 24, T, pid, T}, T = vote sequence + 1.  Bells live in the ctrl region: uncached, mapped
+// across parts, zeroed at every launch (a tag of a previous launch can never match).
+constexpr uint32_t kBellChunks = 8;
+constexpr uint32_t kBellWords = 2 * kBellChunks * 2;  // 8-byte words per forward bell (256 B)
 
 struct RankStats {
     uint64_t bcast_delivered, bcast_sum, originated;
@@ -148,7 +170,8 @@ struct Params {
     uint8_t* vote_region;         // this part's vote in-rings
     uint32_t vote_region_bytes;
     uint32_t vote_cap;            // slots per vote ring (pow2), >= 2 * N
-    uint64_t* ctrl;               // this part's control words (tails / heads of its ranks)
+    uint64_t* ctrl;               // this part's control words (tails / heads of its ranks, doorbells)
+    uint32_t ctrl_bytes;
     uint32_t sys_scope;           // 1: some peer part is on another GPU -> system-scope remote stores
     uint32_t n_parts;
     uint32_t* err_flag[kMaxParts];// every part's error word (ctrl word 0 of each part)

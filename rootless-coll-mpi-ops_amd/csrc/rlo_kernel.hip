@@ -44,6 +44,7 @@ static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
 static constexpr uint32_t kIdleSpin = 256;  // tight re-polls after an idle iteration (~0.1 ms at most)
 static constexpr int kRelQ = 16;  // pull worlds: relay-ring release records (coalesced when full)
+static constexpr uint32_t kBellJudge = 3072;  // doorbell pass: a bell message's judge copy in the stage area
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -367,11 +368,12 @@ __device__ __forceinline__ uint32_t judge_hash(uint64_t seed, uint32_t rank, int
     return (uint32_t)(splitmix64(seed ^ ((uint64_t)rank << 32) ^ (uint32_t)pid) % 1000000u);
 }
 
-// device judge registry.  arg = proposal data at byte offset arg_off of the forward region,
-// data_len bytes, zero-extended (the reference's calloc'd receive buffer).  ISP restates
-// testcases.c:18-37.  The originator's final call passes NULL (:773): device judges approve it.
-__device__ __forceinline__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, uint32_t my_mask, int32_t pid,
-                          uint32_t arg_off, uint32_t data_len) {
+// device judge registry.  arg = proposal data (data_len bytes, zero-extended: the reference's calloc'd
+// receive buffer) read through byte_at(i) -- from the ring slot, or from LDS for a doorbell's message.
+// ISP restates testcases.c:18-37.  The originator's final call passes NULL (:773): device judges approve it.
+template <class F>
+__device__ __forceinline__ int judge_eval_f(const Params& P, int me, uint32_t my_mask, int32_t pid, F byte_at,
+                                            uint32_t data_len) {
     switch (P.judge_kind) {
         case JUDGE_MASK:
             return my_mask ? 0 : 1;
@@ -381,16 +383,20 @@ __device__ __forceinline__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_
             const char* mine = P.judge_isp + P.judge_isp_off[me];
             if (mine[0] == 0) return 1;
             for (uint32_t i = 0;; i++) {  // strcmp(mine, arg)
-                char a = i < data_len ? (char)ld8_sc1(rf, arg_off + i) : 0;
+                char a = i < data_len ? (char)byte_at(i) : 0;
                 if (a != mine[i]) break;
                 if (a == 0) return 1;
             }
-            char a0 = data_len ? (char)ld8_sc1(rf, arg_off) : 0;
+            char a0 = data_len ? (char)byte_at(0u) : 0;
             return ((signed char)a0 < (signed char)mine[0]) ? 0 : 1;
         }
         default:
             return 1;
     }
+}
+__device__ __forceinline__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_t rf, int me, uint32_t my_mask, int32_t pid,
+                                          uint32_t arg_off, uint32_t data_len) {
+    return judge_eval_f(P, me, my_mask, pid, [&](uint32_t i) { return ld8_sc1(rf, arg_off + i); }, data_len);
 }
 
 // one event record: the parity log (MODE_LOG, linear) or the host pickup ring (MODE_HOST, the
@@ -434,14 +440,29 @@ __device__ __forceinline__ bool own_has(const SH& S, const Params& P, int32_t pi
     return hit;
 }
 
-// vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741)
-template <class SH>
+// vote up towards the parent over in-edge k: one 16-byte write-through slot (_vote_back, :728-741),
+// and with doorbells (LLB) the parent's vote bell for this edge, tagged with the vote's sequence
+template <bool LLB, class SH>
 __device__ __forceinline__ void emit_vote(SH& S, const Params& P, int me, uint32_t k,
                                           int origin, int32_t pid, uint32_t pseq, int vote) {
     unsigned long long p = atomicAdd((unsigned long long*)&S.vout_tail[k], 1ull);
     if (p - S.vout_head[k] >= P.vote_cap) {
         set_error(S, P, ERR_VOTE_RING, k);
         return;
+    }
+    if (LLB && (P.mode & MODE_LL)) {  // {origin | pseq << 16 | vote << 24, T, pid, T}: every 8-B half tagged
+        const uint32_t T = (uint32_t)p + 1u;
+        uint64_t* b = reinterpret_cast<uint64_t*>(S.t.vout_bell[k]);
+        const uint64_t w0 = (uint64_t)(((uint32_t)origin & 0xffffu) | ((pseq & 0xffu) << 16) | ((uint32_t)(vote & 0xff) << 24)) |
+                            ((uint64_t)T << 32);
+        const uint64_t w1 = (uint64_t)(uint32_t)pid | ((uint64_t)T << 32);
+        if (P.sys_scope) {
+            __hip_atomic_store(b, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(b + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            __hip_atomic_store(b, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(b + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     const uint64_t lo = (uint64_t)((uint32_t)origin | ((uint32_t)(vote & 0xff) << 24)) | ((uint64_t)(uint32_t)pid << 32);
     const uint64_t hi = (uint64_t)(pseq & 0xffu) | ((uint64_t)(uint32_t)me << 32);
@@ -931,11 +952,11 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
 
 // ------------------------------------------------------------------ the kernel
 
-template <int W, bool BULK>
+template <int W, bool BULK, bool LL>
 __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // pulled payloads (Params.pull) exist only in the 4-wave kernel without bulk messages (slots beyond
     // the small copy path); compiled out of the others
-#define PULL_ON (W == 4 && !BULK && P.pull != 0u)
+#define PULL_ON (W == 4 && !BULK && !LL && P.pull != 0u)
     constexpr int kWaves = W, kBlock = 64 * W, kMaxCand = 64 * W;
     constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at the last 64 candidates
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
@@ -969,8 +990,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
     const int lr = blockIdx.x;
     const int me = P.rank_begin + lr;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const int tid = threadIdx.x, w = tid >> 6;
+    // the lane is re-derived every iteration (opaque to the compiler), so lane-derived values cannot be
+    // hoisted out of the main loop and held in registers for the whole launch: that took 246 / 254
+    // VGPRs (8 / 4 waves) down to 179 / 201, the bulk instantiation from 1 to 2 waves per SIMD, made
+    // room for the doorbell pass, and left the storm's speed as it was (profiles/r3_storm_ab.txt)
+    int lane = tid & 63;
+    uint64_t lt_mask = (1ull << lane) - 1ull;
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1;
@@ -1081,8 +1107,328 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint64_t n_iter = 0, n_busy = 0, n_stalls = 0;
     bool done_w0 = false;
     uint32_t rbase_r = 0, rtake_r = 0, noi_r = 0;  // lane g / oi: this iteration's selection, admitted counts
+    // doorbells (rlo_device.hpp, MODE_LL): on in this launch unless it profiles phases or A/Bs the fast path
+    const bool llm = LL && (P.mode & MODE_LL) && !(P.mode & (MODE_PROF | MODE_NOFAST));
+    const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);  // my part's ctrl region (my bells)
+    const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
+    bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
+
+    // a small message (lane q: slot chunk q, q < nch) into out-rings `need` at their tails: the ring slot,
+    // and with bells the child's doorbell for the edge, tagged (ring sequence + 1) | vc << 31.  The
+    // caller advances out_tail_r
+    auto fwd_small = [&](u32x4 v, uint32_t nch, uint32_t need) {
+        const uint32_t q = (uint32_t)lane;
+        for (uint32_t m = need; m; m &= m - 1) {
+            const int oi = __builtin_ctz(m);
+            const uint64_t slot = rdl64(out_tail_r, oi);
+            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
+            if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+            if (LL && llm && nch <= kBellChunks && q < nch) {
+                const uint32_t T = ((uint32_t)slot + 1u) | ((uint32_t)(oi & 1) << 31);
+                const __amdgpu_buffer_rsrc_t rb = mk_rsrc(reinterpret_cast<void*>(uni64(t.out_bell[oi >> 1])), kBellWords * 8u);
+                st_ring(rb, 32u * q, u32x4{v.x, T, v.y, T}, sys);
+                st_ring(rb, 32u * q + 16u, u32x4{v.z, T, v.w, T}, sys);
+            }
+        }
+    };
+
+    // ---- one lone small message by wave 0 alone: the fast path of phase C (loaded from its ring slot)
+    // and the doorbell pass of phase A (from a bell).  Lane q holds slot chunk q (q < nsmall); it came
+    // on in-ring fg.  Its effects restate phase F line for line, its forward is phase G's (fwd_small),
+    // when every out-ring it needs has room and it is no held proposal.  Returns the out-rings it went to
+    // (bit oi), or ~0u: then nothing changed and the full path takes it.  A proposal's data is judged from
+    // the ring slot (fsrc) or, for a bell's message, from its LDS copy (from_bell).  The doorbell pass
+    // borrows the stage area while the other waves wait at the barrier: bells' data at [0, 1 KiB), votes'
+    // at [1 KiB, 1.125 KiB), a bell message's judge copy at kBellJudge (the area is >= 4 KiB: 256 x 16 B)
+    auto lone = [&](u32x4 v, int fg, uint32_t fsrc, bool from_bell, uint64_t out_head_r) -> uint32_t {
+        const uint32_t q = (uint32_t)lane;
+        const int ffrom = uni(t.in_src[fg >> 1]);
+        const uint32_t fw0 = rdl32(v.x, 0), fid = rdl32(v.y, 0), fw2 = rdl32(v.z, 0), ft0 = rdl32(v.w, 0);
+        const int forg = (int)(fw0 & 0xffffu);
+        const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
+        const uint32_t fpseq = fw2 >> 24;
+        const int fvote = (int)(int8_t)(fw0 >> 24);
+        bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
+                  (ftag == TAG_BCAST || ftag == TAG_DECISION || (!host && ftag == TAG_PROPOSAL)) &&
+                  !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
+        int fjudge = 1;
+        uint32_t fkids = 0, fneed = 0;
+        if (ok) {
+            if (ftag == TAG_PROPOSAL) {  // device judge on the PBuf data (phase D)
+                uint32_t dl = nsmall > 1 ? rdl32(v.z, 1) : 0u;
+                if (dl > flen - 16u) dl = flen > 16u ? flen - 16u : 0u;
+                if (from_bell) {
+                    if (q < kBellChunks) *reinterpret_cast<u32x4*>(stage + kBellJudge + 16u * q) = v;
+                    const uint8_t* d = stage + kBellJudge + kHdr + 16u;
+                    fjudge = judge_eval_f(P, me, my_mask, (int32_t)fid, [&](uint32_t i) { return d[i]; }, dl);
+                } else {
+                    fjudge = judge_eval(P, rf, me, my_mask, (int32_t)fid, fsrc + kHdr + 16u, dl);
+                }
+                fkids = fjudge == 1 ? kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r) : 0u;
+            } else {
+                fkids = kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r);
+            }
+            fneed = need_of(fkids, forg, sll, sl_r);
+            const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
+            // a proposal whose pending entry still holds an earlier proposal of that pool slot
+            // goes the full path (held there until that one's decision was applied)
+            const bool held = ftag == TAG_PROPOSAL && PEND(forg, fpseq).valid != PS_NONE;
+            ok = __ballot(full) == 0 && !held;
+        }
+        if (!ok) return ~0u;
+        uint32_t flog = ~0u;
+        if (ftag == TAG_BCAST) {
+            if (lane == 0) {
+                atomicAdd(&S.bcast_delivered, 1ull);
+                if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
+                flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
+                               (uint32_t)now_ticks() - ft0);
+            }
+            flog = rdl32(flog, 0);
+            if (q < fnch)
+                acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)forg, fid, TAG_BCAST, flen})
+                                  : chunk_mix(q - 1u, v);
+        } else if (ftag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
+            if (lane == 0) {
+                atomicAdd(&S.proposals_recv, 1ull);
+                if (own_has(S, P, (int32_t)fid)) {
+                    set_error(S, P, ERR_PID_COLLISION, fid);  // :690-692
+                } else {
+                    const uint32_t k = (uint32_t)fg >> 1;
+                    atomicAdd(&S.judge_calls, 1ull);
+                    log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
+                    PendState* ps = &PEND(forg, fpseq);
+                    if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
+                        ps->valid = PS_NONE;
+                        emit_vote<LL>(S, P, me, k, forg, (int32_t)fid, fpseq, 0);
+                    } else {
+                        const uint32_t nk = (uint32_t)__builtin_popcount(fkids);
+                        ps->pid = (int32_t)fid;
+                        ps->word = 0;
+                        ps->parent_k = (uint16_t)k;
+                        ps->needed = (uint8_t)nk;
+                        ps->pseq = fpseq | ((flen - 16u) << 8);
+                        ps->valid = PS_ACTIVE;
+                        if (nk == 0) emit_vote<LL>(S, P, me, k, forg, (int32_t)fid, fpseq, 1);
+                    }
+                }
+            }
+        } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
+            PendState* ps = &PEND(forg, fpseq);
+            if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
+                if (fvote != 0) {
+                    atomicAdd(&S.actions, 1ull);
+                    log_put(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8);
+                }
+                ps->valid = PS_NONE;
+            }
+            atomicAdd(&S.dec_delivered, 1ull);
+            if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
+            log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
+        }
+        fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
+        if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
+            st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+        if (ftag == TAG_BCAST && (P.mode & MODE_LAT) && lane == 0) {  // the round's last pickup
+            const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[fid], 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_SYSTEM)
+                                     : atomicAdd(&P.lat_count[fid], 1u);
+            if (old + 1u == (uint32_t)(P.n - 1)) {
+                P.lat_out[fid] = (uint64_t)((uint32_t)now_ticks() - ft0);
+                if (sys) __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        return fneed;
+    };
+
+    // ---- a local origination by wave 0 alone (doorbell pass): header + chunks generated in registers,
+    // stored to every child when all out-rings have room.  Returns false (nothing changed) otherwise
+    auto originate = [&](uint32_t kind, uint32_t w0, uint32_t id, uint32_t w2, uint32_t src, uint64_t out_head_r) -> bool {
+        const uint32_t len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4;
+        if (nch > nsmall || nch > kBellChunks) return false;
+        const uint32_t need = need_of((1u << sll) - 1u, me, sll, sl_r);  // the whole send_list (:1587)
+        if (__ballot(lane < nout && ((need >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap)) return false;
+        const uint32_t q = (uint32_t)lane;
+        const uint32_t hw2 = (w2 & 0xff00ffffu) | (kSlotMark << 16);
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (q == 0) v = u32x4{w0, id, hw2, (uint32_t)now_ticks()};
+        else if (q < nch) v = gen_chunk(P, kind, me, id, len, src, (int)(int8_t)(w0 >> 24), q);
+        fwd_small(v, nch, need);
+        if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
+        return true;
+    };
+
+    // ---- the doorbell pass (MODE_LL), wave 0 in its poll loop while the other waves wait at the
+    // iteration barrier: every complete bell at its ring head (at most one per in-edge), every vote bell
+    // at its vote-ring head, then this rank's own originations (device programs) -- each as the lone fast
+    // path handles it, with no full iteration and no counter round trip on the hop.  Only while the
+    // counters show nothing else: a counter-visible message beside them belongs to the full path, and
+    // the bells' messages with it (through their counters).  Then one drain, and the counters are
+    // published (the eager scheme).  Returns the number of messages handled.
+    auto ll_pass = [&](u32x4 ba, u32x4 bb, u32x4 vb, uint64_t in_tail_r, uint64_t vin_tail_r, uint64_t out_head_r,
+                       uint64_t hpoll, uint32_t latr, uint32_t errf) -> uint32_t {
+        if (__ballot(errf != 0)) return 0u;
+        // the data words to LDS at once (registers are the kernel's scarcest resource): chunk q of in-edge
+        // k's bell at [16 (8 k + q)], child j's vote {word, pid} at [1024 + 8 j]
+        *reinterpret_cast<u32x4*>(stage + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
+        if (lane < sll) *reinterpret_cast<uint2*>(stage + 1024u + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
+        const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
+        const uint32_t lcap = min(nsmall, kBellChunks);
+        // in-ring (k, vc) whose head is h expects (h + 1) | vc << 31 in every half of every granule
+        const uint32_t e0 = (uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk)) + 1u;
+        const uint32_t e1 = ((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk + 1u)) + 1u) | 0x80000000u;
+        const bool inb = (int)bk < n_in;
+        const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
+        const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
+        const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;  // the header's chunks
+        const uint64_t gm = hn <= lcap ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
+        const bool g0 = bq == 0u && gm && (B0 & gm) == gm, g1 = bq == 0u && gm && (B1 & gm) == gm;
+        const uint64_t fh = __ballot(g0 || g1), fv = __ballot(g1);  // bit 8k: in-edge k's bell is whole (on vc fv)
+        const uint32_t evh = (uint32_t)vin_head_r + 1u;
+        const uint64_t vhm = __ballot(!host && lane < sll && vb.y == evh && vb.w == evh);
+        const int rk = lane >> 1;
+        const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
+        const uint64_t ip = lane < n_in2 && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
+        const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
+        if (__ballot(ip > (rhit ? 1ull : 0ull) || vp > (((vhm >> lane) & 1ull) ? 1ull : 0ull))) return 0u;
+        if (host) {  // commands waiting, or too little room in the pickup ring: the full path
+            if (rdl64(hpoll, 0) != S.hin_head) return 0u;
+            const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - rdl64(hpoll, 1));
+            if (pk_free < 2u * (uint32_t)__popcll(fh) + 2u * P.own_pool + 8u) return 0u;
+        }
+        const bool lat_go = (P.mode & MODE_LAT) && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next;
+        const bool iar_dev = (P.mode & MODE_IAR) && !host;
+        if (!fh && !vhm && !lat_go && !iar_dev) return 0u;
+        uint32_t done = 0;
+        // votes (_iar_vote_handler :743-812, _vote_merge :1056-1070): as phase B1
+        for (uint64_t m = vhm; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            const uint2 vv = *reinterpret_cast<const uint2*>(stage + 1024u + 8u * (uint32_t)j);
+            const uint32_t vw = vv.x;
+            const int32_t pid = (int32_t)vv.y;
+            const int origin = (int)(vw & 0xffffu);
+            const uint32_t pseq = (vw >> 16) & 0xffu;
+            const int vote = (int)(int8_t)(vw >> 24);
+            const uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
+            if (lane == 0) {
+                if (origin >= P.n) {
+                    set_error(S, P, ERR_BAD_SLOT, vw);
+                } else if (origin == me) {  // a vote for my own proposal (:756-783)
+                    const uint32_t k = pseq & (P.pend_slots - 1u);
+                    if (S.own_state[k] != 1 || pid != S.own_pid[k]) {
+                        set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+                    } else {
+                        const uint32_t nw = (S.own_word[k] += inc);
+                        if ((nw & 0xffffu) == S.own_needed) {
+                            const int d = (nw >> 16) == 0 ? 1 : 0;
+                            if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
+                                atomicAdd(&S.judge_calls, 1ull);
+                                log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                            }
+                            S.own_decision[k] = (uint32_t)d;
+                            S.own_state[k] = 2;
+                        }
+                    }
+                } else {
+                    PendState* ps = &PEND(origin, pseq);
+                    if (ps->valid != PS_ACTIVE || ps->pid != pid) {
+                        set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+                    } else {
+                        const uint32_t nw = (ps->word += inc);
+                        if ((nw & 0xffffu) == ps->needed)
+                            emit_vote<LL>(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+                    }
+                }
+            }
+            if (lane == j) vin_head_r++;
+            done++;
+        }
+        // the bells' ring messages, each at its ring head
+        for (uint64_t m = fh; m; m &= m - 1) {
+            const int b = __builtin_ctzll(m);  // 8 k
+            const int g = (b >> 2) + (int)((fv >> b) & 1ull);
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (lane < 8) v = *reinterpret_cast<const u32x4*>(stage + 16u * (uint32_t)(b + lane));
+            const uint32_t need = lone(v, g, 0u, true, out_head_r);
+            if (need == ~0u) continue;  // the full path takes it, through its counter
+            if (lane == g) in_head_r++;
+            if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
+            done++;
+        }
+        // my own originations: the pool's decisions, then its next proposals (device programs), or my
+        // latency round
+        if (iar_dev) {
+            const uint32_t ps_ = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
+            for (uint64_t dm = __ballot(ps_ == 2u); dm; dm &= dm - 1) {  // _iar_decision_bcast :908-917
+                const uint32_t k = (uint32_t)__builtin_ctzll(dm);
+                const uint32_t id = (uint32_t)S.own_pid[k], dec = S.own_decision[k];
+                if (!originate(K_DEC, (uint32_t)me | (TAG_DECISION << 16) | ((dec & 0xffu) << 24), id, 23u | (k << 24), 0u,
+                               out_head_r))
+                    break;
+                if (lane == 0) {
+                    atomicAdd(&S.own_decided, 1ull);
+                    if (dec) atomicAdd(&S.own_approved, 1ull);
+                    log_put(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, k);
+                    S.own_state[k] = 0;
+                    S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
+                }
+                done++;
+            }
+            for (;;) {  // RLO_submit_proposal :876-906, up to own_pool in flight
+                const uint32_t ps2 = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
+                const uint64_t busy = __ballot(ps2 != 0u);
+                if (S.own_iter >= (unsigned long long)S.own_n || (uint32_t)__popcll(busy) >= P.own_pool) break;
+                uint32_t k = S.own_rr;
+                while ((busy >> k) & 1ull) k = (k + 1u) & (P.pend_slots - 1u);
+                const int64_t pi = P.prop_off[lr] + (int64_t)S.own_iter;
+                const uint32_t id = (uint32_t)P.prop_pid[pi];
+                if (!originate(K_PROP, (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id,
+                               (16u + P.prop_data_len[pi]) | (k << 24), (uint32_t)pi, out_head_r))
+                    break;
+                if (lane == 0) {  // proposalPool_proposal_add (:1253-1279)
+                    S.own_pid[k] = (int32_t)id;
+                    S.own_word[k] = 0;
+                    S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
+                    S.own_state[k] = 1;
+                    S.own_iter++;
+                    S.own_rr = (k + 1u) & (P.pend_slots - 1u);
+                }
+                done++;
+            }
+        }
+        if (lat_go && originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), S.lat_own_next, P.len, 0u,
+                                out_head_r)) {
+            if (lane == 0) {
+                atomicAdd(&S.originated, 1ull);
+                const uint32_t np = S.lat_pos + 1u;
+                S.lat_pos = np;
+                S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
+            }
+            done++;
+        }
+        if (!done) return 0u;
+        // every store of the pass drained, then the counters (the eager scheme's publish)
+        VM_DRAIN();
+        if (lane < nout && out_tail_r != PUB_OUT) { PUB_OUT = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
+        if (lane < n_in2 && in_head_r != PUB_IN) { PUB_IN = in_head_r; pub64(IHPTR, in_head_r, sys); }
+        if (lane < sll && vin_head_r != PUB_VIN) { PUB_VIN = vin_head_r; pub64(VHPTR, vin_head_r, sys); }
+        if (lane < n_in) {
+            const uint64_t vt = S.vout_tail[lane];
+            if (vt != PUB_VOUT) { PUB_VOUT = vt; pub64(VTPTR, vt, sys); }
+        }
+        if (host && lane == 0 && S.ev_n) {
+            S.pk_tail += S.ev_n;
+            S.log_count += S.ev_n;
+            S.ev_n = 0;
+            pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
+        }
+        return done;
+    };
 
     for (;;) {
+        asm volatile("" : "+v"(lane));  // (see lane's declaration)
+        lt_mask = (1ull << lane) - 1ull;
         // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
         uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
         uint32_t errf = 0, sid = 0, latr = 0;
@@ -1091,6 +1437,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // polled word moves (the other waves wait at the barrier): a message arriving at an
             // idle rank is seen one poll round trip later instead of after a whole idle iteration.
             // Bounded, so the idle clock and the deadline still tick.
+            uint32_t ll_run = 0;
             for (uint32_t sp = 0;; sp++) {
                 // host mode: the host-written counters (pinned host memory: a PCIe read, ~1 us more than
                 // the ring polls) on every 4th re-poll only, so an idle rank still sees a ring message
@@ -1106,6 +1453,24 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if ((P.mode & MODE_LAT) && lane == 1)  // the round in progress (part 0's word when sharded)
                     latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                : poll32(P.lat_round);
+                if constexpr (LL) {
+                    if (llm) {  // my doorbells beside the counters: lane (k, q) chunk q of in-edge k's, lane j child j's vote
+                        const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
+                        u32x4 ba = {0u, 0u, 0u, 0u}, bb = {0u, 0u, 0u, 0u}, vb = {0u, 0u, 0u, 0u};
+                        if ((int)bk < n_in) {
+                            const uint32_t o = (in_bell + bk * kBellWords) * 8u + 32u * bq;
+                            ba = ld_sc1(rc, o);
+                            bb = ld_sc1(rc, o + 16u);
+                        }
+                        if (!host && lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
+                        if (ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf)) {
+                            ll_prog = true;
+                            // keep serving bells from here; every 64 passes the full iteration's bookkeeping runs
+                            if (++ll_run < 64u) { sp = 0; continue; }
+                            break;
+                        }
+                    }
+                }
                 if (!idle_prev || sp >= kIdleSpin) break;
                 bool bmoved = false;
                 if constexpr (BULK) {  // a released heap slot of mine (a bulk origination may wait for it)
@@ -1115,9 +1480,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                       : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != S.b.sdone[lane];
                     }
                 }
-                const bool moved = in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] ||
-                                   out_head_r != S.snap[2][lane] || vout_head_r != S.snap[3][lane] || hpoll != p_h ||
-                                   latr != p_lat || errf != 0 || bmoved;
+                // with doorbells only new work counts: a counter that caught up with what the bells already
+                // delivered, credits (nothing waits for them in an idle iteration), another rank's round
+                const bool moved =
+                    llm ? (in_tail_r != S.snap[0][lane] && in_tail_r > in_head_r) ||
+                              (vin_tail_r != S.snap[1][lane] && vin_tail_r > vin_head_r) || hpoll != p_h ||
+                              (latr != p_lat && rdl32(latr, 1) == S.lat_own_next) || errf != 0
+                        : in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] || out_head_r != S.snap[2][lane] ||
+                              vout_head_r != S.snap[3][lane] || hpoll != p_h || latr != p_lat || errf != 0 || bmoved;
                 if (__ballot(moved)) break;
             }
             S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
@@ -1275,7 +1645,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
             }
             // votes to merge (wave 1), at most 256 per iteration: trim the ring prefixes
-            const uint32_t va = (lane < sll && !hblock) ? (uint32_t)min(vin_tail_r - vin_head_r, (uint64_t)256) : 0u;
+            // (a doorbell may have delivered beyond the counter: head > tail until the counter catches up)
+            const uint32_t va = (lane < sll && !hblock && vin_tail_r > vin_head_r) ? (uint32_t)min(vin_tail_r - vin_head_r, (uint64_t)256) : 0u;
             uint32_t vtot = 0, vex = 0;
             if (__ballot(va > 0)) vex = wave_excl_scan(va, &vtot);
             uint32_t vtake = va;
@@ -1286,7 +1657,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (lane < sll) { S.vbase[lane] = vex; S.va[lane] = vtake; S.vhead[lane] = vin_head_r; }
             vin_head_r += vtake;  // merged by wave 1 before the next publish
             // in-rings: fair per-ring quotas
-            const uint32_t ra = lane < n_in2 ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)kMaxCand) : 0u;
+            const uint32_t ra = lane < n_in2 && in_tail_r > in_head_r ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)kMaxCand) : 0u;
             const uint32_t reserve = host ? kPass + P.pend_slots : ((P.mode & MODE_IAR) ? P.pend_slots + 1u : 0u);  // host: stage block; the pool's originations
             const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
@@ -1456,7 +1827,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (nh) C = hbase + nh;
                 }
             }
-            if ((P.mode & MODE_STORM) && sched_next < sched_n) {
+            if (!LL && (P.mode & MODE_STORM) && sched_next < sched_n) {  // (no storm runs with doorbells)
                 // throttle: originate only into shallow out-rings so forwarding never waits behind originations
                 const bool deep = lane < nout && (out_tail_r - out_head_r) * 2 >= P.fwd_cap;
                 const bool allow = !backlog && R < 2 * kPass && __ballot(deep) == 0;
@@ -1503,119 +1874,22 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             // ---- lone-message fast path (wave 0 alone): exactly one candidate, a small ring bcast,
             // decision or proposal (device judge), no votes, and room in every out-ring it needs ->
-            // load it, apply its effects, store it to its children and drain, here; the other waves
-            // see C == 0 and skip to the bookkeeping.  (My own originations stay on the full path:
-            // built here too, out of line or inline, they tip the kernel over 256 VGPRs -- one wave
-            // per SIMD, and the all-ranks-co-resident check fails.)  A hop of the latency program or of an IAR round costs one slot
-            // load and one store drain instead of the full iteration's seven phases (~17K cycles,
-            // tools/lat_anatomy.py).  Effects restate phase F below line for line.
+            // load it, apply its effects, store it to its children and drain, here (lone(), above); the
+            // other waves see C == 0 and skip to the bookkeeping.  (My own originations stay on the full
+            // path here; the doorbell pass makes them.)  A hop of the latency program or of an IAR round
+            // costs one slot load and one store drain instead of the full iteration's seven phases (~17K
+            // cycles, tools/lat_anatomy.py).
             uint32_t fastdone = 0;
             // (host-service mode too, for bcasts and decisions -- its proposals take the full path for
             // the host-judge hold and the JUDGED events -- when the pickup ring has room for their events)
             if ((!host || hlim >= 2u) && R == 1u && C == 1u && vtot == 0u && !(P.mode & (MODE_PROF | MODE_NOFAST))) {
-                const uint32_t q = (uint32_t)lane;
                 const int fg = __builtin_ctzll(__ballot(lane < n_in2 && take > 0u));
                 const uint64_t h0 = rdl64(in_head_r, fg);
                 const uint32_t fsrc = (uint32_t)uni((int)t.in_data[fg >> 1][fg & 1]) + (uint32_t)(h0 & fcap_m) * P.fwd_stride;
                 u32x4 v = {0u, 0u, 0u, 0u};
-                if (q < nsmall) v = ld_sc1(rf, fsrc + 16u * q);  // header + payload, one trip
-                const int ffrom = uni(t.in_src[fg >> 1]);
-                const uint32_t fw0 = rdl32(v.x, 0), fid = rdl32(v.y, 0), fw2 = rdl32(v.z, 0), ft0 = rdl32(v.w, 0);
-                const int forg = (int)(fw0 & 0xffffu);
-                const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
-                const uint32_t fpseq = fw2 >> 24;
-                const int fvote = (int)(int8_t)(fw0 >> 24);
-                bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
-                     (ftag == TAG_BCAST || ftag == TAG_DECISION || (!host && ftag == TAG_PROPOSAL)) &&
-                     !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
-                int fjudge = 1;
-                uint32_t fkids = 0, fneed = 0;
-                if (ok) {
-                    if (ftag == TAG_PROPOSAL) {  // device judge on the PBuf data (phase D)
-                        uint32_t dl = nsmall > 1 ? rdl32(v.z, 1) : 0u;
-                        if (dl > flen - 16u) dl = flen > 16u ? flen - 16u : 0u;
-                        fjudge = judge_eval(P, rf, me, my_mask, (int32_t)fid, fsrc + kHdr + 16u, dl);
-                        fkids = fjudge == 1 ? kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r) : 0u;
-                    } else {
-                        fkids = kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r);
-                    }
-                    fneed = need_of(fkids, forg, sll, sl_r);
-                    const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
-                    // a proposal whose pending entry still holds an earlier proposal of that pool slot
-                    // goes the full path (held there until that one's decision was applied)
-                    const bool held = ftag == TAG_PROPOSAL && PEND(forg, fpseq).valid != PS_NONE;
-                    ok = __ballot(full) == 0 && !held;
-                }
-                if (ok) {
-                    uint32_t flog = ~0u;
-                    if (ftag == TAG_BCAST) {
-                        if (lane == 0) {
-                            atomicAdd(&S.bcast_delivered, 1ull);
-                            if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
-                            flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
-                                           (uint32_t)now_ticks() - ft0);
-                        }
-                        flog = rdl32(flog, 0);
-                        if (q < fnch)
-                            acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)forg, fid, TAG_BCAST, flen})
-                                              : chunk_mix(q - 1u, v);
-                    } else if (ftag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
-                        if (lane == 0) {
-                            atomicAdd(&S.proposals_recv, 1ull);
-                            if (own_has(S, P, (int32_t)fid)) {
-                                set_error(S, P, ERR_PID_COLLISION, fid);  // :690-692
-                            } else {
-                                const uint32_t k = (uint32_t)fg >> 1;
-                                atomicAdd(&S.judge_calls, 1ull);
-                                log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
-                                PendState* ps = &PEND(forg, fpseq);
-                                if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
-                                    ps->valid = PS_NONE;
-                                    emit_vote(S, P, me, k, forg, (int32_t)fid, fpseq, 0);
-                                } else {
-                                    const uint32_t nk = (uint32_t)__builtin_popcount(fkids);
-                                    ps->pid = (int32_t)fid;
-                                    ps->word = 0;
-                                    ps->parent_k = (uint16_t)k;
-                                    ps->needed = (uint8_t)nk;
-                                    ps->pseq = fpseq | ((flen - 16u) << 8);
-                                    ps->valid = PS_ACTIVE;
-                                    if (nk == 0) emit_vote(S, P, me, k, forg, (int32_t)fid, fpseq, 1);
-                                }
-                            }
-                        }
-                    } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
-                        PendState* ps = &PEND(forg, fpseq);
-                        if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
-                            if (fvote != 0) {
-                                atomicAdd(&S.actions, 1ull);
-                                log_put(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8);
-                            }
-                            ps->valid = PS_NONE;
-                        }
-                        atomicAdd(&S.dec_delivered, 1ull);
-                        if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
-                        log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
-                    }
-                    // forward: the same slot bytes into every needed out-ring (phase G)
-                    for (uint32_t m = fneed; m; m &= m - 1) {
-                        const int oi = __builtin_ctz(m);
-                        const uint64_t slot = rdl64(out_tail_r, oi);
-                        const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
-                        if (q < fnch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
-                    }
-                    if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
-                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
-                    if (ftag == TAG_BCAST && (P.mode & MODE_LAT) && lane == 0) {  // the round's last pickup
-                        const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[fid], 1u, __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_SYSTEM)
-                                                 : atomicAdd(&P.lat_count[fid], 1u);
-                        if (old + 1u == (uint32_t)(P.n - 1)) {
-                            P.lat_out[fid] = (uint64_t)((uint32_t)now_ticks() - ft0);
-                            if (sys) __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            else __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                    }
+                if ((uint32_t)lane < nsmall) v = ld_sc1(rf, fsrc + 16u * (uint32_t)lane);  // header + payload, one trip
+                const uint32_t fneed = lone(v, fg, fsrc, false, out_head_r);
+                if (fneed != ~0u) {
                     VM_DRAIN();  // wave 0's stores: published in the bookkeeping below
                     // the bookkeeping sees: in-ring g admitted its one message (rtake_r), these out-rings one each
                     noi_r = lane < nout ? ((fneed >> lane) & 1u) : 0u;
@@ -1628,11 +1902,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 S.ract = ract;
                 S.vtot = vtot;
                 S.R = R; S.C = C; S.nstorm = nstorm; S.storm_base = storm_base; S.loc_kind = loc_kind;
-                S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = fastdone;
+                S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = fastdone | (ll_prog ? 1u : 0u);
                 S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase; S.nchmax = 0;
                 S.exit_now = done_w0;
                 if (P.mode & MODE_PROF) S.dbg[0] += R;
             }
+            ll_prog = false;
         }
         BAR();  // selection visible
         PST(7, 3);
@@ -1757,7 +2032,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         } else {
                             const uint32_t nw = atomicAdd(&ps->word, inc) + inc;
                             if ((nw & 0xffffu) == ps->needed)
-                                emit_vote(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+                                emit_vote<LL>(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
                         }
                     }
                 }
@@ -2045,7 +2320,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             PendState* ps = &PEND(origin, pseq);
                             if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                                 ps->valid = PS_NONE;
-                                emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 0);
+                                emit_vote<LL>(S, P, me, (uint32_t)k, origin, pid, pseq, 0);
                             } else {
                                 const uint32_t nk = (uint32_t)__builtin_popcount(kids);
                                 ps->pid = pid;
@@ -2054,7 +2329,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 ps->needed = (uint8_t)nk;
                                 ps->pseq = pseq | ((len - 16u) << 8);
                                 ps->valid = PS_ACTIVE;
-                                if (nk == 0) emit_vote(S, P, me, (uint32_t)k, origin, pid, pseq, 1);
+                                if (nk == 0) emit_vote<LL>(S, P, me, (uint32_t)k, origin, pid, pseq, 1);
                             }
                         }
                     } else if (tag == TAG_DECISION) {  // :603-615, _iar_decision_handler :814-859
@@ -2191,7 +2466,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             PST(4, 7);
 
             // ---------------- G1: stage the first round of large-message groups (before any store)
-            const uint32_t nbig = S.nbig;
+            // (the doorbell instantiation runs programs whose every message takes the small path: the
+            // host sets MODE_LL only then, rlo_world.cpp ll_mode)
+            const uint32_t nbig = LL ? 0u : S.nbig;
             // staging rounds of all of stage2: load -> store -> wait.  (MODE_PIPE, A/B: two halves, round r+1's
             // loads in flight while round r is stored -- measured slower, the rounds halve)
             const bool pipe = s2_units >= 2u * kSubMax && (P.mode & MODE_PIPE);
@@ -2658,12 +2935,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 }  // namespace rlo
 
 // C-ABI launch shims used by rlo_world.cpp.  variant: 8 = 8 waves, 4 = 4 waves, 5 = 4 waves with
-// bulk messages (mover workgroups + mixed storm lengths); the Shared / LDS layout depends on it
-template <int W, bool B>
+// bulk messages (mover workgroups + mixed storm lengths); the Shared / LDS layout depends on it.  A
+// program with doorbells (MODE_LL: latency, IAR, host service -- never in bulk worlds) runs the
+// doorbell instantiation of its variant, the storm the one without (its registers untouched)
+template <int W, bool B, bool L>
 static hipError_t grant_dyn_lds(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {  // > 64 KiB of dynamic LDS must be requested explicitly
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B>,
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B, L>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
@@ -2671,25 +2950,36 @@ static hipError_t grant_dyn_lds(size_t dyn_lds) {
     return hipSuccess;
 }
 
-template <int W, bool B>
+template <int W, bool B, bool L>
 static hipError_t launch_v(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
-    hipError_t e = grant_dyn_lds<W, B>(dyn_lds);
+    hipError_t e = grant_dyn_lds<W, B, L>(dyn_lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
+    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B, L>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
     return hipGetLastError();
 }
 
-template <int W, bool B>
+template <int W, bool B, bool L>
 static hipError_t occ_v(int* blocks, size_t dyn_lds) {
-    hipError_t e = grant_dyn_lds<W, B>(dyn_lds);
+    hipError_t e = grant_dyn_lds<W, B, L>(dyn_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B>, 64 * W, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B, L>, 64 * W, dyn_lds);
+}
+
+// both instantiations of a variant must be co-resident: the smaller answer
+template <int W>
+static hipError_t occ_both(int* blocks, size_t dyn_lds) {
+    int a = 0, b = 0;
+    hipError_t e = occ_v<W, false, false>(&a, dyn_lds);
+    if (e == hipSuccess) e = occ_v<W, false, true>(&b, dyn_lds);
+    *blocks = a < b ? a : b;
+    return e;
 }
 
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
-    if (variant == 8) return launch_v<8, false>(p, blocks, dyn_lds, stream);
-    if (variant == 5) return launch_v<4, true>(p, blocks, dyn_lds, stream);
-    return launch_v<4, false>(p, blocks, dyn_lds, stream);
+    const bool ll = (p->mode & rlo::MODE_LL) != 0;
+    if (variant == 8) return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
+    if (variant == 5) return launch_v<4, true, false>(p, blocks, dyn_lds, stream);
+    return ll ? launch_v<4, false, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false>(p, blocks, dyn_lds, stream);
 }
 
 extern "C" size_t rlo_kernel_static_lds(int variant) {
@@ -2699,7 +2989,7 @@ extern "C" size_t rlo_kernel_static_lds(int variant) {
 }
 
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant) {
-    if (variant == 8) return occ_v<8, false>(blocks, dyn_lds);
-    if (variant == 5) return occ_v<4, true>(blocks, dyn_lds);
-    return occ_v<4, false>(blocks, dyn_lds);
+    if (variant == 8) return occ_both<8>(blocks, dyn_lds);
+    if (variant == 5) return occ_v<4, true, false>(blocks, dyn_lds);
+    return occ_both<4>(blocks, dyn_lds);
 }

@@ -162,6 +162,7 @@ struct Layout {
     std::vector<uint64_t> fwd_bytes, vote_bytes, ctrl_words;  // per part
     std::vector<uint64_t> fwd_off, vote_off;                  // per edge (vc 0 ring; vc 1 follows)
     std::vector<uint32_t> inbox, outbox;                      // per rank: word index in its part's ctrl
+    std::vector<uint32_t> fbell, vbell;                       // per rank: its doorbells (rlo_device.hpp) in its ctrl
     std::vector<uint64_t> lat_base;                           // per part: the shared latency block (rlo_device.hpp)
     // bulk messages (rlo_device.hpp): heap slot (r, o, s) and flag line (r, o, s) in r's part, then
     // the done lines (o, s) of the part's origins
@@ -279,6 +280,8 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
     L.lat_base.clear();
     L.inbox.assign(n, 0);
     L.outbox.assign(n, 0);
+    L.fbell.assign(n, 0);
+    L.vbell.assign(n, 0);
     for (int p = 0; p < nparts; p++) {
         uint64_t words = rlo::kCtrlHdrWords;
         for (int r = L.pb[p]; r < L.pb[p + 1]; r++) {
@@ -289,6 +292,12 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
         }
         L.lat_base.push_back(words);
         words += rlo::kLatWords;
+        for (int r = L.pb[p]; r < L.pb[p + 1]; r++) {  // doorbells: forward per in-edge, vote per child
+            L.fbell[r] = (uint32_t)words;
+            words += (uint64_t)L.in_edges[r].size() * rlo::kBellWords;
+            L.vbell[r] = (uint32_t)words;
+            words += (2ull * L.T[r].sll + 15) & ~15ull;
+        }
         L.ctrl_words[p] = words;
     }
     L.heap_bytes.assign(nparts, 0);
@@ -513,6 +522,8 @@ void build_topo(rlo_world* w) {
         t.outbox_ctrl = L.outbox[r];
         t.n_outbox = 2 * t.sll + t.n_in;
         t.orig_data = (uint32_t)L.orig_off[r];
+        t.in_bell = L.fbell[r];
+        t.vin_bell = L.vbell[r];
     }
     for (size_t e = 0; e < L.E.size(); e++) {
         const Edge& ed = L.E[e];
@@ -525,6 +536,7 @@ void build_topo(rlo_world* w) {
             }
             t.vin_data[ed.j] = (uint32_t)L.vote_off[e];
             t.vin_head[ed.j] = (uint64_t)(uintptr_t)(w->pc[pd] + L.outbox[ed.dst] + 2 * L.T[ed.dst].sll + ed.k);
+            t.out_bell[ed.j] = (uint64_t)(uintptr_t)(w->pc[pd] + L.fbell[ed.dst] + (uint64_t)rlo::kBellWords * ed.k);
         }
         if (pd == w->part) {  // I consume its forward rings, produce its votes
             rlo::RankTopo& t = w->topo[ed.dst - w->rb];
@@ -536,6 +548,7 @@ void build_topo(rlo_world* w) {
             t.in_base[ed.k] = (uint64_t)(uintptr_t)w->pf[ps];  // the producer's slots (pulled payloads)
             t.vout_ring[ed.k] = (uint64_t)(uintptr_t)(w->pv[ps] + L.vote_off[e]);
             t.vout_tail[ed.k] = (uint64_t)(uintptr_t)(w->pc[ps] + L.inbox[ed.src] + 2 * L.in_edges[ed.src].size() + ed.j);
+            t.vout_bell[ed.k] = (uint64_t)(uintptr_t)(w->pc[ps] + L.vbell[ed.src] + 2 * ed.j);
         }
     }
 }
@@ -874,6 +887,16 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     return RLO_OK;
 }
 
+// doorbells (rlo_device.hpp) for the latency / IAR / host programs: their lone messages are what a
+// bell carries.  The doorbell instantiation of the kernel has no large-message path, so a program gets
+// it only when its longest message (max_msg payload bytes) takes the small copy path; never in bulk
+// worlds (their kernel has no doorbell instantiation).  RLO_NO_LL (diagnostics build) turns bells off
+static uint32_t ll_mode(const rlo_world* w, uint32_t max_msg) {
+    if (w->L.bulk_max || diag_env("RLO_NO_LL")) return 0u;
+    if ((rlo::kHdr + max_msg + 15u) / 16u > w->nsmall) return 0u;
+    return rlo::MODE_LL;
+}
+
 static void base_params(rlo_world* w) {
     rlo::Params& P = w->P;
     std::memset(&P, 0, sizeof P);
@@ -889,6 +912,7 @@ static void base_params(rlo_world* w) {
     P.vote_region_bytes = (uint32_t)std::max<uint64_t>(w->L.vote_bytes[w->part], 1);
     P.vote_cap = w->L.vote_cap;
     P.ctrl = w->ctrl;
+    P.ctrl_bytes = (uint32_t)(w->L.ctrl_words[w->part] * 8);
     P.sys_scope = (uint32_t)w->sys_scope;
     P.n_parts = (uint32_t)w->L.nparts;
     for (int q = 0; q < w->L.nparts; q++) P.err_flag[q] = reinterpret_cast<uint32_t*>(w->pc[q]);
@@ -1011,7 +1035,8 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     if (w->d_lat_origin.upload(org) || w->d_expect_bcast.upload(expect) || w->d_lat_count.alloc(rounds) ||
         w->d_lat_out.alloc(rounds) || w->d_lat_round.alloc(1) || w->d_lat_obs.alloc(rounds))
         return RLO_E_HIP;
-    P.mode = rlo::MODE_LAT | ((flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u) | ((flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
+    P.mode = rlo::MODE_LAT | ((flags & RLO_FLAG_HIST) ? rlo::MODE_HIST : 0u) | ((flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u) |
+             ll_mode(w, len);
     P.len = len;
     P.seed = seed;
     P.lat_rounds = rounds;
@@ -1107,7 +1132,9 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
     if (w->d_prop_off.upload(off) || w->d_prop_pid.upload(ppid) || w->d_prop_data_off.upload(pdo) ||
         w->d_prop_data_len.upload(pdl) || w->d_prop_data.upload(blob) || w->d_expect_dec.upload(expect))
         return RLO_E_HIP;
-    P.mode = rlo::MODE_IAR | ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u);
+    uint32_t max_msg = 23;  // a decision's PBuf (:908-917); a proposal's is 16 B + its data
+    for (int64_t i = 0; i < nprop; i++) max_msg = std::max<uint32_t>(max_msg, 16u + data_len[i]);
+    P.mode = rlo::MODE_IAR | ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u) | ll_mode(w, max_msg);
     {
         const int jrc = set_judge(w, cfg);
         if (jrc) return jrc;
@@ -1285,7 +1312,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     w->pk_head.assign(nl, 0);
     base_params(w);
     rlo::Params& P = w->P;
-    P.mode = rlo::MODE_HOST | rlo::MODE_IAR;
+    P.mode = rlo::MODE_HOST | rlo::MODE_IAR | ll_mode(w, w->L.stride - rlo::kHdr);  // a command fills up to a slot
     P.own_pool = pool;
     P.host_judge = 1;  // judge(data) / judge(NULL) are the host's callbacks (rlo_host_device_judge: the device's)
     P.log = dev_ev ? const_cast<rlo::LogRec*>(dev_ev) : w->h_ev;

@@ -6,13 +6,18 @@ fallback: if the library is missing the import fails loudly.
 """
 import ctypes
 import os
+import re
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
 # RLO_DIAG_LIB=1: the diagnostics build (make DIAG=1 -> lib_diag/), whose library honours the A/B
-# environment switches the product library ignores (rlo_world.cpp diag_env)
+# environment switches the product library ignores (rlo_world.cpp diag_env).  RLO_LIB_DIR=lib_<name>: an
+# A/B build in the package's lib_<name>/ (tools/ only)
 if os.environ.get("RLO_DIAG_LIB") == "1":
     LIB_PATH = os.path.join(PKG_DIR, "lib_diag", "librlo_hip.so")
+_AB = os.environ.get("RLO_LIB_DIR", "")
+if re.fullmatch(r"lib_[a-z0-9]+", _AB):
+    LIB_PATH = os.path.join(PKG_DIR, _AB, "librlo_hip.so")
 
 RLO_OK = 0
 RLO_E_INVAL, RLO_E_HIP, RLO_E_OCCUPANCY, RLO_E_DEVICE, RLO_E_NOPROGRAM, RLO_E_NODEVICE = -1, -2, -3, -4, -5, -6
