@@ -341,9 +341,11 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
                    "verified": bool(ok)}
             rec["algbw_GBps"] = round(nbytes / rt / 1e9, 2) if rt > 0 else None
             if world == 1 and rt > 0:
-                # one GPU: every receiver's copy written once ((G-1)S), the stripes read once (S) to
-                # all-gather, every receiver reads its copy to verify ((G-1)S): (2G-1)S HBM bytes
-                rec["hbm_GBps"] = round((2 * G - 1) * nbytes / rt / 1e9, 1)
+                # one GPU: the origin's copy written at origination and read by the scatter (2S), every
+                # receiver's copy written once ((G-1)S), the stripes read once to all-gather (S), every
+                # receiver reads its copy to verify ((G-1)S): (2G+1)S HBM bytes
+                rec["hbm_GBps"] = round((2 * G + 1) * nbytes / rt / 1e9, 1)
+                rec["hbm_frac"] = round(rec["hbm_GBps"] / HBM_PEAK_GBS, 4)
             if rank == 0:
                 note("bulk %d MiB: %.3f ms/round" % (mib, rt * 1e3))
             if nccl is not None:

@@ -312,24 +312,35 @@ constexpr int kJctlTilesDone = 36, kJctlGatherWaited = 38, kJctlGatherPassed = 3
               kJctlFault = 47, kJctlWords = 48;
 
 // stripe / chunk / tile plan of a bulk message: a pure function of (N, len, cross-GPU), so every
-// rank derives the same one (cross: parts span GPUs -> pipelined chunks, ~sqrt(len / 4 MiB) of
-// them; one GPU: one chunk).  A tile (what one mover claim moves, then one release + flag add) is
-// the stripe, cut to <= 64 KiB: a mover workgroup stores ~20 GB/s into uncached HBM, so a message is
-// fast only when many movers share it; large enough that the per-tile release stays a small share.
-constexpr uint32_t kBulkTileMax = 64u << 10;
-// a VERIFY job (a receiver's read of its whole copy) is cut into 256-KiB tiles, independent of the
-// stripe plan (at N = 64 a stripe-sized tile made ~63 tiles per copy)
-constexpr uint32_t kVerifyTile = 256u << 10;
+// rank derives the same one.  Chunks pipeline the scatter into the all-gather: the gather of chunk c
+// runs while chunk c + 1 is scattered (cross: parts span GPUs -> ~sqrt(len / 4 MiB) chunks; one GPU:
+// 4-MiB chunks from 8 MiB on, where the messages are long enough for the overlap to pay).  A tile (what
+// one mover claim moves, then one release + flag add) is the stripe cut to <= 64 KiB, or to <= 16 KiB
+// for messages under 8 MiB: a mover workgroup stores ~20 GB/s into uncached HBM, so a message is fast
+// only when many movers share it -- short ones are latency bound and want many small tiles, long ones
+// large tiles so the per-tile release stays a small share.
+constexpr uint32_t kBulkTileMax = 64u << 10, kBulkTileSmall = 16u << 10;
+constexpr uint32_t kBulkChunk1 = 4u << 20;  // one GPU: chunk size, from 2 chunks' worth on
+// a VERIFY job (a receiver's read of its whole copy) is cut into 64-KiB tiles, independent of the
+// stripe plan: many movers read a copy at once (at N = 64 a stripe-sized tile made ~63 tiles per copy)
+constexpr uint32_t kVerifyTile = 64u << 10;
 // a job is posted as at most kMaxSub sub-jobs of consecutive tiles; a mover draws sub-jobs by ticket
-// (one fetch-add, never retried) and moves all of a sub-job's tiles itself
-constexpr uint32_t kMaxSub = 64;
+// (one fetch-add, never retried) and moves all of a sub-job's tiles itself.  Enough sub-jobs that every
+// mover of a class has one while a single message's scatter or verify runs
+constexpr uint32_t kMaxSub = 256;
+// granules in flight per mover thread (16 B each): 256 threads x 8 x 16 B = 32 KiB per round trip
+constexpr int kMoveDepth = 8;
 struct BulkPlan {
     uint32_t nchunks, stripe, chunk, tile;  // chunk = stripe * (N - 1); stripe, tile multiples of 1 KiB
 };
 __host__ __device__ inline BulkPlan bulk_plan(int n, uint32_t len, bool cross) {
     uint32_t k = 1;
-    if (cross)
+    if (cross) {
         while ((uint64_t)(k + 1) * (k + 1) * (4ull << 20) <= len && k < (uint32_t)kBulkMaxChunks) k++;
+    } else if (len >= 2 * kBulkChunk1) {
+        k = len / kBulkChunk1;
+        if (k > (uint32_t)kBulkMaxChunks) k = (uint32_t)kBulkMaxChunks;
+    }
     const uint32_t m = (uint32_t)(n - 1);
     const uint64_t per = ((uint64_t)len + k - 1) / k;
     uint64_t stripe = ((per + m - 1) / m + kBulkKiB - 1) / kBulkKiB * kBulkKiB;
@@ -340,7 +351,8 @@ __host__ __device__ inline BulkPlan bulk_plan(int n, uint32_t len, bool cross) {
     p.stripe = (uint32_t)stripe;
     p.chunk = (uint32_t)chunk;
     p.nchunks = len ? (uint32_t)((len + chunk - 1) / chunk) : 0u;
-    const uint32_t parts = (p.stripe + kBulkTileMax - 1) / kBulkTileMax;
+    const uint32_t tmax = len >= 2 * kBulkChunk1 ? kBulkTileMax : kBulkTileSmall;
+    const uint32_t parts = (p.stripe + tmax - 1) / tmax;
     p.tile = (p.stripe / parts + kBulkKiB - 1) / kBulkKiB * kBulkKiB;
     return p;
 }

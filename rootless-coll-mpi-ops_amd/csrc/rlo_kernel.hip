@@ -44,7 +44,10 @@ static constexpr uint64_t kGolden64 = 0x9E3779B97F4A7C15ull;
 static constexpr int kPass = 64;  // messages per wave per iteration
 static constexpr uint32_t kIdleSpin = 256;  // tight re-polls after an idle iteration (~0.1 ms at most)
 static constexpr int kRelQ = 16;  // pull worlds: relay-ring release records (coalesced when full)
-static constexpr uint32_t kBellJudge = 3072;  // doorbell pass: a bell message's judge copy in the stage area
+// the doorbell pass's scratch in the stage area (>= 4 KiB: 256 candidates x 16 B): bells' data, vote bells'
+// data, loaded votes, loaded ring heads, a message's judge copy
+static constexpr uint32_t kLLBell = 0, kLLBellVote = 1024, kLLVote = 1152, kLLRing = 2176, kBellJudge = 3328;
+static constexpr uint32_t kLLVotes = 4;  // votes per child a doorbell pass takes
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -804,15 +807,28 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                     const int owner = (o + 1 + (int)k) % n;
                     const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, owner, o, s), P.bulk_cap);
                     const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, o, o, s), P.bulk_cap);
-                    for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
-                        u32x4 v[4];
-    #pragma unroll
-                        for (int uu = 0; uu < 4; uu++) {
-                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                            if (g < ngr) v[uu] = jb.gen ? ld_sc1(rs, off0 + 16u * g) : storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g);
+                    if (!jb.gen) {
+                        // a device program's origination: its bytes are first written into the origin's own
+                        // heap slot (the copy an application would have staged, rlo_host_bulk_stage), then
+                        // read back from there like the host's -- the scatter always moves the origin's copy
+                        for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
+#pragma unroll
+                            for (int uu = 0; uu < kMoveDepth; uu++) {
+                                const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                                if (g < ngr) st_ring(rs, off0 + 16u * g, storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g), sys);
+                            }
                         }
-    #pragma unroll
-                        for (int uu = 0; uu < 4; uu++) {
+                        VM_DRAIN();  // this thread's own stores, before it loads the same bytes back (sc1)
+                    }
+                    for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
+                        u32x4 v[kMoveDepth];
+#pragma unroll
+                        for (int uu = 0; uu < kMoveDepth; uu++) {
+                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                            if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
+                        }
+#pragma unroll
+                        for (int uu = 0; uu < kMoveDepth; uu++) {
                             const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
                             if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
                         }
@@ -848,10 +864,10 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                     }
                     __syncthreads();
                     const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
-                    for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
-                        u32x4 v[4];
+                    for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
+                        u32x4 v[kMoveDepth];
     #pragma unroll
-                        for (int uu = 0; uu < 4; uu++) {
+                        for (int uu = 0; uu < kMoveDepth; uu++) {
                             const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
                             if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
                         }
@@ -860,7 +876,7 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                             if (dst == me) continue;
                             const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, dst, o, s), P.bulk_cap);
     #pragma unroll
-                            for (int uu = 0; uu < 4; uu++) {
+                            for (int uu = 0; uu < kMoveDepth; uu++) {
                                 const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
                                 if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
                             }
@@ -889,15 +905,15 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                 const uint32_t ngr = (tlen + 15u) >> 4;
                 const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
                 unsigned long long acc = 0;
-                for (uint32_t g0 = 0; g0 < ngr; g0 += 4u * kT) {
-                    u32x4 v[4];
+                for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
+                    u32x4 v[kMoveDepth];
     #pragma unroll
-                    for (int uu = 0; uu < 4; uu++) {
+                    for (int uu = 0; uu < kMoveDepth; uu++) {
                         const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
                         if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
                     }
     #pragma unroll
-                    for (int uu = 0; uu < 4; uu++) {
+                    for (int uu = 0; uu < kMoveDepth; uu++) {
                         const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
                         if (g < ngr) {
                             const uint32_t off = off0 + 16u * g;
@@ -956,7 +972,7 @@ template <int W, bool BULK, bool LL>
 __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // pulled payloads (Params.pull) exist only in the 4-wave kernel without bulk messages (slots beyond
     // the small copy path); compiled out of the others
-#define PULL_ON (W == 4 && !BULK && !LL && P.pull != 0u)
+#define PULL_ON (W == 4 && !BULK && P.pull != 0u)
     constexpr int kWaves = W, kBlock = 64 * W, kMaxCand = 64 * W;
     constexpr uint32_t kHostBase = kMaxCand - kPass;  // host mode: command run staged at the last 64 candidates
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
@@ -1259,20 +1275,59 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         return true;
     };
 
+    // ---- one vote from child j by lane 0 (_iar_vote_handler :743-812, _vote_merge :1056-1070): phase B1's
+    // merge, for the doorbell pass
+    auto merge_vote = [&](int origin, int32_t pid, uint32_t pseq, int vote, uint32_t vw) {
+        const uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
+        if (origin >= P.n) {
+            set_error(S, P, ERR_BAD_SLOT, vw);
+        } else if (origin == me) {  // a vote for my own proposal (:756-783)
+            const uint32_t k = pseq & (P.pend_slots - 1u);
+            if (S.own_state[k] != 1 || pid != S.own_pid[k]) {
+                set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+            } else {
+                const uint32_t nw = (S.own_word[k] += inc);
+                if ((nw & 0xffffu) == S.own_needed) {
+                    const int d = (nw >> 16) == 0 ? 1 : 0;
+                    if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
+                        atomicAdd(&S.judge_calls, 1ull);
+                        log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                    }
+                    S.own_decision[k] = (uint32_t)d;
+                    S.own_state[k] = 2;
+                }
+            }
+        } else {
+            PendState* ps = &PEND(origin, pseq);
+            if (ps->valid != PS_ACTIVE || ps->pid != pid) {
+                set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+            } else {
+                const uint32_t nw = (ps->word += inc);
+                if ((nw & 0xffffu) == ps->needed)
+                    emit_vote<LL>(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+            }
+        }
+    };
+
     // ---- the doorbell pass (MODE_LL), wave 0 in its poll loop while the other waves wait at the
-    // iteration barrier: every complete bell at its ring head (at most one per in-edge), every vote bell
-    // at its vote-ring head, then this rank's own originations (device programs) -- each as the lone fast
-    // path handles it, with no full iteration and no counter round trip on the hop.  Only while the
-    // counters show nothing else: a counter-visible message beside them belongs to the full path, and
-    // the bells' messages with it (through their counters).  Then one drain, and the counters are
-    // published (the eager scheme).  Returns the number of messages handled.
+    // iteration barrier.  It takes the head message of every in-ring -- from the ring's bell when the bell
+    // holds it (no slot load, and possibly ahead of the counter), else loaded from the slot the counter
+    // shows -- and up to kLLVotes votes of every child (the head one from its vote bell when only the bell
+    // has it), then this rank's own originations (device programs): each as the lone fast path handles
+    // it, with no full iteration.  A backlog (a ring more than 2 deep, a child more than kLLVotes votes
+    // ahead, more rings to load than one round trip covers), a host command, or a message the lone path
+    // refuses is the full iteration's (need_full).  Then one drain, and the counters are published (the
+    // eager scheme).  The stage area is scratch here (the other waves are parked): bells' data at kLLBell,
+    // vote bells' at kLLBellVote, loaded votes at kLLVote, loaded ring heads at kLLRing.  Returns the
+    // number of messages handled.
     auto ll_pass = [&](u32x4 ba, u32x4 bb, u32x4 vb, uint64_t in_tail_r, uint64_t vin_tail_r, uint64_t out_head_r,
-                       uint64_t hpoll, uint32_t latr, uint32_t errf) -> uint32_t {
+                       uint64_t hpoll, uint32_t latr, uint32_t errf, bool& need_full) -> uint32_t {
+        need_full = false;
         if (__ballot(errf != 0)) return 0u;
         // the data words to LDS at once (registers are the kernel's scarcest resource): chunk q of in-edge
-        // k's bell at [16 (8 k + q)], child j's vote {word, pid} at [1024 + 8 j]
-        *reinterpret_cast<u32x4*>(stage + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
-        if (lane < sll) *reinterpret_cast<uint2*>(stage + 1024u + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
+        // k's bell at kLLBell + 16 (8 k + q), child j's vote bell {word, pid} at kLLBellVote + 8 j
+        *reinterpret_cast<u32x4*>(stage + kLLBell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
+        if (lane < sll) *reinterpret_cast<uint2*>(stage + kLLBellVote + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
         const uint32_t lcap = min(nsmall, kBellChunks);
         // in-ring (k, vc) whose head is h expects (h + 1) | vc << 31 in every half of every granule
@@ -1290,68 +1345,81 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const int rk = lane >> 1;
         const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
         const uint64_t ip = lane < n_in2 && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
-        const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
-        if (__ballot(ip > (rhit ? 1ull : 0ull) || vp > (((vhm >> lane) & 1ull) ? 1ull : 0ull))) return 0u;
-        if (host) {  // commands waiting, or too little room in the pickup ring: the full path
-            if (rdl64(hpoll, 0) != S.hin_head) return 0u;
+        const uint64_t vp = !host && lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
+        const bool ldr = lane < n_in2 && ip > 0ull && !rhit;  // a counter-visible head without its bell: load it
+        const uint64_t ldm = __ballot(ldr);
+        if (__ballot(ip > 2ull || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { need_full = true; return 0u; }
+        if (host) {  // commands waiting: the full path; too little room in the pickup ring: wait for the host
+            if (rdl64(hpoll, 0) != S.hin_head) { need_full = true; return 0u; }
             const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - rdl64(hpoll, 1));
-            if (pk_free < 2u * (uint32_t)__popcll(fh) + 2u * P.own_pool + 8u) return 0u;
+            if (pk_free < 2u * (uint32_t)__popcll(__ballot(rhit || ldr)) + 2u * P.own_pool + 8u) return 0u;
         }
-        const bool lat_go = (P.mode & MODE_LAT) && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next;
+        const uint32_t nv = (uint32_t)vp;  // votes to load from child j's vote ring (<= kLLVotes)
+        // (a latency round of bulk messages is originated by the full path: its announcement, heap slot and
+        // scatter job)
+        const bool lat_go = (P.mode & MODE_LAT) && (!BULK || P.len <= P.ring_cap) && S.lat_own_next != 0xffffffffu &&
+                            rdl32(latr, 1) == S.lat_own_next;
         const bool iar_dev = (P.mode & MODE_IAR) && !host;
-        if (!fh && !vhm && !lat_go && !iar_dev) return 0u;
+        const uint64_t nvm = __ballot(nv > 0u);
+        if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev) return 0u;
+        if (ldm || nvm) {
+            // one round trip: lane 8 s + q loads chunk q of the s-th ring head to load, lane kLLVotes j + i
+            // vote i of child j (sc1 loads behind the counters, as phase D0 / B)
+            const uint32_t sl = (uint32_t)lane >> 3, q = (uint32_t)lane & 7u;
+            int gsel = -1;
+            {
+                uint32_t c = 0;
+                for (uint64_t m = ldm; m; m &= m - 1, c++)
+                    if (c == sl) gsel = __builtin_ctzll(m);
+            }
+            const int gs = gsel < 0 ? 0 : gsel;
+            const uint32_t hsel = (uint32_t)__shfl((int)(uint32_t)in_head_r, gs);
+            const uint32_t dsel = t.in_data[gs >> 1][gs & 1];
+            const uint32_t vj = (uint32_t)lane / kLLVotes, vi = (uint32_t)lane % kLLVotes;
+            const uint32_t nvj = (uint32_t)__shfl((int)nv, (int)vj), vhj = (uint32_t)__shfl((int)(uint32_t)vin_head_r, (int)vj);
+            const uint32_t vdat = (int)vj < sll ? t.vin_data[vj] : 0u;
+            u32x4 lv = {0u, 0u, 0u, 0u}, lw = {0u, 0u, 0u, 0u};
+            if (gsel >= 0 && q < lcap) lv = ld_sc1(rf, dsel + (hsel & fcap_m) * P.fwd_stride + 16u * q);
+            if ((int)vj < sll && vi < nvj) lw = ld_sc1(rv, vdat + ((vhj + vi) & vcap_m) * kVoteSlot);
+            *reinterpret_cast<u32x4*>(stage + kLLRing + 16u * (uint32_t)lane) = lv;
+            *reinterpret_cast<u32x4*>(stage + kLLVote + 16u * (uint32_t)lane) = lw;
+        }
         uint32_t done = 0;
-        // votes (_iar_vote_handler :743-812, _vote_merge :1056-1070): as phase B1
-        for (uint64_t m = vhm; m; m &= m - 1) {
+        // votes: child j's next nv_j from its ring (the loaded slots), or its head from its bell
+        for (uint64_t m = nvm | vhm; m; m &= m - 1) {
             const int j = __builtin_ctzll(m);
-            const uint2 vv = *reinterpret_cast<const uint2*>(stage + 1024u + 8u * (uint32_t)j);
-            const uint32_t vw = vv.x;
-            const int32_t pid = (int32_t)vv.y;
-            const int origin = (int)(vw & 0xffffu);
-            const uint32_t pseq = (vw >> 16) & 0xffu;
-            const int vote = (int)(int8_t)(vw >> 24);
-            const uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
+            const uint32_t c = (nvm >> j) & 1ull ? rdl32(nv, j) : 1u;
             if (lane == 0) {
-                if (origin >= P.n) {
-                    set_error(S, P, ERR_BAD_SLOT, vw);
-                } else if (origin == me) {  // a vote for my own proposal (:756-783)
-                    const uint32_t k = pseq & (P.pend_slots - 1u);
-                    if (S.own_state[k] != 1 || pid != S.own_pid[k]) {
-                        set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
-                    } else {
-                        const uint32_t nw = (S.own_word[k] += inc);
-                        if ((nw & 0xffffu) == S.own_needed) {
-                            const int d = (nw >> 16) == 0 ? 1 : 0;
-                            if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
-                                atomicAdd(&S.judge_calls, 1ull);
-                                log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
-                            }
-                            S.own_decision[k] = (uint32_t)d;
-                            S.own_state[k] = 2;
-                        }
-                    }
-                } else {
-                    PendState* ps = &PEND(origin, pseq);
-                    if (ps->valid != PS_ACTIVE || ps->pid != pid) {
-                        set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
-                    } else {
-                        const uint32_t nw = (ps->word += inc);
-                        if ((nw & 0xffffu) == ps->needed)
-                            emit_vote<LL>(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+                for (uint32_t i = 0; i < c; i++) {
+                    if ((nvm >> j) & 1ull) {  // vote slot {origin | vote << 24, pid, pseq, voter}
+                        const u32x4 vs = *reinterpret_cast<const u32x4*>(stage + kLLVote + 16u * ((uint32_t)j * kLLVotes + i));
+                        merge_vote((int)(vs.x & 0xffffu), (int32_t)vs.y, vs.z & 0xffu, (int)(int8_t)(vs.x >> 24), vs.x);
+                    } else {  // vote bell {origin | pseq << 16 | vote << 24, pid}
+                        const uint2 vv = *reinterpret_cast<const uint2*>(stage + kLLBellVote + 8u * (uint32_t)j);
+                        merge_vote((int)(vv.x & 0xffffu), (int32_t)vv.y, (vv.x >> 16) & 0xffu, (int)(int8_t)(vv.x >> 24), vv.x);
                     }
                 }
             }
-            if (lane == j) vin_head_r++;
-            done++;
+            if (lane == j) vin_head_r += c;
+            done += c;
         }
-        // the bells' ring messages, each at its ring head
-        for (uint64_t m = fh; m; m &= m - 1) {
-            const int b = __builtin_ctzll(m);  // 8 k
-            const int g = (b >> 2) + (int)((fv >> b) & 1ull);
+        // ring heads: from the bell, or the loaded slot
+        const uint64_t rhm = __ballot(rhit);
+        for (uint64_t m = rhm | ldm; m; m &= m - 1) {
+            const int g = __builtin_ctzll(m);
+            const bool fromb = (rhm >> g) & 1ull;
+            const uint32_t at = fromb ? kLLBell + 16u * (uint32_t)(8 * (g >> 1)) : kLLRing + 128u * (uint32_t)__popcll(ldm & ((1ull << g) - 1ull));
             u32x4 v = {0u, 0u, 0u, 0u};
-            if (lane < 8) v = *reinterpret_cast<const u32x4*>(stage + 16u * (uint32_t)(b + lane));
+            if ((uint32_t)lane < lcap) v = *reinterpret_cast<const u32x4*>(stage + at + 16u * (uint32_t)lane);
+            if (((kHdr + (rdl32(v.z, 0) & 0xffffu) + 15u) >> 4) > lcap) {  // longer than one load covers
+                need_full = true;
+                continue;
+            }
             const uint32_t need = lone(v, g, 0u, true, out_head_r);
-            if (need == ~0u) continue;  // the full path takes it, through its counter
+            if (need == ~0u) {  // the full path takes it, through its counter
+                if (!fromb) need_full = true;
+                continue;
+            }
             if (lane == g) in_head_r++;
             if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
             done++;
@@ -1463,9 +1531,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             bb = ld_sc1(rc, o + 16u);
                         }
                         if (!host && lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
-                        if (ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf)) {
-                            ll_prog = true;
-                            // keep serving bells from here; every 64 passes the full iteration's bookkeeping runs
+                        bool need_full = false;
+                        const uint32_t nll = ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf, need_full);
+                        if (nll) ll_prog = true;
+                        if (need_full) break;  // the full iteration takes the rest
+                        if (nll) {
+                            // keep serving from here; every 64 passes the full iteration's bookkeeping runs
                             if (++ll_run < 64u) { sp = 0; continue; }
                             break;
                         }
@@ -2466,9 +2537,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             PST(4, 7);
 
             // ---------------- G1: stage the first round of large-message groups (before any store)
-            // (the doorbell instantiation runs programs whose every message takes the small path: the
-            // host sets MODE_LL only then, rlo_world.cpp ll_mode)
-            const uint32_t nbig = LL ? 0u : S.nbig;
+            // (the 8-wave doorbell instantiation runs programs whose every message takes the small path:
+            // the host sets MODE_LL only then, rlo_world.cpp ll_mode; 8-wave worlds have small slots anyway)
+            const uint32_t nbig = (LL && W == 8) ? 0u : S.nbig;
             // staging rounds of all of stage2: load -> store -> wait.  (MODE_PIPE, A/B: two halves, round r+1's
             // loads in flight while round r is stored -- measured slower, the rounds halve)
             const bool pipe = s2_units >= 2u * kSubMax && (P.mode & MODE_PIPE);
@@ -2936,8 +3007,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
 // C-ABI launch shims used by rlo_world.cpp.  variant: 8 = 8 waves, 4 = 4 waves, 5 = 4 waves with
 // bulk messages (mover workgroups + mixed storm lengths); the Shared / LDS layout depends on it.  A
-// program with doorbells (MODE_LL: latency, IAR, host service -- never in bulk worlds) runs the
-// doorbell instantiation of its variant, the storm the one without (its registers untouched)
+// program with doorbells (MODE_LL: latency, IAR, host service) runs the doorbell instantiation of its
+// variant, the storm the one without (its registers untouched)
 template <int W, bool B, bool L>
 static hipError_t grant_dyn_lds(size_t dyn_lds) {
     static size_t granted = 0;
@@ -2965,20 +3036,10 @@ static hipError_t occ_v(int* blocks, size_t dyn_lds) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B, L>, 64 * W, dyn_lds);
 }
 
-// both instantiations of a variant must be co-resident: the smaller answer
-template <int W>
-static hipError_t occ_both(int* blocks, size_t dyn_lds) {
-    int a = 0, b = 0;
-    hipError_t e = occ_v<W, false, false>(&a, dyn_lds);
-    if (e == hipSuccess) e = occ_v<W, false, true>(&b, dyn_lds);
-    *blocks = a < b ? a : b;
-    return e;
-}
-
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
     if (variant == 8) return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
-    if (variant == 5) return launch_v<4, true, false>(p, blocks, dyn_lds, stream);
+    if (variant == 5) return ll ? launch_v<4, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, true, false>(p, blocks, dyn_lds, stream);
     return ll ? launch_v<4, false, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false>(p, blocks, dyn_lds, stream);
 }
 
@@ -2989,7 +3050,15 @@ extern "C" size_t rlo_kernel_static_lds(int variant) {
 }
 
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant) {
-    if (variant == 8) return occ_both<8>(blocks, dyn_lds);
+    if (variant == 8) return occ_v<8, false, false>(blocks, dyn_lds);
     if (variant == 5) return occ_v<4, true, false>(blocks, dyn_lds);
-    return occ_both<4>(blocks, dyn_lds);
+    return occ_v<4, false, false>(blocks, dyn_lds);
+}
+
+// the doorbell instantiation of a variant: the 4-wave ones may take more than 256 registers (one wave
+// per SIMD: worlds whose ranks have a CU each), so a world gets doorbells only where this answer covers it
+extern "C" hipError_t rlo_occupancy_ll(int* blocks, size_t dyn_lds, int variant) {
+    if (variant == 8) return occ_v<8, false, true>(blocks, dyn_lds);
+    if (variant == 5) return occ_v<4, true, true>(blocks, dyn_lds);
+    return occ_v<4, false, true>(blocks, dyn_lds);
 }

@@ -27,6 +27,7 @@
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant);
 extern "C" size_t rlo_kernel_static_lds(int variant);
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant);
+extern "C" hipError_t rlo_occupancy_ll(int* blocks, size_t dyn_lds, int variant);
 
 static_assert(sizeof(rlo_rank_stats_t) == sizeof(rlo::RankStats), "stats ABI");
 static_assert(sizeof(rlo_log_rec_t) == sizeof(rlo::LogRec), "log ABI");
@@ -399,6 +400,7 @@ struct rlo_world {
     float last_ms = 0.f;
     size_t dyn_lds = 0;
     uint32_t nsmall = 8, stage2 = 1024;
+    bool ll_ok = false;  // the doorbell instantiation of the kernel is co-resident at this world's size
     int waves = 4;    // rank-workgroup width: 8 (512 candidates per iteration) when each rank has a CU
     int variant = 4;  // kernel instantiation: 8 / 4 waves, 5 = 4 waves with bulk messages
     // bulk messages (rlo_device.hpp): this part's heap, flag region and job rings (all uncached),
@@ -486,6 +488,11 @@ int size_lds_variant(rlo_world* w, int variant) {
     w->waves = waves;
     w->variant = variant;
     w->blocks_per_cu = std::max(1, api);
+    {  // the doorbell instantiation co-resident too? (else its programs run without bells)
+        int ll = 0;
+        if (rlo_occupancy_ll(&ll, w->dyn_lds, variant) != hipSuccess) ll = 0;
+        w->ll_ok = ll >= need_bpc;
+    }
     if (nblk > w->blocks_per_cu * w->cus) return RLO_E_OCCUPANCY;
     return RLO_OK;
 }
@@ -888,12 +895,13 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
 }
 
 // doorbells (rlo_device.hpp) for the latency / IAR / host programs: their lone messages are what a
-// bell carries.  The doorbell instantiation of the kernel has no large-message path, so a program gets
-// it only when its longest message (max_msg payload bytes) takes the small copy path; never in bulk
-// worlds (their kernel has no doorbell instantiation).  RLO_NO_LL (diagnostics build) turns bells off
+// bell carries.  Where the doorbell instantiation of the world's kernel is co-resident (its 4-wave forms
+// may take one wave per SIMD: worlds whose ranks have a CU each); the 8-wave one has no large-message
+// path, so there the program's longest message (max_msg payload bytes) must take the small copy path.
+// RLO_NO_LL (diagnostics build) turns bells off
 static uint32_t ll_mode(const rlo_world* w, uint32_t max_msg) {
-    if (w->L.bulk_max || diag_env("RLO_NO_LL")) return 0u;
-    if ((rlo::kHdr + max_msg + 15u) / 16u > w->nsmall) return 0u;
+    if (!w->ll_ok || diag_env("RLO_NO_LL")) return 0u;
+    if (w->variant == 8 && (rlo::kHdr + max_msg + 15u) / 16u > w->nsmall) return 0u;
     return rlo::MODE_LL;
 }
 
