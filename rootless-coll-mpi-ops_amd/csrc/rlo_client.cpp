@@ -25,6 +25,7 @@ struct rlo_client {
     const uint8_t* evp = nullptr;
     rlo::ClientBox* box = nullptr;
     uint8_t* cmd = nullptr;
+    uint8_t* llc = nullptr;  // command doorbells (rlo_shm.hpp ll_cmd_put)
     uint8_t* stage = nullptr;
     uint64_t tail = 0, pk_head = 0, req = 0;
 };
@@ -90,6 +91,7 @@ int rlo_client_attach(const char* name, int rank, rlo_client_t** out) {
     c->box = (rlo::ClientBox*)(c->base + h.off_cli) + lr;
     c->cmd = c->base + h.off_cmd + lr * h.cmd_cap * h.stride;
     c->stage = c->base + h.off_stage + lr * h.stage_bytes;
+    c->llc = c->base + h.off_llc + lr * h.cmd_cap * rlo::kLLCmdSlot;
     // the counters this side owns restart where the segment says (a fresh part: 0)
     c->tail = ld_acq(&c->box->mtail);
     c->pk_head = ld_acq(&c->box->mpk);
@@ -126,6 +128,7 @@ int rlo_client_post(rlo_client_t* c, const rlo_cmd_t* cmd, const void* payload, 
     hdr[3] = 0;
     std::memcpy(slot, hdr, sizeof hdr);
     if (len) std::memcpy(slot + rlo::kHdr, payload, len);
+    rlo::ll_cmd_put(c->llc + (c->tail & (h.cmd_cap - 1)) * (uint64_t)rlo::kLLCmdSlot, c->tail, hdr, payload, len);
     c->tail++;
     __atomic_store_n(&c->box->mtail, c->tail, __ATOMIC_RELEASE);
     return RLO_OK;

@@ -236,6 +236,8 @@ struct Params {
     uint64_t* hctl;               // [n_local][kHctlWords] counters the DEVICE writes (pinned host memory)
     uint64_t* hctl_dev;           // [n_local][kHctlWords] counters the HOST writes (uncached VRAM:
                                   //   the CPU stores through the BAR, the kernel polls locally)
+    uint8_t* hll;                 // [n_local][hin_cap] x (kBellChunks x 32 B) command doorbells (rlo_shm.hpp
+                                  //   ll_cmd_put), host memory; null: none (commands in VRAM)
     // bulk messages (the BULK kernel instantiation only; rlo_device.hpp "bulk messages" below)
     uint32_t bulk_slots, bulk_cap;  // B (power of two) heap slots per origin, bytes per slot (x 64 KiB)
     uint32_t n_local, nmov;         // progress workgroups, mover workgroups (blocks [n_local, n_local + nmov))

@@ -48,6 +48,13 @@ static constexpr int kRelQ = 16;  // pull worlds: relay-ring release records (co
 // data, loaded votes, loaded ring heads, a message's judge copy
 static constexpr uint32_t kLLBell = 0, kLLBellVote = 1024, kLLVote = 1152, kLLRing = 2176, kBellJudge = 3328;
 static constexpr uint32_t kLLVotes = 4;  // votes per child a doorbell pass takes
+// host mode: the pass also takes up to kLLCmds host commands, command s's chunk q loaded at kLLCmd + 16 (8 s + q)
+// (the stage area is >= 5 KiB there: 256 candidates x nsmall >= 2 chunks)
+static constexpr uint32_t kLLCmd = 4096, kLLCmds = 8;
+// the command doorbell of the next expected command (rlo_shm.hpp ll_cmd_put), as polled: 16 lanes x 16 B
+static constexpr uint32_t kLLCmdBell = 5120;
+// lone(): a proposal held for the host's verdict (nothing consumed); kAsked: its judge request was written now
+static constexpr uint32_t kHeld = 0xFFFFFFFEu, kAsked = 0xFFFFFFFDu;
 
 enum CandKind : uint32_t { K_RING = 0, K_STORM = 1, K_PROP = 2, K_DEC = 3, K_LAT = 4, K_HOST = 5, K_BAD = 7 };
 // PendState.valid: proposal held at a non-originator / host-judge progress (MODE_HOST)
@@ -1030,6 +1037,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint64_t* const hctl = host ? P.hctl + (size_t)lr * kHctlWords : nullptr;
     uint64_t* const hctl_dev = host ? P.hctl_dev + (size_t)lr * kHctlWords : nullptr;
     const uint32_t hcap_m = host ? P.hin_cap - 1u : 0u;
+    // host mode: the command doorbells of this rank (rlo_shm.hpp), and whether the doorbell pass may take
+    // commands (its scratch at kLLCmd .. kLLCmdBell + 256 must fit the stage area)
+    constexpr uint32_t kLLCmdSlotB = kBellChunks * 32u;
+    const __amdgpu_buffer_rsrc_t rll = mk_rsrc(host && P.hll ? P.hll + (size_t)lr * P.hin_cap * kLLCmdSlotB : P.fwd_region,
+                                               host && P.hll ? P.hin_cap * kLLCmdSlotB : 16u);
+    const bool ll_cmds = host && (uint32_t)kMaxCand * nsmall * 16u >= kLLCmdBell + 256u;
     // bulk messages: pending receptions (o, s) in dynamic LDS [N * B] (BULK instantiation only)
     [[maybe_unused]] BulkPend* const bpend = reinterpret_cast<BulkPend*>(dyn_lds + (BULK ? P.bpend_off : 0u));
     [[maybe_unused]] const uint32_t bsl = BULK ? P.bulk_slots : 1u;
@@ -1156,6 +1169,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // the ring slot (fsrc) or, for a bell's message, from its LDS copy (from_bell).  The doorbell pass
     // borrows the stage area while the other waves wait at the barrier: bells' data at [0, 1 KiB), votes'
     // at [1 KiB, 1.125 KiB), a bell message's judge copy at kBellJudge (the area is >= 4 KiB: 256 x 16 B)
+    // Host judges (hjudge): a proposal without a verdict is held -- its judge request (phase D's LOG_JREQ,
+    // with the PBuf) is written the first time (kAsked), later calls find it asked (kHeld); nothing is
+    // consumed either way.  With the verdict in (PS_JYES / PS_JNO, a CMD_JUDGE applied) it goes on as judged.
     auto lone = [&](u32x4 v, int fg, uint32_t fsrc, bool from_bell, uint64_t out_head_r) -> uint32_t {
         const uint32_t q = (uint32_t)lane;
         const int ffrom = uni(t.in_src[fg >> 1]);
@@ -1165,20 +1181,49 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t fpseq = fw2 >> 24;
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
-                  (ftag == TAG_BCAST || ftag == TAG_DECISION || (!host && ftag == TAG_PROPOSAL)) &&
+                  (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL) &&
                   !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
         int fjudge = 1;
         uint32_t fkids = 0, fneed = 0;
+        uint32_t flog = ~0u;
+        if (ok && ftag == TAG_PROPOSAL && hjudge) {
+            const uint8_t pv = PEND(forg, fpseq).valid;
+            const bool same = PEND(forg, fpseq).pid == (int32_t)fid;
+            if ((pv == PS_JYES || pv == PS_JNO) && same) {
+                fjudge = pv == PS_JYES ? 1 : 0;
+            } else if (pv == PS_JREQ && same) {
+                return kHeld;  // asked already: the verdict is on its way
+            } else if (pv != PS_NONE) {
+                return ~0u;    // the entry still holds an earlier proposal of that pool slot: the full path
+            } else if (own_has(S, P, (int32_t)fid)) {
+                if (lane == 0) set_error(S, P, ERR_PID_COLLISION, fid);  // :690-692
+                return kHeld;
+            } else {  // judge(data) request with the PBuf (the phase-D hold)
+                if (lane == 0) {
+                    PendState* pw = &PEND(forg, fpseq);
+                    pw->pid = (int32_t)fid;
+                    pw->valid = PS_JREQ;
+                    flog = log_put(S, P, lr, LOG_JREQ, forg, ffrom, fid, flen, -1, fpseq);
+                    atomicAdd(&S.hwait, 1u);
+                }
+                flog = rdl32(flog, 0);
+                if (q >= 1u && q < fnch && 16u * q <= P.log_stride)
+                    st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+                return kAsked;
+            }
+        }
         if (ok) {
-            if (ftag == TAG_PROPOSAL) {  // device judge on the PBuf data (phase D)
-                uint32_t dl = nsmall > 1 ? rdl32(v.z, 1) : 0u;
-                if (dl > flen - 16u) dl = flen > 16u ? flen - 16u : 0u;
-                if (from_bell) {
-                    if (q < kBellChunks) *reinterpret_cast<u32x4*>(stage + kBellJudge + 16u * q) = v;
-                    const uint8_t* d = stage + kBellJudge + kHdr + 16u;
-                    fjudge = judge_eval_f(P, me, my_mask, (int32_t)fid, [&](uint32_t i) { return d[i]; }, dl);
-                } else {
-                    fjudge = judge_eval(P, rf, me, my_mask, (int32_t)fid, fsrc + kHdr + 16u, dl);
+            if (ftag == TAG_PROPOSAL) {
+                if (!hjudge) {  // device judge on the PBuf data (phase D)
+                    uint32_t dl = nsmall > 1 ? rdl32(v.z, 1) : 0u;
+                    if (dl > flen - 16u) dl = flen > 16u ? flen - 16u : 0u;
+                    if (from_bell) {
+                        if (q < kBellChunks) *reinterpret_cast<u32x4*>(stage + kBellJudge + 16u * q) = v;
+                        const uint8_t* d = stage + kBellJudge + kHdr + 16u;
+                        fjudge = judge_eval_f(P, me, my_mask, (int32_t)fid, [&](uint32_t i) { return d[i]; }, dl);
+                    } else {
+                        fjudge = judge_eval(P, rf, me, my_mask, (int32_t)fid, fsrc + kHdr + 16u, dl);
+                    }
                 }
                 fkids = fjudge == 1 ? kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r) : 0u;
             } else {
@@ -1187,12 +1232,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             fneed = need_of(fkids, forg, sll, sl_r);
             const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
             // a proposal whose pending entry still holds an earlier proposal of that pool slot
-            // goes the full path (held there until that one's decision was applied)
-            const bool held = ftag == TAG_PROPOSAL && PEND(forg, fpseq).valid != PS_NONE;
+            // goes the full path (held there until that one's decision was applied); with host judges the
+            // entry holds this proposal's verdict (checked above)
+            const bool held = ftag == TAG_PROPOSAL && !hjudge && PEND(forg, fpseq).valid != PS_NONE;
             ok = __ballot(full) == 0 && !held;
         }
         if (!ok) return ~0u;
-        uint32_t flog = ~0u;
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
                 atomicAdd(&S.bcast_delivered, 1ull);
@@ -1212,7 +1257,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else {
                     const uint32_t k = (uint32_t)fg >> 1;
                     atomicAdd(&S.judge_calls, 1ull);
-                    log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
+                    if (!host) log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
+                    else if (!hjudge)  // device judge in host mode: the verdict + PBuf for action() (phase F)
+                        flog = log_put(S, P, lr, LOG_JUDGED, forg, ffrom, fid, flen, fjudge, fpseq);
                     PendState* ps = &PEND(forg, fpseq);
                     if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                         ps->valid = PS_NONE;
@@ -1229,6 +1276,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                 }
             }
+            flog = rdl32(flog, 0);
         } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
             PendState* ps = &PEND(forg, fpseq);
             if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
@@ -1260,6 +1308,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
     // ---- a local origination by wave 0 alone (doorbell pass): header + chunks generated in registers,
     // stored to every child when all out-rings have room.  Returns false (nothing changed) otherwise
+    // (kind K_HOST: the payload chunks are a host command's, loaded to LDS at src by the doorbell pass)
     auto originate = [&](uint32_t kind, uint32_t w0, uint32_t id, uint32_t w2, uint32_t src, uint64_t out_head_r) -> bool {
         const uint32_t len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4;
         if (nch > nsmall || nch > kBellChunks) return false;
@@ -1269,6 +1318,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t hw2 = (w2 & 0xff00ffffu) | (kSlotMark << 16);
         u32x4 v = {0u, 0u, 0u, 0u};
         if (q == 0) v = u32x4{w0, id, hw2, (uint32_t)now_ticks()};
+        else if (q < nch && kind == K_HOST) v = *reinterpret_cast<const u32x4*>(stage + src + 16u * q);
         else if (q < nch) v = gen_chunk(P, kind, me, id, len, src, (int)(int8_t)(w0 >> 24), q);
         fwd_small(v, nch, need);
         if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
@@ -1289,12 +1339,18 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t nw = (S.own_word[k] += inc);
                 if ((nw & 0xffffu) == S.own_needed) {
                     const int d = (nw >> 16) == 0 ? 1 : 0;
-                    if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
-                        atomicAdd(&S.judge_calls, 1ull);
-                        log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                    if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback (phase B1)
+                        log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
+                        atomicAdd(&S.hwait, 1u);
+                        S.own_state[k] = 3;
+                    } else {
+                        if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
+                            atomicAdd(&S.judge_calls, 1ull);
+                            if (!host) log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                        }
+                        S.own_decision[k] = (uint32_t)d;
+                        S.own_state[k] = 2;
                     }
-                    S.own_decision[k] = (uint32_t)d;
-                    S.own_state[k] = 2;
                 }
             }
         } else {
@@ -1341,28 +1397,51 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const bool g0 = bq == 0u && gm && (B0 & gm) == gm, g1 = bq == 0u && gm && (B1 & gm) == gm;
         const uint64_t fh = __ballot(g0 || g1), fv = __ballot(g1);  // bit 8k: in-edge k's bell is whole (on vc fv)
         const uint32_t evh = (uint32_t)vin_head_r + 1u;
-        const uint64_t vhm = __ballot(!host && lane < sll && vb.y == evh && vb.w == evh);
+        const uint64_t vhm = __ballot(lane < sll && vb.y == evh && vb.w == evh);
         const int rk = lane >> 1;
         const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
         const uint64_t ip = lane < n_in2 && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
-        const uint64_t vp = !host && lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
+        const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
         const bool ldr = lane < n_in2 && ip > 0ull && !rhit;  // a counter-visible head without its bell: load it
         const uint64_t ldm = __ballot(ldr);
         if (__ballot(ip > 2ull || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { need_full = true; return 0u; }
-        if (host) {  // commands waiting: the full path; too little room in the pickup ring: wait for the host
-            if (rdl64(hpoll, 0) != S.hin_head) { need_full = true; return 0u; }
+        uint32_t ncmd = 0;  // host commands to take (FIFO order, the first kLLCmds)
+        bool cbell = false;  // ... the one in the command doorbell (already loaded, at kLLCmd)
+        if (host) {  // too little room in the pickup ring: wait for the host
             const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - rdl64(hpoll, 1));
             if (pk_free < 2u * (uint32_t)__popcll(__ballot(rhit || ldr)) + 2u * P.own_pool + 8u) return 0u;
+            if (ll_cmds) {
+                const uint64_t ct = rdl64(hpoll, 0), hh = S.hin_head;
+                ncmd = ct > hh ? (uint32_t)min(ct - hh, (uint64_t)kLLCmds) : 0u;
+                if (!ncmd && P.hll) {
+                    // the tail poll shows nothing new: the next command may be in its doorbell already.  Whole
+                    // when every 8-byte half of its chunks (lanes 2q, 2q + 1 = chunk q) carries hin_head + 1
+                    const u32x4 cv = lane < 16 ? *reinterpret_cast<const u32x4*>(stage + kLLCmdBell + 16u * (uint32_t)lane)
+                                               : u32x4{0u, 0u, 0u, 0u};
+                    const uint32_t T = (uint32_t)hh + 1u;
+                    const uint64_t tok = __ballot(lane < 16 && cv.y == T && cv.w == T);
+                    const uint32_t cn = (kHdr + (rdl32(cv.x, 1) & 0xffffu) + 15u) >> 4;  // header word 2: length
+                    const uint64_t cm = (1ull << (2u * min(cn, kBellChunks))) - 1ull;
+                    if ((tok & 3ull) == 3ull && cn <= kBellChunks && (tok & cm) == cm) {
+                        if (lane < 16) *reinterpret_cast<uint2*>(stage + kLLCmd + 8u * (uint32_t)lane) = make_uint2(cv.x, cv.z);
+                        ncmd = 1;
+                        cbell = true;
+                    }
+                }
+            } else if (rdl64(hpoll, 0) > S.hin_head) {  // (stage too small for the command scratch)
+                need_full = true;
+                return 0u;
+            }
         }
         const uint32_t nv = (uint32_t)vp;  // votes to load from child j's vote ring (<= kLLVotes)
         // (a latency round of bulk messages is originated by the full path: its announcement, heap slot and
         // scatter job)
         const bool lat_go = (P.mode & MODE_LAT) && (!BULK || P.len <= P.ring_cap) && S.lat_own_next != 0xffffffffu &&
                             rdl32(latr, 1) == S.lat_own_next;
-        const bool iar_dev = (P.mode & MODE_IAR) && !host;
+        const bool iar_dev = (P.mode & MODE_IAR) != 0;  // (host mode: decisions only -- its proposals are commands)
         const uint64_t nvm = __ballot(nv > 0u);
-        if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev) return 0u;
-        if (ldm || nvm) {
+        if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev && !ncmd) return 0u;
+        if (ldm || nvm || ncmd) {
             // one round trip: lane 8 s + q loads chunk q of the s-th ring head to load, lane kLLVotes j + i
             // vote i of child j (sc1 loads behind the counters, as phase D0 / B)
             const uint32_t sl = (uint32_t)lane >> 3, q = (uint32_t)lane & 7u;
@@ -1381,10 +1460,83 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             u32x4 lv = {0u, 0u, 0u, 0u}, lw = {0u, 0u, 0u, 0u};
             if (gsel >= 0 && q < lcap) lv = ld_sc1(rf, dsel + (hsel & fcap_m) * P.fwd_stride + 16u * q);
             if ((int)vj < sll && vi < nvj) lw = ld_sc1(rv, vdat + ((vhj + vi) & vcap_m) * kVoteSlot);
+            // host commands: lane 8 s + q chunk q of command s, from the command ring in host memory
+            // (system-scope loads behind the tail poll, as the full path's command DMA)
+            u32x4 lc = {0u, 0u, 0u, 0u};
+            if (!cbell && sl < ncmd && q < lcap) lc = ld_sys(rh, (uint32_t)((S.hin_head + sl) & hcap_m) * P.fwd_stride + 16u * q);
             *reinterpret_cast<u32x4*>(stage + kLLRing + 16u * (uint32_t)lane) = lv;
             *reinterpret_cast<u32x4*>(stage + kLLVote + 16u * (uint32_t)lane) = lw;
+            if (ncmd && !cbell) *reinterpret_cast<u32x4*>(stage + kLLCmd + 16u * (uint32_t)lane) = lc;
         }
         uint32_t done = 0;
+        // host commands in FIFO order, as phase C takes them: judge verdicts first of all (a held proposal
+        // below then goes on in this pass), bcast and proposal originations from the loaded chunks.  The
+        // first command this pass cannot take (quit, bulk, a message longer than the loaded chunks, no room)
+        // ends the run; what is left is the full iteration's (need_full) unless only room was missing
+        if (ncmd) {
+            uint32_t taken = 0;
+            for (; taken < ncmd; taken++) {  // uniform
+                const u32x4 hd = *reinterpret_cast<const u32x4*>(stage + kLLCmd + 128u * taken);
+                const uint32_t htag = (hd.x >> 16) & 0xffu;
+                const int vo = (int)(int8_t)(hd.x >> 24);
+                if (htag == CMD_JUDGE) {  // verdict of judge(data) for a held proposal (:698)
+                    if (lane == 0) {
+                        const int og = (int)(hd.x & 0xffffu);
+                        PendState* ps = &PEND(og < P.n ? og : 0, hd.z >> 24);
+                        if (og < P.n && ps->valid == PS_JREQ && ps->pid == (int32_t)hd.y) {
+                            ps->valid = vo ? PS_JYES : PS_JNO;
+                            atomicSub(&S.hwait, 1u);
+                        } else {
+                            set_error(S, P, ERR_HOST_CMD, hd.x);
+                        }
+                    }
+                } else if (htag == CMD_OWN_JUDGE) {  // final judge(NULL) of my proposal (:770-775)
+                    if (lane == 0) {
+                        const uint32_t k = (hd.z >> 24) & (P.pend_slots - 1u);
+                        if (S.own_state[k] == 3 && S.own_pid[k] == (int32_t)hd.y) {
+                            S.own_decision[k] = vo ? 1u : 0u;
+                            S.own_state[k] = 2;
+                            atomicSub(&S.hwait, 1u);
+                        } else {
+                            set_error(S, P, ERR_HOST_CMD, hd.x);
+                        }
+                    }
+                } else if (htag == TAG_BCAST || htag == TAG_PROPOSAL) {  // RLO_bcast_gen :1581 / RLO_submit_proposal :876
+                    const uint32_t len = hd.z & 0xffffu;
+                    if (((kHdr + len + 15u) >> 4) > lcap || sll == 0) { need_full = true; break; }
+                    if (htag == TAG_BCAST) {
+                        if (!originate(K_HOST, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), hd.y, len,
+                                       kLLCmd + 128u * taken, out_head_r))
+                            break;  // an out-ring is full: later
+                        if (lane == 0) atomicAdd(&S.originated, 1ull);
+                    } else {
+                        // a free pool slot, first from own_rr (phase C's choice); none: later
+                        const uint32_t ps2 = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
+                        const uint64_t busy = __ballot(ps2 != 0u);
+                        if ((uint32_t)__popcll(busy) >= P.own_pool) break;
+                        uint32_t k = S.own_rr;
+                        while ((busy >> k) & 1ull) k = (k + 1u) & (P.pend_slots - 1u);
+                        if (!originate(K_HOST, (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), hd.y, len | (k << 24),
+                                       kLLCmd + 128u * taken, out_head_r))
+                            break;
+                        if (lane == 0) {  // proposalPool_proposal_add (:1253-1279)
+                            S.own_pid[k] = (int32_t)hd.y;
+                            S.own_word[k] = 0;
+                            S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
+                            S.own_state[k] = 1;
+                            S.own_rr = k;
+                        }
+                    }
+                } else {  // quit, bulk: the full iteration's
+                    need_full = true;
+                    break;
+                }
+            }
+            if (taken) {
+                if (lane == 0) S.hin_head += taken;
+                done += taken;
+            }
+        }
         // votes: child j's next nv_j from its ring (the loaded slots), or its head from its bell
         for (uint64_t m = nvm | vhm; m; m &= m - 1) {
             const int j = __builtin_ctzll(m);
@@ -1416,6 +1568,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 continue;
             }
             const uint32_t need = lone(v, g, 0u, true, out_head_r);
+            if (need == kHeld || need == kAsked) {  // waits for the host's verdict (asked now: progress)
+                if (need == kAsked) done++;
+                continue;
+            }
             if (need == ~0u) {  // the full path takes it, through its counter
                 if (!fromb) need_full = true;
                 continue;
@@ -1485,11 +1641,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             const uint64_t vt = S.vout_tail[lane];
             if (vt != PUB_VOUT) { PUB_VOUT = vt; pub64(VTPTR, vt, sys); }
         }
-        if (host && lane == 0 && S.ev_n) {
-            S.pk_tail += S.ev_n;
-            S.log_count += S.ev_n;
-            S.ev_n = 0;
-            pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
+        if (host && lane == 0) {
+            if (ncmd) pub64_sys(&hctl[kHctlInjHead], S.hin_head);  // the commands taken (the host's sends complete)
+            if (S.ev_n) {
+                S.pk_tail += S.ev_n;
+                S.log_count += S.ev_n;
+                S.ev_n = 0;
+                pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
+            }
         }
         return done;
     };
@@ -1511,7 +1670,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // the ring polls) on every 4th re-poll only, so an idle rank still sees a ring message
                 // one VRAM poll after it lands; a command waits at most ~4 re-polls
                 // (every spin while a judge verdict is owed: the host answers within a few microseconds)
-                if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u))
+                // (with command doorbells the next command is polled every spin in its doorbell below)
+                if (host && lane < 2 && ((sp & 3u) == 0u || (S.hwait != 0u && !(llm && ll_cmds && P.hll))))
                     hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
@@ -1530,7 +1690,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             ba = ld_sc1(rc, o);
                             bb = ld_sc1(rc, o + 16u);
                         }
-                        if (!host && lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
+                        if (lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
+                        if (host && ll_cmds && P.hll && lane < 16)  // the next command's doorbell (16 x 16 B), to LDS
+                            *reinterpret_cast<u32x4*>(stage + kLLCmdBell + 16u * (uint32_t)lane) =
+                                ld_sys(rll, (uint32_t)(S.hin_head & hcap_m) * kLLCmdSlotB + 16u * (uint32_t)lane);
                         bool need_full = false;
                         const uint32_t nll = ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf, need_full);
                         if (nll) ll_prog = true;
@@ -1814,7 +1977,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // control commands (judge verdicts, quit) is applied now, the run of originations
                 // behind it becomes candidates in place (a proposal only when no own proposal is
                 // active, and it ends the run)
-                const uint64_t pend_n = rdl64(hpoll, 0) - S.hin_head;
+                // (a command doorbell may have run the head past the tail this poll saw)
+                const uint64_t pend_n = rdl64(hpoll, 0) > S.hin_head ? rdl64(hpoll, 0) - S.hin_head : 0ull;
                 if ((P.mode & MODE_HDIAG) && lane == 0) {  // how long seen commands wait here
                     if (pend_n) {
                         S.hd[0]++;
@@ -1960,7 +2124,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 u32x4 v = {0u, 0u, 0u, 0u};
                 if ((uint32_t)lane < nsmall) v = ld_sc1(rf, fsrc + 16u * (uint32_t)lane);  // header + payload, one trip
                 const uint32_t fneed = lone(v, fg, fsrc, false, out_head_r);
-                if (fneed != ~0u) {
+                if (fneed == kHeld || fneed == kAsked) {  // held for the host's verdict: nothing consumed
+                    VM_DRAIN();  // a judge request's record and PBuf before the pickup tail (bookkeeping)
+                    if (lane == fg) rtake_r = 0u;
+                    R = 0;
+                    C = 0;
+                    fastdone = fneed == kAsked ? 1u : 0u;
+                } else if (fneed != ~0u) {
                     VM_DRAIN();  // wave 0's stores: published in the bookkeeping below
                     // the bookkeeping sees: in-ring g admitted its one message (rtake_r), these out-rings one each
                     noi_r = lane < nout ? ((fneed >> lane) & 1u) : 0u;

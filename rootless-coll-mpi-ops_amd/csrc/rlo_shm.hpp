@@ -27,7 +27,7 @@
 namespace rlo {
 
 constexpr uint32_t kShmMagic = 0x534f4c52u;  // "RLOS"
-constexpr uint32_t kShmVersion = 3;
+constexpr uint32_t kShmVersion = 4;
 
 // a bulk origination: ACQUIRE (the next bulk sequence q, once its heap slot is free; q is not taken
 // yet), PUT the bytes window by window, COMMIT q (taken: the announcement carries it).  A failed PUT
@@ -42,6 +42,7 @@ struct ShmHdr {
     uint32_t stride, max_payload;    // command slot stride, pickup payload stride
     uint64_t bulk_max, stage_bytes;  // bulk message cap; staging window per rank
     uint64_t off_hctl, off_ev, off_evp, off_cli, off_cmd, off_stage, total;
+    uint64_t off_llc;                // command doorbells [nl][cmd_cap] x kLLCmdSlot (ll_cmd_put)
     uint32_t leader_failed, pad;     // the leader gave up (its kernel could not start / ended early)
 };
 
@@ -66,8 +67,27 @@ static_assert(offsetof(ClientBox, mtail) == kHctlInjTail * 8 && offsetof(ClientB
               "ClientBox words where the kernel polls its command tail / pickup head");
 
 struct ShmLayout {
-    uint64_t hctl, ev, evp, cli, cmd, stage, total;
+    uint64_t hctl, ev, evp, cli, cmd, stage, llc, total;
 };
+
+// Command doorbells: a command of at most kBellChunks 16-B chunks (header + 112 B) is also written,
+// data-tagged, into the doorbell slot of its sequence number -- the forward doorbells' format
+// (rlo_device.hpp): chunk q as two LL granule pairs {d0, T, d1, T}, {d2, T, d3, T}, T = sequence + 1,
+// every 8-byte half one atomic CPU store.  The kernel polls the slot of the next command it expects and
+// takes the command from there when every half of its chunks carries T: one PCIe read instead of a tail
+// poll followed by a slot load.  The ring slot and the tail are still written (the full path and longer
+// commands use them); the doorbell slot of sequence s is reused at s + cmd_cap, after the kernel consumed s
+constexpr uint32_t kLLCmdSlot = kBellChunks * 32u;
+inline void ll_cmd_put(uint8_t* slot, uint64_t seq, const uint32_t hdr[4], const void* payload, uint32_t len) {
+    if (kHdr + len > kBellChunks * 16u) return;  // longer commands: the ring slot only
+    const uint64_t T = (uint64_t)(uint32_t)(seq + 1u) << 32;
+    uint32_t w[kBellChunks * 4] = {0};
+    for (int i = 0; i < 4; i++) w[i] = hdr[i];
+    if (len) __builtin_memcpy(reinterpret_cast<uint8_t*>(w) + kHdr, payload, len);
+    const uint32_t nw = 4u * ((kHdr + len + 15u) / 16u);
+    uint64_t* d = reinterpret_cast<uint64_t*>(slot);
+    for (uint32_t i = 0; i < nw; i++) __atomic_store_n(d + i, (uint64_t)w[i] | T, __ATOMIC_RELAXED);
+}
 
 inline uint64_t shm_page(uint64_t x) { return (x + 4095u) & ~uint64_t(4095); }
 
@@ -81,6 +101,7 @@ inline ShmLayout shm_layout(uint32_t nl, uint32_t cmd_cap, uint32_t pk_cap, uint
     L.cli = o; o = shm_page(o + (uint64_t)nl * sizeof(ClientBox));
     L.cmd = o; o = shm_page(o + (uint64_t)nl * cmd_cap * stride);
     L.stage = o; o = shm_page(o + (uint64_t)nl * stage_bytes);
+    L.llc = o; o = shm_page(o + (uint64_t)nl * cmd_cap * kLLCmdSlot);
     L.total = o;
     return L;
 }

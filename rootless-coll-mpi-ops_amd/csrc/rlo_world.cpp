@@ -379,6 +379,7 @@ struct rlo_world {
     uint32_t lat_rounds = 0;
     // host-service program (pinned host memory)
     uint8_t* h_cmd = nullptr;       // [nl][cmd_cap][stride]     uncached VRAM, CPU writes through the BAR
+    uint8_t* h_llc = nullptr;       // [nl][cmd_cap] x kLLCmdSlot command doorbells (pinned host, not in a segment)
     uint64_t* h_ctl = nullptr;      // [nl][kHctlWords]           pinned host: device-written counters
     uint64_t* d_ctl = nullptr;      // [nl][kHctlWords]           uncached VRAM: host-written counters
     volatile uint32_t* hdp = nullptr;  // the GPU's HDP_MEM_COHERENCY_FLUSH_CNTL register (see hdp_flush)
@@ -1167,6 +1168,8 @@ static void host_free(rlo_world* w) {
         if (w->h_cmd) (void)hipFree(w->h_cmd);
         if (w->d_ctl) (void)hipFree(w->d_ctl);
     }
+    if (w->h_llc) (void)hipHostFree(w->h_llc);
+    w->h_llc = nullptr;
     if (w->shm) {  // h_ctl / h_ev / h_evp point into the segment
         (void)hipHostUnregister(w->shm);
         munmap(w->shm, (size_t)w->shm_bytes);
@@ -1214,7 +1217,7 @@ static int host_alloc(void** p, size_t bytes) {
 // created, mapped, registered with HIP (fine-grained: the kernel's counter / event stores reach the
 // clients' polls directly) and described in its header for the clients
 static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec** dev_ev, const uint8_t** dev_evp,
-                     uint8_t** dev_cmd, uint64_t** dev_cli) {
+                     uint8_t** dev_cmd, uint64_t** dev_cli, uint8_t** dev_llc) {
     const uint32_t nl = (uint32_t)w->nl;
     const uint64_t stage = w->L.bulk_max ? w->share_stage : 0;
     const rlo::ShmLayout L = rlo::shm_layout(nl, w->cmd_cap, w->pk_cap, w->L.stride, w->max_payload, stage);
@@ -1251,6 +1254,7 @@ static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec*
     *dev_evp = db + L.evp;
     *dev_cmd = db + L.cmd;
     *dev_cli = (uint64_t*)(db + L.cli);
+    *dev_llc = db + L.llc;
     rlo::ShmHdr* h = (rlo::ShmHdr*)b;
     h->version = rlo::kShmVersion;
     h->nl = nl;
@@ -1264,7 +1268,7 @@ static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec*
     h->bulk_max = w->L.bulk_max;
     h->stage_bytes = stage;
     h->off_hctl = L.hctl; h->off_ev = L.ev; h->off_evp = L.evp; h->off_cli = L.cli; h->off_cmd = L.cmd;
-    h->off_stage = L.stage; h->total = L.total;
+    h->off_stage = L.stage; h->total = L.total; h->off_llc = L.llc;
     __atomic_store_n(&h->magic, rlo::kShmMagic, __ATOMIC_RELEASE);  // clients check it last
     return RLO_OK;
 }
@@ -1307,12 +1311,14 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     const uint8_t* dev_evp = nullptr;
     uint8_t* dev_cmd = nullptr;
     uint64_t* dev_cli = nullptr;
+    uint8_t* dev_llc = nullptr;
     if (!w->shm_name.empty()) {  // rlo_host_share: the host-side rings in the shared segment
-        int rc = shm_build(w, &dev_hctl, &dev_ev, &dev_evp, &dev_cmd, &dev_cli);
+        int rc = shm_build(w, &dev_hctl, &dev_ev, &dev_evp, &dev_cmd, &dev_cli, &dev_llc);
         if (rc) { host_free(w); return rc; }
     } else if (host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
                host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) ||
-               host_alloc((void**)&w->h_evp, nl * pc * w->max_payload)) {
+               host_alloc((void**)&w->h_evp, nl * pc * w->max_payload) ||
+               (w->cmd_host && host_alloc((void**)&w->h_llc, nl * cc * rlo::kLLCmdSlot))) {
         host_free(w);
         return RLO_E_HIP;
     }
@@ -1334,6 +1340,8 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     P.hin_cap = cc;
     P.hctl = dev_hctl ? const_cast<uint64_t*>(dev_hctl) : w->h_ctl;
     P.hctl_dev = direct ? dev_cli : w->d_ctl;
+    // command doorbells (rlo_shm.hpp): wherever the commands are in host memory
+    P.hll = direct ? dev_llc : (w->cmd_host && !dev_cmd ? w->h_llc : nullptr);
     const uint64_t idle = cfg ? cfg->idle_timeout_s : 0;
     P.timeout_ticks = idle ? 100000000ull * idle : ~0ull >> 2;
     P.deadline_ticks = ~0ull >> 2;  // serves until RLO_CMD_QUIT
@@ -1363,6 +1371,8 @@ int rlo_host_post(rlo_world_t* w, int rank, const rlo_cmd_t* c, const void* payl
     hdr[3] = 0;
     std::memcpy(slot, hdr, sizeof hdr);
     if (len) std::memcpy(slot + rlo::kHdr, payload, len);
+    uint8_t* llc = direct ? w->shm + w->SL.llc : w->h_llc;
+    if (llc) rlo::ll_cmd_put(llc + ((size_t)lr * w->cmd_cap + (tail & (w->cmd_cap - 1))) * rlo::kLLCmdSlot, tail, hdr, payload, len);
     if (direct) {
         __atomic_store_n(&box->mtail, tail + 1, __ATOMIC_RELEASE);
         return RLO_OK;

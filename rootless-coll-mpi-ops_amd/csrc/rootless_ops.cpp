@@ -96,7 +96,11 @@ struct progress_engine {
     std::map<int, RLO_proposal_state> props;  // pool_depth > 1: every own proposal by pid
     int own_inflight = 0;            // own proposals posted whose result has not arrived
     std::deque<std::pair<int, std::vector<char>>> held_props;  // submitted beyond the pool: (pid, PBuf)
-    std::map<std::pair<int, int>, std::vector<char>> approved;  // (origin, pid) -> PBuf (queue_iar_pending)
+    std::map<std::pair<int, int>, std::vector<char>> approved;  // (origin, pid) -> PBuf bytes (queue_iar_pending)
+    // the zero-padded receive buffer a judge / action callback reads (the reference's calloc'd buffer): kept
+    // zeroed between calls -- only the bytes written for a call are cleared after it -- so a judge request
+    // costs no 32-KiB allocation on the proposal's path
+    std::vector<char> cbuf;
     long sent_bcast = 0, recved_bcast = 0;  // :1600, :586
     bool failed = false;
     uint32_t poll_tick = 0;
@@ -341,7 +345,10 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
         case RLO_EV_ACTION: {  // decision 1 for a proposal I approved: action(PBuf) (:842)
             auto it = e->approved.find(std::make_pair(ev.origin, (int)ev.id));
             if (it != e->approved.end()) {
-                if (e->action) e->action(it->second.data(), e->ctx);
+                const size_t n = it->second.size();
+                std::memcpy(e->cbuf.data(), it->second.data(), n);
+                if (e->action) e->action(e->cbuf.data(), e->ctx);
+                std::memset(e->cbuf.data(), 0, n);
                 e->approved.erase(it);
             }
             break;
@@ -391,15 +398,15 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
         case RLO_EV_JUDGE: {  // judge(proposal data, ctx) (:698); data is zero-padded like the
             e->n_judge++;
                               // reference's calloc'd receive buffer
-            std::vector<char> pb(RLO_MSG_SIZE_MAX + 16, 0);
             const uint32_t n = ev.len < (uint32_t)RLO_MSG_SIZE_MAX ? ev.len : (uint32_t)RLO_MSG_SIZE_MAX;
-            std::memcpy(pb.data(), payload, n);
-            int v = e->judge ? e->judge(pb.data() + 16, e->ctx) : 1;
+            std::memcpy(e->cbuf.data(), payload, n);
+            int v = e->judge ? e->judge(e->cbuf.data() + 16, e->ctx) : 1;
+            std::memset(e->cbuf.data(), 0, n);
             if (v != 0 && v != 1) {
                 std::printf("%s:%u - rank = %03d: unknown judgment received: %d\n", __func__, __LINE__, e->rank, v);
                 v = 0;
             }
-            if (v == 1) e->approved[std::make_pair(ev.origin, (int)ev.id)] = std::move(pb);
+            if (v == 1) e->approved[std::make_pair(ev.origin, (int)ev.id)].assign((const char*)payload, (const char*)payload + n);
             rlo_cmd_t c;
             std::memset(&c, 0, sizeof c);
             c.kind = RLO_CMD_JUDGE;
@@ -413,10 +420,8 @@ void handle_event(progress_engine* e, const rlo_log_rec_t& ev, const uint8_t* pa
         case RLO_EV_JUDGED: {  // extension: the device judged a proposal here; keep the PBuf for action()
             e->n_judge++;
             if (ev.vote == 1) {
-                std::vector<char> pb(RLO_MSG_SIZE_MAX + 16, 0);
                 const uint32_t n = ev.len < (uint32_t)RLO_MSG_SIZE_MAX ? ev.len : (uint32_t)RLO_MSG_SIZE_MAX;
-                std::memcpy(pb.data(), payload, n);
-                e->approved[std::make_pair(ev.origin, (int)ev.id)] = std::move(pb);
+                e->approved[std::make_pair(ev.origin, (int)ev.id)].assign((const char*)payload, (const char*)payload + n);
             }
             break;
         }
@@ -769,6 +774,7 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     e->slot_bytes = (uint32_t)((cap + 15) & ~(size_t)15);
     e->deliver_max = (uint32_t)cap - (uint32_t)sizeof(int);  // bytes [0, msg_size_max - 4) arrive (:1588)
     e->evbuf.assign(e->slot_bytes + 16, 0);
+    e->cbuf.assign(RLO_MSG_SIZE_MAX + 16, 0);
     int level = 0, lw = 0, scc = 0, sl[16];
     rlo_topology(e->size, e->rank, &level, &lw, &scc, &e->send_list_len, sl);
     proposal_init(&e->own);

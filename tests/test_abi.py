@@ -170,7 +170,7 @@ def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
     o = 4096
     off = {}
     for key, size in (("hctl", nl * 64 * 8), ("ev", nl * pc * rec), ("evp", nl * pc * maxp), ("cli", nl * 512),
-                      ("cmd", nl * cc * stride), ("stage", 0)):
+                      ("cmd", nl * cc * stride), ("stage", 0), ("llc", nl * cc * 256)):
         off[key] = o
         o = page(o + size)
     total = o
@@ -178,8 +178,8 @@ def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
     os.ftruncate(fd, total)
     m = mmap.mmap(fd, total)
     os.close(fd)
-    hdr = struct.pack("<10I9Q2I", 0, 3, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
-                      off["cli"], off["cmd"], off["stage"], total, 0, 0)
+    hdr = struct.pack("<10I10Q2I", 0, 4, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
+                      off["cli"], off["cmd"], off["stage"], total, off["llc"], 0, 0)
     m[:len(hdr)] = hdr
     m[0:4] = struct.pack("<I", 0x534F4C52)  # magic last
     return m, off, rec
@@ -217,6 +217,11 @@ def test_shared_service_client_protocol_without_gpu():
         w0, w1, w2, _ = struct.unpack_from("<4I", m, slot)
         assert (w0 & 0xFFFF, (w0 >> 16) & 0xFF, w1, w2 & 0xFFFFFF) == (5, 0, 7, len(payload))
         assert bytes(m[slot + 16:slot + 16 + len(payload)]) == payload
+        # ... and data-tagged in its command doorbell (rlo_shm.hpp ll_cmd_put): 8-byte halves {word, seq + 1}
+        bell = off["llc"] + (1 * 4 + 2) * 256
+        g = struct.unpack_from("<16I", m, bell)
+        assert g[1::2] == (3,) * 8 and g[0::2][:4] == (w0, w1, w2, 0)
+        assert bytes(struct.pack("<4I", *g[0::2][4:8])) == payload + b"\0"
         m[hctl + 16 * 8:hctl + 17 * 8] = struct.pack("<Q", 3)  # the device consumed 3
         consumed, posted = ctypes.c_uint64(), ctypes.c_uint64()
         lib.rlo_client_cmd_count(c, ctypes.byref(consumed), ctypes.byref(posted))
