@@ -160,6 +160,10 @@ struct Shared {
     // origination progress
     uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen, error, error_aux, progressed;
     uint32_t hwait;  // host mode: judge verdicts the host owes this rank (its command ring is polled every spin then)
+    // host mode with command doorbells: wave 1 polls the host (PCIe) while wave 0 spins on the rings --
+    // the command tail / pickup head it saw last, and the phase-A round wave 0 finished (wave 1 stops)
+    uint64_t hp[2];
+    uint32_t a_done, cseq;
     uint64_t hd[8], hd_t0;  // MODE_HDIAG counters (host mode)
     // pull worlds: my relay ring (slots taken / released), this iteration's allocations, and the release
     // records: relay count rq_relay[e] is released once every out-ring's consumer passed rq_out[e][oi]
@@ -1078,6 +1082,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0; S.hwait = 0;
+            S.hp[0] = 0; S.hp[1] = 0; S.a_done = 0; S.cseq = 0;
             S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
@@ -1138,6 +1143,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint32_t rbase_r = 0, rtake_r = 0, noi_r = 0;  // lane g / oi: this iteration's selection, admitted counts
     // doorbells (rlo_device.hpp, MODE_LL): on in this launch unless it profiles phases or A/Bs the fast path
     const bool llm = LL && (P.mode & MODE_LL) && !(P.mode & (MODE_PROF | MODE_NOFAST));
+    // host mode with doorbells and command doorbells: the host's words (command tail, pickup head, the next
+    // command's doorbell) are polled by wave 1 during phase A, so wave 0's spin is one VRAM round trip, not
+    // a PCIe one (a host-service hop took twice the device program's: tools/host_latency.py)
+    // (4-wave kernels only -- the drop-in's large-slot worlds: the 8-wave doorbell kernel has no registers for it)
+    const bool hpw = W == 4 && host && llm && ll_cmds && P.hll != nullptr;
+    uint32_t a_it = 0;  // phase-A rounds (every wave counts them alike)
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);  // my part's ctrl region (my bells)
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
@@ -1413,19 +1424,22 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (ll_cmds) {
                 const uint64_t ct = rdl64(hpoll, 0), hh = S.hin_head;
                 ncmd = ct > hh ? (uint32_t)min(ct - hh, (uint64_t)kLLCmds) : 0u;
-                if (!ncmd && P.hll) {
-                    // the tail poll shows nothing new: the next command may be in its doorbell already.  Whole
-                    // when every 8-byte half of its chunks (lanes 2q, 2q + 1 = chunk q) carries hin_head + 1
-                    const u32x4 cv = lane < 16 ? *reinterpret_cast<const u32x4*>(stage + kLLCmdBell + 16u * (uint32_t)lane)
-                                               : u32x4{0u, 0u, 0u, 0u};
+                if (!ncmd && hpw) {
+                    // the tail shows nothing new: the next command may be whole in its doorbell already, as wave 1
+                    // copied it (a seqlock: S.cseq = its sequence + 1 before and after the copy is read)
                     const uint32_t T = (uint32_t)hh + 1u;
-                    const uint64_t tok = __ballot(lane < 16 && cv.y == T && cv.w == T);
-                    const uint32_t cn = (kHdr + (rdl32(cv.x, 1) & 0xffffu) + 15u) >> 4;  // header word 2: length
-                    const uint64_t cm = (1ull << (2u * min(cn, kBellChunks))) - 1ull;
-                    if ((tok & 3ull) == 3ull && cn <= kBellChunks && (tok & cm) == cm) {
-                        if (lane < 16) *reinterpret_cast<uint2*>(stage + kLLCmd + 8u * (uint32_t)lane) = make_uint2(cv.x, cv.z);
-                        ncmd = 1;
-                        cbell = true;
+                    const uint32_t s1 = (uint32_t)uni((int)*reinterpret_cast<volatile uint32_t*>(&S.cseq));
+                    if (s1 == T) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        uint64_t d = 0;
+                        if (lane < 16) d = *reinterpret_cast<volatile uint64_t*>(stage + kLLCmdBell + 8u * (uint32_t)lane);
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        const uint32_t s2 = (uint32_t)uni((int)*reinterpret_cast<volatile uint32_t*>(&S.cseq));
+                        if (s2 == T) {
+                            if (lane < 16) *reinterpret_cast<uint64_t*>(stage + kLLCmd + 8u * (uint32_t)lane) = d;
+                            ncmd = 1;
+                            cbell = true;
+                        }
                     }
                 }
             } else if (rdl64(hpoll, 0) > S.hin_head) {  // (stage too small for the command scratch)
@@ -1656,6 +1670,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     for (;;) {
         asm volatile("" : "+v"(lane));  // (see lane's declaration)
         lt_mask = (1ull << lane) - 1ull;
+        a_it++;
         // ---------------- A: wave 0 polls; every wave drains its stores of the last iteration
         uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
         uint32_t errf = 0, sid = 0, latr = 0;
@@ -1671,8 +1686,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // one VRAM poll after it lands; a command waits at most ~4 re-polls
                 // (every spin while a judge verdict is owed: the host answers within a few microseconds)
                 // (with command doorbells the next command is polled every spin in its doorbell below)
-                if (host && lane < 2 && ((sp & 3u) == 0u || (S.hwait != 0u && !(llm && ll_cmds && P.hll))))
+                if (hpw) {
+                    if (lane < 2) hpoll = S.hp[lane];  // wave 1's latest poll
+                } else if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u)) {
                     hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
+                }
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
@@ -1691,9 +1709,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             bb = ld_sc1(rc, o + 16u);
                         }
                         if (lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
-                        if (host && ll_cmds && P.hll && lane < 16)  // the next command's doorbell (16 x 16 B), to LDS
-                            *reinterpret_cast<u32x4*>(stage + kLLCmdBell + 16u * (uint32_t)lane) =
-                                ld_sys(rll, (uint32_t)(S.hin_head & hcap_m) * kLLCmdSlotB + 16u * (uint32_t)lane);
                         bool need_full = false;
                         const uint32_t nll = ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf, need_full);
                         if (nll) ll_prog = true;
@@ -1715,15 +1730,19 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                 }
                 // with doorbells only new work counts: a counter that caught up with what the bells already
-                // delivered, credits (nothing waits for them in an idle iteration), another rank's round
+                // delivered, credits (nothing waits for them in an idle iteration), another rank's round.  Nor
+                // do the host's words: the doorbell pass takes the commands (need_full for the ones it cannot)
+                // and waits for pickup room itself -- a full iteration on every pickup the host consumed would
+                // stand between a judge request and its verdict
                 const bool moved =
                     llm ? (in_tail_r != S.snap[0][lane] && in_tail_r > in_head_r) ||
-                              (vin_tail_r != S.snap[1][lane] && vin_tail_r > vin_head_r) || hpoll != p_h ||
+                              (vin_tail_r != S.snap[1][lane] && vin_tail_r > vin_head_r) ||
                               (latr != p_lat && rdl32(latr, 1) == S.lat_own_next) || errf != 0
                         : in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] || out_head_r != S.snap[2][lane] ||
                               vout_head_r != S.snap[3][lane] || hpoll != p_h || latr != p_lat || errf != 0 || bmoved;
                 if (__ballot(moved)) break;
             }
+            if (hpw && lane == 0) S.a_done = a_it;  // wave 1 stops polling the host
             S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
             S.snap[3][lane] = vout_head_r; p_h = hpoll; p_lat = latr;
             // host mode: a heartbeat for the host's watchdog every 4096 iterations (what this rank's
@@ -1759,6 +1778,35 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
+        } else if (hpw && w == 1) {
+            // the host poller: until wave 0 ends its spin, the next command's doorbell (lanes 0-15, 16 B each,
+            // to LDS at kLLCmdBell: the doorbell pass checks its tags) and the command tail / pickup head
+            // (lanes 16, 17 -> S.hp).  Every load of a round is waited for before the stop word is read, so
+            // the last round's values are in LDS before the barrier
+            for (;;) {
+                const uint64_t hh = uni64(S.hin_head);
+                u32x4 cv = {0u, 0u, 0u, 0u};
+                uint64_t hv = 0;
+                if (lane < 16) cv = ld_sys(rll, (uint32_t)(hh & hcap_m) * kLLCmdSlotB + 16u * (uint32_t)lane);
+                if (lane == 16 || lane == 17) hv = poll64_sys(&hctl_dev[lane == 16 ? kHctlInjTail : kHctlPkHead]);
+                if (lane == 16 || lane == 17) S.hp[lane - 16] = hv;
+                // whole: every 8-byte half of its chunks (lanes 2q, 2q + 1 = chunk q) carries hh + 1.  Then its
+                // words go to LDS under the seqlock S.cseq (0 while they are rewritten), once per command
+                const uint32_t T = (uint32_t)hh + 1u;
+                const uint64_t tok = __ballot(lane < 16 && cv.y == T && cv.w == T);
+                const uint32_t cn = (kHdr + (rdl32(cv.x, 1) & 0xffffu) + 15u) >> 4;  // header word 2: length
+                const uint64_t cm = (1ull << (2u * min(cn, kBellChunks))) - 1ull;
+                if ((tok & 3ull) == 3ull && cn <= kBellChunks && (tok & cm) == cm &&
+                    (uint32_t)uni((int)S.cseq) != T) {
+                    if (lane == 0) *reinterpret_cast<volatile uint32_t*>(&S.cseq) = 0u;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane < 16)
+                        *reinterpret_cast<volatile uint64_t*>(stage + kLLCmdBell + 8u * (uint32_t)lane) = (uint64_t)cv.x | ((uint64_t)cv.z << 32);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane == 0) *reinterpret_cast<volatile uint32_t*>(&S.cseq) = T;
+                }
+                if (__builtin_amdgcn_readfirstlane((int)S.a_done) == (int)a_it) break;
+            }
         }
         VM_DRAIN();
         BAR();  // every payload / vote store of the previous iteration has left its wave
