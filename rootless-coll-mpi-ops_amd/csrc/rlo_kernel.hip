@@ -1667,6 +1667,18 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         return done;
     };
 
+    // world rank 0 observes round completions of the latency program on its own clock (wave 0, latr lane 1 =
+    // the round word just polled): in the spin loop too, where the doorbell pass keeps an idle rank 0 for
+    // many rounds (observed only after it, successive rounds read as 0 us apart)
+    auto lat_observe = [&](uint32_t latr) {
+        const uint32_t done_r = rdl32(latr, 1), seen = S.lat_seen;
+        if (done_r > seen) {
+            const uint64_t tn = now_ticks();
+            for (uint32_t k = seen + (uint32_t)lane; k < done_r && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
+            if (lane == 0) S.lat_seen = done_r;
+        }
+    };
+
     for (;;) {
         asm volatile("" : "+v"(lane));  // (see lane's declaration)
         lt_mask = (1ull << lane) - 1ull;
@@ -1699,6 +1711,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if ((P.mode & MODE_LAT) && lane == 1)  // the round in progress (part 0's word when sharded)
                     latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                : poll32(P.lat_round);
+                if ((P.mode & MODE_LAT) && me == 0) lat_observe(latr);  // every spin: doorbells keep wave 0 here
                 if constexpr (LL) {
                     if (llm) {  // my doorbells beside the counters: lane (k, q) chunk q of in-edge k's, lane j child j's vote
                         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
@@ -1768,14 +1781,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (lane == 0) S.b.cmask[u] = m;
                 }
             }
-            if ((P.mode & MODE_LAT) && me == 0) {  // world rank 0 observes round completions on its clock
-                const uint32_t done_r = rdl32(latr, 1), seen = S.lat_seen;
-                if (done_r > seen) {
-                    const uint64_t tn = now_ticks();
-                    for (uint32_t k = seen + (uint32_t)lane; k < done_r && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
-                    if (lane == 0) S.lat_seen = done_r;
-                }
-            }
+            if ((P.mode & MODE_LAT) && me == 0) lat_observe(latr);
             if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
         } else if (hpw && w == 1) {
