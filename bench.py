@@ -303,7 +303,8 @@ def _world(rlo, dist, R, world, rank, local, **kw):
 def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64), rounds=8):
     """BASELINE configs[2] / SURVEY 8(d) C3: large-message ROOTLESS bcast through the engine -- the
     origin alone decides to send, receivers learn of it from the announcement on the skip-ring tree,
-    the mover workgroups move the bytes (pipelined scatter + all-gather between the ranks' heaps).
+    the mover workgroups move the bytes (one GPU: a fan-out from the origin's copy into every receiver's heap;
+    across GPUs: pipelined scatter + all-gather between the ranks' heaps).
     The latency program: one bcast at a time from random originators, round i+1 starts when every
     rank holds round i; algbw = S / round time (world rank 0's clock).  N > 1: one rank per GPU,
     beside rooted RCCL broadcast of the same bytes from the same root.  N = 1: 8 ranks on the GPU."""
@@ -341,10 +342,10 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
                    "verified": bool(ok)}
             rec["algbw_GBps"] = round(nbytes / rt / 1e9, 2) if rt > 0 else None
             if world == 1 and rt > 0:
-                # one GPU: the origin's copy written at origination and read by the scatter (2S), every
-                # receiver's copy written once ((G-1)S), the stripes read once to all-gather (S), every
-                # receiver reads its copy to verify ((G-1)S): (2G+1)S HBM bytes
-                rec["hbm_GBps"] = round((2 * G + 1) * nbytes / rt / 1e9, 1)
+                # one GPU (direct plan): the origin's copy written at origination and read once by the
+                # fan-out (2S), every receiver's copy written once ((G-1)S) and read back to verify ((G-1)S):
+                # 2G S HBM bytes
+                rec["hbm_GBps"] = round(2 * G * nbytes / rt / 1e9, 1)
                 rec["hbm_frac"] = round(rec["hbm_GBps"] / HBM_PEAK_GBS, 4)
             if rank == 0:
                 note("bulk %d MiB: %.3f ms/round" % (mib, rt * 1e3))
@@ -369,8 +370,9 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
     finally:
         w.close()
     return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "movers_per_part": w.info.get("movers"),
-            "algorithm": "rootless: announcement on the skip-ring tree, mover workgroups scatter + all-gather "
-                         "between per-rank heaps (rlo_kernel.hip mover_run)",
+            "algorithm": "rootless: announcement on the skip-ring tree, mover workgroups move the bytes between "
+                         "per-rank heaps (rlo_kernel.hip mover_run): one GPU a fan-out from the origin's copy, "
+                         "across GPUs scatter + all-gather",
             "timing": "median round time on world rank 0's clock (announce -> every rank holds the bytes -> "
                       "next originator starts)",
             "baseline": "torch.distributed.broadcast, nccl backend (RCCL), same root" if nccl is not None else None,

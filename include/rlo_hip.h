@@ -256,7 +256,8 @@ int rlo_device_count(void);
  * this rank's heap; then post RLO_CMD_BULK_RELEASE with origin = ev->origin, pseq = ev->aux. */
 /* the chunk / stripe / tile plan every rank derives for a bulk message of len bytes in an N-rank
  * world (cross: parts span GPUs); pure host arithmetic (rlo_device.hpp bulk_plan) */
-typedef struct { uint32_t nchunks, stripe, chunk, tile, total_tiles, pad; } rlo_bulk_plan_t;
+/* direct = 1: one GPU -- one stripe (the message), every tile fanned out from the origin's copy */
+typedef struct { uint32_t nchunks, stripe, chunk, tile, total_tiles, direct; } rlo_bulk_plan_t;
 int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out);
 /* the storm program's payload length of bcasts 0..k-1 (rlo_storm_cfg_t len, len_max, seed): the
  * workload generator's host side, for byte accounting (no GPU) */

@@ -278,6 +278,11 @@ struct Params {
 //     bumped; the origin reuses slot s for sequence q + B only when done(o, s) counts every receiver.
 // Mover classes: class A (SCATTER, VERIFY) never waits; class B (GATHER) waits only for class-A
 // scatters, so no cycle of waits exists however announcements interleave.
+// DIRECT plans (every part on one GPU: no links to balance, the copy is HBM bound): one stripe, the
+// whole message; a SCATTER tile is stored straight into EVERY receiver's slot (a fan-out from the
+// origin's copy: read once, written N-1 times) and bumps every receiver's tflag; no GATHER jobs; all
+// movers are class A (nothing waits).  Per byte: the origin's copy read once and N-1 copies written,
+// against a stripe read + a scatter write + N-1 gather writes, and no scatter -> gather hand-off.
 constexpr uint32_t kBulkKiB = 1024;     // stripe granularity
 constexpr int kBulkMaxChunks = 16;
 constexpr uint32_t kBulkLine = 128;     // per (rank, origin, slot): sflag[16] u32 @0, tflag u32 @64
@@ -334,8 +339,20 @@ constexpr uint32_t kMaxSub = 256;
 constexpr int kMoveDepth = 8;
 struct BulkPlan {
     uint32_t nchunks, stripe, chunk, tile;  // chunk = stripe * (N - 1); stripe, tile multiples of 1 KiB
+    uint32_t direct;                        // one GPU: one stripe = chunk = the message, fanned out
 };
 __host__ __device__ inline BulkPlan bulk_plan(int n, uint32_t len, bool cross) {
+    if (!cross) {
+        BulkPlan p;
+        p.direct = 1;
+        p.stripe = p.chunk = len ? (len + kBulkKiB - 1) / kBulkKiB * kBulkKiB : kBulkKiB;
+        p.nchunks = len ? 1u : 0u;
+        const uint32_t tmax = len >= 2 * kBulkChunk1 ? kBulkTileMax : kBulkTileSmall;
+        const uint32_t parts = (p.stripe + tmax - 1) / tmax;
+        p.tile = (p.stripe / parts + kBulkKiB - 1) / kBulkKiB * kBulkKiB;
+        (void)n;
+        return p;
+    }
     uint32_t k = 1;
     if (cross) {
         while ((uint64_t)(k + 1) * (k + 1) * (4ull << 20) <= len && k < (uint32_t)kBulkMaxChunks) k++;
@@ -350,6 +367,7 @@ __host__ __device__ inline BulkPlan bulk_plan(int n, uint32_t len, bool cross) {
     uint64_t chunk = stripe * m;
     while ((len + chunk - 1) / chunk > (uint64_t)kBulkMaxChunks) { stripe *= 2; chunk = stripe * m; }
     BulkPlan p;
+    p.direct = 0;
     p.stripe = (uint32_t)stripe;
     p.chunk = (uint32_t)chunk;
     p.nchunks = len ? (uint32_t)((len + chunk - 1) / chunk) : 0u;
@@ -382,8 +400,9 @@ __host__ __device__ inline uint32_t bulk_total_tiles(const BulkPlan& p, uint32_t
     for (uint32_t c = 0; c < p.nchunks; c++) t += bulk_chunk_tiles(p, len, c);
     return t;
 }
-// tiles of stripe k over all chunks (one receiver's GATHER job)
+// tiles of stripe k over all chunks (one receiver's GATHER job; none in a direct plan)
 __host__ __device__ inline uint32_t bulk_stripe_tiles(const BulkPlan& p, uint32_t len, uint32_t k) {
+    if (p.direct) return 0u;
     uint32_t t = 0;
     for (uint32_t c = 0; c < p.nchunks; c++) t += bulk_tiles_of(p, bulk_stripe_len(p, len, c, k));
     return t;

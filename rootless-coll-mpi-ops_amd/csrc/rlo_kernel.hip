@@ -588,12 +588,28 @@ __device__ __forceinline__ bool bulk_ok(const Params& P, int r, int o, uint32_t 
     return ok;
 }
 
+// the part tables (written by the host before launch, read-only in the kernel) through the constant address
+// space: uniform indices then load with s_load (lgkmcnt), not with vector loads, whose vmcnt wait would also
+// wait for every store in flight -- inside the movers' copy loops that was a full drain per destination
+template <class T>
+__device__ __forceinline__ T ldc(const T* p, int i) {
+    return ((const __attribute__((address_space(4))) T*)(uintptr_t)p)[i];
+}
 // heap slot (r, o, s), its flag line and the origin's done word, in whichever part holds r / o
 __device__ __forceinline__ uint8_t* bulk_heap(const Params& P, int r, int o, uint32_t s) {
     if (!bulk_ok(P, r, o, s, 1)) return nullptr;  // a null rsrc base: every access is dropped
-    const int p = P.part_of[r];
-    const uint64_t lr = (uint64_t)(r - P.part_begin[p]);
-    return reinterpret_cast<uint8_t*>(P.bheap[p]) + ((lr * (uint64_t)P.n + (uint64_t)o) * P.bulk_slots + s) * P.bulk_cap;
+    const int p = ldc(P.part_of, r);
+    const uint64_t lr = (uint64_t)(r - ldc(P.part_begin, p));
+    return reinterpret_cast<uint8_t*>(ldc(P.bheap, p)) + ((lr * (uint64_t)P.n + (uint64_t)o) * P.bulk_slots + s) * P.bulk_cap;
+}
+// heap slot (r, o, s) as a buffer resource in SGPRs -- the address is uniform, but it is computed from
+// loaded table words, and a VGPR resource makes the compiler wrap every access in a waterfall loop --
+// cut to bytes [off, off + bytes) of that slot: accesses past the end are dropped by the hardware's
+// range check (loads return zeros), which is what lets the copy loops below run without per-granule guards
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bulk_rsrc_at(const Params& P, int r, int o, uint32_t s, uint32_t off,
+                                                              uint32_t bytes) {
+    return mk_rsrc(reinterpret_cast<void*>(uni64(reinterpret_cast<uint64_t>(bulk_heap(P, r, o, s)) + off)),
+                   (uint32_t)uni((int)bytes));
 }
 __device__ __forceinline__ uint32_t* bulk_flags(const Params& P, int r, int o, uint32_t s) {
     if (!bulk_ok(P, r, o, s, 2)) return reinterpret_cast<uint32_t*>(P.jctl + kJctlSink);
@@ -670,14 +686,26 @@ __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t
     atomicAdd((unsigned long long*)&P.jctl[kJctlPostsByKind + kind], 1ull);  // diagnostics: posts by kind (41..43)
     const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
     const uint64_t t0 = now_ticks();
-    for (uint32_t u = 0; u < nsub; u++) {
-        const uint64_t j = j0 + u;
-        while (__hip_atomic_load(&P.jfree[cls * P.jslots + (uint32_t)(j & jm)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-               (j >> lg)) {
-            __builtin_amdgcn_s_sleep(1);
-            if (now_ticks() - t0 > P.timeout_ticks) {  // cannot happen unless a mover died: stop loudly
-                atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
-                return;
+    // the slots' generation words 16 at a time, loads issued together (one round trip per 16 sub-jobs;
+    // a dependent load per sub-job made a 1-MiB scatter's 70 sub-jobs cost ~70 round trips)
+    uint64_t* const jf = P.jfree + (size_t)cls * P.jslots;
+    for (uint32_t u0 = 0; u0 < nsub; u0 += 16u) {
+        uint64_t g[16];
+#pragma unroll
+        for (uint32_t i = 0; i < 16u; i++) {
+            const uint64_t j = j0 + min(u0 + i, nsub - 1u);  // (past the end: the last one again)
+            g[i] = __hip_atomic_load(&jf[(uint32_t)(j & jm)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 16u; i++) {
+            const uint64_t j = j0 + min(u0 + i, nsub - 1u);
+            while (g[i] != (j >> lg)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (now_ticks() - t0 > P.timeout_ticks) {  // cannot happen unless a mover died: stop loudly
+                    atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                    return;
+                }
+                g[i] = __hip_atomic_load(&jf[(uint32_t)(j & jm)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -698,6 +726,41 @@ __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t
         uint64_t* dst = reinterpret_cast<uint64_t*>(P.jobs + (size_t)cls * P.jslots + (uint32_t)((j0 + u) & jm));
         __hip_atomic_store(dst, (uint64_t)(uint32_t)(j0 + u + 1u) | ((uint64_t)kind << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// One tile of the movers' copy: granules [0, ngr) of src into ndst destinations (dst(j): the j-th one's
+// resource, cut to the tile like src).  No branch per granule: with one, the compiler could not count the
+// stores in flight and put a vmcnt(0) before EVERY store, so each 16-B-per-lane store waited for the
+// previous one's write acknowledgement (a mover moved ~5 GB/s).  The next batch's loads are issued before
+// this batch's stores: vmcnt retires in issue order, so waiting for those loads never waits for the stores.
+template <bool SYS, int W, class F>
+__device__ __forceinline__ void tile_copy(__amdgpu_buffer_rsrc_t rs, uint32_t ngr, int tid, int ndst, F dst) {
+    constexpr int kT = 64 * W, D = kMoveDepth;
+    constexpr uint32_t step = (uint32_t)D * kT;
+    u32x4 a[D], b[D];
+    auto load = [&](u32x4 (&v)[D], uint32_t g0) {
+#pragma unroll
+        for (int u = 0; u < D; u++) {
+            const uint32_t off = 16u * (g0 + (uint32_t)(u * kT + tid));
+            v[u] = SYS ? ld_sys(rs, off) : ld_sc1(rs, off);
+        }
+    };
+    auto store = [&](const u32x4 (&v)[D], uint32_t g0) {
+        for (int j = 0; j < ndst; j++) {
+            const __amdgpu_buffer_rsrc_t rd = dst(j);
+#pragma unroll
+            for (int u = 0; u < D; u++) st_ring(rd, 16u * (g0 + (uint32_t)(u * kT + tid)), v[u], SYS);
+        }
+    };
+    // ping-pong, no register copies; a prefetch past the tile reads zeros (range check) and is not stored
+    load(a, 0u);
+    for (uint32_t g0 = 0; g0 < ngr; g0 += 2u * step) {
+        load(b, g0 + step);
+        store(a, g0);
+        if (g0 + step >= ngr) break;
+        load(a, g0 + 2u * step);
+        store(b, g0 + step);
     }
 }
 
@@ -722,7 +785,8 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
     constexpr int kT = 64 * W;
     const uint32_t mi = blockIdx.x - P.n_local;
     const uint32_t na = (P.nmov + 1u) / 2u;
-    const uint32_t cls = mi < na ? JCLS_A : JCLS_B;
+    // (direct plans -- one GPU -- post no GATHER jobs: every mover serves class A)
+    const uint32_t cls = (P.bulk_cross == 0u || mi < na) ? JCLS_A : JCLS_B;
     const bool sys = P.sys_scope != 0;
     const int n = P.n;
     const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
@@ -775,7 +839,20 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
         }
         BAR();
         if (S.mv_stop) return;
-        const BulkJob jb = S.mv_job;  // uniform (LDS broadcast)
+        // the sub-job, made wave-uniform explicitly: read from LDS it lives in VGPRs, and every heap
+        // address derived from it would be a VGPR buffer resource -- the compiler then wraps EACH load and
+        // store of the copy loops in a readfirstlane waterfall loop (the movers ran at ~5 GB/s each)
+        BulkJob jb;
+        {
+            const u32x4* js = reinterpret_cast<const u32x4*>(&S.mv_job);
+            u32x4 q[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const u32x4 v = js[i];
+                q[i] = u32x4{(uint32_t)uni((int)v.x), (uint32_t)uni((int)v.y), (uint32_t)uni((int)v.z), (uint32_t)uni((int)v.w)};
+            }
+            __builtin_memcpy(&jb, q, sizeof jb);
+        }
         if (!(jb.kind >= JOB_SCATTER && jb.kind <= JOB_VERIFY && (uint32_t)jb.origin < (uint32_t)n &&
               (uint32_t)jb.lr < P.n_local && jb.slot < P.bulk_slots && jb.len > 0 && jb.len <= P.bulk_cap &&
               jb.ntiles > 0 && jb.ti0 + jb.ntiles <= jb.total && jb.parent <= jm)) {
@@ -816,38 +893,44 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                 const uint32_t ngr = (tlen + 15u) >> 4;
                 if (jb.kind == JOB_SCATTER) {
                     const int owner = (o + 1 + (int)k) % n;
-                    const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, owner, o, s), P.bulk_cap);
-                    const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, o, o, s), P.bulk_cap);
+                    const __amdgpu_buffer_rsrc_t rs = bulk_rsrc_at(P, o, o, s, off0, 16u * ngr);
                     if (!jb.gen) {
                         // a device program's origination: its bytes are first written into the origin's own
                         // heap slot (the copy an application would have staged, rlo_host_bulk_stage), then
-                        // read back from there like the host's -- the scatter always moves the origin's copy
+                        // read back from there like the host's -- the scatter always moves the origin's copy.
+                        // (Each thread reads back only granules it wrote: same-thread order, no drain.)
                         for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
 #pragma unroll
                             for (int uu = 0; uu < kMoveDepth; uu++) {
                                 const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                                if (g < ngr) st_ring(rs, off0 + 16u * g, storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g), sys);
+                                st_ring(rs, 16u * g, storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g), sys);
                             }
                         }
-                        VM_DRAIN();  // this thread's own stores, before it loads the same bytes back (sc1)
                     }
-                    for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
-                        u32x4 v[kMoveDepth];
-#pragma unroll
-                        for (int uu = 0; uu < kMoveDepth; uu++) {
-                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                            if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
+                    if (pl.direct) {
+                        // one GPU: the tile straight into every receiver's copy, then every receiver's tflag
+                        auto recv = [&](int jj) { return bulk_rsrc_at(P, (o + 1 + jj) % n, o, s, off0, 16u * ngr); };
+                        if (sys) tile_copy<true, W>(rs, ngr, tid, n - 1, recv);
+                        else tile_copy<false, W>(rs, ngr, tid, n - 1, recv);
+                        VM_DRAIN();
+                        __syncthreads();
+                        if (tid < 64) {
+                            if (sys) bulk_release(true);
+                            for (int d = 1 + tid; d < n; d += 64) bflag_add(bulk_flags(P, (o + d) % n, o, s) + kBulkTflag, 1u, sys);
                         }
-#pragma unroll
-                        for (int uu = 0; uu < kMoveDepth; uu++) {
-                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                            if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
-                        }
+                        continue;
                     }
+                    const __amdgpu_buffer_rsrc_t rd = bulk_rsrc_at(P, owner, o, s, off0, 16u * ngr);
+                    auto one = [&](int) { return rd; };
+                    if (sys) tile_copy<true, W>(rs, ngr, tid, 1, one);
+                    else tile_copy<false, W>(rs, ngr, tid, 1, one);
                     VM_DRAIN();
                     __syncthreads();
                     if (tid == 0) {
-                        bulk_release(sys);
+                        // one GPU: the drain of every storing wave + barrier + one agent-scope add is the
+                        // proven hand-off for sc1 stores (MI355X_MICROARCH.md "Valid forms" row 1), no L2
+                        // write-back; across GPUs the system-scope release stays
+                        if (sys) bulk_release(true);
                         uint32_t* f = bulk_flags(P, owner, o, s);
                         bflag_add(f + c, 1u, sys);
                         bflag_add(f + kBulkTflag, 1u, sys);
@@ -874,29 +957,19 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                         atomicAdd((unsigned long long*)&P.jctl[kJctlGatherPassed], 1ull);  // diagnostics: gather waits passed
                     }
                     __syncthreads();
-                    const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
-                    for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
-                        u32x4 v[kMoveDepth];
-    #pragma unroll
-                        for (int uu = 0; uu < kMoveDepth; uu++) {
-                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                            if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
-                        }
-                        for (int d = 1; d < n; d++) {  // every other non-originator (uniform)
-                            const int dst = (o + d) % n;
-                            if (dst == me) continue;
-                            const __amdgpu_buffer_rsrc_t rd = mk_rsrc(bulk_heap(P, dst, o, s), P.bulk_cap);
-    #pragma unroll
-                            for (int uu = 0; uu < kMoveDepth; uu++) {
-                                const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                                if (g < ngr) st_ring(rd, off0 + 16u * g, v[uu], sys);
-                            }
-                        }
-                    }
+                    const __amdgpu_buffer_rsrc_t rs = bulk_rsrc_at(P, me, o, s, off0, 16u * ngr);
+                    // every other non-originator: (o + d) mod n for d = 1 .. n - 1 but my own d
+                    const int dme = (me - o + n) % n;
+                    auto other = [&](int jj) {
+                        const int d = jj + 1 + (jj + 1 >= dme ? 1 : 0);
+                        return bulk_rsrc_at(P, (o + d) % n, o, s, off0, 16u * ngr);
+                    };
+                    if (sys) tile_copy<true, W>(rs, ngr, tid, n - 2, other);
+                    else tile_copy<false, W>(rs, ngr, tid, n - 2, other);
                     VM_DRAIN();
                     __syncthreads();
                     if (tid < 64) {
-                        bulk_release(sys);
+                        if (sys) bulk_release(true);  // (one GPU: drain + barrier + agent add, as the scatter)
                         // every other receiver got this tile; and so did my own count: my copy may not be
                         // released (the origin may not reuse it) before my pushes out of it are done
                         for (int d = 1 + tid; d < n; d += 64) {
@@ -914,25 +987,40 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                 const uint32_t off0 = ti * kVerifyTile;
                 const uint32_t tlen = min(kVerifyTile, len - off0);
                 const uint32_t ngr = (tlen + 15u) >> 4;
-                const __amdgpu_buffer_rsrc_t rs = mk_rsrc(bulk_heap(P, me, o, s), P.bulk_cap);
+                // cut to the tile: the loads carry no branch (past the end they read zeros), only the sum does
+                const __amdgpu_buffer_rsrc_t rs = bulk_rsrc_at(P, me, o, s, off0, 16u * ngr);
                 unsigned long long acc = 0;
-                for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
-                    u32x4 v[kMoveDepth];
-    #pragma unroll
-                    for (int uu = 0; uu < kMoveDepth; uu++) {
-                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                        if (g < ngr) v[uu] = sys ? ld_sys(rs, off0 + 16u * g) : ld_sc1(rs, off0 + 16u * g);
-                    }
-    #pragma unroll
-                    for (int uu = 0; uu < kMoveDepth; uu++) {
-                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
-                        if (g < ngr) {
-                            const uint32_t off = off0 + 16u * g;
-                            const int b0 = (int)len - (int)off;  // the reference's zero-padded tail
-                            const u32x4 w = {mask_bytes(v[uu].x, b0), mask_bytes(v[uu].y, b0 - 4), mask_bytes(v[uu].z, b0 - 8),
-                                             mask_bytes(v[uu].w, b0 - 12)};
-                            acc += chunk_mix(off >> 4, w);
+                {
+                    // two batches in flight: the next one's loads are issued before this one is summed
+                    constexpr uint32_t step = (uint32_t)kMoveDepth * kT;
+                    u32x4 va[kMoveDepth], vb[kMoveDepth];
+                    auto load = [&](u32x4 (&v)[kMoveDepth], uint32_t g0) {
+#pragma unroll
+                        for (int uu = 0; uu < kMoveDepth; uu++) {
+                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                            v[uu] = sys ? ld_sys(rs, 16u * g) : ld_sc1(rs, 16u * g);
                         }
+                    };
+                    auto sum = [&](const u32x4 (&v)[kMoveDepth], uint32_t g0) {
+#pragma unroll
+                        for (int uu = 0; uu < kMoveDepth; uu++) {
+                            const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                            if (g < ngr) {
+                                const uint32_t off = off0 + 16u * g;
+                                const int b0 = (int)len - (int)off;  // the reference's zero-padded tail
+                                const u32x4 w = {mask_bytes(v[uu].x, b0), mask_bytes(v[uu].y, b0 - 4),
+                                                 mask_bytes(v[uu].z, b0 - 8), mask_bytes(v[uu].w, b0 - 12)};
+                                acc += chunk_mix(off >> 4, w);
+                            }
+                        }
+                    };
+                    load(va, 0u);
+                    for (uint32_t g0 = 0; g0 < ngr; g0 += 2u * step) {
+                        load(vb, g0 + step);
+                        sum(va, g0);
+                        if (g0 + step >= ngr) break;
+                        load(va, g0 + 2u * step);
+                        sum(vb, g0 + step);
                     }
                 }
                 // workgroup sum of this tile -> the sub-job's sum (LDS; added to the job's once, below)

@@ -1628,7 +1628,7 @@ int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out) {
     out->chunk = p.chunk;
     out->tile = p.tile;
     out->total_tiles = rlo::bulk_total_tiles(p, (uint32_t)len);
-    out->pad = 0;
+    out->direct = p.direct;
     return RLO_OK;
 }
 

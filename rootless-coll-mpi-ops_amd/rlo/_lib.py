@@ -98,7 +98,7 @@ class RankStats(ctypes.Structure):
 
 class BulkPlan(ctypes.Structure):
     _fields_ = [("nchunks", ctypes.c_uint32), ("stripe", ctypes.c_uint32), ("chunk", ctypes.c_uint32),
-                ("tile", ctypes.c_uint32), ("total_tiles", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("tile", ctypes.c_uint32), ("total_tiles", ctypes.c_uint32), ("direct", ctypes.c_uint32)]
 
 
 class LogRec(ctypes.Structure):

@@ -231,7 +231,7 @@ def bulk_plan(n, nbytes, cross=False):
     out = L.BulkPlan()
     check(L.load().rlo_bulk_plan(n, nbytes, 1 if cross else 0, ctypes.byref(out)), "rlo_bulk_plan")
     return {"nchunks": out.nchunks, "stripe": out.stripe, "chunk": out.chunk, "tile": out.tile,
-            "total_tiles": out.total_tiles}
+            "total_tiles": out.total_tiles, "direct": out.direct}
 
 
 def storm_lengths(seed, k, length, len_max=0):

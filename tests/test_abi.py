@@ -99,12 +99,12 @@ def test_children_cover_exact_spanning_tree():
 
 
 def test_bulk_plan_geometry():
-    """rlo_bulk_plan (the plan every rank derives for a bulk message, rlo_device.hpp bulk_plan):
-    stripes are whole KiB, a chunk is N-1 stripes, <= 16 chunks cover the message: on one GPU one chunk
-    below 8 MiB and ~4-MiB chunks from there, ~sqrt(len / 4 MiB) across GPUs; tiles <= 16 KiB below
-    8 MiB, <= 64 KiB from there.  The scatter tiles (every stripe of every
-    chunk, cut into tiles) cover every byte exactly once, and total_tiles -- each receiver's completion
-    count -- equals the tiles of its own stripe (scatter) plus the other stripes (gather)."""
+    """rlo_bulk_plan (the plan every rank derives for a bulk message, rlo_device.hpp bulk_plan).
+    Across GPUs: stripes are whole KiB, a chunk is N-1 stripes, ~sqrt(len / 4 MiB) <= 16 chunks cover
+    the message.  One GPU: a DIRECT plan -- one chunk, one stripe holding the whole message (KiB-rounded),
+    every tile fanned out from the origin's copy to every receiver.  Tiles <= 16 KiB below 8 MiB, <= 64 KiB
+    from there.  The scatter tiles (every stripe of every chunk, cut into tiles) cover every byte exactly
+    once, and total_tiles -- each receiver's completion count -- equals the tiles of every stripe."""
     import math
 
     import rlo
@@ -115,19 +115,19 @@ def test_bulk_plan_geometry():
             for cross in (False, True):
                 p = rlo.bulk_plan(n, nbytes, cross)
                 st, ch, tile = p["stripe"], p["chunk"], p["tile"]
-                assert st % 1024 == 0 and st >= 1024 and ch == st * (n - 1), (n, nbytes, p)
+                assert p["direct"] == (0 if cross else 1), (n, nbytes, p)
+                if not cross:
+                    assert st == ch == -(-nbytes // 1024) * 1024 and p["nchunks"] == 1, (n, nbytes, p)
+                else:
+                    assert st % 1024 == 0 and st >= 1024 and ch == st * (n - 1), (n, nbytes, p)
                 tmax = (64 << 10) if nbytes >= 8 * MiB else (16 << 10)
                 assert tile % 1024 == 0 and 1024 <= tile <= min(st, tmax), (n, nbytes, p)
                 assert p["nchunks"] == -(-nbytes // ch) <= 16, (n, nbytes, p)
-                if not cross and nbytes < 8 * MiB:
-                    assert p["nchunks"] == 1, (n, nbytes, p)
-                if not cross and nbytes >= 8 * MiB:  # ~4-MiB chunks (stripes rounded up to KiB), at most 16
-                    assert p["nchunks"] == min(16, nbytes // (4 * MiB)) or st * (n - 1) * 16 < nbytes * 2, (n, nbytes, p)
                 covered = 0
                 per_stripe = [0] * (n - 1)
                 for c in range(p["nchunks"]):
                     clen = min(ch, nbytes - c * ch)
-                    for k in range(n - 1):
+                    for k in range(n - 1 if cross else 1):
                         slen = max(0, min(st, clen - k * st))
                         t = -(-slen // tile)
                         per_stripe[k] += t
@@ -140,7 +140,7 @@ def test_bulk_plan_geometry():
                 if cross and nbytes >= 16 * MiB:
                     assert p["nchunks"] >= max(1, math.isqrt(nbytes // (4 * MiB))) - 1
     assert rlo.bulk_plan(8, 64 * MiB, True)["nchunks"] == 4
-    assert rlo.bulk_plan(8, 64 * MiB, False)["nchunks"] == 16 and rlo.bulk_plan(8, MiB, False)["nchunks"] == 1
+    assert rlo.bulk_plan(8, 64 * MiB, False)["total_tiles"] == 1024 and rlo.bulk_plan(8, MiB, False)["total_tiles"] == 64
     for bad in ((1, MiB), (8, 0)):
         with pytest.raises(rlo.RloError):
             rlo.bulk_plan(*bad)

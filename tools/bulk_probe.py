@@ -23,5 +23,5 @@ for mv in movers:
             d = np.diff(obs[obs > 0])
             rt = float(np.median(d)) * 1e-8 if len(d) else float("nan")
             print("movers %3d (%3d) %2d MiB: round %8.1f us  kernel %7.3f ms  hbm %7.1f GB/s (frac %.3f)" %
-                  (mv, w.info["movers"], mib, rt * 1e6, w.kernel_ms(), (2 * G + 1) * nb / rt / 1e9,
-                   (2 * G + 1) * nb / rt / 8e12), flush=True)
+                  (mv, w.info["movers"], mib, rt * 1e6, w.kernel_ms(), 2 * G * nb / rt / 1e9,
+                   2 * G * nb / rt / 8e12), flush=True)

@@ -16,7 +16,11 @@ constexpr int kT = 256;
 constexpr uint32_t kTile = 64u << 10;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs_of(void* p) {
-    return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7fffffff, 0x00020000);
+    // the pointer made wave-uniform: a VGPR resource would wrap every access in a waterfall loop
+    const uint64_t v = (uint64_t)p;
+    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, 0x7fffffff, 0x00020000);
 }
 __device__ __forceinline__ u32x4 ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
