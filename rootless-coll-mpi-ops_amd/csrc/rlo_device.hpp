@@ -335,6 +335,11 @@ constexpr uint32_t kVerifyTile = 64u << 10;
 // (one fetch-add, never retried) and moves all of a sub-job's tiles itself.  Enough sub-jobs that every
 // mover of a class has one while a single message's scatter or verify runs
 constexpr uint32_t kMaxSub = 256;
+// ... except a SCATTER job: one tile per sub-job up to 1024 (a direct 64-MiB message's 1024 tiles): with
+// 4-tile sub-jobs, 256 of them over 248 movers left 8 movers a second sub-job each -- the round took two
+// sub-job times; with single tiles the tail is one tile
+constexpr uint32_t kMaxSubScatter = 1024;
+__host__ __device__ inline uint32_t max_sub(uint32_t kind) { return kind == 1u /* JOB_SCATTER */ ? kMaxSubScatter : kMaxSub; }
 // granules in flight per mover thread (16 B each): 256 threads x 8 x 16 B = 32 KiB per round trip
 constexpr int kMoveDepth = 8;
 struct BulkPlan {

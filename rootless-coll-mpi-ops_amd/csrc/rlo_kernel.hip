@@ -82,7 +82,17 @@ struct CandL {          // one message of this iteration, kept for the copy phas
 };
 
 // bulk-message state (the BULK instantiation only)
+// a job post decided by one lane (phase C / F), queued in LDS and written out by all of wave 0 at a
+// converged point (flush_posts): one lane writing a 4-MiB message's 256 sub-job records alone took
+// ~60 us -- longer than moving the bytes
+struct PostReq {
+    uint32_t cls, kind, origin, lr, slot, bid, len, ntiles, from, logidx, q, gen;
+    uint64_t j0;
+};
+constexpr uint32_t kPostQ = 16;
 struct BulkSh {
+    PostReq pq[kPostQ];         // progress: queued job posts
+    uint32_t npost;
     BulkJob mv_job;             // mover: the job of the claimed tile
     uint32_t mv_ti, mv_stop;
     unsigned long long mv_sum;
@@ -633,6 +643,20 @@ __device__ __forceinline__ void bflag_add(uint32_t* p, uint32_t v, bool sys) {
     if (sys) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a receiver's completion count (tiles landed in its copy).  Direct plans (one GPU) keep it in 16 shards
+// -- the line's words 0..15, which only the scatter -> gather hand-off of chunked plans uses -- each mover
+// adding to shard (mover & 15): hundreds of movers adding to ONE word of uncached memory serialise on it
+// (a 4-MiB message's 256 tiles x 7 receivers); chunked plans count in word kBulkTflag
+__device__ __forceinline__ uint32_t bulk_tcount(const Params& P, uint32_t* f, bool sys) {
+    if (P.bulk_cross) return bflag_ld(f + kBulkTflag, sys);
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = bflag_ld(f + i, sys);
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) t += v[i];
+    return t;
+}
 // release / acquire around the bulk flags (the proven form of the first bulk kernel: a fence on
 // both sides, MI355X_MICROARCH.md "Valid forms" first bullet; explicit vmcnt after the release,
 // "Compiler hazard")
@@ -653,7 +677,7 @@ __device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o,
     atomicAdd((unsigned long long*)&P.jctl[kJctlReleases], 1ull);  // diagnostics: releases
     uint32_t* f = bulk_flags(P, r, o, s);
     if (want) {  // the reception must be complete here: a release mid-reception would lose it
-        const uint32_t tf = bflag_ld(f + kBulkTflag, sys);
+        const uint32_t tf = bulk_tcount(P, f, sys);
         if (tf < want && atomicCAS((unsigned long long*)&P.jctl[kJctlFault], 0ull,
                                    (0xEEull << 56) | ((uint64_t)(r & 0xff) << 48) | ((uint64_t)(o & 0xff) << 40) |
                                        ((uint64_t)(s & 0xf) << 36) | ((uint64_t)(bid & 0xfff) << 24) | ((tf & 0xfffu) << 12) |
@@ -681,7 +705,7 @@ __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t
         bulk_fault(P, 6, (kind << 20) | (len & 0xfffffu));
         return;
     }
-    const uint32_t per = (ntiles + kMaxSub - 1u) / kMaxSub, nsub = (ntiles + per - 1u) / per;
+    const uint32_t per = (ntiles + max_sub(kind) - 1u) / max_sub(kind), nsub = (ntiles + per - 1u) / per;
     const uint64_t j0 = atomicAdd((unsigned long long*)&P.jctl[cls * 16 + kJctlPost], (unsigned long long)nsub);
     atomicAdd((unsigned long long*)&P.jctl[kJctlPostsByKind + kind], 1ull);  // diagnostics: posts by kind (41..43)
     const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
@@ -727,6 +751,89 @@ __device__ __forceinline__ void post_job(const Params& P, uint32_t cls, uint32_t
         __hip_atomic_store(dst, (uint64_t)(uint32_t)(j0 + u + 1u) | ((uint64_t)kind << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// queue a post (any lane, divergent); a full queue posts it from this lane alone
+__device__ __forceinline__ void queue_job(BulkSh& B, const Params& P, uint32_t cls, uint32_t kind, int origin, int lr,
+                                          uint32_t slot_s, uint32_t bid, uint32_t len, uint32_t ntiles, int from,
+                                          uint32_t logidx, uint32_t q, uint32_t gen) {
+    const uint32_t i = atomicAdd(&B.npost, 1u);
+    if (i >= kPostQ) {
+        post_job(P, cls, kind, origin, lr, slot_s, bid, len, ntiles, from, logidx, q, gen);
+        return;
+    }
+    PostReq& r = B.pq[i];
+    r.cls = cls; r.kind = kind; r.origin = (uint32_t)origin; r.lr = (uint32_t)lr; r.slot = slot_s; r.bid = bid;
+    r.len = len; r.ntiles = ntiles; r.from = (uint32_t)from; r.logidx = logidx; r.q = q; r.gen = gen;
+}
+__device__ __forceinline__ void queue_job(NoBulkSh&, const Params&, uint32_t, uint32_t, int, int, uint32_t, uint32_t,
+                                          uint32_t, uint32_t, int, uint32_t, uint32_t, uint32_t) {}  // (no bulk messages)
+// write out the queued posts (wave 0, all lanes): post_job's protocol with sub-job u on lane u mod 64 --
+// the slots' generation checks, the record bodies, one drain, then the sequence words
+__device__ __forceinline__ void flush_posts(BulkSh& B, const Params& P, int lane) {
+    const uint32_t np = min((uint32_t)uni((int)B.npost), kPostQ);
+    if (!np) return;
+    const uint32_t jm = P.jslots - 1u, lg = (uint32_t)__builtin_ctz(P.jslots);
+    const uint64_t t0 = now_ticks();
+    for (uint32_t i = 0; i < np; i++) {
+        const PostReq& r = B.pq[i];
+        const uint32_t cls = (uint32_t)uni((int)r.cls), kind = (uint32_t)uni((int)r.kind), lr = (uint32_t)uni((int)r.lr);
+        const uint32_t origin = (uint32_t)uni((int)r.origin), slot_s = (uint32_t)uni((int)r.slot), len = (uint32_t)uni((int)r.len);
+        const uint32_t ntiles = (uint32_t)uni((int)r.ntiles);
+        if (!(kind >= JOB_SCATTER && kind <= JOB_VERIFY && cls <= JCLS_B && origin < (uint32_t)P.n && lr < P.n_local &&
+              slot_s < P.bulk_slots && len > 0 && len <= P.bulk_cap && ntiles > 0)) {
+            if (lane == 0) {
+                bulk_fault(P, 6, (kind << 20) | (len & 0xfffffu));
+                B.pq[i].ntiles = 0u;  // skipped below
+            }
+            continue;
+        }
+        const uint32_t per = (ntiles + max_sub(kind) - 1u) / max_sub(kind), nsub = (ntiles + per - 1u) / per;
+        uint64_t j0 = 0;
+        if (lane == 0) {
+            j0 = atomicAdd((unsigned long long*)&P.jctl[cls * 16 + kJctlPost], (unsigned long long)nsub);
+            atomicAdd((unsigned long long*)&P.jctl[kJctlPostsByKind + kind], 1ull);  // diagnostics: posts by kind
+            B.pq[i].j0 = j0;
+        }
+        j0 = rdl64(j0, 0);
+        uint64_t* const jf = P.jfree + (size_t)cls * P.jslots;
+        const uint32_t parent = (uint32_t)(j0 & jm);
+        for (uint32_t u = (uint32_t)lane; u < nsub; u += 64u) {
+            const uint64_t j = j0 + u;
+            bool ok = true;
+            while (__hip_atomic_load(&jf[(uint32_t)(j & jm)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (j >> lg)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (now_ticks() - t0 > P.timeout_ticks) {  // cannot happen unless a mover died: stop loudly
+                    atomicCAS(P.error_flag, 0u, (uint32_t)ERR_TIMEOUT);
+                    ok = false;
+                    break;
+                }
+            }
+            if (!ok) break;
+            u32x4* dst = reinterpret_cast<u32x4*>(P.jobs + (size_t)cls * P.jslots + (uint32_t)(j & jm));
+            const uint32_t a = u * per, nt = min(per, ntiles - a);
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + 1, (uint64_t)origin | ((uint64_t)lr << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            st_sys16(dst + 1, u32x4{slot_s, (uint32_t)uni((int)r.bid), len, nt});
+            st_sys16(dst + 2, u32x4{a, parent, (uint32_t)uni((int)r.from), (uint32_t)uni((int)r.logidx)});
+            st_sys16(dst + 3, u32x4{(uint32_t)uni((int)r.q), (uint32_t)uni((int)r.gen), ntiles, (uint32_t)j0});
+        }
+    }
+    VM_DRAIN();
+    for (uint32_t i = 0; i < np; i++) {
+        const PostReq& r = B.pq[i];
+        const uint32_t ntiles = (uint32_t)uni((int)r.ntiles);
+        if (!ntiles) continue;
+        const uint32_t cls = (uint32_t)uni((int)r.cls), kind = (uint32_t)uni((int)r.kind);
+        const uint32_t per = (ntiles + max_sub(kind) - 1u) / max_sub(kind), nsub = (ntiles + per - 1u) / per;
+        const uint64_t j0 = uni64(r.j0);
+        for (uint32_t u = (uint32_t)lane; u < nsub; u += 64u) {
+            uint64_t* dst = reinterpret_cast<uint64_t*>(P.jobs + (size_t)cls * P.jslots + (uint32_t)((j0 + u) & jm));
+            __hip_atomic_store(dst, (uint64_t)(uint32_t)(j0 + u + 1u) | ((uint64_t)kind << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (lane == 0) B.npost = 0u;
 }
 
 // One tile of the movers' copy: granules [0, ngr) of src into ndst destinations (dst(j): the j-th one's
@@ -863,6 +970,32 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
         const int o = jb.origin;
         const int me = P.rank_begin + jb.lr;
         const BulkPlan pl = bulk_plan(n, len, P.bulk_cross != 0);
+        if (jb.kind == JOB_SCATTER && pl.direct) {
+            // one GPU (direct plan): the sub-job's tiles are one contiguous range of the message -- moved as
+            // one (a fan-out from the origin's copy into every receiver's), then ONE add of its tile count to
+            // this mover's shard of every receiver's completion count
+            const uint32_t off0 = jb.ti0 * pl.tile;
+            const uint32_t ngr = (min(jb.ntiles * pl.tile, len - off0) + 15u) >> 4;
+            const __amdgpu_buffer_rsrc_t rs = bulk_rsrc_at(P, o, o, s, off0, 16u * ngr);
+            if (!jb.gen) {  // a device program's origination: its bytes into the origin's copy first (see below)
+                for (uint32_t g0 = 0; g0 < ngr; g0 += (uint32_t)kMoveDepth * kT) {
+#pragma unroll
+                    for (int uu = 0; uu < kMoveDepth; uu++) {
+                        const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+                        st_ring(rs, 16u * g, storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g), sys);
+                    }
+                }
+            }
+            auto recv = [&](int jj) { return bulk_rsrc_at(P, (o + 1 + jj) % n, o, s, off0, 16u * ngr); };
+            if (sys) tile_copy<true, W>(rs, ngr, tid, n - 1, recv);
+            else tile_copy<false, W>(rs, ngr, tid, n - 1, recv);
+            VM_DRAIN();
+            __syncthreads();
+            if (tid < 64) {
+                if (sys) bulk_release(true);
+                for (int d = 1 + tid; d < n; d += 64) bflag_add(bulk_flags(P, (o + d) % n, o, s) + (mi & 15u), jb.ntiles, sys);
+            }
+        } else
         for (uint32_t ti = jb.ti0; ti < jb.ti0 + jb.ntiles; ti++) {
             if (jb.kind == JOB_SCATTER || jb.kind == JOB_GATHER) {
                 // tile -> (chunk c, stripe k, tile i of that stripe-chunk)
@@ -906,19 +1039,6 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                                 st_ring(rs, 16u * g, storm_granule((uint32_t)o, jb.bid, len, off0 + 16u * g), sys);
                             }
                         }
-                    }
-                    if (pl.direct) {
-                        // one GPU: the tile straight into every receiver's copy, then every receiver's tflag
-                        auto recv = [&](int jj) { return bulk_rsrc_at(P, (o + 1 + jj) % n, o, s, off0, 16u * ngr); };
-                        if (sys) tile_copy<true, W>(rs, ngr, tid, n - 1, recv);
-                        else tile_copy<false, W>(rs, ngr, tid, n - 1, recv);
-                        VM_DRAIN();
-                        __syncthreads();
-                        if (tid < 64) {
-                            if (sys) bulk_release(true);
-                            for (int d = 1 + tid; d < n; d += 64) bflag_add(bulk_flags(P, (o + d) % n, o, s) + kBulkTflag, 1u, sys);
-                        }
-                        continue;
                     }
                     const __amdgpu_buffer_rsrc_t rd = bulk_rsrc_at(P, owner, o, s, off0, 16u * ngr);
                     auto one = [&](int) { return rd; };
@@ -1173,7 +1293,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.hp[0] = 0; S.hp[1] = 0; S.a_done = 0; S.cseq = 0;
             S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
             if constexpr (BULK) {
-                S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0;
+                S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0; S.b.npost = 0;
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
                 for (int i = 0; i < kMaxPend / 32; i++) S.b.bonw[i] = 0;
             }
@@ -1280,7 +1400,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t fpseq = fw2 >> 24;
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
-                  (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL) &&
+                  (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL || (BULK && ftag == TAG_BULK)) &&
                   !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
         int fjudge = 1;
         uint32_t fkids = 0, fneed = 0;
@@ -1376,6 +1496,25 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
             }
             flog = rdl32(flog, 0);
+        } else if (BULK && ftag == TAG_BULK) {
+            // a bulk announcement (phase F's registration, restated): pending until my copy is complete;
+            // its payload is the descriptor {len, bulk sequence} (chunk 1).  On the fast path a hop of the
+            // announcement costs what a lone bcast's does, not a full iteration per tree level
+            if constexpr (BULK) {
+                const uint32_t dlen = rdl32(v.x, 1), dq = rdl32(v.y, 1);
+                const uint32_t sl = dq & (bsl - 1u);
+                const BulkPlan pl = bulk_plan(P.n, dlen, P.bulk_cross != 0);
+                const uint32_t e = (uint32_t)forg * bsl + sl;
+                const uint32_t nt = P.n > 2 ? bulk_stripe_tiles(pl, dlen, (uint32_t)((me - forg - 1 + P.n) % P.n)) : 0u;
+                if (lane == 0) {
+                    const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
+                    if ((ob >> (e & 31u)) & 1u) bulk_fault(P, 10, (e << 12) | (fid & 0xfffu));  // still live: announced twice
+                    bpend[e] = BulkPend{fid, dlen, bulk_total_tiles(pl, dlen) + nt, ffrom, ft0, dq,
+                                        0x5A000000u | ((uint32_t)forg << 8) | sl, 0u};
+                    S.b.bact[atomicAdd(&S.b.nbact, 1u)] = e;
+                    if (nt) queue_job(S.b, P, JCLS_B, JOB_GATHER, forg, lr, sl, fid, dlen, nt, ffrom, ~0u, dq, 0u);
+                }
+            }
         } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
             PendState* ps = &PEND(forg, fpseq);
             if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
@@ -1822,6 +1961,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                 }
                 if (!idle_prev || sp >= kIdleSpin) break;
+                if constexpr (BULK) {  // a reception the doorbell pass registered: its completion is polled per iteration
+                    if (uni((int)S.b.nbact) != 0) break;
+                }
                 bool bmoved = false;
                 if constexpr (BULK) {  // a released heap slot of mine (a bulk origination may wait for it)
                     if (lane < (int)bsl) {
@@ -1863,7 +2005,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (i < nb) {
                         const uint32_t e = S.b.bact[i];
                         if (e >= (uint32_t)P.n * bsl) bulk_fault(P, 7, e); else
-                        dn = bflag_ld(bulk_flags(P, me, (int)(e / bsl), e % bsl) + kBulkTflag, sys) >= bpend[e].ntiles;
+                        dn = bulk_tcount(P, bulk_flags(P, me, (int)(e / bsl), e % bsl), sys) >= bpend[e].ntiles;
                     }
                     const uint64_t m = __ballot(dn);
                     if (lane == 0) S.b.cmask[u] = m;
@@ -1988,7 +2130,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 atomicAdd(&S.bcast_delivered, 1ull);
                                 const uint32_t li =
                                     log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
-                                post_job(P, JCLS_A, JOB_VERIFY, o, lr, sl, pe.bid, pe.len,
+                                queue_job(S.b, P, JCLS_A, JOB_VERIFY, o, lr, sl, pe.bid, pe.len,
                                          (pe.len + kVerifyTile - 1u) / kVerifyTile, pe.from, li, pe.q, 0u);
                                 if (P.mode & MODE_LAT) {  // the last of N-1 pickups completes the round
                                     const uint32_t old =
@@ -2294,7 +2436,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
         BAR();  // selection visible
         PST(7, 3);
-        if (S.exit_now) break;  // the final counters are published
+        if (S.exit_now) {  // the final counters are published
+            if constexpr (BULK) {
+                if (w == 0) flush_posts(S.b, P, lane);  // (phase C's last posts, e.g. a VERIFY)
+            }
+            break;
+        }
         const uint32_t R = S.R, C = S.C;
         const uint32_t nstorm = S.nstorm, storm_base = S.storm_base, loc_kind = S.loc_kind;
 
@@ -2750,7 +2897,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
                         if ((ob >> (e & 31u)) & 1u) {  // still live: which message was, which one came
                             const BulkPend od = bpend[e];
-                            const uint32_t tf = bflag_ld(bulk_flags(P, me, origin, sl) + kBulkTflag, sys);
+                            const uint32_t tf = bulk_tcount(P, bulk_flags(P, me, origin, sl), sys);
                             if (atomicCAS((unsigned long long*)&P.jctl[kJctlFault], 0ull,
                                           ((uint64_t)me << 56) | ((uint64_t)(e & 0xffu) << 48) | ((uint64_t)(od.bid & 0xffffu) << 32) |
                                               ((uint64_t)(id & 0xffffu) << 16) | ((tf & 0xffu) << 8) | (od.ntiles & 0xffu)) == 0ull)
@@ -2760,7 +2907,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                                       0x5A000000u | ((uint32_t)origin << 8) | sl, 0u};
                         bpend[e] = np_;
                         S.b.bact[atomicAdd(&S.b.nbact, 1u)] = e;
-                        if (nt) post_job(P, JCLS_B, JOB_GATHER, origin, lr, sl, id, dsc.x, nt, from, ~0u, dsc.y, 0u);
+                        if (nt) queue_job(S.b, P, JCLS_B, JOB_GATHER, origin, lr, sl, id, dsc.x, nt, from, ~0u, dsc.y, 0u);
                       }
                     }
                 } else if (kind == K_PROP || (kind == K_HOST && tag == TAG_PROPOSAL)) {
@@ -2793,7 +2940,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         blen = dsc.x;
                         bq = dsc.y;
                     }
-                    post_job(P, JCLS_A, JOB_SCATTER, me, lr, bq & (bsl - 1u), id, blen,
+                    queue_job(S.b, P, JCLS_A, JOB_SCATTER, me, lr, bq & (bsl - 1u), id, blen,
                              bulk_total_tiles(bulk_plan(P.n, blen, P.bulk_cross != 0), blen), -1, ~0u, bq,
                              kind == K_HOST ? 1u : 0u);
                 }
@@ -2847,6 +2994,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             BAR();  // olist / cand / n_oi / big complete
             PST(4, 7);
+            if constexpr (BULK) {
+                if (w == 0) flush_posts(S.b, P, lane);  // this iteration's job posts, before its copies
+            }
 
             // ---------------- G1: stage the first round of large-message groups (before any store)
             // (the 8-wave doorbell instantiation runs programs whose every message takes the small path:
@@ -2922,8 +3072,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             // a reference that is not one (unwritten / torn chunk): stop loudly, load nothing
                             const bool rok = uni((int)ref.y) == (int)~roff && (uint32_t)uni((int)ref.z) == kRefMagic;
                             if (!rok && lane == 0) set_error(S, P, ERR_BAD_SLOT, 0x5EF0000u | (pq & 0xffffu));
+                            // (the extent made uniform too: read from LDS it is a VGPR, and a VGPR resource
+                            // wraps every LDS-DMA load of the pulled payloads in a readfirstlane waterfall loop)
                             const __amdgpu_buffer_rsrc_t rr =
-                                mk_rsrc(reinterpret_cast<void*>(uni64(t.in_base[cl.group >> 1]) + roff), rok ? (pch + 1u) * 16u : 0u);
+                                mk_rsrc(reinterpret_cast<void*>(uni64(t.in_base[cl.group >> 1]) + roff),
+                                        (uint32_t)uni((int)(rok ? (pch + 1u) * 16u : 0u)));
                             if (rok && pq < pch) {
                                 if (sys) __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * (pq + 1u), 0, 0, kAuxSc1 | 1);
                                 else __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, lds_ptr(dst), 16, 16u * (pq + 1u), 0, 0, kAuxSc1);
@@ -3135,6 +3288,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
         // ---------------- consume (wave 0): in-ring prefixes, producer counts, bookkeeping
         if (w == 0) {
+            if constexpr (BULK) flush_posts(S.b, P, lane);  // posts of an iteration without phase F (phase C's)
             if (lane < n_in2) {
                 const uint32_t bse = rbase_r, tk = rtake_r, fb = S.first_bad[lane];
                 if (fb < bse + tk) n_stalls++;  // lane 0's copy is flushed (sum over lanes at exit)
@@ -3269,7 +3423,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.dbg[0] = ((uint64_t)S.b.bulk_q << 32) | nb;
             for (uint32_t i = 0; i < 3 && i < nb; i++) {
                 const uint32_t e = S.b.bact[i];
-                const uint32_t tf = bflag_ld(bulk_flags(P, me, (int)(e / bsl), e % bsl) + kBulkTflag, sys);
+                const uint32_t tf = bulk_tcount(P, bulk_flags(P, me, (int)(e / bsl), e % bsl), sys);
                 const uint32_t sf = bflag_ld(bulk_flags(P, me, (int)(e / bsl), e % bsl), sys);
                 S.dbg[1 + 2 * i] = ((uint64_t)e << 32) | bpend[e].ntiles;
                 S.dbg[2 + 2 * i] = ((uint64_t)sf << 32) | tf;

@@ -664,7 +664,7 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
             const uint64_t tv = (bm + rlo::kVerifyTile - 1) / rlo::kVerifyTile;
             const uint64_t K = rlo::kMaxSub;
             const uint64_t nl = (uint64_t)w->nl, B = w->L.bslots, N = (uint64_t)w->L.n;
-            const uint64_t need = nl * B * std::min(K, ts) + nl * N * B * (std::min(K, tg) + std::min(K, tv)) + 64;
+            const uint64_t need = nl * B * std::min<uint64_t>(rlo::kMaxSubScatter, ts) + nl * N * B * (std::min(K, tg) + std::min(K, tv)) + 64;
             if (need > (1ull << 26)) { delete w; return RLO_E_INVAL; }
             w->jslots = pow2_ceil((uint32_t)need);
         }
