@@ -104,6 +104,8 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
  * Every part must rlo_reset before ANY part launches (host barrier in between). */
 #define RLO_PART_BLOB_BYTES 512u
 #define RLO_PART_UNCACHED 1u /* allocate the part's rings uncached (for peer GPUs writing over xGMI) */
+#define RLO_PART_CHUNKED 2u  /* bulk messages take the multi-GPU plan (chunked scatter + all-gather) even when every
+                                 * part is on one GPU: the 8-GPU path, rehearsed on one (every part must set it alike) */
 typedef struct {
     int32_t n_ranks;           /* world size                                               */
     int32_t n_parts, part;     /* number of parts, this part                                */

@@ -944,7 +944,7 @@ static void base_params(rlo_world* w) {
         P.bulk_slots = w->L.bslots;
         P.bulk_cap = w->L.bcap;
         P.nmov = w->nmov;
-        P.bulk_cross = (uint32_t)w->sys_scope;
+        P.bulk_cross = (w->sys_scope || (w->flags & RLO_PART_CHUNKED)) ? 1u : 0u;  // the chunked plan (rlo_device.hpp)
         P.bheap = w->d_bheap.p;
         P.bflag = w->d_bflag.p;
         P.part_of = w->d_part_of.p;

@@ -25,6 +25,7 @@ RLO_E_NOTCONNECTED = -7
 RLO_E_AGAIN = -8
 RLO_PART_BLOB_BYTES = 512
 RLO_PART_UNCACHED = 1
+RLO_PART_CHUNKED = 2
 RLO_LAUNCH_NO_RESET = 1
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3

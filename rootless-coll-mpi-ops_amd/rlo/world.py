@@ -49,9 +49,10 @@ class World:
 
     @classmethod
     def part(cls, n, n_parts, part, part_begin=None, max_payload=4096, ring_slots=0, device=-1, uncached=False,
-             bulk_max=0, bulk_slots=0, movers=0, proposal_pool=0):
+             bulk_max=0, bulk_slots=0, movers=0, proposal_pool=0, chunked=False):
         return cls(n, max_payload, ring_slots, device,
-                   _part=(n_parts, part, part_begin, L.RLO_PART_UNCACHED if uncached else 0), bulk_max=bulk_max,
+                   _part=(n_parts, part, part_begin, (L.RLO_PART_UNCACHED if uncached else 0) |
+                          (L.RLO_PART_CHUNKED if chunked else 0)), bulk_max=bulk_max,
                    bulk_slots=bulk_slots, movers=movers, proposal_pool=proposal_pool)
 
     def _query(self):

@@ -1,7 +1,8 @@
 """GPU parity of bulk messages -- bcasts longer than a ring slot (BASELINE configs[2]
 and [4]): rootless like every bcast (the origin alone decides to send; receivers learn of it from the
-announcement that travels the skip-ring tree), the bytes moved by the mover workgroups as a
-pipelined scatter + all-gather between the ranks' heaps.
+announcement that travels the skip-ring tree), the bytes moved by the mover workgroups: on one GPU a
+fan-out from the origin's copy into every receiver's heap (the direct plan), across GPUs a pipelined
+scatter + all-gather (the chunked plan -- rehearsed here on one GPU with RLO_PART_CHUNKED).
 
 Parity against the oracle (oracle/rlo_oracle.c orc_storm2, extended for messages beyond the
 reference's 32,764-byte cap): per rank, the delivery set (bcast id, origin, tree parent of the
@@ -142,3 +143,39 @@ def test_bulk_repeatable_and_world_reuse(rlo):
     exp = orc.storm_expected(n, 1, k, 64, len_max=256 << 10, order=1)
     for s_ in sums:
         assert np.array_equal(s_, exp["sum"])
+
+
+# ---- the chunked plan (scatter + all-gather, what an 8-GPU world runs), rehearsed on one GPU with
+# RLO_PART_CHUNKED: every part of the world takes it although all share this GPU
+@pytest.mark.parametrize("n,bounds,k", [(16, [0, 8, 16], 96), (8, [0, 3, 8], 48)])
+def test_c5_mixed_storm_chunked_plan(rlo, n, bounds, k):
+    from rlo import sharded
+
+    lo, hi, cap, seed = 64, 1 << 20, 4096, 17
+    spec = {"kind": "storm", "k": k, "len": lo, "len_max": hi, "order": 1, "seed": seed, "log": True,
+            "log_cap": k + 8}
+    (st, logs, _), rcs = sharded.run_inprocess(n, bounds, spec, max_payload=cap, bulk_max=hi, movers=16, chunked=True)
+    assert rcs == [0, 0], (st["error"], st["error_aux"])
+    assert _check(st, logs, n, k, lo, hi, seed, 1, cap) > 0
+
+
+@pytest.mark.parametrize("ln", [(16 << 20) + 48, (36 << 20) + 5])
+def test_bulk_chunked_plan_latency_rounds(rlo, ln):
+    """one multi-chunk message at a time (chunks pipelined: each chunk's all-gather behind its scatter) in
+    a two-part world on the chunked plan; every receiver's checksum of every round"""
+    from rlo import sharded
+
+    n, rounds, seed = 8, 4, 9
+    assert rlo.bulk_plan(n, ln, True)["nchunks"] >= 2
+    spec = {"kind": "lat", "rounds": rounds, "len": ln, "seed": seed}
+    (st, _, _), rcs = sharded.run_inprocess(n, [0, 4, 8], spec, max_payload=64, bulk_max=ln, movers=16, chunked=True)
+    assert rcs == [0, 0], (st["error"], st["error_aux"])
+    org = [orc.origin_of(seed, i, n) for i in range(rounds)]
+    want = np.zeros(n, dtype=np.uint64)
+    for i, o in enumerate(org):
+        cs = np.uint64(orc.msg_checksum(o, i, 0, orc.payload(o, i, ln)))
+        for r in range(n):
+            if r != o:
+                want[r] += cs
+    assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]
+    assert np.array_equal(st["bcast_sum"], want)
