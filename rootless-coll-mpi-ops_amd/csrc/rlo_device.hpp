@@ -339,7 +339,12 @@ constexpr uint32_t kMaxSub = 256;
 // 4-tile sub-jobs, 256 of them over 248 movers left 8 movers a second sub-job each -- the round took two
 // sub-job times; with single tiles the tail is one tile
 constexpr uint32_t kMaxSubScatter = 1024;
-__host__ __device__ inline uint32_t max_sub(uint32_t kind) { return kind == 1u /* JOB_SCATTER */ ? kMaxSubScatter : kMaxSub; }
+// ... and a VERIFY job (reads only) in at most 64: its sub-jobs are cheap to move, so their claim overhead
+// (ticket, record, accounting) is what a finer cut would add
+constexpr uint32_t kMaxSubVerify = 64;
+__host__ __device__ inline uint32_t max_sub(uint32_t kind) {
+    return kind == 1u /* JOB_SCATTER */ ? kMaxSubScatter : (kind == 3u /* JOB_VERIFY */ ? kMaxSubVerify : kMaxSub);
+}
 // granules in flight per mover thread (16 B each): 256 threads x 8 x 16 B = 32 KiB per round trip
 constexpr int kMoveDepth = 8;
 struct BulkPlan {
