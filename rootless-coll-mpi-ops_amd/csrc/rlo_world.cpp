@@ -234,8 +234,10 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
     const uint64_t max_rings = *std::max_element(rings.begin(), rings.end());
     // default depth (tools/sweep.py, profiles/r1s5_sweep64.log): small slots (the 8-wave path,
     // payload <= 112 B) keep the wall ranks' hot rings from refusing: 64 B storm at 256 ranks
-    // 512 slots 16.1M, 1024 25.8M, 2048 29.2M, 4096 29.4M bcast/s; larger slots stay at 512
-    uint32_t cap = ring_slots ? pow2_ceil(ring_slots) : (L.stride <= 128u ? 2048u : 512u);
+    // 512 slots 16.1M, 1024 25.8M, 2048 29.2M, 4096 29.4M bcast/s; medium slots (the small copy path,
+    // payload <= 368 B) too: 256 B storm 6.58M -> 7.04M (profiles/r3_storm_slots.txt); large slots stay at
+    // 512 (1 KiB: no gain)
+    uint32_t cap = ring_slots ? pow2_ceil(ring_slots) : (L.stride <= 384u ? 2048u : 512u);
     const uint64_t limit = 0xFFFF0000ull;
     if (max_rings * cap * L.stride > limit) cap = pow2_floor(limit / (max_rings * L.stride));
     if (cap < 16) return RLO_E_INVAL;
