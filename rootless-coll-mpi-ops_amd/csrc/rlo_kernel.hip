@@ -1681,7 +1681,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             rdl32(latr, 1) == S.lat_own_next;
         const bool iar_dev = (P.mode & MODE_IAR) != 0;  // (host mode: decisions only -- its proposals are commands)
         const uint64_t nvm = __ballot(nv > 0u);
-        if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev && !ncmd) return 0u;
+        // a bulk round of the latency program (its slot free by the release counts phase A last read): the
+        // announcement by this pass too, and its scatter posted here -- not a full iteration per round
+        [[maybe_unused]] bool blat = false;
+        if constexpr (BULK) {
+            blat = (P.mode & MODE_LAT) && P.len > P.ring_cap && S.lat_own_next != 0xffffffffu &&
+                   rdl32(latr, 1) == S.lat_own_next &&
+                   S.b.sdone[S.b.bulk_q & (bsl - 1u)] >= (uint64_t)(S.b.bulk_q / bsl) * (uint64_t)(P.n - 1);
+        }
+        if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev && !ncmd && !blat) return 0u;
         if (ldm || nvm || ncmd) {
             // one round trip: lane 8 s + q loads chunk q of the s-th ring head to load, lane kLLVotes j + i
             // vote i of child j (sc1 loads behind the counters, as phase D0 / B)
@@ -1871,6 +1879,29 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
             }
             done++;
+        }
+        if constexpr (BULK) {
+            if (blat) {
+                const uint32_t q = S.b.bulk_q, id = S.lat_own_next;
+                // the announcement's payload, the descriptor {len, bulk sequence}, as chunk 1 of a K_HOST-style
+                // origination from the stage scratch (the judge copy's area: free at this point of the pass)
+                if (lane == 0) *reinterpret_cast<u32x4*>(stage + kBellJudge + 16u) = u32x4{P.len, q, 0u, 0u};
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (originate(K_HOST, (uint32_t)me | (TAG_BULK << 16) | (0xffu << 24), id, 16u, kBellJudge, out_head_r)) {
+                    if (lane == 0) {
+                        atomicAdd(&S.originated, 1ull);
+                        S.b.bulk_q = q + 1u;
+                        const uint32_t np = S.lat_pos + 1u;
+                        S.lat_pos = np;
+                        S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
+                        queue_job(S.b, P, JCLS_A, JOB_SCATTER, me, lr, q & (bsl - 1u), id, P.len,
+                                  bulk_total_tiles(bulk_plan(P.n, P.len, P.bulk_cross != 0), P.len), -1, ~0u, q, 0u);
+                    }
+                    flush_posts(S.b, P, lane);
+                    done++;
+                    need_full = true;  // then the bookkeeping (this may have been the program's last origination)
+                }
+            }
         }
         if (!done) return 0u;
         // every store of the pass drained, then the counters (the eager scheme's publish)

@@ -4,5 +4,4 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_bulk.py tests/test_gpu_engine.py tests/test_gpu_dropin.py -k "bulk or c5 or storm or pulled" -x -v --timeout 150 --timeout-method thread > gpurun_out/r3_bulk_tests.log 2>&1
 rc=$?; grep -E "FAILED|ERROR|passed|failed" gpurun_out/r3_bulk_tests.log | tail -8; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 240 python3 tools/bulk_probe.py 0 1,4,16,64 8 2>&1 | tee gpurun_out/r3_bulk_probe11.txt || exit 1
-timeout -k 10 300 python3 tools/storm_slots.py 256,1024 512,2048 2>&1 | tee gpurun_out/r3_storm_slots.txt
+timeout -k 10 240 python3 tools/bulk_probe.py 0 16k,1,4,16,64 2,8 2>&1 | tee gpurun_out/r3_bulk_probe13.txt || exit 1
