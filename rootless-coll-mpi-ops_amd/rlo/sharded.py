@@ -61,8 +61,10 @@ def merge(results):
     return st, logs, [r["ms"] for r in results]
 
 
-def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, **world_kw):
-    """world_kw: bulk_max / bulk_slots / movers (World.part)"""
+def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, blobs_for=None,
+                  **world_kw):
+    """world_kw: bulk_max / bulk_slots / movers / chunked (World.part).  blobs_for(p, blobs): the blobs part p
+    connects with (tests: a forged PCI bus puts a peer "on another GPU", so the part runs system scope)"""
     from . import _lib as L
     from .world import World
 
@@ -73,8 +75,8 @@ def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
                      device=devices[p], uncached=uncached, **world_kw) for p in range(parts)]
     try:
         blobs = [w.export() for w in ws]
-        for w in ws:
-            w.connect(blobs)
+        for p, w in enumerate(ws):
+            w.connect(blobs_for(p, blobs) if blobs_for else blobs)
         for w in ws:
             _program(w, spec)
         for w in ws:

@@ -59,6 +59,32 @@ def test_cross_gpu_peer_switches_to_system_scope(rlo):
         w1.close()
 
 
+def test_bulk_cross_gpu_path_system_scope(rlo):
+    """the bulk leg of the 8-GPU run, on one GPU: both parts see the other "on another GPU" (forged bus), so
+    both run system scope AND the chunked plan (scatter + all-gather, system-scope releases and flags) --
+    every receiver's checksum of every 16-MiB round equals the oracle's"""
+    from rlo import sharded
+
+    n, rounds, seed, ln = 4, 4, 21, (16 << 20) + 32
+
+    def forge(p, blobs):
+        return [b if q == p else _forge_bus(b) for q, b in enumerate(blobs)]
+
+    spec = {"kind": "lat", "rounds": rounds, "len": ln, "seed": seed}
+    (st, _, _), rcs = sharded.run_inprocess(n, [0, 2, 4], spec, max_payload=64, bulk_max=ln, movers=16, uncached=True,
+                                            blobs_for=forge)
+    assert rcs == [0, 0], (st["error"], st["error_aux"])
+    org = [orc.origin_of(seed, i, n) for i in range(rounds)]
+    want = np.zeros(n, dtype=np.uint64)
+    for i, o in enumerate(org):
+        cs = np.uint64(orc.msg_checksum(o, i, 0, orc.payload(o, i, ln)))
+        for r in range(n):
+            if r != o:
+                want[r] += cs
+    assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]
+    assert np.array_equal(st["bcast_sum"], want)
+
+
 def _merged(recs, name):
     """one leg's per-rank statistics of every part, by world rank"""
     parts = sorted((r[name] for r in recs), key=lambda x: x["rank_begin"])
