@@ -68,13 +68,14 @@ typedef struct {
      * rings, moved by mover workgroups of the same launch (DESIGN.md "Bulk messages").
      * bulk_max 0 = no bulk messages */
     uint64_t bulk_max;
-    uint32_t bulk_slots;  /* heap slots per origin (power of two <= 8, N * slots <= 256); 0 = 2 */
+    uint32_t bulk_slots;  /* heap slots per origin (power of two <= 8, N * slots <= 1024); 0 = 2 (1 beyond 512 ranks) */
     uint32_t movers;      /* mover workgroups of the part (>= 2, half scatter, half gather); 0 = auto */
     /* proposal pool (PROPOSAL_POOL_SIZE, rootless_ops.c:30): pending-proposal entries per origin
-     * in every rank's table (power of two <= 16; LDS N x pool x 16 B per rank); 0 = 2.  An iar
+     * in every rank's table (power of two <= 16; N x pool x 16 B per rank, in LDS, or in HBM where it
+     * would crowd the small copy path's stage out of LDS: rlo_world_info_t.pend_hbm); 0 = 2.  An iar
      * program keeps up to rlo_iar_cfg_t.pool <= this many own proposals in flight per rank */
     uint32_t proposal_pool;
-    uint32_t pad;
+    uint32_t flags;       /* RLO_PART_* (RLO_PART_PEND_HBM, RLO_PART_CHUNKED); 0 = none              */
 } rlo_world_cfg_t;
 
 typedef struct {
@@ -91,6 +92,12 @@ typedef struct {
     uint32_t proposal_pool;                      /* pending entries per origin (own proposals in flight) */
     uint32_t pull;                               /* 1: large bcasts cross edges as header + reference into
                                                     the sender's relay ring (pulled payloads)           */
+    /* the part's LDS layout (rlo_layout_plan gives the same answer without a GPU) */
+    uint32_t nsmall;       /* 16-B chunks staged per message (the small copy path takes slots of <= nsmall) */
+    uint32_t stage2_bytes; /* large-message LDS stage                                                 */
+    uint32_t ll_ok;        /* 1: the latency / iar / host programs run with doorbells                 */
+    uint32_t pend_hbm;     /* 1: the pending-proposal tables live in HBM, not LDS (large N x pool)     */
+    uint32_t dyn_lds, static_lds; /* bytes of LDS per rank-workgroup                                  */
 } rlo_world_info_t;
 
 /* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522
@@ -104,6 +111,8 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
  * Every part must rlo_reset before ANY part launches (host barrier in between). */
 #define RLO_PART_BLOB_BYTES 512u
 #define RLO_PART_UNCACHED 1u /* allocate the part's rings uncached (for peer GPUs writing over xGMI) */
+#define RLO_PART_PEND_HBM 4u /* the pending-proposal tables in HBM whatever the world size (the layout an 8-GPU
+                                 * world takes, rehearsed at smaller N; every part must set it alike) */
 #define RLO_PART_CHUNKED 2u  /* bulk messages take the multi-GPU plan (chunked scatter + all-gather) even when every
                                  * part is on one GPU: the 8-GPU path, rehearsed on one (every part must set it alike) */
 typedef struct {
@@ -261,6 +270,18 @@ int rlo_device_count(void);
 /* direct = 1: one GPU -- one stripe (the message), every tile fanned out from the origin's copy */
 typedef struct { uint32_t nchunks, stripe, chunk, tile, total_tiles, direct; } rlo_bulk_plan_t;
 int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out);
+/* the LDS layout a part of this world would get (rlo_world_query's waves, nsmall, stage2_bytes, ll_ok,
+ * pend_hbm, blocks_per_cu, ...), pure host arithmetic: no GPU needed.  The occupancy answers come from the
+ * build's register guarantees (rlo_progress_kernel keeps 2 waves per SIMD in its 8-wave and 4-wave
+ * non-doorbell forms, Makefile), not from the runtime; a part created on a GPU takes the runtime's */
+typedef struct {
+    int32_t n_ranks, n_parts, part;  /* even contiguous split, as rlo_part_create with part_begin NULL */
+    uint32_t max_payload, ring_slots, flags;
+    uint64_t bulk_max;
+    uint32_t bulk_slots, movers, proposal_pool;
+    int32_t cus;                     /* CUs of the GPU; 0 = 256 (MI355X)                                */
+} rlo_plan_cfg_t;
+int rlo_layout_plan(const rlo_plan_cfg_t* cfg, rlo_world_info_t* out);
 /* the storm program's payload length of bcasts 0..k-1 (rlo_storm_cfg_t len, len_max, seed): the
  * workload generator's host side, for byte accounting (no GPU) */
 int rlo_storm_lengths(uint64_t seed, uint64_t k, uint32_t len, uint32_t len_max, uint32_t* out);

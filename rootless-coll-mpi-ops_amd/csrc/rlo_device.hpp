@@ -206,6 +206,7 @@ struct Params {
     // originator keeps up to own_pool <= pend_slots own proposals in flight, in slots it takes
     // round-robin, and reuses a slot only after that slot's decision went out
     uint32_t pend_slots, own_pool;
+    struct PendState* pend_hbm;   // non-null: the pending tables in HBM, [n_local][n][pend_slots] x 16 B (uncached)
     // pulled payloads (slots beyond the small copy path, no bulk): a large bcast travels each edge as
     // its header (mark kRefMark) + a reference chunk {byte offset of the sender's copy in the sender's
     // part}.  The sender's copy sits in its RELAY ring (one per rank, fwd_cap slots): an originator or
@@ -288,7 +289,7 @@ constexpr int kBulkMaxChunks = 16;
 constexpr uint32_t kBulkLine = 128;     // per (rank, origin, slot): sflag[16] u32 @0, tflag u32 @64
 constexpr uint32_t kBulkTflag = 16;     // word index of tflag in the line
 constexpr uint64_t kJobTileMask = (1ull << 40) - 1;  // post counter: jobs << 40 | tiles
-constexpr int kMaxPend = 256;           // pending bulk receptions per rank (N * B <= 256)
+constexpr int kMaxPend = 1024;          // pending bulk receptions per rank (N * B <= 1024: C5 at 8 GPUs, 512 ranks)
 enum JobKind : uint32_t { JOB_SCATTER = 1, JOB_GATHER = 2, JOB_VERIFY = 3 };
 enum JobClass : uint32_t { JCLS_A = 0, JCLS_B = 1 };
 

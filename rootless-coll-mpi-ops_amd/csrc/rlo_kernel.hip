@@ -1187,7 +1187,12 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
 
 // ------------------------------------------------------------------ the kernel
 
-template <int W, bool BULK, bool LL>
+// PH: the pending-proposal tables live in HBM (Params.pend_hbm; worlds whose N x pool entries would crowd
+// the small copy path's stage out of LDS: the 8-GPU worlds), instantiated for the programs that hold
+// proposals (iar, host service).  Every other launch of such a world runs PH = false and never touches
+// the table.  All PendState traffic is the rank's own workgroup's, and every iteration that changed an
+// entry ends with a drain + barrier (the eager scheme) before any wave reads it again
+template <int W, bool BULK, bool LL, bool PH = false>
 __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // pulled payloads (Params.pull) exist only in the 4-wave kernel without bulk messages (slots beyond
     // the small copy path); compiled out of the others
@@ -1206,8 +1211,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     }
     const uint32_t nsmall = P.nsmall;  // chunks per staged message
     const uint32_t nmagic = nsmall > 1 ? 0xFFFFFFFFu / nsmall + 1u : 0u;
-    const uint32_t pend_bytes = 16u * (uint32_t)P.n * P.pend_slots;
-    PendState* pend = reinterpret_cast<PendState*>(dyn_lds);                   // [n][pend_slots]
+    const uint32_t pend_bytes = P.pend_hbm ? 0u : 16u * (uint32_t)P.n * P.pend_slots;
+    PendState* pend;  // [n][pend_slots]: dynamic LDS, or (PH) this rank's table in HBM (global-address typed:
+                      // no flat instructions, no extra registers on the LDS instantiations)
+    if constexpr (PH)
+        pend = (PendState*)(__attribute__((address_space(1))) PendState*)(P.pend_hbm + (size_t)blockIdx.x * (uint32_t)P.n * P.pend_slots);
+    else
+        pend = reinterpret_cast<PendState*>(dyn_lds);
     uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + pend_bytes);       // [oi][256]
     uint8_t* stage = dyn_lds + pend_bytes + P.nout_max * (2u * kMaxCand);      // [message][q] x 16 B
     uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
@@ -1264,7 +1274,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&P.topo[lr]);
         uint32_t* dst = reinterpret_cast<uint32_t*>(&S.t);
         for (int i = tid; i < (int)(sizeof(RankTopo) / 4); i += kBlock) dst[i] = src[i];
-        for (int i = tid; i < P.n * (int)P.pend_slots; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
+        if (PH || !P.pend_hbm)  // (a PH world's other programs: no table in LDS at all)
+            for (int i = tid; i < P.n * (int)P.pend_slots; i += kBlock) pend[i] = PendState{0, 0, 0, 0, 0, 0};
         if constexpr (BULK) {
             for (int i = tid; i < P.n * (int)P.bulk_slots; i += kBlock) bpend[i] = BulkPend{0u, 0u, 0u, -1, 0u, 0u, 0u, 0u};
         }
@@ -1299,8 +1310,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
         }
     }
+    if constexpr (PH) VM_DRAIN();  // the table's zeros land before any wave (the doorbell pass) reads them
     BAR();
     if (host && tid == 0) pub64_sys(&hctl[kHctlState], 1ull);  // serving (rlo_host_wait_started)
+    // a program that holds proposals in a PH world runs the PH instantiation (rlo_launch_progress)
+    if (!PH && P.pend_hbm && (P.mode & (MODE_IAR | MODE_HOST)) && tid == 0) set_error(S, P, ERR_HOST_CMD, 0x9E4Du);
     const uint64_t t_start = now_ticks();
     unsigned long long acc_sum = 0;  // checksum of delivered bcast chunks (this thread's share)
 
@@ -3506,11 +3520,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 // bulk messages (mover workgroups + mixed storm lengths); the Shared / LDS layout depends on it.  A
 // program with doorbells (MODE_LL: latency, IAR, host service) runs the doorbell instantiation of its
 // variant, the storm the one without (its registers untouched)
-template <int W, bool B, bool L>
+template <int W, bool B, bool L, bool H>
 static hipError_t grant_dyn_lds(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {  // > 64 KiB of dynamic LDS must be requested explicitly
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B, L>,
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B, L, H>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
@@ -3518,23 +3532,33 @@ static hipError_t grant_dyn_lds(size_t dyn_lds) {
     return hipSuccess;
 }
 
-template <int W, bool B, bool L>
+template <int W, bool B, bool L, bool H = false>
 static hipError_t launch_v(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
-    hipError_t e = grant_dyn_lds<W, B, L>(dyn_lds);
+    hipError_t e = grant_dyn_lds<W, B, L, H>(dyn_lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B, L>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
+    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B, L, H>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
     return hipGetLastError();
 }
 
-template <int W, bool B, bool L>
+template <int W, bool B, bool L, bool H = false>
 static hipError_t occ_v(int* blocks, size_t dyn_lds) {
-    hipError_t e = grant_dyn_lds<W, B, L>(dyn_lds);
+    hipError_t e = grant_dyn_lds<W, B, L, H>(dyn_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B, L>, 64 * W, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B, L, H>, 64 * W, dyn_lds);
+}
+
+// programs that hold proposals in a world with HBM pending tables run the PH instantiations (no bulk
+// worlds: their N x B bound keeps the table small)
+static bool wants_ph(const rlo::Params* p) {
+    return p->pend_hbm != nullptr && (p->mode & (rlo::MODE_IAR | rlo::MODE_HOST)) != 0;
 }
 
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
+    if (wants_ph(p) && variant != 5) {
+        if (variant == 8) return ll ? launch_v<8, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false, true>(p, blocks, dyn_lds, stream);
+        return ll ? launch_v<4, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false, true>(p, blocks, dyn_lds, stream);
+    }
     if (variant == 8) return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
     if (variant == 5) return ll ? launch_v<4, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, true, false>(p, blocks, dyn_lds, stream);
     return ll ? launch_v<4, false, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false>(p, blocks, dyn_lds, stream);
@@ -3546,7 +3570,10 @@ extern "C" size_t rlo_kernel_static_lds(int variant) {
     return sizeof(rlo::Shared<4, false>);
 }
 
+// variant | RLO_VARIANT_PH (16): the PH instantiation of variant 8 / 4
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant) {
+    if (variant == (8 | 16)) return occ_v<8, false, false, true>(blocks, dyn_lds);
+    if (variant == (4 | 16)) return occ_v<4, false, false, true>(blocks, dyn_lds);
     if (variant == 8) return occ_v<8, false, false>(blocks, dyn_lds);
     if (variant == 5) return occ_v<4, true, false>(blocks, dyn_lds);
     return occ_v<4, false, false>(blocks, dyn_lds);
@@ -3555,6 +3582,8 @@ extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant) {
 // the doorbell instantiation of a variant: the 4-wave ones may take more than 256 registers (one wave
 // per SIMD: worlds whose ranks have a CU each), so a world gets doorbells only where this answer covers it
 extern "C" hipError_t rlo_occupancy_ll(int* blocks, size_t dyn_lds, int variant) {
+    if (variant == (8 | 16)) return occ_v<8, false, true, true>(blocks, dyn_lds);
+    if (variant == (4 | 16)) return occ_v<4, false, true, true>(blocks, dyn_lds);
     if (variant == 8) return occ_v<8, false, true>(blocks, dyn_lds);
     if (variant == 5) return occ_v<4, true, true>(blocks, dyn_lds);
     return occ_v<4, false, true>(blocks, dyn_lds);

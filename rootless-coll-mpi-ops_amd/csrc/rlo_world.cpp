@@ -306,7 +306,8 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
     L.heap_bytes.assign(nparts, 0);
     L.bflag_bytes.assign(nparts, 0);
     if (bulk_max) {
-        L.bslots = bulk_slots ? bulk_slots : 2u;
+        // 2 heap slots per origin by default, 1 where N x 2 would pass the pending-reception bound (C5 at 8 GPUs)
+        L.bslots = bulk_slots ? bulk_slots : ((uint64_t)n * 2u <= (uint64_t)rlo::kMaxPend ? 2u : 1u);
         if ((L.bslots & (L.bslots - 1)) || L.bslots > 8 || (uint64_t)n * L.bslots > (uint64_t)rlo::kMaxPend) return RLO_E_INVAL;
         if (bulk_max > 0xFFF00000ull) return RLO_E_INVAL;  // a slot is addressed by one buffer resource
         L.bulk_max = bulk_max;
@@ -404,6 +405,8 @@ struct rlo_world {
     size_t dyn_lds = 0;
     uint32_t nsmall = 8, stage2 = 1024;
     bool ll_ok = false;  // the doorbell instantiation of the kernel is co-resident at this world's size
+    bool pend_hbm = false;  // the pending-proposal tables in HBM (plan_lds), nl x N x pool x 16 B, uncached
+    uint8_t* pend_mem = nullptr;
     int waves = 4;    // rank-workgroup width: 8 (512 candidates per iteration) when each rank has a CU
     int variant = 4;  // kernel instantiation: 8 / 4 waves, 5 = 4 waves with bulk messages
     // bulk messages (rlo_device.hpp): this part's heap, flag region and job rings (all uncached),
@@ -447,71 +450,139 @@ JobMem job_mem(uint32_t J, uint32_t nl) {
     return m;
 }
 
-// co-residency of the part's workgroups (rank-workgroups, plus the mover workgroups of a bulk
-// world): largest small-path stage (nsmall chunks per message, <= 24) and then the largest stage2
-// (<= 64 KiB) at which the occupancy calculator (LDS allocation granularity, registers, waves)
-// still co-schedules them
-int size_lds_variant(rlo_world* w, int variant) {
-    const Layout& L = w->L;
+// ---- LDS layout of a part: (kernel variant, staged chunks per message, large-message stage, where the
+// pending-proposal table lives, doorbells).  A pure function of the world layout, the local rank count and
+// an occupancy oracle: the HIP runtime's answer when the part is created on a GPU, the build's register
+// guarantees (Makefile guard) when rlo_layout_plan asks on a host without one.
+//
+// The small copy path needs every chunk of a small / medium slot staged (nsmall = slot chunks, <= 24), and
+// large slots stage 5 chunks (header + 64 B: a 64-B message and a proposal stay on the small path).  That
+// count is never lowered to make a layout fit: a world that cannot stage it in LDS moves its
+// pending-proposal table (N x pool x 16 B per rank, the one per-rank LDS array that grows with the WORLD
+// size) to HBM, then drops to 4 waves -- instead of silently moving every message onto the large path, as
+// the 8-GPU world (N = 2048: a 64-KiB table) did up to round 3.
+struct LdsPlan {
+    int variant = 4, waves = 4, blocks_per_cu = 1;
+    uint32_t nsmall = 0, stage2 = 0, bpend_off = 0;
+    size_t dyn_lds = 0;
+    bool ll_ok = false, pend_hbm = false;
+};
+// occupancy oracle: blocks of `variant` (| kVariantPH: its PH instantiation; ll: its doorbell form) per CU
+// at `dyn_lds` bytes of dynamic LDS
+typedef int (*OccFn)(int variant, bool ll, size_t dyn_lds);
+constexpr int kVariantPH = 16;  // rlo_kernel.hip rlo_occupancy: variant | 16 = the PH instantiation
+constexpr size_t kLdsPerCU = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
+
+int occ_device(int variant, bool ll, size_t dyn_lds) {
+    int b = 0;
+    if ((ll ? rlo_occupancy_ll(&b, dyn_lds, variant) : rlo_occupancy(&b, dyn_lds, variant)) != hipSuccess) return 0;
+    return b;
+}
+// no GPU: LDS (512-B allocation granules), 32 waves per CU, and the waves per SIMD every instantiation is
+// built to (the Makefile's register guard fails the build of an 8-wave one, or a 4-wave one without
+// doorbells, that drops below 2 per SIMD; the 4-wave doorbell and bulk ones may take one)
+int occ_model(int variant, bool ll, size_t dyn_lds) {
+    const int v = variant & ~kVariantPH;
+    const int W = v == 8 ? 8 : 4;
+    const size_t lds = ((rlo_kernel_static_lds(v) + dyn_lds + 511) & ~(size_t)511);
+    const int by_lds = lds ? (int)(kLdsPerCU / lds) : 8;
+    const int per_simd = (v == 8 || (v == 4 && !ll)) ? 2 : 1;
+    const int by_regs = per_simd * 4 / W;
+    return std::min(by_lds, std::min(by_regs, 32 / W));
+}
+
+// one variant (8 / 4 / 5), the pending table in LDS or HBM
+int plan_variant(const Layout& L, int nl, int nmov, int cus, int variant, bool pend_hbm, OccFn occ, uint32_t ns_force,
+                 LdsPlan* out) {
     const int waves = variant == 8 ? 8 : 4;
-    const size_t lds_cu = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md)
-    const int nblk = w->nl + (variant == 5 ? (int)w->nmov : 0);
-    const int need_bpc = (nblk + w->cus - 1) / w->cus;
-    const size_t per_block = lds_cu / need_bpc;
+    const int nblk = nl + (variant == 5 ? nmov : 0);
+    const int need_bpc = (nblk + cus - 1) / cus;
+    const size_t per_block = kLdsPerCU / need_bpc;
     const size_t cand = (size_t)64 * waves, stat = rlo_kernel_static_lds(variant);
     const size_t bpend = variant == 5 ? (size_t)L.n * L.bslots * 32 : 0;  // pending bulk receptions
+    const size_t ptab = pend_hbm ? 0 : (size_t)16 * L.n * L.pend_slots;
+    // every message of a medium slot (<= 24 chunks: payload <= 368 B) takes the small copy path (packed
+    // (message, chunk) copies; the large-message path moves one message per LDS block: 256 B storm 2.0M
+    // bcast/s, profiles/r2s2_diag_sizes.log); large slots stage 5 chunks -- header + 64 B -- and leave the
+    // LDS to the large-message rounds (4 KiB storm 109 -> 104 ms, 1 KiB 40.4 -> 38.4, r2s4_nsmall_ab.txt)
+    const uint32_t ns = ns_force ? ns_force : (L.stride / 16u <= 24u ? L.stride / 16u : 5u);
+    // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
+    const size_t fixed = stat + ptab + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
+    if (per_block < fixed + 1024 + 512) return RLO_E_OCCUPANCY;
+    size_t s2 = std::min<size_t>(128 * 1024, (per_block - fixed - 512) & ~(size_t)1023);  // two halves of <= 64 blocks
+    const int vph = variant | (pend_hbm && variant != 5 ? kVariantPH : 0);
     int api = 0;
-    bool ok = false;
-    // every message of a medium slot (<= 24 chunks: payload <= 368 B) takes the small copy path when the
-    // stage fits (packed (message, chunk) copies; the large-message path moves one message per LDS
-    // block: 256 B storm 2.0M bcast/s, profiles/r2s2_diag_sizes.log)
-    // (large slots stage 5 chunks -- header + 64 B, so a 64-B message or a proposal still takes the small
-    // path -- and leave the LDS to the large-message rounds: 4 KiB storm 109 -> 104 ms, 1 KiB 40.4 -> 38.4,
-    // profiles/r2s4_nsmall_ab.txt)
-    uint32_t ns0 = L.stride / 16u <= 24u ? L.stride / 16u : 5u;
-    if (const char* e = diag_env("RLO_NSMALL"))  // A/B: staged chunks per candidate in large-slot worlds
-        if (L.stride / 16u > 24u) ns0 = std::max(2u, std::min(8u, (uint32_t)std::atoi(e)));
-    for (uint32_t ns = ns0; ns >= 1 && !ok; ns--) {
-        // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
-        const size_t fixed = stat + (size_t)16 * L.n * L.pend_slots + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
-        if (per_block < fixed + 1024 + 512) continue;
-        size_t s2 = std::min<size_t>(128 * 1024, (per_block - fixed - 512) & ~(size_t)1023);  // two halves of <= 64 blocks
-        for (;;) {
-            w->dyn_lds = fixed - stat + s2;
-            if (rlo_occupancy(&api, w->dyn_lds, variant) != hipSuccess) api = 0;
-            if (api >= need_bpc) { ok = true; break; }
-            if (s2 <= 1024) break;
-            s2 -= 1024;
-        }
-        w->nsmall = ns;
-        w->stage2 = (uint32_t)s2;
-        w->bpend_off = (uint32_t)(fixed - stat - bpend + s2);
+    for (;;) {
+        const size_t dyn = fixed - stat + s2;
+        api = occ(variant, false, dyn);
+        if (api >= need_bpc && vph != variant) api = std::min(api, occ(vph, false, dyn));
+        if (api >= need_bpc) break;
+        if (s2 <= 1024) return RLO_E_OCCUPANCY;
+        s2 -= 1024;
     }
-    if (!ok) return RLO_E_OCCUPANCY;
-    w->waves = waves;
-    w->variant = variant;
-    w->blocks_per_cu = std::max(1, api);
+    LdsPlan p;
+    p.variant = variant;
+    p.waves = waves;
+    p.nsmall = ns;
+    p.stage2 = (uint32_t)s2;
+    p.dyn_lds = fixed - stat + s2;
+    p.bpend_off = (uint32_t)(fixed - stat - bpend + s2);
+    p.blocks_per_cu = std::max(1, api);
+    p.pend_hbm = pend_hbm;
     {  // the doorbell instantiation co-resident too? (else its programs run without bells)
-        int ll = 0;
-        if (rlo_occupancy_ll(&ll, w->dyn_lds, variant) != hipSuccess) ll = 0;
-        w->ll_ok = ll >= need_bpc;
+        int ll = occ(variant, true, p.dyn_lds);
+        if (vph != variant) ll = std::min(ll, occ(vph, true, p.dyn_lds));
+        p.ll_ok = ll >= need_bpc;
     }
-    if (nblk > w->blocks_per_cu * w->cus) return RLO_E_OCCUPANCY;
+    if (nblk > p.blocks_per_cu * cus) return RLO_E_OCCUPANCY;
+    *out = p;
     return RLO_OK;
 }
 
-// 8-wave rank-workgroups (512 candidates per iteration) when every local rank gets a CU of its own,
-// every message fits the small copy path (slot <= 8 chunks: payloads <= 112 B) and the 8-wave layout
-// fits; else 4 waves (larger slots need the LDS for the large-message stage: 64 B storm 12.1 -> 16.0 M
-// bcast/s with 8 waves, but 256 B .. 4 KiB 30-40 % slower).  RLO_WAVES=4 / 8 forces one (A/B)
-int size_lds(rlo_world* w) {
-    if (w->L.bulk_max) return size_lds_variant(w, 5);  // bulk worlds: the 4-wave kernel with movers
+// 8-wave rank-workgroups (512 candidates per iteration) when every local rank gets a CU of its own and
+// every message fits the small copy path (slot <= 8 chunks: payloads <= 112 B); else 4 waves (larger slots
+// need the LDS for the large-message stage: 64 B storm 12.1 -> 16.0 M bcast/s with 8 waves, but 256 B ..
+// 4 KiB 30-40 % slower).  Per variant: the pending table in LDS, else in HBM (RLO_PART_PEND_HBM: always
+// HBM, the tests' way to run the 8-GPU layout's proposal path on one GPU).  Bulk worlds: the 4-wave
+// kernel with movers, table in LDS (N x B <= kMaxPend keeps them small).  RLO_WAVES / RLO_NSMALL: A/B
+int plan_lds(const Layout& L, int nl, int nmov, int cus, uint32_t flags, OccFn occ, LdsPlan* out) {
+    uint32_t ns_force = 0;
+    if (const char* e = diag_env("RLO_NSMALL"))  // A/B: staged chunks per candidate in large-slot worlds
+        if (L.stride / 16u > 24u) ns_force = std::max(2u, std::min(8u, (uint32_t)std::atoi(e)));
+    if (L.bulk_max) return plan_variant(L, nl, nmov, cus, 5, false, occ, ns_force, out);
     const char* env = diag_env("RLO_WAVES");
     const int force = env ? std::atoi(env) : 0;
-    const bool small = w->L.stride <= 8u * 16u;
-    if (force != 4 && (small || force == 8) && w->nl <= w->cus && size_lds_variant(w, 8) == RLO_OK) return RLO_OK;
+    const bool small = L.stride <= 8u * 16u;
+    const bool hbm_only = (flags & RLO_PART_PEND_HBM) != 0;
+    if (force != 4 && (small || force == 8) && nl <= cus) {
+        if (!hbm_only && plan_variant(L, nl, nmov, cus, 8, false, occ, ns_force, out) == RLO_OK) return RLO_OK;
+        if (plan_variant(L, nl, nmov, cus, 8, true, occ, ns_force, out) == RLO_OK) return RLO_OK;
+    }
     if (force == 8) return RLO_E_OCCUPANCY;
-    return size_lds_variant(w, 4);
+    // 4 waves (two rank-workgroups per CU beyond 256 local ranks): a full stage first, with the table in LDS
+    // or HBM; only then fewer staged chunks (the 4-wave kernel's large-message path takes the rest)
+    const uint32_t ns0 = ns_force ? ns_force : (L.stride / 16u <= 24u ? L.stride / 16u : 5u);
+    for (uint32_t ns = ns0; ns >= 1; ns--) {
+        if (!hbm_only && plan_variant(L, nl, nmov, cus, 4, false, occ, ns, out) == RLO_OK) return RLO_OK;
+        if (plan_variant(L, nl, nmov, cus, 4, true, occ, ns, out) == RLO_OK) return RLO_OK;
+    }
+    return RLO_E_OCCUPANCY;
+}
+
+int size_lds(rlo_world* w) {
+    LdsPlan p;
+    const int rc = plan_lds(w->L, w->nl, (int)w->nmov, w->cus, w->flags, occ_device, &p);
+    if (rc) return rc;
+    w->variant = p.variant;
+    w->waves = p.waves;
+    w->nsmall = p.nsmall;
+    w->stage2 = p.stage2;
+    w->dyn_lds = p.dyn_lds;
+    w->bpend_off = p.bpend_off;
+    w->blocks_per_cu = p.blocks_per_cu;
+    w->ll_ok = p.ll_ok;
+    w->pend_hbm = p.pend_hbm;
+    return RLO_OK;
 }
 
 // RankTopo of every local rank, with remote ends resolved to addresses in this process
@@ -679,6 +750,13 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         rlo_world_destroy(w);
         return RLO_E_HIP;
     }
+    if (w->pend_hbm) {  // uncached: a launch's workgroup may sit on another XCD than the previous launch's
+        const uint32_t keep = w->flags;
+        w->flags |= RLO_PART_UNCACHED;
+        const int e = alloc_region(w, (void**)&w->pend_mem, (uint64_t)w->nl * w->L.n * w->L.pend_slots * 16u);
+        w->flags = keep;
+        if (e) { rlo_world_destroy(w); return RLO_E_HIP; }
+    }
     if (w->L.bulk_max) {  // heap, flags and job rings: uncached (peers and other XCDs write them)
         w->jmem_bytes = job_mem(w->jslots, (uint32_t)w->nl).bytes;
         const uint32_t keep = w->flags;
@@ -830,6 +908,7 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
     pc.bulk_slots = cfg->bulk_slots;
     pc.movers = cfg->movers;
     pc.proposal_pool = cfg->proposal_pool;
+    pc.flags = cfg->flags & (RLO_PART_PEND_HBM | RLO_PART_CHUNKED);
     rlo_world* w = nullptr;
     int rc = rlo_part_create(&pc, &w);
     if (rc) return rc;
@@ -853,6 +932,7 @@ int rlo_world_destroy(rlo_world_t* w) {
     if (w->heap) (void)hipFree(w->heap);
     if (w->bflag) (void)hipFree(w->bflag);
     if (w->jmem) (void)hipFree(w->jmem);
+    if (w->pend_mem) (void)hipFree(w->pend_mem);
     w->d_bheap.release(); w->d_bflag.release(); w->d_part_of.release(); w->d_part_begin.release();
     w->d_topo.release(); w->d_stats.release();
     w->d_sched_off.release(); w->d_expect_bcast.release(); w->d_prop_off.release(); w->d_expect_dec.release();
@@ -894,6 +974,12 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->heap_bytes = w->L.heap_bytes[w->part];
     o->proposal_pool = w->L.pend_slots;
     o->pull = w->L.pull && w->nsmall >= 2 ? 1u : 0u;  // as Params.pull
+    o->nsmall = w->nsmall;
+    o->stage2_bytes = w->stage2;
+    o->ll_ok = w->ll_ok ? 1u : 0u;
+    o->pend_hbm = w->pend_hbm ? 1u : 0u;
+    o->dyn_lds = (uint32_t)w->dyn_lds;
+    o->static_lds = (uint32_t)rlo_kernel_static_lds(w->variant);
     return RLO_OK;
 }
 
@@ -938,6 +1024,7 @@ static void base_params(rlo_world* w) {
     P.n_local = (uint32_t)w->nl;
     P.ring_cap = w->L.stride - rlo::kHdr;
     P.pend_slots = w->L.pend_slots;
+    P.pend_hbm = reinterpret_cast<rlo::PendState*>(w->pend_mem);
     P.pull = w->L.pull && w->nsmall >= 2 ? 1u : 0u;  // the reference chunk is staged as chunk 1
     P.relay_cap = w->L.relay_cap;
     P.own_pool = 1;  // one own proposal per engine (rootless_ops.c:241) unless a program asks for more
@@ -1440,7 +1527,12 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     if (w->have_program && (w->P.mode & rlo::MODE_HOST)) {  // the kernel is not running: rings restart at 0
         std::memset(w->h_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
         std::memset(w->d_ctl, 0, (size_t)w->nl * rlo::kHctlWords * 8);
+        // the command doorbells restart too: the kernel takes a doorbell whose tag is the sequence it expects
+        // next (ll_cmd_put), without the tail, so a relaunch that left the previous launch's tags in place
+        // would replay that launch's first commands before the host posts anything
+        if (w->h_llc) std::memset(w->h_llc, 0, (size_t)w->nl * w->cmd_cap * rlo::kLLCmdSlot);
         if (w->shm) {  // shared service: the clients' boxes restart too
+            std::memset(w->shm + w->SL.llc, 0, (size_t)w->nl * w->cmd_cap * rlo::kLLCmdSlot);
             std::memset(w->shm + w->SL.cli, 0, (size_t)w->nl * sizeof(rlo::ClientBox));
             std::fill(w->cli_req.begin(), w->cli_req.end(), 0);
             __atomic_store_n(&((rlo::ShmHdr*)w->shm)->leader_failed, 0u, __ATOMIC_RELEASE);
@@ -1631,6 +1723,56 @@ int rlo_bulk_plan(int n, uint64_t len, int cross, rlo_bulk_plan_t* out) {
     out->tile = p.tile;
     out->total_tiles = rlo::bulk_total_tiles(p, (uint32_t)len);
     out->direct = p.direct;
+    return RLO_OK;
+}
+
+int rlo_layout_plan(const rlo_plan_cfg_t* cfg, rlo_world_info_t* o) {
+    if (!cfg || !o || cfg->n_parts < 1 || cfg->part < 0 || cfg->part >= cfg->n_parts) return RLO_E_INVAL;
+    Layout L;
+    const uint32_t mp = (std::max<uint32_t>(cfg->max_payload ? cfg->max_payload : 4096u, 16u) + 15u) & ~15u;
+    if (mp > 65520u) return RLO_E_INVAL;
+    const uint32_t pp = cfg->proposal_pool ? cfg->proposal_pool : 2u;
+    if ((pp & (pp - 1u)) || pp > (uint32_t)rlo::kPoolMax) return RLO_E_INVAL;
+    L.pend_slots = pp;
+    int rc = build_layout(cfg->n_ranks, cfg->n_parts, nullptr, mp, cfg->ring_slots, cfg->bulk_max, cfg->bulk_slots, L);
+    if (rc) return rc;
+    const int cus = cfg->cus > 0 ? cfg->cus : 256;
+    const int nl = L.pb[cfg->part + 1] - L.pb[cfg->part];
+    int nmov = 0;
+    if (L.bulk_max) nmov = cfg->movers ? (int)cfg->movers : (std::max(16, cus - nl) & ~1);
+    LdsPlan p;
+    rc = plan_lds(L, nl, nmov, cus, cfg->flags, occ_model, &p);
+    if (rc) return rc;
+    std::memset(o, 0, sizeof *o);
+    o->n_ranks = L.n;
+    o->max_in_degree = L.max_in;
+    o->max_fanout = L.max_fan;
+    o->edges = (int)L.E.size();
+    o->ring_slots = L.cap;
+    o->slot_stride = L.stride;
+    o->vote_slots = L.vote_cap;
+    o->fwd_bytes = L.fwd_bytes[cfg->part];
+    o->vote_bytes = L.vote_bytes[cfg->part];
+    o->ctrl_bytes = L.ctrl_words[cfg->part] * 8;
+    o->cus = cus;
+    o->blocks_per_cu = p.blocks_per_cu;
+    o->part = cfg->part;
+    o->n_parts = L.nparts;
+    o->rank_begin = L.pb[cfg->part];
+    o->rank_end = L.pb[cfg->part + 1];
+    o->waves = p.waves;
+    o->bulk_slots = L.bslots;
+    o->movers = (uint32_t)nmov;
+    o->bulk_max = L.bulk_max;
+    o->heap_bytes = L.heap_bytes[cfg->part];
+    o->proposal_pool = L.pend_slots;
+    o->pull = L.pull && p.nsmall >= 2 ? 1u : 0u;
+    o->nsmall = p.nsmall;
+    o->stage2_bytes = p.stage2;
+    o->ll_ok = p.ll_ok ? 1u : 0u;
+    o->pend_hbm = p.pend_hbm ? 1u : 0u;
+    o->dyn_lds = (uint32_t)p.dyn_lds;
+    o->static_lds = (uint32_t)rlo_kernel_static_lds(p.variant);
     return RLO_OK;
 }
 

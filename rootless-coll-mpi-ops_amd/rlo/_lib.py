@@ -26,6 +26,7 @@ RLO_E_AGAIN = -8
 RLO_PART_BLOB_BYTES = 512
 RLO_PART_UNCACHED = 1
 RLO_PART_CHUNKED = 2
+RLO_PART_PEND_HBM = 4
 RLO_LAUNCH_NO_RESET = 1
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
@@ -43,7 +44,7 @@ RLO_EV_ACTION, RLO_EV_RESULT, RLO_EV_JUDGE, RLO_EV_OWN_JUDGE, RLO_EV_JUDGED = 3,
 class WorldCfg(ctypes.Structure):
     _fields_ = [("n_ranks", ctypes.c_int32), ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("bulk_max", ctypes.c_uint64), ("bulk_slots", ctypes.c_uint32),
-                ("movers", ctypes.c_uint32), ("proposal_pool", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("movers", ctypes.c_uint32), ("proposal_pool", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
 class WorldInfo(ctypes.Structure):
@@ -55,7 +56,16 @@ class WorldInfo(ctypes.Structure):
                 ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),
                 ("waves", ctypes.c_int32), ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32),
                 ("bulk_max", ctypes.c_uint64), ("heap_bytes", ctypes.c_uint64), ("proposal_pool", ctypes.c_uint32),
-                ("pull", ctypes.c_uint32)]
+                ("pull", ctypes.c_uint32), ("nsmall", ctypes.c_uint32), ("stage2_bytes", ctypes.c_uint32),
+                ("ll_ok", ctypes.c_uint32), ("pend_hbm", ctypes.c_uint32), ("dyn_lds", ctypes.c_uint32),
+                ("static_lds", ctypes.c_uint32)]
+
+
+class PlanCfg(ctypes.Structure):
+    _fields_ = [("n_ranks", ctypes.c_int32), ("n_parts", ctypes.c_int32), ("part", ctypes.c_int32),
+                ("max_payload", ctypes.c_uint32), ("ring_slots", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("bulk_max", ctypes.c_uint64), ("bulk_slots", ctypes.c_uint32), ("movers", ctypes.c_uint32),
+                ("proposal_pool", ctypes.c_uint32), ("cus", ctypes.c_int32)]
 
 
 class PartCfg(ctypes.Structure):
@@ -115,7 +125,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_strerror", "rlo_last_hip_error",
            "rlo_device_error", "rlo_bulk_debug",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
-           "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan",
+           "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan", "rlo_layout_plan",
            "rlo_storm_lengths", "rlo_host_share", "rlo_host_unlink", "rlo_host_proxy", "rlo_host_wait_started",
            "rlo_host_fail", "rlo_client_attach", "rlo_client_detach", "rlo_client_state", "rlo_client_post",
            "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_client_hdiag", "rlo_client_fwd", "rlo_host_device_judge"]
@@ -165,6 +175,7 @@ def load():
                                       ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_host_bulk_copy.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp]
     L.rlo_bulk_plan.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(BulkPlan)]
+    L.rlo_layout_plan.argtypes = [ctypes.POINTER(PlanCfg), ctypes.POINTER(WorldInfo)]
     L.rlo_storm_lengths.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_host_device_judge.argtypes = [vp, ctypes.POINTER(IarCfg)]

@@ -26,9 +26,12 @@ def pbuf(pid, vote, data):
 
 
 class HostWorld:
-    def __init__(self, n, max_payload=256, device=-1, cmd_slots=0, pickup_slots=0, idle_timeout_s=60, pool=1):
-        """pool: own proposals a rank may keep in flight (the proposal pool; 1 = my_own_proposal)"""
-        self.world = World(n, max_payload=max_payload, device=device, proposal_pool=max(2, 1 << (pool - 1).bit_length()))
+    def __init__(self, n, max_payload=256, device=-1, cmd_slots=0, pickup_slots=0, idle_timeout_s=60, pool=1,
+                 pend_hbm=False):
+        """pool: own proposals a rank may keep in flight (the proposal pool; 1 = my_own_proposal);
+        pend_hbm: the pending-proposal tables in HBM (the 8-GPU layout, rehearsed)"""
+        self.world = World(n, max_payload=max_payload, device=device, proposal_pool=max(2, 1 << (pool - 1).bit_length()),
+                           pend_hbm=pend_hbm)
         self.lib = self.world.lib
         self.h = self.world.h
         self.n = n
@@ -111,6 +114,19 @@ class HostWorld:
     def stats(self):
         """per-rank counters; complete only after close() (see final_stats)"""
         return self.world.stats()
+
+    def relaunch(self):
+        """QUIT every rank, wait for the kernel, and launch the same world again (rings, counters and
+        command doorbells restart at 0: rlo_reset)"""
+        for r in range(self.n):
+            self.backlog[r].clear()
+            q = L.Cmd(L.RLO_CMD_QUIT, 0, 0, 0, 0, 0)
+            while self.lib.rlo_host_post(self.h, r, ctypes.byref(q), None, 0) == L.RLO_E_AGAIN:
+                self.poll(r)
+        self.world.wait()
+        self.inflight = [0] * self.n
+        self.held = [[] for _ in range(self.n)]
+        check(self.lib.rlo_launch_ex(self.h, self.stream, 0), "rlo_launch_ex")
 
     def close(self, raise_on_device_error=True):
         if self.closed:

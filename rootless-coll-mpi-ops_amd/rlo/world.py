@@ -22,15 +22,17 @@ class World:
     part of a sharded world (export() -> exchange blobs -> connect(blobs))."""
 
     def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None, bulk_max=0, bulk_slots=0, movers=0,
-                 proposal_pool=0):
+                 proposal_pool=0, pend_hbm=False):
         """bulk_max > 0: messages longer than max_payload (up to bulk_max bytes) are bulk messages --
         announced through the rings, moved by `movers` mover workgroups (0 = auto) between per-rank
         heaps of bulk_slots slots per origin (rlo_hip.h).  proposal_pool: pending entries per origin
-        = the most own proposals a rank can keep in flight (power of two <= 16; 0 = 2)."""
+        = the most own proposals a rank can keep in flight (power of two <= 16; 0 = 2).  pend_hbm: the
+        pending-proposal tables in HBM whatever N (the 8-GPU world's layout, rehearsed at a smaller N)."""
         self.lib = L.load()
         h = ctypes.c_void_p()
         if _part is None:
-            cfg = L.WorldCfg(n, max_payload, ring_slots, device, bulk_max, bulk_slots, movers, proposal_pool)
+            cfg = L.WorldCfg(n, max_payload, ring_slots, device, bulk_max, bulk_slots, movers, proposal_pool,
+                             L.RLO_PART_PEND_HBM if pend_hbm else 0)
             check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
         else:
             n_parts, part, begin, flags = _part
@@ -49,10 +51,13 @@ class World:
 
     @classmethod
     def part(cls, n, n_parts, part, part_begin=None, max_payload=4096, ring_slots=0, device=-1, uncached=False,
-             bulk_max=0, bulk_slots=0, movers=0, proposal_pool=0, chunked=False):
+             bulk_max=0, bulk_slots=0, movers=0, proposal_pool=0, chunked=False, pend_hbm=False):
+        """pend_hbm: the pending-proposal tables in HBM whatever N (the layout of the 8-GPU world's parts,
+        rehearsed at a smaller N)"""
         return cls(n, max_payload, ring_slots, device,
                    _part=(n_parts, part, part_begin, (L.RLO_PART_UNCACHED if uncached else 0) |
-                          (L.RLO_PART_CHUNKED if chunked else 0)), bulk_max=bulk_max,
+                          (L.RLO_PART_CHUNKED if chunked else 0) | (L.RLO_PART_PEND_HBM if pend_hbm else 0)),
+                   bulk_max=bulk_max,
                    bulk_slots=bulk_slots, movers=movers, proposal_pool=proposal_pool)
 
     def _query(self):
@@ -233,6 +238,17 @@ def bulk_plan(n, nbytes, cross=False):
     check(L.load().rlo_bulk_plan(n, nbytes, 1 if cross else 0, ctypes.byref(out)), "rlo_bulk_plan")
     return {"nchunks": out.nchunks, "stripe": out.stripe, "chunk": out.chunk, "tile": out.tile,
             "total_tiles": out.total_tiles, "direct": out.direct}
+
+
+def layout_plan(n, n_parts=1, part=0, max_payload=4096, ring_slots=0, bulk_max=0, bulk_slots=0, movers=0,
+                proposal_pool=0, pend_hbm=False, cus=256):
+    """rlo_layout_plan: the LDS layout (waves, nsmall, stage2_bytes, ll_ok, pend_hbm, ...) a part of this world
+    would get, from host arithmetic and the build's register guarantees (no GPU)"""
+    cfg = L.PlanCfg(n, n_parts, part, max_payload, ring_slots, L.RLO_PART_PEND_HBM if pend_hbm else 0, bulk_max,
+                    bulk_slots, movers, proposal_pool, cus)
+    out = L.WorldInfo()
+    check(L.load().rlo_layout_plan(ctypes.byref(cfg), ctypes.byref(out)), "rlo_layout_plan")
+    return {f: getattr(out, f) for f, _ in L.WorldInfo._fields_}
 
 
 def storm_lengths(seed, k, length, len_max=0):

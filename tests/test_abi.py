@@ -260,7 +260,7 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
 
     pairs = {"rlo_world_cfg_t": L.WorldCfg, "rlo_world_info_t": L.WorldInfo, "rlo_part_cfg_t": L.PartCfg,
              "rlo_storm_cfg_t": L.StormCfg, "rlo_iar_cfg_t": L.IarCfg, "rlo_host_cfg_t": L.HostCfg,
-             "rlo_cmd_t": L.Cmd, "rlo_log_rec_t": L.LogRec}
+             "rlo_cmd_t": L.Cmd, "rlo_log_rec_t": L.LogRec, "rlo_plan_cfg_t": L.PlanCfg}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rlo_hip.h"', 'int main(void) {']
     for cname, py in pairs.items():
         lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))

@@ -291,17 +291,39 @@ def test_iar_concurrent_exact_sets(rlo, n, p, ppm, pool):
     iar_sets.check(logs, n, p, ppm, pool)
 
 
-def test_latency_program(rlo):
-    n, rounds = 32, 64
-    with rlo.World(n) as w:
-        w.program_latency(rounds, 64, seed=5)
+@pytest.mark.parametrize("n,ln,maxp", [(4, 64, 64), (8, 64, 64), (32, 64, 64), (256, 64, 64), (4, 112, 112),
+                                        (8, 112, 112), (32, 112, 112), (256, 112, 112), (32, 64, 4096)])
+def test_latency_program(rlo, n, ln, maxp):
+    """The latency program (one bcast at a time: the doorbell path, fwd_small / ll_pass, carries every
+    message where the world has bells) at the world sizes the bench quotes p50 for, 64 B and the bell's
+    limit (112 B): per-rank delivery counts and checksums, and from a logged run every delivery's tree
+    parent and payload bytes, against the oracle (_bc_forward rootless_ops.c:1104-1225)"""
+    rounds, seed = 64, 5
+    with rlo.World(n, max_payload=maxp) as w:
+        if maxp <= 112:
+            assert w.info["waves"] == 8 and w.info["ll_ok"] == 1, w.info  # the bench's small-world shape
+        w.program_latency(rounds, ln, seed=seed)
         w.run()
         lat = w.latencies_ticks()
         rt = w.round_ticks().astype(np.int64)
         st = w.stats()
-    assert (st["error"] == 0).all()
+        w.program_latency(rounds, ln, seed=seed, log=True)
+        w.run()
+        st2 = w.stats()
+        logs = [w.log(r, cap=rounds + 8, payload=True) for r in range(n)]
+    assert (st["error"] == 0).all() and (st2["error"] == 0).all()
     assert len(lat) == rounds and (lat > 0).all()
     seen = rt[rt > 0]  # rank 0's clock at each completion it saw
     assert len(seen) >= rounds - 1 and (np.diff(seen) >= 0).all()
-    org = [orc.origin_of(5, i, n) for i in range(rounds)]
-    assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]
+    ref = orc.storm(n, seed, rounds, ln, want_parent=True)  # bcast i of round i, from origin_of(seed, i, n)
+    for s in (st, st2):
+        assert np.array_equal(s["bcast_delivered"].astype(np.int64), ref["count"])
+        assert np.array_equal(s["bcast_sum"], ref["sum"])
+    for r in range(n):
+        rows, payload = logs[r]
+        got = sorted((row[4], row[2], row[3]) for row in rows if row[0] == LOG_DELIVER)
+        want = sorted((b, orc.origin_of(seed, b, n), int(ref["parent"][b, r])) for b in range(rounds)
+                      if orc.origin_of(seed, b, n) != r)
+        assert got == want, r
+        for row in rows:
+            assert row[5] == ln and bytes(payload[row[8]][:ln]) == orc.payload(row[2], row[4], ln), (r, row)

@@ -70,7 +70,7 @@ def test_host_bcast_matches_oracle(rlo, n, k, ln, maxp):
     assert (st["originated"] == k).all()
 
 
-def _run_iar(rlo, n, proposals, decline, pool=1):
+def _run_iar(rlo, n, proposals, decline, pool=1, pend_hbm=False):
     """proposals: (origin, pid, data); at most `pool` per origin (pool 1: one own proposal per engine,
     rootless_ops.c:241; more: the proposal pool, :30 -- all submitted at once, the kernel keeps up
     to `pool` in flight and holds the rest in the command ring)."""
@@ -103,7 +103,8 @@ def _run_iar(rlo, n, proposals, decline, pool=1):
         else:
             raise AssertionError(ev)
 
-    with rlo.HostWorld(n, max_payload=256, pool=pool) as hw:
+    with rlo.HostWorld(n, max_payload=256, pool=pool, pend_hbm=pend_hbm) as hw:
+        assert hw.world.info["pend_hbm"] == (1 if pend_hbm else hw.world.info["pend_hbm"])
         hw_ref.append(hw)
         for o, pid, data in proposals:
             hw.propose(o, pid, data)
@@ -115,17 +116,21 @@ def _run_iar(rlo, n, proposals, decline, pool=1):
     return judge, actions, pickups, results
 
 
+@pytest.mark.parametrize("pend_hbm", [False, True])
 @pytest.mark.parametrize("n,origins,mask_ranks,per,pool", [(8, [1], [4], 1, 1), (8, [0, 3, 5, 6], [], 1, 1),
                                                            (16, [0, 5, 9, 15], [6, 12], 1, 1),
                                                            (64, list(range(0, 64, 5)), [7, 33], 1, 1),
                                                            (256, [0, 77, 128, 255], [3], 1, 1),
                                                            (8, [0, 3, 5, 6], [], 12, 4), (16, [0, 5, 9, 15], [6, 12], 20, 16),
                                                            (64, list(range(0, 64, 7)), [7, 33], 6, 8)])
-def test_host_iar_matches_oracle(rlo, n, origins, mask_ranks, per, pool):
+def test_host_iar_matches_oracle(rlo, n, origins, mask_ranks, per, pool, pend_hbm):
+    """pend_hbm: the same with the pending-proposal tables in HBM (the 8-GPU world's layout)"""
+    if pend_hbm and n not in (16, 256):
+        pytest.skip("HBM tables: two worlds suffice")
     decline = np.zeros(n, dtype=np.uint8)
     decline[mask_ranks] = 1
     props = [(o, 1000 + i * n + o, ("proposal-%d-from-%d" % (i, o)).encode()) for i in range(per) for o in origins]
-    judge, actions, pickups, results = _run_iar(rlo, n, props, decline, pool=pool)
+    judge, actions, pickups, results = _run_iar(rlo, n, props, decline, pool=pool, pend_hbm=pend_hbm)
     cfg, keep = orc.judge_cfg(orc.ORC_JUDGE_MASK, decline=decline)
     ev = orc.iar(n, props, cfg, pool=pool if per > 1 else 0)
     assert not [e for e in ev if e[0] == orc.ORC_EV_ERROR]
@@ -137,3 +142,38 @@ def test_host_iar_matches_oracle(rlo, n, origins, mask_ranks, per, pool):
     assert sorted(actions) == want_a
     assert sorted(pickups) == want_p
     assert sorted(results) == want_r
+
+
+def test_host_relaunch_replays_nothing(rlo):
+    """a relaunched host-service world must not take the previous launch's command
+    doorbells for new commands.  Launch 1 posts two bcasts (doorbell slots 0 and 1 hold tags 1 and 2)
+    and quits; launch 2 must deliver nothing until the host posts, then exactly what it posts."""
+    import time
+
+    n, ln = 8, 48
+    with rlo.HostWorld(n, max_payload=64) as hw:
+        for i, o in enumerate((0, 5)):
+            assert hw.bcast(o, orc.payload(o, i, ln), seq=i)
+        got = {r: [] for r in range(n)}
+        t0 = time.time()
+        while sum(len(v) for v in got.values()) < 2 * (n - 1) and time.time() - t0 < 20:
+            for r in range(n):
+                got[r] += hw.poll(r)
+        assert sum(len(v) for v in got.values()) == 2 * (n - 1)
+        hw.relaunch()
+        time.sleep(0.3)
+        for r in range(n):
+            assert hw.poll(r) == [], r  # a replayed command would deliver here
+        assert hw.bcast(3, orc.payload(3, 7, ln), seq=7)
+        got = {r: [] for r in range(n)}
+        t0 = time.time()
+        while sum(len(v) for v in got.values()) < n - 1 and time.time() - t0 < 20:
+            for r in range(n):
+                got[r] += hw.poll(r)
+        time.sleep(0.1)
+        for r in range(n):
+            got[r] += hw.poll(r)
+            if r == 3:
+                assert got[r] == [], got[r]
+            else:
+                assert [(e["origin"], e["id"], e["payload"][:ln]) for e in got[r]] == [(3, 7, orc.payload(3, 7, ln))], r

@@ -162,25 +162,29 @@ def test_iar_sharded_processes(rlo):
     assert (st["actions"] == (n - 1) * p).all()
 
 
-def _check_lat(st, n, rounds, seed):
+def _check_lat(st, n, rounds, seed, ln=64):
     assert (st["error"] == 0).all(), (st["error"], st["error_aux"])
     org = [orc.origin_of(seed, i, n) for i in range(rounds)]
     assert [int(x) for x in st["bcast_delivered"]] == [sum(o != r for o in org) for r in range(n)]
+    # the bytes every rank picked up (the doorbell path carries them): checksums vs the oracle
+    assert np.array_equal(st["bcast_sum"], orc.storm(n, seed, rounds, ln)["sum"])
     rt = st["round_ticks"].astype(np.int64)
     seen = rt[rt > 0]
     # world rank 0 saw (nearly) every round complete, on its own clock, in order
     assert len(seen) >= rounds - 1 and (np.diff(seen) >= 0).all()
 
 
-@pytest.mark.parametrize("n,bounds", [(32, [0, 16, 32]), (64, [0, 10, 40, 64])])
-def test_latency_sharded_inprocess(rlo, n, bounds):
+@pytest.mark.parametrize("n,bounds,ln", [(32, [0, 16, 32], 64), (64, [0, 10, 40, 64], 64), (8, [0, 4, 8], 112),
+                                         (256, [0, 128, 256], 64), (256, [0, 100, 256], 112)])
+def test_latency_sharded_inprocess(rlo, n, bounds, ln):
     """Latency program over parts: the round word and counts are part 0's, peer-mapped."""
     from rlo import sharded
 
     rounds, seed = 64, 5
-    (st, _, _), rcs = sharded.run_inprocess(n, bounds, {"kind": "lat", "rounds": rounds, "len": 64, "seed": seed})
+    (st, _, _), rcs = sharded.run_inprocess(n, bounds, {"kind": "lat", "rounds": rounds, "len": ln, "seed": seed},
+                                            max_payload=ln)
     assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
-    _check_lat(st, n, rounds, seed)
+    _check_lat(st, n, rounds, seed, ln)
 
 
 def test_latency_sharded_processes(rlo):
