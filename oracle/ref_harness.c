@@ -330,11 +330,14 @@ static void mode_pool(int per, unsigned mask) {
  * the rank whose attach fails): every rank must get NULL back, promptly (the leaders stop their kernels);
  * then the process builds a second engine and runs mode_parents on it. */
 static void mode_parents(int len);
+int rlo_dropin_test_fault(int what, int rank); /* librootless_ops.so test hook (not in rootless_ops.h) */
 static void mode_setupfail(int len) {
+    const char* fa = getenv("RLO_FAULT_ATTACH");
+    if (fa) rlo_dropin_test_fault(1, atoi(fa));
     RLO_engine_t* e = RLO_progress_engine_new(MPI_COMM_WORLD, RLO_MSG_SIZE_MAX, NULL, NULL, NULL);
     emit("{\"ev\":\"first\",\"rank\":%d,\"ok\":%d}", g_rank, e != NULL);
     if (e) RLO_progress_engine_cleanup(e);
-    unsetenv("RLO_FAULT_ATTACH");
+    rlo_dropin_test_fault(1, -1);
     MPI_Barrier(MPI_COMM_WORLD);
     mode_parents(len);
 }

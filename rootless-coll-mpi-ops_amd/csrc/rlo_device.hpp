@@ -123,16 +123,21 @@ struct RankTopo {
 // rank forwards on its own -- a lone ring message, a local origination -- is also written, data-tagged,
 // into the child's DOORBELL for the edge: one per directed edge (both virtual channels), kBellChunks
 // 16-B chunks (header + 112 B) as 32-B pairs of LL granules {d0, T, d1, T}, {d2, T, d3, T} where
-// T = (ring sequence + 1) | vc << 31.  Every 8-byte half carries T, so a reader that finds T in all of
+// T = bell_tag(ring sequence) | vc << 31.  Every 8-byte half carries T, so a reader that finds T in all of
 // them holds the message, whatever order the halves landed in (MI355X_MICROARCH.md handoff-1to1: the
 // data is the flag).  The consumer polls the bell beside its ring counters: a bell tagged with the
 // sequence at its ring head IS the head message -- no counter poll, no slot load, no producer drain on
 // the hop.  The ring slot and the counter are still written (a bell is overwritten by the next message
 // on the edge; whatever the consumer does not take from a bell it takes through the counter), so the
 // batched path is unchanged.  A vote bell (child -> parent) is one granule pair {origin | pseq << 16 |
-// vote << 24, T, pid, T}, T = vote sequence + 1.  Bells live in the ctrl region: uncached, mapped
+// vote << 24, T, pid, T}, T = bell_tag(vote sequence).  Bells live in the ctrl region: uncached, mapped
 // across parts, zeroed at every launch (a tag of a previous launch can never match).
 constexpr uint32_t kBellChunks = 8;
+// the data tag of the s-th message (0-based) of a forward edge, a vote ring or a command ring: never 0 (a
+// zeroed bell matches nothing) and 30 bits wide, so a forward bell's bit 31 carries only the virtual channel
+// -- after 2^31 messages on one edge a vc-0 tag could otherwise read as vc 1.  Tags of one bell
+// repeat every 2^30 messages, far beyond the <= 4,096 a ring holds in flight
+__host__ __device__ inline uint32_t bell_tag(uint64_t s) { return ((uint32_t)s & 0x3fffffffu) + 1u; }
 constexpr uint32_t kBellWords = 2 * kBellChunks * 2;  // 8-byte words per forward bell (256 B)
 
 struct RankStats {
@@ -320,15 +325,15 @@ constexpr int kJctlTilesDone = 36, kJctlGatherWaited = 38, kJctlGatherPassed = 3
               kJctlFault = 47, kJctlWords = 48;
 
 // stripe / chunk / tile plan of a bulk message: a pure function of (N, len, cross-GPU), so every
-// rank derives the same one.  Chunks pipeline the scatter into the all-gather: the gather of chunk c
-// runs while chunk c + 1 is scattered (cross: parts span GPUs -> ~sqrt(len / 4 MiB) chunks; one GPU:
-// 4-MiB chunks from 8 MiB on, where the messages are long enough for the overlap to pay).  A tile (what
+// rank derives the same one.  One GPU: the direct plan (one stripe = the message, fanned out).  Across
+// GPUs (and RLO_PART_CHUNKED): chunks pipeline the scatter into the all-gather, the gather of chunk c
+// running while chunk c + 1 is scattered, ~sqrt(len / 4 MiB) chunks.  A tile (what
 // one mover claim moves, then one release + flag add) is the stripe cut to <= 64 KiB, or to <= 16 KiB
 // for messages under 8 MiB: a mover workgroup stores ~20 GB/s into uncached HBM, so a message is fast
 // only when many movers share it -- short ones are latency bound and want many small tiles, long ones
 // large tiles so the per-tile release stays a small share.
 constexpr uint32_t kBulkTileMax = 64u << 10, kBulkTileSmall = 16u << 10;
-constexpr uint32_t kBulkChunk1 = 4u << 20;  // one GPU: chunk size, from 2 chunks' worth on
+constexpr uint32_t kBulkChunk1 = 4u << 20;  // chunked plan: ~sqrt(len / kBulkChunk1) chunks; 64-KiB tiles from 2x this
 // a VERIFY job (a receiver's read of its whole copy) is cut into 64-KiB tiles, independent of the
 // stripe plan: many movers read a copy at once (at N = 64 a stripe-sized tile made ~63 tiles per copy)
 constexpr uint32_t kVerifyTile = 64u << 10;
@@ -366,12 +371,7 @@ __host__ __device__ inline BulkPlan bulk_plan(int n, uint32_t len, bool cross) {
         return p;
     }
     uint32_t k = 1;
-    if (cross) {
-        while ((uint64_t)(k + 1) * (k + 1) * (4ull << 20) <= len && k < (uint32_t)kBulkMaxChunks) k++;
-    } else if (len >= 2 * kBulkChunk1) {
-        k = len / kBulkChunk1;
-        if (k > (uint32_t)kBulkMaxChunks) k = (uint32_t)kBulkMaxChunks;
-    }
+    while ((uint64_t)(k + 1) * (k + 1) * kBulkChunk1 <= len && k < (uint32_t)kBulkMaxChunks) k++;
     const uint32_t m = (uint32_t)(n - 1);
     const uint64_t per = ((uint64_t)len + k - 1) / k;
     uint64_t stripe = ((per + m - 1) / m + kBulkKiB - 1) / kBulkKiB * kBulkKiB;

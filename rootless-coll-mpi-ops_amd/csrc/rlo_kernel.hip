@@ -475,7 +475,7 @@ __device__ __forceinline__ void emit_vote(SH& S, const Params& P, int me, uint32
         return;
     }
     if (LLB && (P.mode & MODE_LL)) {  // {origin | pseq << 16 | vote << 24, T, pid, T}: every 8-B half tagged
-        const uint32_t T = (uint32_t)p + 1u;
+        const uint32_t T = bell_tag(p);
         uint64_t* b = reinterpret_cast<uint64_t*>(S.t.vout_bell[k]);
         const uint64_t w0 = (uint64_t)(((uint32_t)origin & 0xffffu) | ((pseq & 0xffu) << 16) | ((uint32_t)(vote & 0xff) << 24)) |
                             ((uint64_t)T << 32);
@@ -1376,7 +1376,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
 
     // a small message (lane q: slot chunk q, q < nch) into out-rings `need` at their tails: the ring slot,
-    // and with bells the child's doorbell for the edge, tagged (ring sequence + 1) | vc << 31.  The
+    // and with bells the child's doorbell for the edge, tagged bell_tag(ring sequence) | vc << 31.  The
     // caller advances out_tail_r
     auto fwd_small = [&](u32x4 v, uint32_t nch, uint32_t need) {
         const uint32_t q = (uint32_t)lane;
@@ -1386,7 +1386,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
             if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
             if (LL && llm && nch <= kBellChunks && q < nch) {
-                const uint32_t T = ((uint32_t)slot + 1u) | ((uint32_t)(oi & 1) << 31);
+                const uint32_t T = bell_tag(slot) | ((uint32_t)(oi & 1) << 31);
                 const __amdgpu_buffer_rsrc_t rb = mk_rsrc(reinterpret_cast<void*>(uni64(t.out_bell[oi >> 1])), kBellWords * 8u);
                 st_ring(rb, 32u * q, u32x4{v.x, T, v.y, T}, sys);
                 st_ring(rb, 32u * q + 16u, u32x4{v.z, T, v.w, T}, sys);
@@ -1638,9 +1638,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (lane < sll) *reinterpret_cast<uint2*>(stage + kLLBellVote + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
         const uint32_t lcap = min(nsmall, kBellChunks);
-        // in-ring (k, vc) whose head is h expects (h + 1) | vc << 31 in every half of every granule
-        const uint32_t e0 = (uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk)) + 1u;
-        const uint32_t e1 = ((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk + 1u)) + 1u) | 0x80000000u;
+        // in-ring (k, vc) whose head is h expects bell_tag(h) | vc << 31 in every half of every granule
+        const uint32_t e0 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk)));
+        const uint32_t e1 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk + 1u))) | 0x80000000u;
         const bool inb = (int)bk < n_in;
         const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
         const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
@@ -1648,7 +1648,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint64_t gm = hn <= lcap ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
         const bool g0 = bq == 0u && gm && (B0 & gm) == gm, g1 = bq == 0u && gm && (B1 & gm) == gm;
         const uint64_t fh = __ballot(g0 || g1), fv = __ballot(g1);  // bit 8k: in-edge k's bell is whole (on vc fv)
-        const uint32_t evh = (uint32_t)vin_head_r + 1u;
+        const uint32_t evh = bell_tag(vin_head_r);
         const uint64_t vhm = __ballot(lane < sll && vb.y == evh && vb.w == evh);
         const int rk = lane >> 1;
         const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
@@ -1667,8 +1667,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 ncmd = ct > hh ? (uint32_t)min(ct - hh, (uint64_t)kLLCmds) : 0u;
                 if (!ncmd && hpw) {
                     // the tail shows nothing new: the next command may be whole in its doorbell already, as wave 1
-                    // copied it (a seqlock: S.cseq = its sequence + 1 before and after the copy is read)
-                    const uint32_t T = (uint32_t)hh + 1u;
+                    // copied it (a seqlock: S.cseq = its tag before and after the copy is read)
+                    const uint32_t T = bell_tag(hh);
                     const uint32_t s1 = (uint32_t)uni((int)*reinterpret_cast<volatile uint32_t*>(&S.cseq));
                     if (s1 == T) {
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2073,7 +2073,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if (lane == 16 || lane == 17) S.hp[lane - 16] = hv;
                 // whole: every 8-byte half of its chunks (lanes 2q, 2q + 1 = chunk q) carries hh + 1.  Then its
                 // words go to LDS under the seqlock S.cseq (0 while they are rewritten), once per command
-                const uint32_t T = (uint32_t)hh + 1u;
+                const uint32_t T = bell_tag(hh);
                 const uint64_t tok = __ballot(lane < 16 && cv.y == T && cv.w == T);
                 const uint32_t cn = (kHdr + (rdl32(cv.x, 1) & 0xffffu) + 15u) >> 4;  // header word 2: length
                 const uint64_t cm = (1ull << (2u * min(cn, kBellChunks))) - 1ull;

@@ -72,7 +72,7 @@ struct ShmLayout {
 
 // Command doorbells: a command of at most kBellChunks 16-B chunks (header + 112 B) is also written,
 // data-tagged, into the doorbell slot of its sequence number -- the forward doorbells' format
-// (rlo_device.hpp): chunk q as two LL granule pairs {d0, T, d1, T}, {d2, T, d3, T}, T = sequence + 1,
+// (rlo_device.hpp): chunk q as two LL granule pairs {d0, T, d1, T}, {d2, T, d3, T}, T = bell_tag(sequence),
 // every 8-byte half one atomic CPU store.  The kernel polls the slot of the next command it expects and
 // takes the command from there when every half of its chunks carries T: one PCIe read instead of a tail
 // poll followed by a slot load.  The ring slot and the tail are still written (the full path and longer
@@ -80,7 +80,7 @@ struct ShmLayout {
 constexpr uint32_t kLLCmdSlot = kBellChunks * 32u;
 inline void ll_cmd_put(uint8_t* slot, uint64_t seq, const uint32_t hdr[4], const void* payload, uint32_t len) {
     if (kHdr + len > kBellChunks * 16u) return;  // longer commands: the ring slot only
-    const uint64_t T = (uint64_t)(uint32_t)(seq + 1u) << 32;
+    const uint64_t T = (uint64_t)bell_tag(seq) << 32;
     uint32_t w[kBellChunks * 4] = {0};
     for (int i = 0; i < 4; i++) w[i] = hdr[i];
     if (len) __builtin_memcpy(reinterpret_cast<uint8_t*>(w) + kHdr, payload, len);

@@ -128,6 +128,7 @@ namespace {
 
 progress_engine* g_engines = nullptr;  // Active_Engines (:40)
 int g_engines_ever = 0;
+int g_fault_attach_rank = -1;  // rlo_dropin_test_fault
 std::vector<RLO_msg_t*> g_pool;         // recycled received messages
 
 int64_t now_ns() {
@@ -960,10 +961,10 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     setup_trace(e->rank, "launched+started");
     if (ok) {  // members map their ranks through the leader's segment
         MPI_Bcast(shm_name, (int)sizeof shm_name, MPI_CHAR, 0, e->group);
-        // RLO_FAULT_ATTACH=r (fault injection for tests): rank r's attach fails, after every kernel was
-        // launched -- the path on which the leaders must stop their serving kernels cleanly
-        const char* fa = std::getenv("RLO_FAULT_ATTACH");
-        if (fa && std::atoi(fa) == e->rank) shm_name[1] = '!';
+        // fault injection, armed only by a test calling rlo_dropin_test_fault (no environment switch in the
+        // product library): rank r's attach fails after every kernel was launched -- the path on which the
+        // leaders must stop their serving kernels cleanly
+        if (g_fault_attach_rank >= 0 && g_fault_attach_rank == e->rank) shm_name[1] = '!';
         rc = rlo_client_attach(shm_name, e->rank, &e->cl);
         ok = agree(rc == RLO_OK);
         if (e->leader) rlo_host_unlink(e->w);  // every client attached (or gave up): drop the name
@@ -1011,6 +1012,14 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
 }  // namespace
 
 extern "C" {
+
+// test hook (tests/test_gpu_dropin.py::test_engine_setup_failure_is_clean through oracle/ref_harness.c):
+// what 1 = the next engine setup's attach of `rank` fails; rank -1 disarms.  Not in the reference API
+int rlo_dropin_test_fault(int what, int rank) {
+    if (what != 1) return -1;
+    g_fault_attach_rank = rank;
+    return 0;
+}
 
 RLO_engine_t* RLO_progress_engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb_func, void* app_ctx,
                                       void* app_proposal_action) {
