@@ -174,8 +174,12 @@ def _check_lat(st, n, rounds, seed, ln=64):
     assert len(seen) >= rounds - 1 and (np.diff(seen) >= 0).all()
 
 
+# (256 ranks fill the GPU, one 8-wave rank-workgroup per CU, and a launch deals its workgroups round-robin
+# over the 8 XCDs of 32 CUs: uneven parts must split on multiples of 8 ranks, or an XCD is dealt 33 of them
+# and the last workgroups wait for a CU forever -- [0, 100, 256] did, a placement limit of the one-GPU
+# rehearsal, not of the protocol: on 8 GPUs every part has a GPU of its own)
 @pytest.mark.parametrize("n,bounds,ln", [(32, [0, 16, 32], 64), (64, [0, 10, 40, 64], 64), (8, [0, 4, 8], 112),
-                                         (256, [0, 128, 256], 64), (256, [0, 100, 256], 112)])
+                                         (256, [0, 128, 256], 64), (256, [0, 96, 256], 112)])
 def test_latency_sharded_inprocess(rlo, n, bounds, ln):
     """Latency program over parts: the round word and counts are part 0's, peer-mapped."""
     from rlo import sharded
