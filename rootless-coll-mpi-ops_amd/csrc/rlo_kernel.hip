@@ -3192,8 +3192,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (qb >= nq) { qb -= nq; rb++; }
                     const uint32_t ea = OL(oi, r);
                     const uint32_t eb = i + 64u < b ? (uint32_t)OL(oi, rb) : (uint32_t)kBigFlag;
+#ifdef RLO_AB_HDRONLY  // A/B probe (wrong bytes by design): forward header + one chunk only, as pulled payloads would
+                    const bool va = !(ea & kBigFlag) && q < min(2u, (ea >> 9) & 0x3fu);
+                    const bool vb = !(eb & kBigFlag) && qb < min(2u, (eb >> 9) & 0x3fu);
+#else
                     const bool va = !(ea & kBigFlag) && q < ((ea >> 9) & 0x3fu);
                     const bool vb = !(eb & kBigFlag) && qb < ((eb >> 9) & 0x3fu);
+#endif
                     u32x4 xa = {0u, 0u, 0u, 0u}, xb = {0u, 0u, 0u, 0u};
                     if (va) xa = *reinterpret_cast<const u32x4*>(stage + __umul24(ea & 0x1ffu, stg_msg) + (q << 4));
                     if (vb) xb = *reinterpret_cast<const u32x4*>(stage + __umul24(eb & 0x1ffu, stg_msg) + (qb << 4));
