@@ -3187,6 +3187,35 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
                 uint32_t i = a + (uint32_t)lane;
                 uint32_t r = div_small(i, qmagic), q = i - r * nq;
+#ifdef RLO_AB_G2U4  // A/B: four items per round (their olist reads, then their stage reads, then the stores)
+                for (; i < b; i += 256u) {
+                    uint32_t rr[4], qq[4], e[4];
+                    rr[0] = r;
+                    qq[0] = q;
+#pragma unroll
+                    for (int u = 1; u < 4; u++) {
+                        rr[u] = rr[u - 1] + dr;
+                        qq[u] = qq[u - 1] + dq;
+                        if (qq[u] >= nq) { qq[u] -= nq; rr[u]++; }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) e[u] = i + 64u * u < b ? (uint32_t)OL(oi, rr[u]) : (uint32_t)kBigFlag;
+                    u32x4 x[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const bool v = !(e[u] & kBigFlag) && qq[u] < ((e[u] >> 9) & 0x3fu);
+                        x[u] = u32x4{0u, 0u, 0u, 0u};
+                        if (v) x[u] = *reinterpret_cast<const u32x4*>(stage + __umul24(e[u] & 0x1ffu, stg_msg) + (qq[u] << 4));
+                        e[u] = v ? 1u : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (e[u]) st_ring(ro, __umul24((s0 + rr[u]) & fcap_m, stride) + (qq[u] << 4), x[u], sys);
+                    r = rr[3] + dr;
+                    q = qq[3] + dq;
+                    if (q >= nq) { q -= nq; r++; }
+                }
+#else
                 for (; i < b; i += 128u) {
                     uint32_t rb = r + dr, qb = q + dq;
                     if (qb >= nq) { qb -= nq; rb++; }
@@ -3208,6 +3237,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     q = qb + dq;
                     if (q >= nq) { q -= nq; r++; }
                 }
+#endif
             }
             if (admitted && !isbig && kind == K_RING && tag == TAG_BCAST) {  // pickup: checksum (+ log payload)
                 const uint32_t nch = (kHdr + len + 15u) >> 4;

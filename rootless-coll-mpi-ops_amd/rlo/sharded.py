@@ -99,30 +99,33 @@ def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
 
 
 def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, blob_q, blobs_q, barrier, out_q,
-            world_kw):
+            world_kw, repeat=1):
     try:
         from .world import World
 
-        w = World.part(n, len(bounds) - 1, part, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
-                       device=device, uncached=uncached, **world_kw)
-        blob_q.put((part, w.export()))
-        blobs = blobs_q.get(timeout=120)
-        w.connect(blobs)
-        _program(w, spec)
-        w.reset()
-        barrier.wait(timeout=120)  # every part is reset before any part launches
-        w.launch(no_reset=True)
-        rc = w.wait(raise_on_device_error=False)
-        res = _collect(w, spec)
-        barrier.wait(timeout=120)  # no peer still stores into this part's rings
-        w.close()
-        out_q.put((part, rc, res, None))
+        for it in range(repeat):
+            w = World.part(n, len(bounds) - 1, part, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
+                           device=device, uncached=uncached, **world_kw)
+            blob_q.put((part, w.export()))
+            blobs = blobs_q.get(timeout=120)
+            w.connect(blobs)
+            _program(w, spec)
+            w.reset()
+            barrier.wait(timeout=120)  # every part is reset before any part launches
+            w.launch(no_reset=True)
+            rc = w.wait(raise_on_device_error=False)
+            res = _collect(w, spec)
+            barrier.wait(timeout=120)  # no peer still stores into this part's rings
+            w.close()
+            out_q.put((part, rc, res, None))
     except Exception as e:  # report instead of hanging the parent
         out_q.put((part, -99, None, repr(e)))
 
 
 def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None, uncached=False, timeout=300,
-                  **world_kw):
+                  repeat=1, **world_kw):
+    """repeat > 1: every part process creates, connects (hipIpc), runs and destroys the world `repeat` times
+    in a row -- the per-leg churn of bench.py's N-part run; returns the list of per-repeat results"""
     parts = len(bounds) - 1
     devices = devices or [0] * parts
     ctx = mp.get_context("spawn")
@@ -130,21 +133,25 @@ def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
     blobs_qs = [ctx.Queue() for _ in range(parts)]
     barrier = ctx.Barrier(parts)
     procs = [ctx.Process(target=_worker, args=(n, bounds, p, devices[p], spec, max_payload, ring_slots, uncached,
-                                               blob_q, blobs_qs[p], barrier, out_q, world_kw)) for p in range(parts)]
+                                               blob_q, blobs_qs[p], barrier, out_q, world_kw, repeat))
+             for p in range(parts)]
     for p in procs:
         p.start()
+    runs = []
     try:
-        got = dict(blob_q.get(timeout=timeout) for _ in range(parts))
-        blobs = [got[p] for p in range(parts)]
-        for q in blobs_qs:
-            q.put(blobs)
-        outs = [out_q.get(timeout=timeout) for _ in range(parts)]
+        for _ in range(repeat):
+            got = dict(blob_q.get(timeout=timeout) for _ in range(parts))
+            blobs = [got[p] for p in range(parts)]
+            for q in blobs_qs:
+                q.put(blobs)
+            outs = [out_q.get(timeout=timeout) for _ in range(parts)]
+            errs = [(p, e) for p, rc, r, e in outs if e]
+            if errs:
+                raise RuntimeError("part failed: %s" % errs)
+            runs.append((merge([r for _, _, r, _ in outs]), [rc for _, rc, _, _ in sorted(outs, key=lambda x: x[0])]))
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    errs = [(p, e) for p, rc, r, e in outs if e]
-    if errs:
-        raise RuntimeError("part failed: %s" % errs)
-    return merge([r for _, _, r, _ in outs]), [rc for _, rc, _, _ in sorted(outs, key=lambda x: x[0])]
+    return runs[0] if repeat == 1 else runs
