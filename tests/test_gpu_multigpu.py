@@ -105,15 +105,17 @@ def test_bulk_world_churn_processes(rlo):
         for r in range(n):
             if r != o:
                 want[r] += cs
-    for (st, _, _), rcs in runs:
-        assert rcs == [0, 0], (st["error"], st["error_aux"])
-        assert np.array_equal(st["bcast_sum"], want)
+    for it, ((st, _, _), rcs) in enumerate(runs):
+        assert rcs == [0, 0], (it, st["error"], st["error_aux"])
+        assert np.array_equal(st["bcast_sum"], want), it
     k = 256
     runs = sharded.run_processes(16, [0, 8, 16], {"kind": "storm", "k": k, "len": 64, "seed": seed}, max_payload=64,
                                  uncached=True, repeat=3)
     ref = orc.storm(16, seed, k, 64)
-    for (st, _, _), rcs in runs:
-        assert rcs == [0, 0] and np.array_equal(st["bcast_sum"], ref["sum"])
+    for it, ((st, _, _), rcs) in enumerate(runs):
+        bad = [(r, int(st["error"][r]), hex(int(st["error_aux"][r]))) for r in range(16) if st["error"][r]]
+        assert rcs == [0, 0], (it, rcs, bad)
+        assert np.array_equal(st["bcast_sum"], ref["sum"]), it
 
 
 def _merged(recs, name):
