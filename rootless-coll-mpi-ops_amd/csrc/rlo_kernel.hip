@@ -144,7 +144,7 @@ struct Shared {
     uint32_t wcnt[kWaves][kMaxOut];
     uint32_t first_bad[kGroups];
     CandL cand[kMaxCand];
-    uint16_t pos[kMaxCand][kMaxFanout];  // large messages: slot in out-ring (j, vc) relative to tail0
+    alignas(16) uint16_t pos[kMaxCand][kMaxFanout];  // admitted message c: its slot in out-ring (j, vc) - out_tail0
     uint16_t big[kMaxCand];              // admitted messages too large for the stage path
     uint32_t nbig, bm, bq0, nblk;
     uint32_t blk_c[128], blk_q0[128];    // large-message blocks staged in stage2 (two halves when pipelined)
@@ -1227,6 +1227,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // costs, so the fewer groups per byte the better; one unit where registers are short (8 waves)
     constexpr uint32_t kSubMax = W == 4 ? 4u : 1u;
     constexpr uint32_t kPair = W == 4 ? 2u : 1u;  // units in registers at once
+    // phase G2's copy loop: message-major (a wave's own messages, every out-ring from the same registers), or
+    // ring-major through the olist in the doorbell kernels (no registers to spare)
+#ifdef RLO_AB_OLDG2  // A/B: the ring-major copy loop everywhere
+    constexpr bool kG2Own = false;
+#else
+    constexpr bool kG2Own = !LL;
+#endif
     const uint32_t s2_units = P.stage2_bytes >> 10;
 #define STG(c, q) (stage + (((uint32_t)(c) * nsmall + (uint32_t)(q)) << 4))
 #define OL(oi, r) olist[(uint32_t)(oi) * (uint32_t)kMaxCand + (uint32_t)(r)]
@@ -2847,8 +2854,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint64_t b = __ballot(bit);
                 if (bit) {
                     const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
-                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 9)));  // c < 512: 9 bits; nch <= 63: 6 bits
-                    if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
+                    S.pos[c][oi >> 1] = (uint16_t)rel;  // (a message goes to child j on one virtual channel)
+                    if constexpr (!kG2Own)  // the doorbell kernels' copy loop walks the rings (G2 below)
+                        OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 9)));  // c < 512: 9 bits; nch <= 63: 6 bits
                 }
             }
             const uint64_t amask = __ballot(admitted);
@@ -3164,9 +3172,76 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 ACQ_NEXT();
             }
 
+            if constexpr (kG2Own) {
+            // ---------------- G2: small messages.  A wave copies ITS OWN admitted messages: lane = one (message,
+            // 16-B chunk) item, read from the stage once and stored from the same registers into every out-ring the
+            // message goes to, at out_tail0[oi] + pos[c][oi >> 1] (phase E) -- the message's whole pos row read with
+            // the chunk, so a round of 64 items waits for LDS once, whatever the fan-out; the pickup checksum rides
+            // the same pass.  Consecutive lanes hold consecutive chunks of consecutive messages, and consecutive
+            // messages of a wave going to out-ring oi take consecutive slots of it: every store instruction writes
+            // contiguous slot bytes.  (The ring-major walk below, kept for the doorbell kernels, took two dependent
+            // LDS reads per item and ~30 instructions per 2 items: ~800 cycles per 128 items, the whole copy phase of
+            // a wall rank -- storing 60 % fewer bytes took no time off it, profiles/r4_storm_ab.txt)
+                const uint32_t nq = max(S.nchmax, 1u);  // items per message: the largest small message
+                const uint32_t qmagic = nq > 1 ? 0xFFFFFFFFu / nq + 1u : 0u;
+                const uint32_t stg_msg = nsmall << 4, stride = P.fwd_stride;
+                const bool smsg = admitted && !isbig;
+                const bool pick = smsg && kind == K_RING && tag == TAG_BCAST;  // delivered here: checksummed
+                const uint32_t an_s = smsg ? an : 0u;
+                const uint32_t nch_l = (kHdr + len + 15u) >> 4;
+                const uint64_t wm = __ballot(an_s != 0u || pick);
+                if (wm) {
+                    // the out-rings' start tails and bases lane-distributed (lane oi), read per store with v_readlane
+                    const uint32_t s0_r = lane < nout ? (uint32_t)S.out_tail0[lane] : 0u;  // mod fwd_cap (pow2)
+                    const uint64_t ob_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;
+                    const uint32_t nit = (64u - (uint32_t)__builtin_clzll(wm)) * nq;
+                    for (uint32_t i0 = 0; i0 < nit; i0 += 64u) {
+                        const uint32_t i = i0 + (uint32_t)lane;
+                        const uint32_t r = min(div_small(i, qmagic), 63u), q = i - r * nq;
+                        const uint32_t need_i = (uint32_t)__shfl((int)an_s, (int)r);
+                        const uint32_t nch_i = (uint32_t)__shfl((int)nch_l, (int)r);
+                        const bool pick_i = __shfl((int)pick, (int)r) != 0;
+                        const bool v = i < nit && q < nch_i && (need_i != 0u || pick_i);
+                        const uint32_t cc = (uint32_t)w * 64u + r;
+                        u32x4 x = {0u, 0u, 0u, 0u}, p0 = {0u, 0u, 0u, 0u}, p1 = {0u, 0u, 0u, 0u};
+                        const uint32_t nd = v ? need_i : 0u;
+                        if (v) x = *reinterpret_cast<const u32x4*>(stage + __umul24(cc, stg_msg) + (q << 4));
+                        if (nd) {
+                            p0 = *reinterpret_cast<const u32x4*>(&S.pos[cc][0]);
+                            p1 = *reinterpret_cast<const u32x4*>(&S.pos[cc][8]);
+                        }
+                        const uint32_t um = wave_or(nd);  // the out-rings this round stores into
+#pragma unroll
+                        for (int oi = 0; oi < kMaxOut; oi++) {
+                            if ((um >> oi) & 1u) {  // uniform
+                                const int j = oi >> 1;
+                                const uint32_t pw = j < 8 ? (j < 2 ? (j == 0 ? p0.x : p0.x) : j < 4 ? p0.y : j < 6 ? p0.z : p0.w)
+                                                          : (j < 10 ? p1.x : j < 12 ? p1.y : j < 14 ? p1.z : p1.w);
+                                const uint32_t pv = (j & 1) ? (pw >> 16) : (pw & 0xffffu);
+                                if ((nd >> oi) & 1u) {
+                                    const uint32_t slot = (rdl32(s0_r, oi) + pv) & fcap_m;
+                                    st_ring(mk_rsrc(reinterpret_cast<void*>(rdl64(ob_r, oi)), oring_bytes),
+                                            __umul24(slot, stride) + (q << 4), x, sys);
+                                }
+                            }
+                        }
+                        if (v && pick_i)  // the reference's pickup of a bcast (:938-979): its bytes, checksummed
+                            acc_sum += q == 0u ? chunk_mix(0xFFFFFFFFu, u32x4{x.x & 0xffffu, x.y, TAG_BCAST, x.z & 0xffffu})
+                                               : chunk_mix(q - 1u, x);
+                    }
+                }
+                if ((P.mode & MODE_LOG) && pick && logidx != ~0u)  // parity logs: the delivered payload bytes
+                    for (uint32_t q = 1; q < nch_l; q++)
+                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + logidx) * P.log_stride + 16u * (q - 1),
+                                 *reinterpret_cast<const u32x4*>(STG(c, q)));
+            } else {
             // ---------------- G2: small messages.  Out-ring oi (oi = w, w + 4, ...) receives its
             // admitted messages' staged slots as contiguous (message, chunk) items
+#ifdef RLO_AB_NQ2  // A/B probe (wrong bytes by design): the copy loop walks 2 chunks per message
+            const uint32_t nq = min(max(S.nchmax, 1u), 2u);
+#else
             const uint32_t nq = max(S.nchmax, 1u);  // items per message: the largest small message
+#endif
             const uint32_t qmagic = nq > 1 ? 0xFFFFFFFFu / nq + 1u : 0u;
             // the (out-ring, message, chunk) items of all out-rings form one sequence split evenly over
             // the four waves (a rank whose traffic sits on every other out-ring -- rank 0 sends on the
@@ -3248,6 +3323,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (logidx != ~0u)
                         st_sys16(P.log_payload + ((size_t)lr * P.log_cap + logidx) * P.log_stride + 16u * (q - 1), v);
                 }
+            }
+
             }
 
             // ---------------- G3: large messages, 64 x 16 B per wave store instruction.  The out-rings'
