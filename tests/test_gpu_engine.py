@@ -186,6 +186,33 @@ def test_storm_pulled_payloads_small_rings(rlo, n, ln, slots, pull):
     assert np.array_equal(st["bcast_sum"], exp["sum"])
 
 
+@pytest.mark.parametrize("n,ln,slots", [(256, 256, 0), (64, 200, 32), (32, 368, 16), (256, 112, 0), (16, 250, 16)])
+def test_storm_small_pulled_medium_slots(rlo, n, ln, slots):
+    """medium slots (the small copy path, <= 24 chunks) in pull worlds: a storm message going to >= 3 children
+    crosses those edges as header + reference to the sender's relay copy, and the receiver loads the payload
+    chunks from there into its stage (phase D0) -- the wall ranks' copy volume.  Every delivery's parent
+    and bytes at every rank, and every rank's checksum, against the oracle; small rings (16/32 slots) put
+    the relay release records under pressure"""
+    k, seed = (4096 if n >= 64 else 3000), 29
+    with rlo.World(n, max_payload=ln, ring_slots=slots) as w:
+        assert w.info["pull"] == (1 if (16 + ln + 15) // 16 > 8 else 0), w.info
+        w.program_storm(k, ln, seed=seed, window=64, log=True, log_cap=k + 8)
+        w.run()
+        st = w.stats()
+        logs = [w.log(r, cap=k + 8, payload=True) for r in range(n)]
+    ref = orc.storm(n, seed, k, ln, want_parent=True)
+    assert (st["error"] == 0).all(), st["error"]
+    assert np.array_equal(st["bcast_delivered"].astype(np.int64), ref["count"])
+    assert np.array_equal(st["bcast_sum"], ref["sum"])
+    for r in range(n):
+        rows, payload = logs[r]
+        got = sorted((row[4], row[2], row[3]) for row in rows if row[0] == LOG_DELIVER)
+        want = sorted((b, orc.origin_of(seed, b, n), int(ref["parent"][b, r])) for b in range(k) if orc.origin_of(seed, b, n) != r)
+        assert got == want, r
+        for row in rows:
+            assert bytes(payload[row[8]][:ln]) == orc.payload(row[2], row[4], ln), (r, row[2], row[4])
+
+
 def _iar_device(rlo, n, proposals, judge, mask=None, isp=None):
     with rlo.World(n) as w:
         w.program_iar(proposals, judge=judge, mask=mask, isp=isp, log=True, log_cap=4096)

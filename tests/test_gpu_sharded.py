@@ -70,6 +70,19 @@ def test_storm_sharded_inprocess_full_size(rlo):
     _check_storm(st, logs, n, k, ln, seed, False)
 
 
+@pytest.mark.parametrize("n,bounds,ln", [(64, [0, 24, 64], 256), (256, [0, 128, 256], 256)])
+def test_storm_sharded_small_pulled(rlo, n, bounds, ln):
+    """medium slots over parts: small pulled messages whose relay copy sits in another part (the receiver loads
+    it through the peer mapping)"""
+    from rlo import sharded
+
+    k, seed = 4 * n, 31
+    spec = {"kind": "storm", "k": k, "len": ln, "seed": seed, "log": True, "log_cap": k + 8}
+    (st, logs, _), rcs = sharded.run_inprocess(n, bounds, spec, max_payload=ln, uncached=True)
+    assert rcs == [0] * (len(bounds) - 1), (st["error"], st["error_aux"])
+    _check_storm(st, logs, n, k, ln, seed, True)
+
+
 def test_storm_sharded_uncached_rings(rlo):
     """The allocation used when parts sit on different GPUs (uncached), exercised on one GPU."""
     from rlo import sharded
