@@ -219,8 +219,7 @@ struct Params {
     // write it into their own relay ring if they forward it on), and a relay slot is reused only after
     // every child consumed the references written up to it (a release queue on the out-ring heads).
     // A wall rank then stores header + reference per child instead of the whole payload per child.
-    uint32_t pull, relay_cap;     // pull: bit 0 large messages, bit 1 small-path ones of fan-out >= kPullFan (storm);
-                                  // relay slots per rank (power of two)
+    uint32_t pull, relay_cap;     // relay slots per rank (power of two)
     // outputs
     RankStats* stats;             // [n_local]
     LogRec* log;                  // [n_local * log_cap]

@@ -179,7 +179,6 @@ struct Shared {
     // records: relay count rq_relay[e] is released once every out-ring's consumer passed rq_out[e][oi]
     uint64_t relay_tail, relay_rel;
     uint32_t relay_n, ref_any, rq_n, rq_h, relay_free;
-    uint32_t nrelay_s;  // this iteration's relay slots taken by small pulled messages (the first ones: phase E)
     uint64_t rq_relay[kRelQ];
     uint64_t rq_out[kRelQ][kMaxOut];
     // counters
@@ -333,12 +332,6 @@ static constexpr uint32_t kSlotMark = 0xA5u;
 // chunk is the reference {byte offset of the sender's relay slot in the sender's part, ~offset, kRefMagic, 0}
 static constexpr uint32_t kRefMark = 0x5Au;
 static constexpr uint32_t kRefMagic = 0x52454631u;  // "REF1": reference chunk = {off, ~off, magic, 0}
-// pull worlds, storm program: a SMALL-path bcast going to at least kPullFan children is pulled too -- its header
-// + reference (2 chunks) to each child, its slot once into my relay ring -- instead of pushed whole to each.
-// What a wall rank's copy phase costs is its store instructions (one per 64 (message, chunk) items), so this
-// is what a wall rank, forwarding ~7 copies of every bcast, saves (RLO_AB_NQ2 probe: walking 2 chunks per
-// message took 35 % off the 256-B storm, profiles/r4_storm_ab.txt)
-static constexpr int kPullFan = 3;
 
 __device__ __forceinline__ uint32_t mask_bytes(uint32_t w, int keep) {  // keep the low `keep` bytes
     return keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
@@ -1225,11 +1218,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         pend = (PendState*)(__attribute__((address_space(1))) PendState*)(P.pend_hbm + (size_t)blockIdx.x * (uint32_t)P.n * P.pend_slots);
     else
         pend = reinterpret_cast<PendState*>(dyn_lds);
-    uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + pend_bytes);       // [oi][256]; row nout: my relay ring
-    uint8_t* stage = dyn_lds + pend_bytes + (P.nout_max + 1u) * (2u * kMaxCand);  // [message][q] x 16 B
-    // pull worlds: a small pulled message's header (kRefMark) + reference, what its children get [message] x 32 B
-    [[maybe_unused]] uint8_t* const refstg = stage + (uint32_t)kMaxCand * nsmall * 16u;
-    uint8_t* stage2 = refstg + (PULL_ON && (P.pull & 2u) ? (uint32_t)kMaxCand * 32u : 0u);  // [block][lane] x 16 B
+    uint16_t* olist = reinterpret_cast<uint16_t*>(dyn_lds + pend_bytes);       // [oi][256]
+    uint8_t* stage = dyn_lds + pend_bytes + P.nout_max * (2u * kMaxCand);      // [message][q] x 16 B
+    uint8_t* stage2 = stage + (uint32_t)kMaxCand * nsmall * 16u;                    // [block][lane] x 16 B
     // large messages move in groups of up to kSubMax 1-KiB units (64 payload chunks, one per lane) of
     // one message, packed into stage2: a 4-KiB payload is one group of four units, a 1-KiB payload one
     // group of one unit.  The per-group work (LDS metadata, out-ring walk) is what a staging round
@@ -1313,7 +1304,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0; S.hwait = 0;
             S.hp[0] = 0; S.hp[1] = 0; S.a_done = 0; S.cseq = 0;
             S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
-            S.nrelay_s = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0; S.b.npost = 0;
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
@@ -2571,74 +2561,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if (i < nit) *reinterpret_cast<u32x4*>(STG(c_lo, 0) + (i << 4)) = sv[u];
                     }
                 }
-                if constexpr (W == 4 && !BULK) {
-                    // small pulled messages (kPullFan): what came is the header (kRefMark) + a reference to the
-                    // sender's relay slot; the payload chunks 1 .. nch-1 are loaded from there now (sc1, behind the
-                    // same counter poll that released the reference: the sender drained its relay stores before
-                    // publishing), into the stage, and the header's mark restored -- from here on the message is
-                    // an ordinary small one (forwarded, picked up, checksummed from the stage).  A reference that is
-                    // not one is a device error.  The sender reuses the relay slot only after this rank's head
-                    // passed the reference (RelQ records), i.e. after these loads
-                    if ((P.pull & 2u) && (P.mode & MODE_STORM)) {
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staged slots
-                        bool isr = false;
-                        uint32_t roff = 0, rn = 0;
-                        int rk = 0;
-                        if (cc < c_hi) {
-                            const u32x4 h = *reinterpret_cast<const u32x4*>(STG(cc, 0));
-                            const uint32_t rl = h.z & 0xffffu, nch = (kHdr + rl + 15u) >> 4;
-                            if (((h.z >> 16) & 0xffu) == kRefMark && ((h.x >> 16) & 0xffu) == TAG_BCAST && nch <= nsmall) {
-                                const u32x4 rc = *reinterpret_cast<const u32x4*>(STG(cc, 1));
-                                if (rc.y == ~rc.x && rc.z == kRefMagic && nch >= 2u) {
-                                    isr = true;
-                                    roff = rc.x;
-                                    rn = nch;
-                                    rk = (int)(S.cand[cc].group >> 1);
-                                } else {
-                                    set_error(S, P, ERR_BAD_SLOT, 0x5EF1000u | (cc & 0xfffu));
-                                }
-                            }
-                        }
-                        for (uint64_t rm = __ballot(isr); rm;) {  // per producer (in-edge k), uniform
-                            const int k = __shfl(rk, __builtin_ctzll(rm));
-                            const bool mine = isr && rk == k;
-                            const uint64_t km = __ballot(mine);
-                            rm &= ~km;
-                            // lane m <- the lane of this producer's m-th pulled message (ds_permute pushes)
-                            const uint32_t rank_l = (uint32_t)__popcll(km & lt_mask);
-                            const int inv = __builtin_amdgcn_ds_permute((int)(mine ? rank_l : 63u) << 2, lane);
-                            const __amdgpu_buffer_rsrc_t rr = mk_rsrc(reinterpret_cast<void*>(uni64(t.in_base[k])), 0xFFFFFFF0u);
-                            const uint32_t per = nsmall - 1u, pmag = per > 1u ? 0xFFFFFFFFu / per + 1u : 0u;
-                            const uint32_t nrit = (uint32_t)__popcll(km) * per;
-                            for (uint32_t i0 = 0; i0 < nrit; i0 += 512u) {
-                                u32x4 pv[8];
-                                uint32_t pd[8];
-#pragma unroll
-                                for (int u = 0; u < 8; u++) {
-                                    pd[u] = ~0u;
-                                    if (i0 + (uint32_t)u * 64u < nrit) {  // uniform: every lane takes part in the shuffles
-                                        const uint32_t i = i0 + (uint32_t)u * 64u + (uint32_t)lane;
-                                        const uint32_t m = div_small(i, pmag), q = 1u + (i - m * per);
-                                        const int sl = __shfl(inv, (int)(m & 63u));
-                                        const uint32_t so = (uint32_t)__shfl((int)roff, sl), sn = (uint32_t)__shfl((int)rn, sl);
-                                        if (i < nrit && q < sn) {
-                                            pv[u] = sys ? ld_sys(rr, so + 16u * q) : ld_sc1(rr, so + 16u * q);
-                                            pd[u] = ((c_lo + (uint32_t)sl) * nsmall + q) << 4;
-                                        }
-                                    }
-                                }
-                                VM_DRAIN();
-#pragma unroll
-                                for (int u = 0; u < 8; u++)
-                                    if (pd[u] != ~0u) *reinterpret_cast<u32x4*>(stage + pd[u]) = pv[u];
-                            }
-                        }
-                        if (isr) {  // an ordinary small message from here on
-                            uint32_t* hz = reinterpret_cast<uint32_t*>(STG(cc, 0)) + 2;
-                            *hz = (*hz & 0xff00ffffu) | (kSlotMark << 16);
-                        }
-                    }
-                }
             }
             VM_DRAIN();  // wave 1: its vote loads
             PST(1, 7);
@@ -2909,33 +2831,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t mx = wave_max(admitted && !isbig ? (kHdr + len + 15u) >> 4 : 0u);
                 if (lane == 0 && mx) atomicMax(&S.nchmax, mx);
             }
-            // small pulled messages (kPullFan): a slot of my relay ring each, the first of this iteration's (large
-            // pulled messages take theirs in phase F), listed in olist row nout in slot order; their children's
-            // header + reference written to refstg now
-            uint32_t srly = ~0u;
-            if constexpr (W == 4 && !BULK) {
-                if ((P.pull & 2u) && (P.mode & MODE_STORM)) {
-                    const bool sp = admitted && !isbig && ((w0 >> 16) & 0xffu) == TAG_BCAST && (kind == K_RING || kind == K_STORM) &&
-                                    __builtin_popcount(an) >= kPullFan && nch_s >= 2u;
-                    const uint64_t bm = __ballot(sp);
-                    if (bm) {
-                        uint32_t rb0 = 0;
-                        if (lane == 0) {
-                            rb0 = atomicAdd(&S.relay_n, (uint32_t)__popcll(bm));
-                            atomicAdd(&S.nrelay_s, (uint32_t)__popcll(bm));
-                        }
-                        rb0 = rdl32(rb0, 0);
-                        const uint32_t rb = rb0 + (uint32_t)__popcll(bm & lt_mask), rfree = S.relay_free;
-                        if (sp && rb < rfree) {
-                            srly = t.orig_data + (uint32_t)((S.relay_tail + rb) & (P.relay_cap - 1u)) * P.fwd_stride;
-                            *reinterpret_cast<u32x4*>(refstg + ((uint32_t)c << 5)) = u32x4{w0, id, (w2 & 0xff00ffffu) | (kRefMark << 16), t0};
-                            *reinterpret_cast<u32x4*>(refstg + ((uint32_t)c << 5) + 16u) = u32x4{srly, ~srly, kRefMagic, 0u};
-                            OL(nout, rb) = (uint16_t)(c | (nch_s << 9));  // the whole slot into my relay ring
-                        }
-                        if (lane == 0 && rb0 < rfree) S.ref_any = 1;
-                    }
-                }
-            }
             BAR();
             uint32_t pre_r = 0;  // lane oi: slots of out-ring oi taken by lower waves
             if (lane < nout) {
@@ -2953,8 +2848,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint64_t b = __ballot(bit);
                 if (bit) {
                     const uint32_t rel = rdl32(pre_r, oi) + (uint32_t)__popcll(b & lt_mask);
-                    // c < 512: 9 bits; nch <= 63: 6 bits; a small pulled message (4 waves: c < 256): bit 8 + 2 chunks
-                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : srly != ~0u ? (0x100u | (2u << 9)) : (nch_s << 9)));
+                    OL(oi, rel) = (uint16_t)(c | (isbig ? kBigFlag : (nch_s << 9)));  // c < 512: 9 bits; nch <= 63: 6 bits
                     if (isbig) S.pos[c][oi >> 1] = (uint16_t)rel;
                 }
             }
@@ -3291,9 +3185,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // from a wave's own messages (each chunk read once) took 20 % / 50 % more (fewer lanes per store)
             const uint32_t dr = div_small(64u, qmagic), dq = 64u - dr * nq;
             const uint32_t stg_msg = nsmall << 4, stride = P.fwd_stride;
-            // (pull worlds: lane nout = my relay ring, the slots of this iteration's small pulled messages)
-            const uint32_t nrs = PULL_ON ? min(S.nrelay_s, S.relay_free) : 0u;
-            const uint32_t nit_r = lane < nout ? S.n_oi[lane] * nq : (lane == nout ? nrs * nq : 0u);
+            const uint32_t nit_r = lane < nout ? S.n_oi[lane] * nq : 0u;
             uint32_t items = 0;
             const uint32_t ibase_r = wave_excl_scan(nit_r, &items);
             const uint32_t lo = items * (uint32_t)w / (uint32_t)kWaves, hi = items * (uint32_t)(w + 1) / (uint32_t)kWaves;
@@ -3301,17 +3193,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const int oi = __builtin_ctzll(mo);
                 const uint32_t ib = rdl32(ibase_r, oi), ie = ib + rdl32(nit_r, oi);
                 const uint32_t a = max(lo, ib) - ib, b = min(hi, ie) - ib;  // this wave's items of ring oi
-                const bool rly = PULL_ON && oi == nout;  // my relay ring (uniform)
-                uint32_t s0 = 0, smask = fcap_m, obase = 0;  // slot arithmetic mod the ring's slots (pow2)
-                __amdgpu_buffer_rsrc_t ro = rf;
-                if (rly) {
-                    s0 = (uint32_t)S.relay_tail;
-                    smask = P.relay_cap - 1u;
-                    obase = t.orig_data;
-                } else {
-                    s0 = (uint32_t)S.out_tail0[oi];
-                    ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
-                }
+                const uint32_t s0 = (uint32_t)S.out_tail0[oi];  // slot arithmetic mod fwd_cap (pow2)
+                const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
                 uint32_t i = a + (uint32_t)lane;
                 uint32_t r = div_small(i, qmagic), q = i - r * nq;
                 for (; i < b; i += 256u) {
@@ -3331,17 +3214,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     for (int u = 0; u < 4; u++) {
                         const bool v = !(e[u] & kBigFlag) && qq[u] < ((e[u] >> 9) & 0x3fu);
                         x[u] = u32x4{0u, 0u, 0u, 0u};
-                        if (v) {
-                            if (W == 4 && (e[u] & 0x100u))  // a small pulled message: header + reference (refstg)
-                                x[u] = *reinterpret_cast<const u32x4*>(refstg + ((e[u] & 0xffu) << 5) + (qq[u] << 4));
-                            else
-                                x[u] = *reinterpret_cast<const u32x4*>(stage + __umul24(e[u] & 0x1ffu, stg_msg) + (qq[u] << 4));
-                        }
+                        if (v) x[u] = *reinterpret_cast<const u32x4*>(stage + __umul24(e[u] & 0x1ffu, stg_msg) + (qq[u] << 4));
                         e[u] = v ? 1u : 0u;
                     }
 #pragma unroll
                     for (int u = 0; u < 4; u++)
-                        if (e[u]) st_ring(ro, obase + __umul24((s0 + rr[u]) & smask, stride) + (qq[u] << 4), x[u], sys);
+                        if (e[u]) st_ring(ro, __umul24((s0 + rr[u]) & fcap_m, stride) + (qq[u] << 4), x[u], sys);
                     r = rr[3] + dr;
                     q = qq[3] + dq;
                     if (q >= nq) { q -= nq; r++; }
@@ -3515,7 +3393,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (qn < (uint32_t)kRelQ) S.rq_n = qn + 1u;
                 }
                 S.relay_n = 0;
-                S.nrelay_s = 0;
                 S.ref_any = 0;
             }
             if (lane < nout) {

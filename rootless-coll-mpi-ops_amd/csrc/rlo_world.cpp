@@ -226,8 +226,7 @@ int build_layout(int n, int nparts, const int32_t* pb, uint32_t max_payload, uin
     // storm 37.6 -> 35.8 ms, 4 KiB 86.8 -> 79.3 ms, profiles/r2s5_sizes_groups_ab.txt)
     {
         const char* pe = std::getenv("RLO_PULL");
-        // (round 4: medium slots too -- their storms pull the small-path messages of high fan-out, kPullFan)
-        const bool want = pe ? std::atoi(pe) != 0 : L.stride / 16u > 8u;
+        const bool want = pe ? std::atoi(pe) != 0 : L.stride / 16u > 24u;
         L.pull = want && L.stride > 8u * 16u && !bulk_max;
     }
     if (L.pull)
@@ -507,10 +506,8 @@ int plan_variant(const Layout& L, int nl, int nmov, int cus, int variant, bool p
     // bcast/s, profiles/r2s2_diag_sizes.log); large slots stage 5 chunks -- header + 64 B -- and leave the
     // LDS to the large-message rounds (4 KiB storm 109 -> 104 ms, 1 KiB 40.4 -> 38.4, r2s4_nsmall_ab.txt)
     const uint32_t ns = ns_force ? ns_force : (L.stride / 16u <= 24u ? L.stride / 16u : 5u);
-    // [pending proposals N x pend_slots x 16 B][olist (2 maxfan + 1) x cand x 2 B][stage cand x ns x 16 B]
-    // [pull, 4 waves: refstg cand x 32 B][stage2][bulk pending]
-    const size_t refstg = variant == 4 && L.pull && L.stride / 16u <= 24u ? cand * 32 : 0;  // Params.pull bit 1
-    const size_t fixed = stat + ptab + (size_t)(2 * L.max_fan + 1) * cand * 2 + cand * ns * 16 + refstg + bpend;
+    // [pending proposals N x pend_slots x 16 B][olist 2 maxfan x cand x 2 B][stage cand x ns x 16 B][stage2][bulk pending]
+    const size_t fixed = stat + ptab + (size_t)2 * L.max_fan * cand * 2 + cand * ns * 16 + bpend;
     if (per_block < fixed + 1024 + 512) return RLO_E_OCCUPANCY;
     size_t s2 = std::min<size_t>(128 * 1024, (per_block - fixed - 512) & ~(size_t)1023);  // two halves of <= 64 blocks
     const int vph = variant | (pend_hbm && variant != 5 ? kVariantPH : 0);
@@ -1028,9 +1025,7 @@ static void base_params(rlo_world* w) {
     P.ring_cap = w->L.stride - rlo::kHdr;
     P.pend_slots = w->L.pend_slots;
     P.pend_hbm = reinterpret_cast<rlo::PendState*>(w->pend_mem);
-    // the reference chunk is staged as chunk 1; bit 1: small-path messages of medium slots are pulled too (the
-    // storm program; their refstg block in LDS, plan_variant)
-    P.pull = w->L.pull && w->nsmall >= 2 ? (1u | (w->variant == 4 && w->L.stride / 16u <= 24u ? 2u : 0u)) : 0u;
+    P.pull = w->L.pull && w->nsmall >= 2 ? 1u : 0u;  // the reference chunk is staged as chunk 1
     P.relay_cap = w->L.relay_cap;
     P.own_pool = 1;  // one own proposal per engine (rootless_ops.c:241) unless a program asks for more
     if (w->L.bulk_max) {

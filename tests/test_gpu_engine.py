@@ -187,15 +187,12 @@ def test_storm_pulled_payloads_small_rings(rlo, n, ln, slots, pull):
 
 
 @pytest.mark.parametrize("n,ln,slots", [(256, 256, 0), (64, 200, 32), (32, 368, 16), (256, 112, 0), (16, 250, 16)])
-def test_storm_small_pulled_medium_slots(rlo, n, ln, slots):
-    """medium slots (the small copy path, <= 24 chunks) in pull worlds: a storm message going to >= 3 children
-    crosses those edges as header + reference to the sender's relay copy, and the receiver loads the payload
-    chunks from there into its stage (phase D0) -- the wall ranks' copy volume.  Every delivery's parent
-    and bytes at every rank, and every rank's checksum, against the oracle; small rings (16/32 slots) put
-    the relay release records under pressure"""
+def test_storm_medium_slots_logged(rlo, n, ln, slots):
+    """medium slots (<= 24 chunks: the small copy path of the 4-wave kernel, four items per copy round) and
+    the 8-wave kernel's largest slot (112 B): every delivery's parent and bytes at every rank, and every
+    rank's checksum, against the oracle; small rings (16/32 slots) keep the copy rounds' ring wrap busy"""
     k, seed = (4096 if n >= 64 else 3000), 29
     with rlo.World(n, max_payload=ln, ring_slots=slots) as w:
-        assert w.info["pull"] == (1 if (16 + ln + 15) // 16 > 8 else 0), w.info
         w.program_storm(k, ln, seed=seed, window=64, log=True, log_cap=k + 8)
         w.run()
         st = w.stats()

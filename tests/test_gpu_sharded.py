@@ -71,9 +71,8 @@ def test_storm_sharded_inprocess_full_size(rlo):
 
 
 @pytest.mark.parametrize("n,bounds,ln", [(64, [0, 24, 64], 256), (256, [0, 128, 256], 256)])
-def test_storm_sharded_small_pulled(rlo, n, bounds, ln):
-    """medium slots over parts: small pulled messages whose relay copy sits in another part (the receiver loads
-    it through the peer mapping)"""
+def test_storm_sharded_medium_slots(rlo, n, bounds, ln):
+    """medium slots (the 4-wave small copy path) over parts, uncached as across GPUs"""
     from rlo import sharded
 
     k, seed = 4 * n, 31
