@@ -425,6 +425,9 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
                 # 2G S HBM bytes
                 rec["hbm_GBps"] = round(2 * G * nbytes / rt / 1e9, 1)
                 rec["hbm_frac"] = round(rec["hbm_GBps"] / HBM_PEAK_GBS, 4)
+                # the data movement alone, without the receivers' VERIFY read-back (the benchmark's own check):
+                # the origin's copy written and read once, G-1 receiver copies written -- (G+1) S
+                rec["hbm_frac_no_verify"] = round((G + 1) * nbytes / rt / 1e9 / HBM_PEAK_GBS, 4)
             if rank == 0:
                 note("bulk %d MiB: %.3f ms/round" % (mib, rt * 1e3))
             if nccl is not None:
