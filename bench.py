@@ -137,8 +137,9 @@ def pmc_traffic(ranks, length, k, device, timeout_s=120):
 
 
 def kfd_census():
-    """processes holding KFD (GPU) queues right now: /sys/class/kfd/kfd/proc/<pid>/queues (what the
-    GPU's hardware scheduler maps).  {pid: (comm, queues)}; unreadable entries are skipped"""
+    """processes holding KFD (GPU) queues right now: /sys/class/kfd/kfd/proc/<pid>/queues/<q>/gpuid (what the
+    GPUs' hardware schedulers map; DESIGN.md 4.2).  {pid: (comm, {gpuid: queues})}, every GPU of the node;
+    unreadable entries are skipped"""
     root = "/sys/class/kfd/kfd/proc"
     out = {}
     try:
@@ -146,44 +147,68 @@ def kfd_census():
     except OSError:
         return None
     for pid in pids:
+        qs = {}
         try:
-            nq = len(os.listdir(os.path.join(root, pid, "queues")))
+            for q in os.listdir(os.path.join(root, pid, "queues")):
+                try:
+                    g = open(os.path.join(root, pid, "queues", q, "gpuid")).read().strip()
+                except OSError:
+                    g = "?"
+                qs[g] = qs.get(g, 0) + 1
         except OSError:
             continue
         try:
             comm = open("/proc/%s/comm" % pid).read().strip()
         except OSError:
             comm = "?"
-        out[int(pid)] = (comm, nq)
+        out[int(pid)] = (comm, qs)
     return out
 
 
+def cpu_throttle():
+    """(nr_throttled, throttled_usec) of this cgroup (v2 cpu.stat): the box's CPU quota throttles spinning threads"""
+    try:
+        kv = dict(ln.split() for ln in open("/sys/fs/cgroup/cpu.stat"))
+        return int(kv.get("nr_throttled", 0)), int(kv.get("throttled_usec", 0))
+    except (OSError, ValueError):
+        return None
+
+
 def _run_sampled(cmd, timeout_s, env=None, period=0.05):
-    """run cmd; meanwhile sample the KFD census: the most processes seen holding queues at once, and the
-    ones that were not the leg's own (rlo_api_bench)"""
+    """run cmd; meanwhile sample the KFD census: on the GPU(s) the leg's own processes (rlo_api_bench) hold
+    queues on, the most processes holding queues at once and the other processes among them; and the CPU
+    quota throttling of this cgroup over the run"""
     import threading
 
-    stop, seen = threading.Event(), {"max_procs": 0, "max_queues": 0, "others": set(), "samples": 0}
+    stop = threading.Event()
+    seen = {"max_procs_our_gpu": 0, "others_our_gpu": set(), "our_gpuids": set(), "samples": 0}
 
     def sample():
         while not stop.is_set():
             c = kfd_census()
             if c is not None:
                 seen["samples"] += 1
-                busy = {p: v for p, v in c.items() if v[1] > 0}
-                seen["max_procs"] = max(seen["max_procs"], len(busy))
-                seen["max_queues"] = max(seen["max_queues"], sum(v[1] for v in busy.values()))
-                seen["others"].update("%s:%d" % (v[0], p) for p, v in busy.items() if v[0] != "rlo_api_bench")
+                ours = set(g for comm, qs in c.values() if comm == "rlo_api_bench" for g in qs)
+                seen["our_gpuids"] |= ours
+                on = {p: v for p, v in c.items() if any(g in seen["our_gpuids"] for g in v[1])}
+                seen["max_procs_our_gpu"] = max(seen["max_procs_our_gpu"], len(on))
+                seen["others_our_gpu"].update("%s:%d" % (v[0], p) for p, v in on.items() if v[0] != "rlo_api_bench")
             stop.wait(period)
 
     th = threading.Thread(target=sample, daemon=True)
+    t0 = cpu_throttle()
     th.start()
     try:
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20, env=env)
     finally:
         stop.set()
         th.join(timeout=2)
-    seen["others"] = sorted(seen["others"])[:8]
+    t1 = cpu_throttle()
+    if t0 and t1:
+        seen["cpu_throttled_periods"] = t1[0] - t0[0]
+        seen["cpu_throttled_ms"] = round((t1[1] - t0[1]) * 1e-3, 1)
+    seen["others_our_gpu"] = sorted(seen["others_our_gpu"])[:8]
+    seen["our_gpuids"] = sorted(seen["our_gpuids"])
     return r, seen
 
 
@@ -231,6 +256,8 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
                         res = json.loads(lines[-1]) if lines else {"error": "rc=%d" % r.returncode}
                         if name == "ours":
                             res["kfd"] = seen
+                        else:
+                            res["cpu_throttled_ms"] = seen.get("cpu_throttled_ms")
                     except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
                         res = {"error": str(e)[:200]}
                     runs[name].setdefault(leg, []).append(res)
@@ -249,9 +276,14 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
                 if "seconds" in good[0]:
                     med["runs_seconds"] = [x.get("seconds") for x in good]
                 if name == "ours":
-                    med["kfd_max_procs_with_queues"] = max(x["kfd"]["max_procs"] for x in good)
-                    med["kfd_other_procs"] = sorted(set(p for x in good for p in x["kfd"]["others"]))
+                    # the census of the GPU our rank processes used: processes holding queues on it at once
+                    # (ours: one leader per GPU), the other processes among them, the CPU quota's throttling
+                    med["kfd_max_procs_our_gpu"] = max(x["kfd"]["max_procs_our_gpu"] for x in good)
+                    med["kfd_others_our_gpu"] = sorted(set(p for x in good for p in x["kfd"]["others_our_gpu"]))
+                    med["runs_cpu_throttled_ms"] = [x["kfd"].get("cpu_throttled_ms") for x in good]
                     med.pop("kfd", None)
+                else:
+                    med["runs_cpu_throttled_ms"] = [x.get("cpu_throttled_ms") for x in good]
                 rec[name][leg] = med
         try:
             o, f = rec["ours"], rec["reference_host_mpi"]
