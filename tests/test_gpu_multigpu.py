@@ -92,7 +92,7 @@ def test_bulk_world_churn_processes(rlo):
     legs use no shared-memory names), and what differs between legs is exactly their churn: every leg
     creates, exports, maps, runs and destroys its world again, in both processes.  Here two part processes
     do that 6 times in a row with the bulk leg's world (uncached heaps, IPC-mapped across processes), then
-    3 times with a 16-rank storm world, and every repeat must map and deliver the oracle's bytes"""
+    6 times with a 16-rank storm world, and every repeat must map and deliver the oracle's bytes"""
     from rlo import sharded
 
     n, rounds, seed, ln = 4, 4, 33, (1 << 20) + 48
@@ -110,7 +110,7 @@ def test_bulk_world_churn_processes(rlo):
         assert np.array_equal(st["bcast_sum"], want), it
     k = 256
     runs = sharded.run_processes(16, [0, 8, 16], {"kind": "storm", "k": k, "len": 64, "seed": seed}, max_payload=64,
-                                 uncached=True, repeat=3)
+                                 uncached=True, repeat=6)
     ref = orc.storm(16, seed, k, 64)
     for it, ((st, _, _), rcs) in enumerate(runs):
         bad = [(r, int(st["error"][r]), hex(int(st["error_aux"][r]))) for r in range(16) if st["error"][r]]
