@@ -38,6 +38,8 @@ extern "C" {
 #define RLO_E_NOTCONNECTED (-7) /* part created but rlo_part_connect not called yet          */
 #define RLO_E_AGAIN (-8)     /* host-service ring full / nothing to do, retry after progress  */
 #define RLO_E_TIMEOUT (-9)   /* shared host service: the leader did not answer in time         */
+#define RLO_E_STALE (-10)    /* a peer part's memory, as mapped here, is not what that part holds now (an IPC
+                                mapping of an earlier allocation): rlo_part_connect checks every mapped region */
 
 /* device error codes (rlo_rank_stats_t.error) */
 #define RLO_DERR_TIMEOUT 1

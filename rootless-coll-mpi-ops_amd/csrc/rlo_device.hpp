@@ -32,6 +32,7 @@ constexpr int kHistBins = 128;    // latency histogram: 4 sub-bins per octave of
 constexpr int kMaxParts = 64;     // parts (processes x GPUs) of one world
 constexpr int kPoolMax = 16;      // own proposals in flight per rank (PROPOSAL_POOL_SIZE, rootless_ops.c:30)
 constexpr int kCtrlHdrWords = 16; // per-part control words before the rank blocks: [0] error flag
+constexpr int kCtrlNonceWord = 15;  // [15] the part's creation nonce (rlo_part_connect checks it; rlo_reset keeps it)
 // latency program of a world split over parts: the round word and the per-round delivery counts are
 // one world-wide copy in part 0's control region (peer-mapped like the ring counters), after its rank
 // blocks: [round word, own 128-B line][counts: kLatCap x u32]

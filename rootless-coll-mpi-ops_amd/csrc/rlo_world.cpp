@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstddef>
 #include <cstdio>
@@ -333,6 +334,7 @@ struct PartBlob {
     hipIpcMemHandle_t hf, hv, hc;
     uint64_t heap_ptr, bflag_ptr, heap_bytes, bflag_bytes;
     hipIpcMemHandle_t hh, hb;
+    uint64_t nonce;  // written at the start of every region at creation: a peer's mapping must show it
 };
 static_assert(sizeof(PartBlob) <= RLO_PART_BLOB_BYTES, "blob");
 constexpr uint32_t kBlobMagic = 0x524C4F50u;  // "RLOP"
@@ -406,6 +408,7 @@ struct rlo_world {
     uint32_t nsmall = 8, stage2 = 1024;
     bool ll_ok = false;  // the doorbell instantiation of the kernel is co-resident at this world's size
     bool pend_hbm = false;  // the pending-proposal tables in HBM (plan_lds), nl x N x pool x 16 B, uncached
+    uint64_t nonce = 0;     // this part's creation nonce (PartBlob.nonce)
     uint8_t* pend_mem = nullptr;
     int waves = 4;    // rank-workgroup width: 8 (512 candidates per iteration) when each rank has a CU
     int variant = 4;  // kernel instantiation: 8 / 4 waves, 5 = 4 waves with bulk messages
@@ -654,6 +657,7 @@ const char* rlo_strerror(int code) {
         case RLO_E_NOTCONNECTED: return "part not connected";
         case RLO_E_AGAIN: return "ring full, retry";
         case RLO_E_TIMEOUT: return "shared host service: no answer in time";
+        case RLO_E_STALE: return "a peer part's mapped memory is not that part's current memory (stale IPC mapping)";
         default: return "unknown";
     }
 }
@@ -772,6 +776,19 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     (void)hipMemset(w->vote, 0, std::max<uint64_t>(w->L.vote_bytes[me], 1));
     (void)hipMemset(w->ctrl, 0, w->L.ctrl_words[me] * 8);
     if (w->d_stats.alloc(w->nl)) { rlo_world_destroy(w); return RLO_E_HIP; }
+    {  // the creation nonce, in the regions a peer's rlo_part_connect reads it back from through its mapping
+       // (control header word kCtrlNonceWord, which rlo_reset keeps; the first word of the vote and heap
+       // regions, which no reset clears and only a launch -- after every part connected -- writes): a mapping
+       // that shows an earlier allocation fails the connection loudly instead of carrying messages into
+       // memory that is not this part's any more
+        static std::atomic<uint64_t> seq{0};
+        w->nonce = splitmix64(process_token() ^ (++seq * 0x9E3779B97F4A7C15ull) ^
+                              (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
+        if (!w->nonce) w->nonce = 1;
+        void* regs[3] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, w->heap};
+        for (void* r : regs)
+            if (r && hipMemcpy(r, &w->nonce, 8, hipMemcpyHostToDevice) != hipSuccess) { rlo_world_destroy(w); return RLO_E_HIP; }
+    }
     // the null stream only: another part's persistent kernel may already run on this device
     // (a second engine in the process), and a device-wide sync would wait for it forever
     (void)hipStreamSynchronize(nullptr);
@@ -795,6 +812,7 @@ int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap) {
     b.stride = w->L.stride;
     b.vote_cap = w->L.vote_cap;
     b.token = process_token();
+    b.nonce = w->nonce;
     b.fwd_ptr = (uint64_t)(uintptr_t)w->fwd;
     b.vote_ptr = (uint64_t)(uintptr_t)w->vote;
     b.ctrl_ptr = (uint64_t)(uintptr_t)w->ctrl;
@@ -875,6 +893,14 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
                 HIPCHK(hipIpcOpenMemHandle(&p, b.hb, hipIpcMemLazyEnablePeerAccess));
                 w->opened.push_back(p);
                 w->pbf[q] = (uint8_t*)p;
+            }
+            // every mapped region must show the peer's creation nonce (rlo_part_create)
+            const void* regs[3] = {w->pc[q] + rlo::kCtrlNonceWord, w->pv[q], L.bulk_max ? w->ph[q] : nullptr};
+            for (const void* r : regs) {
+                if (!r) continue;
+                uint64_t got = 0;
+                HIPCHK(hipMemcpy(&got, r, 8, hipMemcpyDeviceToHost));
+                if (got != b.nonce) return RLO_E_STALE;
             }
         }
     }
@@ -1541,7 +1567,9 @@ int rlo_reset(rlo_world_t* w, void* stream) {
         std::fill(w->cmd_tail.begin(), w->cmd_tail.end(), 0);
         std::fill(w->pk_head.begin(), w->pk_head.end(), 0);
     }
-    HIPCHK(hipMemsetAsync(w->ctrl, 0, w->L.ctrl_words[w->part] * 8, s));
+    // every control word but the creation nonce (a peer still connecting may read it)
+    HIPCHK(hipMemsetAsync(w->ctrl, 0, rlo::kCtrlNonceWord * 8, s));
+    HIPCHK(hipMemsetAsync(w->ctrl + rlo::kCtrlHdrWords, 0, (w->L.ctrl_words[w->part] - rlo::kCtrlHdrWords) * 8, s));
     // zeroed rings: a slot whose bytes are not visible yet reads without the header's slot mark
     // (rlo_device.hpp) and is reloaded, in every launch, not only in a fresh world
     HIPCHK(hipMemsetAsync(w->fwd, 0, w->L.fwd_bytes[w->part], s));
