@@ -138,6 +138,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 #define RLO_FLAG_LOG 1u  /* record every delivery / judge / action / result (+ payload bytes) */
 #define RLO_FLAG_HIST 2u /* per-delivery latency histogram                                  */
 #define RLO_FLAG_PROF 4u /* per-phase cycle accounting (diagnostic)                         */
+#define RLO_FLAG_TIMELINE 8u /* latency program: per-round event clocks (rlo_timeline; diagnostic, no path change) */
 
 #define RLO_ORDER_RANDOM 0u /* origin of bcast b = splitmix64(seed + b) % N                      */
 #define RLO_ORDER_SLOTS 1u  /* origin of bcast b = b % N: every rank originates in every "slot" of N
@@ -162,6 +163,13 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg);
  * rlo_round_ticks() (on the part holding world rank 0) returns the clock of world rank 0 when it
  * saw round i complete: successive differences are closed-loop round times on ONE clock. */
 int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags);
+
+/* RLO_FLAG_TIMELINE: the first min(rounds, 64) rounds' event clocks (low 32 bits of the 10-ns clock; 0 =
+ * not seen on this part), row r = [8 global events][arrival per local rank][bulk completion per local rank]:
+ * global 0 origination, 1 scatter job posted, 2 claimed by a mover, 3 moved (completion counts added),
+ * 4 round complete (last pickup), 5 last receiver's VERIFY done.  Copies rows * *stride words to out
+ * (cap words), returns the rows copied. */
+int rlo_timeline(rlo_world_t* w, uint32_t* out, uint64_t cap, uint32_t* stride);
 
 #define RLO_JUDGE_APPROVE 0u /* approve everything                                           */
 #define RLO_JUDGE_MASK 1u    /* decline iff mask[rank] != 0 (arg != NULL)                     */

@@ -32,7 +32,11 @@ constexpr int kHistBins = 128;    // latency histogram: 4 sub-bins per octave of
 constexpr int kMaxParts = 64;     // parts (processes x GPUs) of one world
 constexpr int kPoolMax = 16;      // own proposals in flight per rank (PROPOSAL_POOL_SIZE, rootless_ops.c:30)
 constexpr int kCtrlHdrWords = 16; // per-part control words before the rank blocks: [0] error flag
-constexpr int kCtrlNonceWord = 15;  // [15] the part's creation nonce (rlo_part_connect checks it; rlo_reset keeps it)
+constexpr int kCtrlNonceWord = 15;
+// MODE_TL timeline of a latency round: global events (the part where each happens writes it), then per local
+// rank the arrival of the round's message (or bulk announcement) and the completion of its bulk copy
+constexpr uint32_t kTlRoundsMax = 64, kTlGlobal = 8;
+enum TlEvent : uint32_t { TL_ORIGIN = 0, TL_POSTED = 1, TL_CLAIMED = 2, TL_MOVED = 3, TL_ROUND = 4, TL_VERIFIED = 5 };  // [15] the part's creation nonce (rlo_part_connect checks it; rlo_reset keeps it)
 // latency program of a world split over parts: the round word and the per-round delivery counts are
 // one world-wide copy in part 0's control region (peer-mapped like the ring counters), after its rank
 // blocks: [round word, own 128-B line][counts: kLatCap x u32]
@@ -58,6 +62,7 @@ enum Mode : uint32_t {
     MODE_HDIAG = 4096u,   // diagnostic, host mode: command-wait counters into hctl[kHctlDiag..] at exit
     MODE_PIPE = 8192u,    // A/B: large-message staging rounds pipelined over two halves of stage2
     MODE_LL = 16384u,     // doorbells (below): lone messages and originations hop without a counter round trip
+    MODE_TL = 32768u,     // latency program: per-round event clocks into Params.tl (RLO_FLAG_TIMELINE; no path changes)
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
 };
@@ -193,6 +198,8 @@ struct Params {
     uint64_t* lat_out;            // [lat_rounds] completion ticks
     uint32_t* lat_round;          // current round (global; part 0's control region when sharded)
     uint64_t* lat_obs;            // [lat_rounds] observer clock (world rank 0) when round i completed
+    uint32_t* tl;                 // MODE_TL: [tl_rounds][kTlGlobal + 2 n_local] low 32 bits of the 100-MHz clock
+    uint32_t tl_rounds;
     const uint32_t* lat_own_off;  // [n_local + 1] CSR of the rounds each local rank originates
     const uint32_t* lat_own;
     // IAR workload

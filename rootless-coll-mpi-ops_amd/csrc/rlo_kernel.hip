@@ -265,6 +265,11 @@ __device__ __forceinline__ uint32_t poll32(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+// MODE_TL: the clock of event `ev` of latency round r (rlo_device.hpp kTlGlobal; the latest writer wins)
+__device__ __forceinline__ void tl_mark(const Params& P, uint32_t r, uint32_t ev) {
+    if ((P.mode & MODE_TL) && r < P.tl_rounds)
+        atomicMax(&P.tl[r * (kTlGlobal + 2u * P.n_local) + ev], (uint32_t)now_ticks());
+}
 
 // per-ring state lives lane-distributed in registers; a wave-uniform index reads it with v_readlane
 __device__ __forceinline__ uint32_t rdl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
@@ -832,6 +837,7 @@ __device__ __forceinline__ void flush_posts(BulkSh& B, const Params& P, int lane
             __hip_atomic_store(dst, (uint64_t)(uint32_t)(j0 + u + 1u) | ((uint64_t)kind << 32), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        if (kind == JOB_SCATTER && lane == 0) tl_mark(P, (uint32_t)uni((int)r.bid), TL_POSTED);
     }
     if (lane == 0) B.npost = 0u;
 }
@@ -969,6 +975,7 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
         const uint32_t len = jb.len, s = jb.slot;
         const int o = jb.origin;
         const int me = P.rank_begin + jb.lr;
+        if (tid == 0 && jb.kind == JOB_SCATTER && jb.ti0 == 0u) tl_mark(P, jb.bid, TL_CLAIMED);
         const BulkPlan pl = bulk_plan(n, len, P.bulk_cross != 0);
         if (jb.kind == JOB_SCATTER && pl.direct) {
             // one GPU (direct plan): the sub-job's tiles are one contiguous range of the message -- moved as
@@ -994,6 +1001,7 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
             if (tid < 64) {
                 if (sys) bulk_release(true);
                 for (int d = 1 + tid; d < n; d += 64) bflag_add(bulk_flags(P, (o + d) % n, o, s) + (mi & 15u), jb.ntiles, sys);
+                if (tid == 0) tl_mark(P, jb.bid, TL_MOVED);
             }
         } else
         for (uint32_t ti = jb.ti0; ti < jb.ti0 + jb.ntiles; ti++) {
@@ -1172,6 +1180,7 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                                  u32x4{len, 0xffffffffu, (uint32_t)tot, (uint32_t)(tot >> 32)});
                     const uint32_t nt = n > 2 ? bulk_stripe_tiles(pl, len, (uint32_t)((me - o - 1 + n) % n)) : 0u;
                     bulk_slot_release(P, me, o, s, sys, bulk_total_tiles(pl, len) + nt, jb.bid);
+                    tl_mark(P, jb.bid, TL_VERIFIED);
                     __hip_atomic_store(&P.jdone[cls * P.jslots + ps], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&P.jsum[cls * P.jslots + ps], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1474,6 +1483,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (!ok) return ~0u;
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
+                tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
                 atomicAdd(&S.bcast_delivered, 1ull);
                 if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
                 flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
@@ -1522,6 +1532,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t e = (uint32_t)forg * bsl + sl;
                 const uint32_t nt = P.n > 2 ? bulk_stripe_tiles(pl, dlen, (uint32_t)((me - forg - 1 + P.n) % P.n)) : 0u;
                 if (lane == 0) {
+                    tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
                     const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
                     if ((ob >> (e & 31u)) & 1u) bulk_fault(P, 10, (e << 12) | (fid & 0xfffu));  // still live: announced twice
                     bpend[e] = BulkPend{fid, dlen, bulk_total_tiles(pl, dlen) + nt, ffrom, ft0, dq,
@@ -1551,6 +1562,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                                               __HIP_MEMORY_SCOPE_SYSTEM)
                                      : atomicAdd(&P.lat_count[fid], 1u);
             if (old + 1u == (uint32_t)(P.n - 1)) {
+                tl_mark(P, fid, TL_ROUND);
                 P.lat_out[fid] = (uint64_t)((uint32_t)now_ticks() - ft0);
                 if (sys) __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else __hip_atomic_store(P.lat_round, fid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1888,6 +1900,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (lat_go && originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), S.lat_own_next, P.len, 0u,
                                 out_head_r)) {
             if (lane == 0) {
+                tl_mark(P, S.lat_own_next, TL_ORIGIN);
                 atomicAdd(&S.originated, 1ull);
                 const uint32_t np = S.lat_pos + 1u;
                 S.lat_pos = np;
@@ -1904,6 +1917,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (originate(K_HOST, (uint32_t)me | (TAG_BULK << 16) | (0xffu << 24), id, 16u, kBellJudge, out_head_r)) {
                     if (lane == 0) {
+                        tl_mark(P, id, TL_ORIGIN);
                         atomicAdd(&S.originated, 1ull);
                         S.b.bulk_q = q + 1u;
                         const uint32_t np = S.lat_pos + 1u;
@@ -2173,6 +2187,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             if (host) {
                                 log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, sl);
                             } else {
+                                tl_mark(P, pe.bid, kTlGlobal + P.n_local + (uint32_t)lr);
                                 atomicAdd(&S.bcast_delivered, 1ull);
                                 const uint32_t li =
                                     log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
@@ -2184,6 +2199,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                                                      __HIP_MEMORY_SCOPE_SYSTEM)
                                             : atomicAdd(&P.lat_count[pe.bid], 1u);
                                     if (old + 1u == (uint32_t)(P.n - 1)) {
+                                        tl_mark(P, pe.bid, TL_ROUND);
                                         P.lat_out[pe.bid] = (uint64_t)((uint32_t)now_ticks() - pe.t0);
                                         if (sys) __hip_atomic_store(P.lat_round, pe.bid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                                         else __hip_atomic_store(P.lat_round, pe.bid + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2869,6 +2885,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             const uint64_t tn = now_ticks();
                             if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)tn - t0)], 1u);
                             if (P.mode & MODE_LAT) {  // round bookkeeping after the forwards are issued (G)
+                                tl_mark(P, id, kTlGlobal + (uint32_t)lr);
                                 lat_deliv = true;
                                 lat_tn = (uint32_t)tn - t0;
                             }
@@ -2940,6 +2957,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                               ((uint64_t)(from & 0xffff) << 16) | (pv.from & 0xffff)) == 0ull)
                                 bulk_fault(P, 12, (e << 12) | (id & 0xfffu));
                         }
+                        tl_mark(P, id, kTlGlobal + (uint32_t)lr);
                         const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
                         if ((ob >> (e & 31u)) & 1u) {  // still live: which message was, which one came
                             const BulkPend od = bpend[e];
@@ -2972,6 +2990,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     S.own_state[k] = 0;
                     S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
                 } else if (kind == K_LAT) {
+                    tl_mark(P, id, TL_ORIGIN);
                     const uint32_t np = S.lat_pos + 1u;
                     S.lat_pos = np;
                     S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
@@ -3339,6 +3358,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : atomicAdd(&P.lat_count[id], 1u);
                 if (old + 1u == (uint32_t)(P.n - 1)) {
+                    tl_mark(P, id, TL_ROUND);
                     P.lat_out[id] = (uint64_t)lat_tn;  // one clock only when the world is one part
                     if (sys) __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     else __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

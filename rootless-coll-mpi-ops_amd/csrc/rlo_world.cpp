@@ -378,6 +378,8 @@ struct rlo_world {
     DevBuf<uint32_t> d_lat_own_off, d_lat_own;
     DevBuf<int32_t> d_lat_origin, d_prop_pid;
     DevBuf<uint64_t> d_lat_out, d_lat_obs;
+    DevBuf<uint32_t> d_tl;  // RLO_FLAG_TIMELINE rows
+    uint32_t tl_rows = 0;
     DevBuf<uint8_t> d_mask, d_prop_data, d_log_payload;
     DevBuf<char> d_isp;
     DevBuf<rlo::LogRec> d_log;
@@ -427,6 +429,7 @@ struct rlo_world {
 
 namespace {
 
+constexpr uint64_t kNonceTail = 256;  // bytes past a region that hold its creation nonce (rlo_part_create)
 int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
     if (bytes == 0) bytes = 256;
     hipError_t e;
@@ -749,7 +752,8 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     rc = size_lds(w);
     if (rc) { delete w; return rc; }
     const int me = w->part;
-    if (alloc_region(w, (void**)&w->fwd, w->L.fwd_bytes[me]) || alloc_region(w, (void**)&w->vote, w->L.vote_bytes[me]) ||
+    // (forward rings and bulk flags: + kNonceTail bytes past the region for the creation nonce, which no reset clears)
+    if (alloc_region(w, (void**)&w->fwd, w->L.fwd_bytes[me] + kNonceTail) || alloc_region(w, (void**)&w->vote, w->L.vote_bytes[me]) ||
         alloc_region(w, (void**)&w->ctrl, w->L.ctrl_words[me] * 8)) {
         rlo_world_destroy(w);
         return RLO_E_HIP;
@@ -766,7 +770,7 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         const uint32_t keep = w->flags;
         w->flags |= RLO_PART_UNCACHED;
         const int e = alloc_region(w, (void**)&w->heap, w->L.heap_bytes[me]) ||
-                      alloc_region(w, (void**)&w->bflag, w->L.bflag_bytes[me]) || alloc_region(w, (void**)&w->jmem, w->jmem_bytes);
+                      alloc_region(w, (void**)&w->bflag, w->L.bflag_bytes[me] + kNonceTail) || alloc_region(w, (void**)&w->jmem, w->jmem_bytes);
         w->flags = keep;
         if (e) { rlo_world_destroy(w); return RLO_E_HIP; }
         (void)hipMemset(w->bflag, 0, w->L.bflag_bytes[me]);
@@ -776,16 +780,17 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     (void)hipMemset(w->vote, 0, std::max<uint64_t>(w->L.vote_bytes[me], 1));
     (void)hipMemset(w->ctrl, 0, w->L.ctrl_words[me] * 8);
     if (w->d_stats.alloc(w->nl)) { rlo_world_destroy(w); return RLO_E_HIP; }
-    {  // the creation nonce, in the regions a peer's rlo_part_connect reads it back from through its mapping
+    {  // the creation nonce, in every region a peer's rlo_part_connect reads it back from through its mapping
        // (control header word kCtrlNonceWord, which rlo_reset keeps; the first word of the vote and heap
-       // regions, which no reset clears and only a launch -- after every part connected -- writes): a mapping
-       // that shows an earlier allocation fails the connection loudly instead of carrying messages into
-       // memory that is not this part's any more
+       // regions, which no reset clears and only a launch -- after every part connected -- writes; past the
+       // end of the forward rings and the bulk flags): a mapping that shows an earlier allocation fails the
+       // connection loudly instead of carrying messages into memory that is not this part's any more
         static std::atomic<uint64_t> seq{0};
         w->nonce = splitmix64(process_token() ^ (++seq * 0x9E3779B97F4A7C15ull) ^
                               (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
         if (!w->nonce) w->nonce = 1;
-        void* regs[3] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, w->heap};
+        void* regs[5] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, w->heap, w->fwd + w->L.fwd_bytes[me],
+                         w->bflag ? w->bflag + w->L.bflag_bytes[me] : nullptr};
         for (void* r : regs)
             if (r && hipMemcpy(r, &w->nonce, 8, hipMemcpyHostToDevice) != hipSuccess) { rlo_world_destroy(w); return RLO_E_HIP; }
     }
@@ -895,12 +900,18 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
                 w->pbf[q] = (uint8_t*)p;
             }
             // every mapped region must show the peer's creation nonce (rlo_part_create)
-            const void* regs[3] = {w->pc[q] + rlo::kCtrlNonceWord, w->pv[q], L.bulk_max ? w->ph[q] : nullptr};
-            for (const void* r : regs) {
-                if (!r) continue;
+            const void* regs[5] = {w->pc[q] + rlo::kCtrlNonceWord, w->pv[q], L.bulk_max ? w->ph[q] : nullptr,
+                                   w->pf[q] + L.fwd_bytes[q], L.bulk_max ? w->pbf[q] + L.bflag_bytes[q] : nullptr};
+            for (int i = 0; i < 5; i++) {
+                if (!regs[i]) continue;
                 uint64_t got = 0;
-                HIPCHK(hipMemcpy(&got, r, 8, hipMemcpyDeviceToHost));
-                if (got != b.nonce) return RLO_E_STALE;
+                HIPCHK(hipMemcpy(&got, regs[i], 8, hipMemcpyDeviceToHost));
+                if (got != b.nonce) {
+                    static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
+                    std::fprintf(stderr, "rlo: part %d: the %s region of part %d, as mapped here, shows %016llx, not its nonce %016llx\n",
+                                 w->part, names[i], q, (unsigned long long)got, (unsigned long long)b.nonce);
+                    return RLO_E_STALE;
+                }
             }
         }
     }
@@ -1178,6 +1189,16 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     P.lat_own = w->d_lat_own.p;
     P.expect_bcast = w->d_expect_bcast.p;
     w->lat_rounds = rounds;
+    w->tl_rows = 0;
+    P.tl = nullptr;
+    P.tl_rounds = 0;
+    if (flags & RLO_FLAG_TIMELINE) {
+        w->tl_rows = std::min<uint32_t>(rounds, rlo::kTlRoundsMax);
+        if (w->d_tl.alloc((size_t)w->tl_rows * (rlo::kTlGlobal + 2u * (uint32_t)w->nl))) return RLO_E_HIP;
+        P.tl = w->d_tl.p;
+        P.tl_rounds = w->tl_rows;
+        P.mode |= rlo::MODE_TL;
+    }
     int rc = setup_log(w, flags, 0, true);
     if (rc) return rc;
     w->have_program = true;
@@ -1584,6 +1605,8 @@ int rlo_reset(rlo_world_t* w, void* stream) {
         HIPCHK(hipMemsetAsync(w->d_lat_out.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
         HIPCHK(hipMemsetAsync(w->d_lat_round.p, 0, sizeof(uint32_t), s));
         HIPCHK(hipMemsetAsync(w->d_lat_obs.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
+        if (w->tl_rows)
+            HIPCHK(hipMemsetAsync(w->d_tl.p, 0, sizeof(uint32_t) * w->tl_rows * (rlo::kTlGlobal + 2u * (uint32_t)w->nl), s));
         // sharded: part 0's control memset above clears the shared round word and counts
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -1725,6 +1748,17 @@ int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
     HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipMemcpy(ticks, w->d_lat_out.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+int rlo_timeline(rlo_world_t* w, uint32_t* out, uint64_t cap, uint32_t* stride) {
+    if (!w || !out) return RLO_E_INVAL;
+    const uint32_t st = rlo::kTlGlobal + 2u * (uint32_t)w->nl;
+    if (stride) *stride = st;
+    if (!w->tl_rows || !w->d_tl.p) return 0;
+    const uint32_t rows = (uint32_t)std::min<uint64_t>(w->tl_rows, cap / st);
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipMemcpy(out, w->d_tl.p, sizeof(uint32_t) * rows * st, hipMemcpyDeviceToHost));
+    return (int)rows;
 }
 
 int rlo_round_ticks(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {

@@ -28,7 +28,7 @@ RLO_PART_UNCACHED = 1
 RLO_PART_CHUNKED = 2
 RLO_PART_PEND_HBM = 4
 RLO_LAUNCH_NO_RESET = 1
-RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF = 1, 2, 4
+RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF, RLO_FLAG_TIMELINE = 1, 2, 4, 8
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
 DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot", 7: "host command",
         8: "bulk index"}
@@ -122,7 +122,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_part_create", "rlo_part_export", "rlo_part_connect", "rlo_reset", "rlo_launch_ex",
            "rlo_stream_create", "rlo_stream_destroy",
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
-           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_strerror", "rlo_last_hip_error",
+           "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_timeline", "rlo_strerror", "rlo_last_hip_error",
            "rlo_device_error", "rlo_bulk_debug",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
            "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan", "rlo_layout_plan",
@@ -165,6 +165,7 @@ def load():
     L.rlo_log.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), ctypes.c_uint32, vp, ctypes.c_uint32]
     L.rlo_latencies.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     L.rlo_round_ticks.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    L.rlo_timeline.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_program_host.argtypes = [vp, ctypes.POINTER(HostCfg)]
     L.rlo_host_post.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Cmd), vp, ctypes.c_uint32]
     L.rlo_host_poll.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp, ctypes.c_uint32]

@@ -106,8 +106,9 @@ class World:
         cfg = L.StormCfg(seed, k, length, window, flags, log_cap, len_max, order)
         check(self.lib.rlo_program_storm(self.h, ctypes.byref(cfg)), "rlo_program_storm")
 
-    def program_latency(self, rounds, length, seed=0x5EED, hist=False, log=False, prof=False):
+    def program_latency(self, rounds, length, seed=0x5EED, hist=False, log=False, prof=False, timeline=False):
         flags = (L.RLO_FLAG_LOG if log else 0) | (L.RLO_FLAG_HIST if hist else 0) | (L.RLO_FLAG_PROF if prof else 0)
+        flags |= L.RLO_FLAG_TIMELINE if timeline else 0
         check(self.lib.rlo_program_latency(self.h, rounds, length, seed, flags), "rlo_program_latency")
         self._lat_rounds = rounds
 
@@ -213,6 +214,17 @@ class World:
         arr = (ctypes.c_uint64 * self._lat_rounds)()
         n = check(self.lib.rlo_round_ticks(self.h, arr, self._lat_rounds), "rlo_round_ticks")
         return np.array(arr[:n], dtype=np.uint64)
+
+
+    def timeline(self):
+        """RLO_FLAG_TIMELINE rows (rlo_hip.h rlo_timeline): uint32 array [rounds][8 global + 2 x local ranks]
+        of 10-ns clock values (0 = not seen on this part)."""
+        stride = ctypes.c_uint32()
+        check(self.lib.rlo_timeline(self.h, (ctypes.c_uint32 * 1)(), 0, ctypes.byref(stride)), "rlo_timeline")
+        cap = 64 * stride.value
+        arr = (ctypes.c_uint32 * cap)()
+        n = check(self.lib.rlo_timeline(self.h, arr, cap, ctypes.byref(stride)), "rlo_timeline")
+        return np.array(arr[:n * stride.value], dtype=np.uint32).reshape(n, stride.value)
 
 
 def hist_percentile(hist, p):

@@ -1,0 +1,55 @@
+"""Where a latency round's time goes (RLO_FLAG_TIMELINE): per round the device clock of the origination, the
+scatter job's post / claim / completion-count adds (bulk), every rank's arrival (message or bulk announcement)
+and bulk completion, the round's last pickup, and the start of the next round; medians over rounds, in us
+after the origination.  One GPU, one part.
+    python tools/round_timeline.py [--n 8] [--sizes 64,16384,1048576] [--rounds 64]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rootless-coll-mpi-ops_amd"))
+import rlo  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=8)
+ap.add_argument("--sizes", default="64,16384,1048576")
+ap.add_argument("--rounds", type=int, default=64)
+ap.add_argument("--bulk-max", type=int, default=64 << 20)
+a = ap.parse_args()
+
+
+def rel(t, t0):
+    """clock difference in us (32-bit wrap), NaN where the event was not seen"""
+    d = ((t.astype(np.int64) - t0.astype(np.int64)) + (1 << 31)) % (1 << 32) - (1 << 31)
+    return np.where(t == 0, np.nan, d * 0.01)
+
+
+sizes = [int(x) for x in a.sizes.split(",")]
+nl = a.n
+for ln in sizes:
+    # ring-slot sizes in a world without bulk messages (the latency bench's), larger ones as bulk messages
+    with (rlo.World(a.n, max_payload=max(64, ln)) if ln <= 112 else
+          rlo.World(a.n, max_payload=64, bulk_max=a.bulk_max)) as w:
+        w.program_latency(a.rounds, ln, seed=0x7100 + ln, timeline=True)
+        w.run()
+        st = w.stats()
+        assert (st["error"] == 0).all(), (st["error"], st["error_aux"])
+        tl = w.timeline()
+        t0 = tl[:, 0]
+        g = {k: rel(tl[:, i], t0) for i, k in enumerate(["origin", "posted", "claimed", "moved", "round", "verified"])}
+        arr = rel(tl[:, 8:8 + nl], t0[:, None])
+        comp = rel(tl[:, 8 + nl:8 + 2 * nl], t0[:, None])
+        nxt = np.append(rel(tl[1:, 0], tl[:-1, 4]), np.nan)  # this round's last pickup -> next origination
+        per = np.append(rel(tl[1:, 0], tl[:-1, 0]), np.nan)
+        sl = slice(2, None)  # the first rounds warm the caches
+        md = lambda x: float(np.nanmedian(x[sl])) if np.isfinite(x[sl]).any() else float("nan")  # noqa: E731
+        line = "n %d len %8d: round %6.2f us | posted %5.2f claimed %5.2f moved %5.2f | arrival med %5.2f max %5.2f" % (
+            a.n, ln, md(per), md(g["posted"]), md(g["claimed"]), md(g["moved"]), md(np.nanmedian(arr, axis=1)),
+            md(np.nanmax(arr, axis=1)))
+        if np.isfinite(comp).any():
+            line += " | completion med %5.2f max %5.2f" % (md(np.nanmedian(comp, axis=1)), md(np.nanmax(comp, axis=1)))
+        line += " | last pickup %5.2f -> next origin +%5.2f | verified %5.2f" % (md(g["round"]), md(nxt), md(g["verified"]))
+        print(line, flush=True)
