@@ -268,7 +268,11 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 // MODE_TL: the clock of event `ev` of latency round r (rlo_device.hpp kTlGlobal; the latest writer wins)
 __device__ __forceinline__ void tl_mark(const Params& P, uint32_t r, uint32_t ev) {
     if ((P.mode & MODE_TL) && r < P.tl_rounds)
-        atomicMax(&P.tl[r * (kTlGlobal + 2u * P.n_local) + ev], (uint32_t)now_ticks());
+        atomicMax(&P.tl[r * (kTlGlobal + 3u * P.n_local) + ev], (uint32_t)now_ticks());
+}
+// MODE_TL: local rank lr's tree parent for round r (+1; the third per-rank column)
+__device__ __forceinline__ void tl_parent(const Params& P, uint32_t r, int lr, int from) {
+    if ((P.mode & MODE_TL) && r < P.tl_rounds) P.tl[r * (kTlGlobal + 3u * P.n_local) + kTlGlobal + 2u * P.n_local + lr] = (uint32_t)(from + 1);
 }
 
 // per-ring state lives lane-distributed in registers; a wave-uniform index reads it with v_readlane
@@ -1422,6 +1426,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const int forg = (int)(fw0 & 0xffffu);
         const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
         const uint32_t fpseq = fw2 >> 24;
+        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
                   (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL || (BULK && ftag == TAG_BULK)) &&
@@ -1483,7 +1488,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (!ok) return ~0u;
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
-                tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
+                tl_parent(P, fid, lr, ffrom);
                 atomicAdd(&S.bcast_delivered, 1ull);
                 if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
                 flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
@@ -1533,6 +1538,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t nt = P.n > 2 ? bulk_stripe_tiles(pl, dlen, (uint32_t)((me - forg - 1 + P.n) % P.n)) : 0u;
                 if (lane == 0) {
                     tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
+                    tl_parent(P, fid, lr, ffrom);
                     const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
                     if ((ob >> (e & 31u)) & 1u) bulk_fault(P, 10, (e << 12) | (fid & 0xfffu));  // still live: announced twice
                     bpend[e] = BulkPend{fid, dlen, bulk_total_tiles(pl, dlen) + nt, ffrom, ft0, dq,
@@ -1555,6 +1561,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
         fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
+        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
         if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
             st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
         if (ftag == TAG_BCAST && (P.mode & MODE_LAT) && lane == 0) {  // the round's last pickup
@@ -2886,6 +2893,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)tn - t0)], 1u);
                             if (P.mode & MODE_LAT) {  // round bookkeeping after the forwards are issued (G)
                                 tl_mark(P, id, kTlGlobal + (uint32_t)lr);
+                                tl_parent(P, id, lr, from);
                                 lat_deliv = true;
                                 lat_tn = (uint32_t)tn - t0;
                             }
@@ -2958,6 +2966,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                 bulk_fault(P, 12, (e << 12) | (id & 0xfffu));
                         }
                         tl_mark(P, id, kTlGlobal + (uint32_t)lr);
+                        tl_parent(P, id, lr, from);
                         const uint32_t ob = atomicOr(&S.b.bonw[e >> 5], 1u << (e & 31u));
                         if ((ob >> (e & 31u)) & 1u) {  // still live: which message was, which one came
                             const BulkPend od = bpend[e];

@@ -42,6 +42,7 @@ for ln in sizes:
         g = {k: rel(tl[:, i], t0) for i, k in enumerate(["origin", "posted", "claimed", "moved", "round", "verified"])}
         arr = rel(tl[:, 8:8 + nl], t0[:, None])
         comp = rel(tl[:, 8 + nl:8 + 2 * nl], t0[:, None])
+        par = tl[:, 8 + 2 * nl:8 + 3 * nl].astype(np.int64) - 1
         nxt = np.append(rel(tl[1:, 0], tl[:-1, 4]), np.nan)  # this round's last pickup -> next origination
         per = np.append(rel(tl[1:, 0], tl[:-1, 0]), np.nan)
         sl = slice(2, None)  # the first rounds warm the caches
@@ -49,7 +50,24 @@ for ln in sizes:
         line = "n %d len %8d: round %6.2f us | posted %5.2f claimed %5.2f moved %5.2f | arrival med %5.2f max %5.2f" % (
             a.n, ln, md(per), md(g["posted"]), md(g["claimed"]), md(g["moved"]), md(np.nanmedian(arr, axis=1)),
             md(np.nanmax(arr, axis=1)))
-        if np.isfinite(comp).any():
+        if ln > 112 and np.isfinite(comp).any():
             line += " | completion med %5.2f max %5.2f" % (md(np.nanmedian(comp, axis=1)), md(np.nanmax(comp, axis=1)))
+        elif np.isfinite(comp).any():
+            # per hop: parent's forwards issued (the origin: its origination) -> child's doorbell pass took it;
+            # per rank: took it -> its own forwards issued
+            hop, proc = [], []
+            for r in range(2, len(tl)):
+                for c in range(nl):
+                    p = par[r, c]
+                    if p < 0 or not np.isfinite(arr[r, c]):
+                        continue
+                    sent = 0.0 if np.isnan(arr[r, p]) else comp[r, p]  # (the origin takes nothing: its origination)
+                    if np.isfinite(sent):
+                        hop.append(arr[r, c] - sent)
+                    if np.isfinite(comp[r, c]):
+                        proc.append(comp[r, c] - arr[r, c])
+            if hop:
+                line += " | hop med %5.2f p90 %5.2f, take->forwarded med %5.2f (%d hops)" % (
+                    np.median(hop), np.percentile(hop, 90), np.median(proc) if proc else np.nan, len(hop))
         line += " | last pickup %5.2f -> next origin +%5.2f | verified %5.2f" % (md(g["round"]), md(nxt), md(g["verified"]))
         print(line, flush=True)
