@@ -268,11 +268,14 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 // MODE_TL: the clock of event `ev` of latency round r (rlo_device.hpp kTlGlobal; the latest writer wins)
 __device__ __forceinline__ void tl_mark(const Params& P, uint32_t r, uint32_t ev) {
     if ((P.mode & MODE_TL) && r < P.tl_rounds)
-        atomicMax(&P.tl[r * (kTlGlobal + 3u * P.n_local) + ev], (uint32_t)now_ticks());
+        atomicMax(&P.tl[r * (kTlGlobal + kTlCols * P.n_local) + ev], (uint32_t)now_ticks());
 }
-// MODE_TL: local rank lr's tree parent for round r (+1; the third per-rank column)
+// MODE_TL: per-rank column col (rlo_device.hpp TlCol) of local rank lr for round r := v
+__device__ __forceinline__ void tl_put(const Params& P, uint32_t r, uint32_t col, int lr, uint32_t v) {
+    if ((P.mode & MODE_TL) && r < P.tl_rounds) P.tl[r * (kTlGlobal + kTlCols * P.n_local) + kTlGlobal + col * P.n_local + lr] = v;
+}
 __device__ __forceinline__ void tl_parent(const Params& P, uint32_t r, int lr, int from) {
-    if ((P.mode & MODE_TL) && r < P.tl_rounds) P.tl[r * (kTlGlobal + 3u * P.n_local) + kTlGlobal + 2u * P.n_local + lr] = (uint32_t)(from + 1);
+    tl_put(P, r, TLC_PARENT, lr, (uint32_t)(from + 1));
 }
 
 // per-ring state lives lane-distributed in registers; a wave-uniform index reads it with v_readlane
@@ -1388,6 +1391,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);  // my part's ctrl region (my bells)
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
+    uint32_t tl_issue = 0, tl_done = 0;  // MODE_TL: clock when the spin's polls were issued / the doorbell pass began
 
     // a small message (lane q: slot chunk q, q < nch) into out-rings `need` at their tails: the ring slot,
     // and with bells the child's doorbell for the edge, tagged bell_tag(ring sequence) | vc << 31.  The
@@ -1426,7 +1430,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const int forg = (int)(fw0 & 0xffffu);
         const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
         const uint32_t fpseq = fw2 >> 24;
-        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
+        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) {
+            tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
+            tl_put(P, fid, TLC_ISSUE, lr, tl_issue);
+            tl_put(P, fid, TLC_PASS, lr, tl_done);
+        }
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
                   (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL || (BULK && ftag == TAG_BULK)) &&
@@ -1655,6 +1663,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         // the data words to LDS at once (registers are the kernel's scarcest resource): chunk q of in-edge
         // k's bell at kLLBell + 16 (8 k + q), child j's vote bell {word, pid} at kLLBellVote + 8 j
         *reinterpret_cast<u32x4*>(stage + kLLBell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
+        if (P.mode & MODE_TL) tl_done = (uint32_t)now_ticks();
         if (lane < sll) *reinterpret_cast<uint2*>(stage + kLLBellVote + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
         const uint32_t lcap = min(nsmall, kBellChunks);
@@ -1997,6 +2006,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u)) {
                     hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 }
+                if (P.mode & MODE_TL) tl_issue = (uint32_t)now_ticks();
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);

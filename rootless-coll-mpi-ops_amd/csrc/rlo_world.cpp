@@ -1194,7 +1194,7 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     P.tl_rounds = 0;
     if (flags & RLO_FLAG_TIMELINE) {
         w->tl_rows = std::min<uint32_t>(rounds, rlo::kTlRoundsMax);
-        if (w->d_tl.alloc((size_t)w->tl_rows * (rlo::kTlGlobal + 3u * (uint32_t)w->nl))) return RLO_E_HIP;
+        if (w->d_tl.alloc((size_t)w->tl_rows * (rlo::kTlGlobal + rlo::kTlCols * (uint32_t)w->nl))) return RLO_E_HIP;
         P.tl = w->d_tl.p;
         P.tl_rounds = w->tl_rows;
         P.mode |= rlo::MODE_TL;
@@ -1606,7 +1606,7 @@ int rlo_reset(rlo_world_t* w, void* stream) {
         HIPCHK(hipMemsetAsync(w->d_lat_round.p, 0, sizeof(uint32_t), s));
         HIPCHK(hipMemsetAsync(w->d_lat_obs.p, 0, sizeof(uint64_t) * w->lat_rounds, s));
         if (w->tl_rows)
-            HIPCHK(hipMemsetAsync(w->d_tl.p, 0, sizeof(uint32_t) * w->tl_rows * (rlo::kTlGlobal + 3u * (uint32_t)w->nl), s));
+            HIPCHK(hipMemsetAsync(w->d_tl.p, 0, sizeof(uint32_t) * w->tl_rows * (rlo::kTlGlobal + rlo::kTlCols * (uint32_t)w->nl), s));
         // sharded: part 0's control memset above clears the shared round word and counts
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -1752,7 +1752,7 @@ int rlo_latencies(rlo_world_t* w, uint64_t* ticks, uint32_t cap) {
 
 int rlo_timeline(rlo_world_t* w, uint32_t* out, uint64_t cap, uint32_t* stride) {
     if (!w || !out) return RLO_E_INVAL;
-    const uint32_t st = rlo::kTlGlobal + 3u * (uint32_t)w->nl;
+    const uint32_t st = rlo::kTlGlobal + rlo::kTlCols * (uint32_t)w->nl;
     if (stride) *stride = st;
     if (!w->tl_rows || !w->d_tl.p) return 0;
     const uint32_t rows = (uint32_t)std::min<uint64_t>(w->tl_rows, cap / st);

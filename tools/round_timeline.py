@@ -43,6 +43,8 @@ for ln in sizes:
         arr = rel(tl[:, 8:8 + nl], t0[:, None])
         comp = rel(tl[:, 8 + nl:8 + 2 * nl], t0[:, None])
         par = tl[:, 8 + 2 * nl:8 + 3 * nl].astype(np.int64) - 1
+        iss = rel(tl[:, 8 + 3 * nl:8 + 4 * nl], t0[:, None])
+        pas = rel(tl[:, 8 + 4 * nl:8 + 5 * nl], t0[:, None])
         nxt = np.append(rel(tl[1:, 0], tl[:-1, 4]), np.nan)  # this round's last pickup -> next origination
         per = np.append(rel(tl[1:, 0], tl[:-1, 0]), np.nan)
         sl = slice(2, None)  # the first rounds warm the caches
@@ -55,7 +57,7 @@ for ln in sizes:
         elif np.isfinite(comp).any():
             # per hop: parent's forwards issued (the origin: its origination) -> child's doorbell pass took it;
             # per rank: took it -> its own forwards issued
-            hop, proc = [], []
+            hop, proc, wait, rtt, pre = [], [], [], [], []
             for r in range(2, len(tl)):
                 for c in range(nl):
                     p = par[r, c]
@@ -64,10 +66,17 @@ for ln in sizes:
                     sent = 0.0 if np.isnan(arr[r, p]) else comp[r, p]  # (the origin takes nothing: its origination)
                     if np.isfinite(sent):
                         hop.append(arr[r, c] - sent)
+                        if np.isfinite(iss[r, c]) and 0 <= pas[r, c] - iss[r, c] < 20:  # (taken by the doorbell pass)
+                            wait.append(iss[r, c] - sent)
+                            rtt.append(pas[r, c] - iss[r, c])
+                            pre.append(arr[r, c] - pas[r, c])
                     if np.isfinite(comp[r, c]):
                         proc.append(comp[r, c] - arr[r, c])
             if hop:
                 line += " | hop med %5.2f p90 %5.2f, take->forwarded med %5.2f (%d hops)" % (
                     np.median(hop), np.percentile(hop, 90), np.median(proc) if proc else np.nan, len(hop))
+            if wait:
+                line += " [sent -> poll issued %5.2f, poll -> pass %5.2f, pass -> taken %5.2f; %d]" % (
+                    np.median(wait), np.median(rtt), np.median(pre), len(wait))
         line += " | last pickup %5.2f -> next origin +%5.2f | verified %5.2f" % (md(g["round"]), md(nxt), md(g["verified"]))
         print(line, flush=True)
