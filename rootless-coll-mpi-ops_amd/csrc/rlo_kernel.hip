@@ -185,6 +185,7 @@ struct Shared {
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
     uint64_t prof[8], prof_t, dbg[8];
+    uint32_t tl_clk[2];  // MODE_TL: when wave 0's spin issued its polls, when the doorbell pass began
     int64_t expect_dec;
     uint32_t hist[kHistBins];
 };
@@ -1391,7 +1392,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);  // my part's ctrl region (my bells)
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
-    uint32_t tl_issue = 0, tl_done = 0;  // MODE_TL: clock when the spin's polls were issued / the doorbell pass began
 
     // a small message (lane q: slot chunk q, q < nch) into out-rings `need` at their tails: the ring slot,
     // and with bells the child's doorbell for the edge, tagged bell_tag(ring sequence) | vc << 31.  The
@@ -1432,8 +1432,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t fpseq = fw2 >> 24;
         if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) {
             tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
-            tl_put(P, fid, TLC_ISSUE, lr, tl_issue);
-            tl_put(P, fid, TLC_PASS, lr, tl_done);
+            tl_put(P, fid, TLC_ISSUE, lr, S.tl_clk[0]);
+            tl_put(P, fid, TLC_PASS, lr, S.tl_clk[1]);
         }
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
@@ -1663,7 +1663,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         // the data words to LDS at once (registers are the kernel's scarcest resource): chunk q of in-edge
         // k's bell at kLLBell + 16 (8 k + q), child j's vote bell {word, pid} at kLLBellVote + 8 j
         *reinterpret_cast<u32x4*>(stage + kLLBell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
-        if (P.mode & MODE_TL) tl_done = (uint32_t)now_ticks();
+        if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[1] = (uint32_t)now_ticks();
         if (lane < sll) *reinterpret_cast<uint2*>(stage + kLLBellVote + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
         const uint32_t lcap = min(nsmall, kBellChunks);
@@ -2006,7 +2006,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u)) {
                     hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 }
-                if (P.mode & MODE_TL) tl_issue = (uint32_t)now_ticks();
+                if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[0] = (uint32_t)now_ticks();
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
