@@ -100,9 +100,11 @@ struct BulkSh {
     uint32_t blen[kPass];       // storm candidate i -> payload length
     uint32_t bact[kMaxPend];    // pending receptions (o * B + s), compact
     uint32_t nbact, ncomp;
-    // pending entries [0, nstable) as left by the last compaction (phase C): the only ones wave 0 may
-    // evaluate in phase A, which runs before the iteration's barrier while other waves can still be
-    // appending (an append's nbact increment can be seen before its bact store lands)
+    uint64_t fbase, dbase;      // progress: my flag lines (o, s) at fbase + (o B + s) kBulkLine, my done words
+                                // (s) at dbase + s kBulkLine -- no part-table loads on the poll path
+    // pending entries [0, nstable): the ones the last evaluation (bulk_eval, wave 0) covered, the range phase
+    // C may deliver from.  Other waves append only in phase F; wave 0 evaluates after the consume phase's
+    // barrier (every append of the iteration landed) and before the next phase F, so it sees whole entries
     uint32_t nstable;
     uint64_t cmask[kMaxPend / 64];  // completion bits by position in bact (phase A poll)
     uint32_t bonw[kMaxPend / 32];   // live receptions by (o * B + s): a guard (register twice / complete
@@ -186,6 +188,7 @@ struct Shared {
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
     uint64_t prof[8], prof_t, dbg[8];
     uint32_t tl_clk[2];  // MODE_TL: when wave 0's spin issued its polls, when the doorbell pass began
+    uint32_t tl_bfid;    // MODE_TL: a bulk announcement the doorbell pass took (+1), for its TLC_NEXT clock
     int64_t expect_dec;
     uint32_t hist[kHistBins];
 };
@@ -292,6 +295,12 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 // i / d for the small d = nsmall (<= 24) and i < 2^16: multiply-high by ceil(2^32 / d)
 __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { return magic ? __umulhi(i, magic) : i; }
 
+// MODE_TL (wave 0): why the spin ended -- dbg[0] the last iteration was not idle, [1] spin bound, [2] the doorbell
+// pass needs the full iteration, [3] 64 passes, [4] job posts queued, [5] a bulk copy complete, [6] a polled word moved
+#define SPIN_WHY(k)                                           \
+    do {                                                      \
+        if ((P.mode & MODE_TL) && lane == 0) S.dbg[(k)]++;    \
+    } while (0)
 // MODE_PROF: thread 0 charges the shader cycles since the last stamp to phase `ph`
 #define PROF_STAMP(ph)                                  \
     do {                                                \
@@ -781,6 +790,9 @@ __device__ __forceinline__ void queue_job(BulkSh& B, const Params& P, uint32_t c
 }
 __device__ __forceinline__ void queue_job(NoBulkSh&, const Params&, uint32_t, uint32_t, int, int, uint32_t, uint32_t,
                                           uint32_t, uint32_t, int, uint32_t, uint32_t, uint32_t) {}  // (no bulk messages)
+// registered bulk receptions (wave-uniform)
+__device__ __forceinline__ uint32_t nact_of(const BulkSh& B) { return (uint32_t)uni((int)B.nbact); }
+__device__ __forceinline__ uint32_t nact_of(const NoBulkSh&) { return 0u; }
 // write out the queued posts (wave 0, all lanes): post_job's protocol with sub-job u on lane u mod 64 --
 // the slots' generation checks, the record bodies, one drain, then the sequence words
 __device__ __forceinline__ void flush_posts(BulkSh& B, const Params& P, int lane) {
@@ -1001,11 +1013,13 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                     }
                 }
             }
+            if (tid == 0 && jb.ti0 == 0u) tl_mark(P, jb.bid, TL_GEN);
             auto recv = [&](int jj) { return bulk_rsrc_at(P, (o + 1 + jj) % n, o, s, off0, 16u * ngr); };
             if (sys) tile_copy<true, W>(rs, ngr, tid, n - 1, recv);
             else tile_copy<false, W>(rs, ngr, tid, n - 1, recv);
             VM_DRAIN();
             __syncthreads();
+            if (tid == 0 && jb.ti0 == 0u) tl_mark(P, jb.bid, TL_DRAINED);
             if (tid < 64) {
                 if (sys) bulk_release(true);
                 for (int d = 1 + tid; d < n; d += 64) bflag_add(bulk_flags(P, (o + d) % n, o, s) + (mi & 15u), jb.ntiles, sys);
@@ -1301,6 +1315,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         for (int i = tid; i < 4 * 64; i += kBlock) { (&S.pubw[0][0])[i] = 0; (&S.snap[0][0])[i] = 0; }
         if (tid < kMaxIn) { S.vout_tail[tid] = 0; S.vout_head[tid] = 0; }
         if (tid < 8) { S.prof[tid] = 0; S.dbg[tid] = 0; S.hd[tid] = 0; }
+        if (tid == 0) S.tl_bfid = 0;
         if (tid == 0) {
             S.prof_t = __builtin_amdgcn_s_memtime();
             for (int k = 0; k < kPoolMax; k++) {  // proposalPools_reset, :1351-1362
@@ -1323,6 +1338,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0; S.b.npost = 0;
+                S.b.fbase = reinterpret_cast<uint64_t>(bulk_flags(P, me, 0, 0));
+                S.b.dbase = reinterpret_cast<uint64_t>(bulk_done(P, me, 0u));
                 for (int i = 0; i < kMaxPend / 64; i++) S.b.cmask[i] = 0;
                 for (int i = 0; i < kMaxPend / 32; i++) S.b.bonw[i] = 0;
             }
@@ -1569,6 +1586,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
         fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
+        if constexpr (BULK) {
+            if ((P.mode & MODE_TL) && ftag == TAG_BULK && lane == 0) {
+                tl_put(P, fid, TLC_FWD, lr, (uint32_t)now_ticks());
+                S.tl_bfid = fid + 1u;
+            }
+        }
         if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
         if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
             st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
@@ -1982,6 +2005,49 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
     };
 
+    // BULK, wave 0: which pending receptions are complete -- S.b.cmask over every registered one (nstable := that
+    // count, the range phase C's delivery may take); whether any is
+    auto bulk_eval = [&]() -> bool {
+        bool any = false;
+        if constexpr (BULK) {
+            const uint32_t nb = (uint32_t)uni((int)S.b.nbact);
+            if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[1] = (uint32_t)now_ticks();
+            // my flag lines through one resource: a line's 16 count shards in four 16-B loads (sixteen 4-B loads
+            // of one line queued behind each other at the memory: ~1.8 us per poll, vs one load's round trip)
+            const __amdgpu_buffer_rsrc_t rfl = mk_rsrc(reinterpret_cast<void*>(uni64(S.b.fbase)), (uint32_t)P.n * bsl * kBulkLine);
+            for (uint32_t u = 0; u * 64u < nb; u++) {
+                const uint32_t i = u * 64u + (uint32_t)lane;
+                bool dn = false;
+                if (i < nb) {
+                    const uint32_t e = S.b.bact[i];
+                    uint32_t tc = 0;
+                    if (e >= (uint32_t)P.n * bsl) {
+                        bulk_fault(P, 7, e);
+                    } else if (P.bulk_cross) {
+                        tc = bflag_ld(reinterpret_cast<uint32_t*>(uni64(S.b.fbase) + (uint64_t)e * kBulkLine) + kBulkTflag, sys);
+                    } else {
+                        u32x4 q[4];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) q[k] = sys ? ld_sys(rfl, e * kBulkLine + 16u * k) : ld_sc1(rfl, e * kBulkLine + 16u * k);
+#pragma unroll
+                        for (int k = 0; k < 4; k++) tc += q[k].x + q[k].y + q[k].z + q[k].w;
+                    }
+                    dn = e < (uint32_t)P.n * bsl && tc >= bpend[e].ntiles;
+                    // MODE_TL: when the evaluation that found the copy complete began, when its loads were back
+                    if ((P.mode & MODE_TL) && dn) {
+                        tl_put(P, bpend[e].bid, TLC_PASS, lr, (uint32_t)now_ticks());
+                        tl_put(P, bpend[e].bid, TLC_ISSUE, lr, S.tl_clk[1]);
+                    }
+                }
+                const uint64_t m = __ballot(dn);
+                any |= m != 0ull;
+                if (lane == 0) S.b.cmask[u] = m;
+            }
+            if (lane == 0) S.b.nstable = nb;
+        }
+        return any;
+    };
+
     for (;;) {
         asm volatile("" : "+v"(lane));  // (see lane's declaration)
         lt_mask = (1ull << lane) - 1ull;
@@ -1995,7 +2061,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // idle rank is seen one poll round trip later instead of after a whole idle iteration.
             // Bounded, so the idle clock and the deadline still tick.
             uint32_t ll_run = 0;
+            bool bev = false;  // BULK: this spin evaluated the pending receptions after its doorbell pass
+            uint64_t dnw = 0;  // BULK, lane s < B: my heap slot s's release count (done word), polled every spin
             for (uint32_t sp = 0;; sp++) {
+                bev = false;
                 // host mode: the host-written counters (pinned host memory: a PCIe read, ~1 us more than
                 // the ring polls) on every 4th re-poll only, so an idle rank still sees a ring message
                 // one VRAM poll after it lands; a command waits at most ~4 re-polls
@@ -2006,12 +2075,22 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u)) {
                     hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 }
-                if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[0] = (uint32_t)now_ticks();
+                if ((P.mode & MODE_TL) && lane == 0) {
+                    S.tl_clk[0] = (uint32_t)now_ticks();
+                    if (BULK && S.tl_bfid) { tl_put(P, S.tl_bfid - 1u, TLC_NEXT, lr, S.tl_clk[0]); S.tl_bfid = 0; }
+                }
                 if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
                 if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
                 if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
                 if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
                 if (lane == 0) errf = poll32(P.error_flag);
+                if constexpr (BULK) {
+                    if (lane < (int)bsl) {
+                        uint64_t* d = reinterpret_cast<uint64_t*>(uni64(S.b.dbase) + (uint64_t)lane * kBulkLine);
+                        dnw = sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                  : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
                 if ((P.mode & MODE_LAT) && lane == 1)  // the round in progress (part 0's word when sharded)
                     latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                : poll32(P.lat_round);
@@ -2027,27 +2106,33 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         }
                         if (lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
                         bool need_full = false;
+                        const uint32_t nb0 = nact_of(S.b);
                         const uint32_t nll = ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf, need_full);
                         if (nll) ll_prog = true;
-                        if (need_full) break;  // the full iteration takes the rest
+                        if (need_full) { SPIN_WHY(2); break; }  // the full iteration takes the rest
+                        // a bulk announcement registered: its copy is often complete already (the movers started at
+                        // the origination, the announcement walks the tree) -- evaluated and delivered right away
+                        if (BULK && nact_of(S.b) != nb0) { SPIN_WHY(3); break; }
                         if (nll) {
                             // keep serving from here; every 64 passes the full iteration's bookkeeping runs
                             if (++ll_run < 64u) { sp = 0; continue; }
+                            SPIN_WHY(3);
                             break;
                         }
                     }
                 }
-                if (!idle_prev || sp >= kIdleSpin) break;
-                if constexpr (BULK) {  // a reception the doorbell pass registered: its completion is polled per iteration
-                    if (uni((int)S.b.nbact) != 0) break;
-                }
+                if (!idle_prev || sp >= kIdleSpin) { SPIN_WHY(idle_prev ? 1 : 0); break; }
+                // pending receptions: their completion counts are polled here, every spin, and the first complete
+                // one ends the spin (phase C delivers it) -- not a full iteration per poll.  Queued job posts (a
+                // reception's GATHER) are the full iteration's to write out
                 bool bmoved = false;
-                if constexpr (BULK) {  // a released heap slot of mine (a bulk origination may wait for it)
-                    if (lane < (int)bsl) {
-                        uint64_t* d = bulk_done(P, me, (uint32_t)lane);
-                        bmoved = (sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                      : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != S.b.sdone[lane];
+                if constexpr (BULK) {
+                    if (uni((int)S.b.npost) != 0) { SPIN_WHY(4); break; }
+                    if (uni((int)S.b.nbact) != 0) {
+                        bev = true;
+                        if (bulk_eval()) { SPIN_WHY(5); break; }
                     }
+                    bmoved = lane < (int)bsl && dnw != S.b.sdone[lane];  // a released heap slot of mine (an origination may wait)
                 }
                 // with doorbells only new work counts: a counter that caught up with what the bells already
                 // delivered, credits (nothing waits for them in an idle iteration), another rank's round.  Nor
@@ -2060,7 +2145,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                               (latr != p_lat && rdl32(latr, 1) == S.lat_own_next) || errf != 0
                         : in_tail_r != S.snap[0][lane] || vin_tail_r != S.snap[1][lane] || out_head_r != S.snap[2][lane] ||
                               vout_head_r != S.snap[3][lane] || hpoll != p_h || latr != p_lat || errf != 0 || bmoved;
-                if (__ballot(moved)) break;
+                if (__ballot(moved)) { SPIN_WHY(6); break; }
             }
             if (hpw && lane == 0) S.a_done = a_it;  // wave 1 stops polling the host
             S.snap[0][lane] = in_tail_r; S.snap[1][lane] = vin_tail_r; S.snap[2][lane] = out_head_r;
@@ -2069,24 +2154,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // wave 0 last saw of its command tail / pickup head, and how far it got)
             if (host && (n_iter & 4095u) == 0 && lane < 3) pub64_sys(&hctl[kHctlBeat + lane], lane == 2 ? n_iter : hpoll);
             if constexpr (BULK) {
-                // my heap slots' release counts, and which pending receptions are complete
-                if (lane < (int)bsl) {
-                    uint64_t* d = bulk_done(P, me, (uint32_t)lane);
-                    S.b.sdone[lane] = sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                          : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                const uint32_t nb = S.b.nstable;
-                for (uint32_t u = 0; u * 64u < nb; u++) {
-                    const uint32_t i = u * 64u + (uint32_t)lane;
-                    bool dn = false;
-                    if (i < nb) {
-                        const uint32_t e = S.b.bact[i];
-                        if (e >= (uint32_t)P.n * bsl) bulk_fault(P, 7, e); else
-                        dn = bulk_tcount(P, bulk_flags(P, me, (int)(e / bsl), e % bsl), sys) >= bpend[e].ntiles;
-                    }
-                    const uint64_t m = __ballot(dn);
-                    if (lane == 0) S.b.cmask[u] = m;
-                }
+                // my heap slots' release counts (the last spin's poll), and which pending receptions are complete
+                if (lane < (int)bsl) S.b.sdone[lane] = dnw;
+                if (!bev) (void)bulk_eval();  // (else the spin's last evaluation stands: nothing was registered since)
             }
             if ((P.mode & MODE_LAT) && me == 0) lat_observe(latr);
             if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
@@ -2177,8 +2247,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // checksummed by a VERIFY job (which then releases the slot); host mode: one pickup
                 // event each (the host copies the bytes out and posts RLO_CMD_BULK_RELEASE)
                 const uint32_t nb = S.b.nbact;
-                // phase A evaluated exactly [0, nst): an entry appended since has no valid mask bit
-                // (cmask words past phase A's range keep older iterations' bits)
+                // the last bulk_eval covered exactly [0, nst): an entry appended since has no valid mask bit
+                // (cmask words past that range keep older iterations' bits)
                 const uint32_t nst = S.b.nstable;
                 if (nb) {
                     uint32_t climit = kMaxPend;
@@ -3503,10 +3573,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             done_w0 = __builtin_amdgcn_readfirstlane((int)done_w0) != 0;  // lane 0 updated these
             sched_next = (int64_t)uni64((uint64_t)sched_next);
-            // (BULK: no tight re-poll while receptions are pending: their flags are polled once per iteration)
-            bool bidle = true;
-            if constexpr (BULK) bidle = S.b.nbact == 0;
-            idle_prev = bidle && C == 0 && S.vtot == 0 && !done_w0 && !(P.mode & MODE_NOSPIN);
+            // (BULK: pending receptions are polled in the spin, bulk_eval)
+            idle_prev = C == 0 && S.vtot == 0 && !done_w0 && !(P.mode & MODE_NOSPIN);
         }
         PROF_STAMP(6);
     }
@@ -3524,7 +3592,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
     // ---------------- flush statistics
     if constexpr (BULK) {
-        if (tid == 0 && !(P.mode & MODE_PROF)) {  // diagnostics in stats.dbg: pending receptions at exit
+        if (tid == 0 && !(P.mode & (MODE_PROF | MODE_TL))) {  // diagnostics in stats.dbg: pending receptions at exit
             const uint32_t nb = S.b.nbact;
             S.dbg[0] = ((uint64_t)S.b.bulk_q << 32) | nb;
             for (uint32_t i = 0; i < 3 && i < nb; i++) {

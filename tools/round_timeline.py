@@ -18,6 +18,7 @@ ap.add_argument("--n", type=int, default=8)
 ap.add_argument("--sizes", default="64,16384,1048576")
 ap.add_argument("--rounds", type=int, default=64)
 ap.add_argument("--bulk-max", type=int, default=64 << 20)
+ap.add_argument("--dump", type=int, default=0, help="print this many rounds' per-rank clocks")
 a = ap.parse_args()
 
 
@@ -39,21 +40,26 @@ for ln in sizes:
         assert (st["error"] == 0).all(), (st["error"], st["error_aux"])
         tl = w.timeline()
         t0 = tl[:, 0]
-        g = {k: rel(tl[:, i], t0) for i, k in enumerate(["origin", "posted", "claimed", "moved", "round", "verified"])}
+        g = {k: rel(tl[:, i], t0) for i, k in enumerate(["origin", "posted", "claimed", "moved", "round", "verified", "gen", "drained"])}
         arr = rel(tl[:, 8:8 + nl], t0[:, None])
         comp = rel(tl[:, 8 + nl:8 + 2 * nl], t0[:, None])
         par = tl[:, 8 + 2 * nl:8 + 3 * nl].astype(np.int64) - 1
         iss = rel(tl[:, 8 + 3 * nl:8 + 4 * nl], t0[:, None])
         pas = rel(tl[:, 8 + 4 * nl:8 + 5 * nl], t0[:, None])
+        fwdb = rel(tl[:, 8 + 5 * nl:8 + 6 * nl], t0[:, None])
+        nxts = rel(tl[:, 8 + 6 * nl:8 + 7 * nl], t0[:, None])
         nxt = np.append(rel(tl[1:, 0], tl[:-1, 4]), np.nan)  # this round's last pickup -> next origination
         per = np.append(rel(tl[1:, 0], tl[:-1, 0]), np.nan)
         sl = slice(2, None)  # the first rounds warm the caches
         md = lambda x: float(np.nanmedian(x[sl])) if np.isfinite(x[sl]).any() else float("nan")  # noqa: E731
-        line = "n %d len %8d: round %6.2f us | posted %5.2f claimed %5.2f moved %5.2f | arrival med %5.2f max %5.2f" % (
-            a.n, ln, md(per), md(g["posted"]), md(g["claimed"]), md(g["moved"]), md(np.nanmedian(arr, axis=1)),
+        line = "n %d len %8d: round %6.2f us | posted %5.2f claimed %5.2f gen %5.2f drained %5.2f moved %5.2f | arrival med %5.2f max %5.2f" % (
+            a.n, ln, md(per), md(g["posted"]), md(g["claimed"]), md(g["gen"]), md(g["drained"]), md(g["moved"]), md(np.nanmedian(arr, axis=1)),
             md(np.nanmax(arr, axis=1)))
         if ln > 112 and np.isfinite(comp).any():
             line += " | completion med %5.2f max %5.2f" % (md(np.nanmedian(comp, axis=1)), md(np.nanmax(comp, axis=1)))
+            # per receiver: the last poll that found its copy incomplete, the one that found it complete
+            line += " [complete poll issued med %5.2f, its loads back med %5.2f]" % (
+                md(np.nanmedian(iss, axis=1)), md(np.nanmedian(pas, axis=1)))
         elif np.isfinite(comp).any():
             # per hop: parent's forwards issued (the origin: its origination) -> child's doorbell pass took it;
             # per rank: took it -> its own forwards issued
@@ -80,3 +86,15 @@ for ln in sizes:
                     np.median(wait), np.median(rtt), np.median(pre), len(wait))
         line += " | last pickup %5.2f -> next origin +%5.2f | verified %5.2f" % (md(g["round"]), md(nxt), md(g["verified"]))
         print(line, flush=True)
+        for r in range(2, 2 + a.dump):
+            print("    round %d: origin %d, posted %.2f claimed %.2f moved %.2f round %.2f" % (
+                r, int(np.argmax(np.isnan(arr[r]))), g["posted"][r], g["claimed"][r], g["moved"][r], g["round"][r]))
+            for c in range(nl):
+                print("      rank %3d parent %3d: arrival %6.2f  poll %6.2f  pass/complete-poll %6.2f  done %6.2f"
+                      "  fwd %6.2f  next-spin %6.2f" % (
+                          c, par[r, c], arr[r, c], iss[r, c], pas[r, c], comp[r, c],
+                          fwdb[r, c], nxts[r, c]))
+        why = st["dbg"][:, :7].astype(np.int64)  # wave 0's spin exits (rlo_kernel.hip SPIN_WHY)
+        print("    spin exits over ranks: not-idle %d bound %d need-full %d 64-passes %d posts %d bulk-done %d moved %d;"
+              " iterations %d (%.1f per round per rank)" % (*why.sum(axis=0), int(st["iterations"].sum()),
+                                                            st["iterations"].sum() / a.rounds / nl), flush=True)
