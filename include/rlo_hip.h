@@ -165,12 +165,13 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg);
 int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t seed, uint32_t flags);
 
 /* RLO_FLAG_TIMELINE: the first min(rounds, 64) rounds' event clocks (low 32 bits of the 10-ns clock; 0 =
- * not seen on this part), row r = [8 global events][7 columns x local ranks]: global 0 origination, 1 scatter
+ * not seen on this part), row r = [8 global events][9 columns x local ranks]: global 0 origination, 1 scatter
  * job posted, 2 claimed by a mover, 3 moved (completion counts added), 4 round complete (last pickup), 5 last
  * receiver's VERIFY done; per rank: arrival, bulk completion (ring-slot messages: their forwards issued),
  * tree parent + 1, and for a message the doorbell pass took, when the polls that found it were issued and
  * when that pass began (bulk: when the poll that found the copy complete began, when its loads were back), and for
- * a bulk announcement when its forwards were issued and when wave 0's next spin began.  Copies rows * *stride words to out (cap words), returns the rows copied. */
+ * a bulk announcement when its forwards were issued and when wave 0's next spin began (a ring-slot message the
+ * doorbell pass took: two probes inside that pass), two probes inside the lone-message path.  Copies rows * *stride words to out (cap words), returns the rows copied. */
 int rlo_timeline(rlo_world_t* w, uint32_t* out, uint64_t cap, uint32_t* stride);
 
 #define RLO_JUDGE_APPROVE 0u /* approve everything                                           */

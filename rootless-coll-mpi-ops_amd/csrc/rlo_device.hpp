@@ -35,12 +35,13 @@ constexpr int kCtrlHdrWords = 16; // per-part control words before the rank bloc
 constexpr int kCtrlNonceWord = 15;
 // MODE_TL timeline of a latency round: global events (the part where each happens writes it), then per local
 // rank the arrival of the round's message (or bulk announcement) and the completion of its bulk copy
-constexpr uint32_t kTlRoundsMax = 64, kTlGlobal = 8, kTlCols = 7;
+constexpr uint32_t kTlRoundsMax = 64, kTlGlobal = 8, kTlCols = 9;
 // per-rank columns: arrival, bulk completion (ring-slot messages: forwards issued), tree parent + 1, and for a
 // message the doorbell pass took: when the spin's polls that found it were issued, when the pass began
 enum TlCol : uint32_t { TLC_ARRIVE = 0, TLC_DONE = 1, TLC_PARENT = 2, TLC_ISSUE = 3, TLC_PASS = 4,
                         TLC_FWD = 5,    // bulk announcement: its forwards issued
-                        TLC_NEXT = 6 }; // bulk announcement: the next spin of wave 0 began
+                        TLC_NEXT = 6,   // bulk announcement: the next spin of wave 0 began
+                        TLC_P1 = 7, TLC_P2 = 8 };  // ring-slot message taken by the doorbell pass: probes in lone()
 enum TlEvent : uint32_t { TL_ORIGIN = 0, TL_POSTED = 1, TL_CLAIMED = 2, TL_MOVED = 3, TL_ROUND = 4, TL_VERIFIED = 5,
                           TL_GEN = 6, TL_DRAINED = 7 };  // (the first sub-job's mover: origin copy written, copy drained)  // [15] the part's creation nonce (rlo_part_connect checks it; rlo_reset keeps it)
 // latency program of a world split over parts: the round word and the per-round delivery counts are

@@ -187,7 +187,7 @@ struct Shared {
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
     uint64_t prof[8], prof_t, dbg[8];
-    uint32_t tl_clk[2];  // MODE_TL: when wave 0's spin issued its polls, when the doorbell pass began
+    uint32_t tl_clk[4];  // MODE_TL: when wave 0's spin issued its polls, when the doorbell pass began, its probes
     uint32_t tl_bfid;    // MODE_TL: a bulk announcement the doorbell pass took (+1), for its TLC_NEXT clock
     int64_t expect_dec;
     uint32_t hist[kHistBins];
@@ -1451,6 +1451,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
             tl_put(P, fid, TLC_ISSUE, lr, S.tl_clk[0]);
             tl_put(P, fid, TLC_PASS, lr, S.tl_clk[1]);
+            tl_put(P, fid, TLC_FWD, lr, S.tl_clk[2]);
+            tl_put(P, fid, TLC_NEXT, lr, S.tl_clk[3]);
         }
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
@@ -1511,6 +1513,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             ok = __ballot(full) == 0 && !held;
         }
         if (!ok) return ~0u;
+        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P1, lr, (uint32_t)now_ticks());
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
                 tl_parent(P, fid, lr, ffrom);
@@ -1585,6 +1588,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
             log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
+        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
         fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
         if constexpr (BULK) {
             if ((P.mode & MODE_TL) && ftag == TAG_BULK && lane == 0) {
@@ -1756,6 +1760,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                    S.b.sdone[S.b.bulk_q & (bsl - 1u)] >= (uint64_t)(S.b.bulk_q / bsl) * (uint64_t)(P.n - 1);
         }
         if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev && !ncmd && !blat) return 0u;
+        if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[2] = (uint32_t)now_ticks();
         if (ldm || nvm || ncmd) {
             // one round trip: lane 8 s + q loads chunk q of the s-th ring head to load, lane kLLVotes j + i
             // vote i of child j (sc1 loads behind the counters, as phase D0 / B)
@@ -1882,6 +1887,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 need_full = true;
                 continue;
             }
+            if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[3] = (uint32_t)now_ticks();
             const uint32_t need = lone(v, g, 0u, true, out_head_r);
             if (need == kHeld || need == kAsked) {  // waits for the host's verdict (asked now: progress)
                 if (need == kAsked) done++;

@@ -217,7 +217,7 @@ class World:
 
 
     def timeline(self):
-        """RLO_FLAG_TIMELINE rows (rlo_hip.h rlo_timeline): uint32 array [rounds][8 global + 7 x local ranks]
+        """RLO_FLAG_TIMELINE rows (rlo_hip.h rlo_timeline): uint32 array [rounds][8 global + 9 x local ranks]
         of 10-ns clock values (0 = not seen on this part); the third per-rank column is the tree parent + 1."""
         stride = ctypes.c_uint32()
         check(self.lib.rlo_timeline(self.h, (ctypes.c_uint32 * 1)(), 0, ctypes.byref(stride)), "rlo_timeline")

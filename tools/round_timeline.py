@@ -48,6 +48,8 @@ for ln in sizes:
         pas = rel(tl[:, 8 + 4 * nl:8 + 5 * nl], t0[:, None])
         fwdb = rel(tl[:, 8 + 5 * nl:8 + 6 * nl], t0[:, None])
         nxts = rel(tl[:, 8 + 6 * nl:8 + 7 * nl], t0[:, None])
+        p1 = rel(tl[:, 8 + 7 * nl:8 + 8 * nl], t0[:, None])
+        p2 = rel(tl[:, 8 + 8 * nl:8 + 9 * nl], t0[:, None])
         nxt = np.append(rel(tl[1:, 0], tl[:-1, 4]), np.nan)  # this round's last pickup -> next origination
         per = np.append(rel(tl[1:, 0], tl[:-1, 0]), np.nan)
         sl = slice(2, None)  # the first rounds warm the caches
@@ -63,7 +65,7 @@ for ln in sizes:
         elif np.isfinite(comp).any():
             # per hop: parent's forwards issued (the origin: its origination) -> child's doorbell pass took it;
             # per rank: took it -> its own forwards issued
-            hop, proc, wait, rtt, pre = [], [], [], [], []
+            hop, proc, wait, rtt, pre, pa, pb, l1, l2, l3 = [], [], [], [], [], [], [], [], [], []
             for r in range(2, len(tl)):
                 for c in range(nl):
                     p = par[r, c]
@@ -76,14 +78,21 @@ for ln in sizes:
                             wait.append(iss[r, c] - sent)
                             rtt.append(pas[r, c] - iss[r, c])
                             pre.append(arr[r, c] - pas[r, c])
+                            pa.append(fwdb[r, c] - pas[r, c])
+                            pb.append(nxts[r, c] - fwdb[r, c])
                     if np.isfinite(comp[r, c]):
                         proc.append(comp[r, c] - arr[r, c])
+                        l1.append(p1[r, c] - arr[r, c])
+                        l2.append(p2[r, c] - p1[r, c])
+                        l3.append(comp[r, c] - p2[r, c])
             if hop:
                 line += " | hop med %5.2f p90 %5.2f, take->forwarded med %5.2f (%d hops)" % (
                     np.median(hop), np.percentile(hop, 90), np.median(proc) if proc else np.nan, len(hop))
+            if l1:
+                line += " [take: checks %5.2f, effects %5.2f, forwards %5.2f]" % (np.median(l1), np.median(l2), np.median(l3))
             if wait:
-                line += " [sent -> poll issued %5.2f, poll -> pass %5.2f, pass -> taken %5.2f; %d]" % (
-                    np.median(wait), np.median(rtt), np.median(pre), len(wait))
+                line += " [sent -> poll issued %5.2f, poll -> pass %5.2f, pass -> taken %5.2f (preamble %5.2f, to the ring loop %5.2f); %d]" % (
+                    np.median(wait), np.median(rtt), np.median(pre), np.median(pa), np.median(pb), len(wait))
         line += " | last pickup %5.2f -> next origin +%5.2f | verified %5.2f" % (md(g["round"]), md(nxt), md(g["verified"]))
         print(line, flush=True)
         for r in range(2, 2 + a.dump):
