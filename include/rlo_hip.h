@@ -138,7 +138,8 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 #define RLO_FLAG_LOG 1u  /* record every delivery / judge / action / result (+ payload bytes) */
 #define RLO_FLAG_HIST 2u /* per-delivery latency histogram                                  */
 #define RLO_FLAG_PROF 4u /* per-phase cycle accounting (diagnostic)                         */
-#define RLO_FLAG_TIMELINE 8u /* latency program: per-round event clocks (rlo_timeline; diagnostic, no path change) */
+#define RLO_FLAG_TIMELINE 8u /* latency program: per-round event clocks (rlo_timeline); diagnostics build only
+                                (make DIAG=1 -> lib_diag/; the product library refuses it with RLO_E_INVAL) */
 
 #define RLO_ORDER_RANDOM 0u /* origin of bcast b = splitmix64(seed + b) % N                      */
 #define RLO_ORDER_SLOTS 1u  /* origin of bcast b = b % N: every rank originates in every "slot" of N

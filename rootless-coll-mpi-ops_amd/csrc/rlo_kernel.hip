@@ -269,14 +269,21 @@ __device__ __forceinline__ uint32_t poll32(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+// MODE_TL (the timeline of a latency round) exists in the diagnostics build only (make DIAG=1, -DRLO_DIAG): its
+// clocks and probes sit on wave 0's hop path, and the product kernel carries none of that code
+#ifdef RLO_DIAG
+#define TL_ON(P) (((P).mode & MODE_TL) != 0u)
+#else
+#define TL_ON(P) false
+#endif
 // MODE_TL: the clock of event `ev` of latency round r (rlo_device.hpp kTlGlobal; the latest writer wins)
 __device__ __forceinline__ void tl_mark(const Params& P, uint32_t r, uint32_t ev) {
-    if ((P.mode & MODE_TL) && r < P.tl_rounds)
+    if (TL_ON(P) && r < P.tl_rounds)
         atomicMax(&P.tl[r * (kTlGlobal + kTlCols * P.n_local) + ev], (uint32_t)now_ticks());
 }
 // MODE_TL: per-rank column col (rlo_device.hpp TlCol) of local rank lr for round r := v
 __device__ __forceinline__ void tl_put(const Params& P, uint32_t r, uint32_t col, int lr, uint32_t v) {
-    if ((P.mode & MODE_TL) && r < P.tl_rounds) P.tl[r * (kTlGlobal + kTlCols * P.n_local) + kTlGlobal + col * P.n_local + lr] = v;
+    if (TL_ON(P) && r < P.tl_rounds) P.tl[r * (kTlGlobal + kTlCols * P.n_local) + kTlGlobal + col * P.n_local + lr] = v;
 }
 __device__ __forceinline__ void tl_parent(const Params& P, uint32_t r, int lr, int from) {
     tl_put(P, r, TLC_PARENT, lr, (uint32_t)(from + 1));
@@ -299,7 +306,7 @@ __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { retu
 // pass needs the full iteration, [3] 64 passes, [4] job posts queued, [5] a bulk copy complete, [6] a polled word moved
 #define SPIN_WHY(k)                                           \
     do {                                                      \
-        if ((P.mode & MODE_TL) && lane == 0) S.dbg[(k)]++;    \
+        if (TL_ON(P) && lane == 0) S.dbg[(k)]++;    \
     } while (0)
 // MODE_PROF: thread 0 charges the shader cycles since the last stamp to phase `ph`
 #define PROF_STAMP(ph)                                  \
@@ -1447,7 +1454,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const int forg = (int)(fw0 & 0xffffu);
         const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
         const uint32_t fpseq = fw2 >> 24;
-        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) {
+        if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) {
             tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
             tl_put(P, fid, TLC_ISSUE, lr, S.tl_clk[0]);
             tl_put(P, fid, TLC_PASS, lr, S.tl_clk[1]);
@@ -1513,7 +1520,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             ok = __ballot(full) == 0 && !held;
         }
         if (!ok) return ~0u;
-        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P1, lr, (uint32_t)now_ticks());
+        if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P1, lr, (uint32_t)now_ticks());
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
                 tl_parent(P, fid, lr, ffrom);
@@ -1588,15 +1595,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
             log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
-        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
+        if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
         fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
         if constexpr (BULK) {
-            if ((P.mode & MODE_TL) && ftag == TAG_BULK && lane == 0) {
+            if (TL_ON(P) && ftag == TAG_BULK && lane == 0) {
                 tl_put(P, fid, TLC_FWD, lr, (uint32_t)now_ticks());
                 S.tl_bfid = fid + 1u;
             }
         }
-        if ((P.mode & MODE_TL) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
+        if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
         if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
             st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
         if (ftag == TAG_BCAST && (P.mode & MODE_LAT) && lane == 0) {  // the round's last pickup
@@ -1690,7 +1697,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         // the data words to LDS at once (registers are the kernel's scarcest resource): chunk q of in-edge
         // k's bell at kLLBell + 16 (8 k + q), child j's vote bell {word, pid} at kLLBellVote + 8 j
         *reinterpret_cast<u32x4*>(stage + kLLBell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
-        if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[1] = (uint32_t)now_ticks();
+        if (TL_ON(P) && lane == 0) S.tl_clk[1] = (uint32_t)now_ticks();
         if (lane < sll) *reinterpret_cast<uint2*>(stage + kLLBellVote + 8u * (uint32_t)lane) = make_uint2(vb.x, vb.z);
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
         const uint32_t lcap = min(nsmall, kBellChunks);
@@ -1760,7 +1767,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                    S.b.sdone[S.b.bulk_q & (bsl - 1u)] >= (uint64_t)(S.b.bulk_q / bsl) * (uint64_t)(P.n - 1);
         }
         if (!fh && !ldm && !vhm && !nvm && !lat_go && !iar_dev && !ncmd && !blat) return 0u;
-        if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[2] = (uint32_t)now_ticks();
+        if (TL_ON(P) && lane == 0) S.tl_clk[2] = (uint32_t)now_ticks();
         if (ldm || nvm || ncmd) {
             // one round trip: lane 8 s + q loads chunk q of the s-th ring head to load, lane kLLVotes j + i
             // vote i of child j (sc1 loads behind the counters, as phase D0 / B)
@@ -1887,7 +1894,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 need_full = true;
                 continue;
             }
-            if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[3] = (uint32_t)now_ticks();
+            if (TL_ON(P) && lane == 0) S.tl_clk[3] = (uint32_t)now_ticks();
             const uint32_t need = lone(v, g, 0u, true, out_head_r);
             if (need == kHeld || need == kAsked) {  // waits for the host's verdict (asked now: progress)
                 if (need == kAsked) done++;
@@ -2017,7 +2024,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         bool any = false;
         if constexpr (BULK) {
             const uint32_t nb = (uint32_t)uni((int)S.b.nbact);
-            if ((P.mode & MODE_TL) && lane == 0) S.tl_clk[1] = (uint32_t)now_ticks();
+            if (TL_ON(P) && lane == 0) S.tl_clk[1] = (uint32_t)now_ticks();
             // my flag lines through one resource: a line's 16 count shards in four 16-B loads (sixteen 4-B loads
             // of one line queued behind each other at the memory: ~1.8 us per poll, vs one load's round trip)
             const __amdgpu_buffer_rsrc_t rfl = mk_rsrc(reinterpret_cast<void*>(uni64(S.b.fbase)), (uint32_t)P.n * bsl * kBulkLine);
@@ -2040,7 +2047,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                     dn = e < (uint32_t)P.n * bsl && tc >= bpend[e].ntiles;
                     // MODE_TL: when the evaluation that found the copy complete began, when its loads were back
-                    if ((P.mode & MODE_TL) && dn) {
+                    if (TL_ON(P) && dn) {
                         tl_put(P, bpend[e].bid, TLC_PASS, lr, (uint32_t)now_ticks());
                         tl_put(P, bpend[e].bid, TLC_ISSUE, lr, S.tl_clk[1]);
                     }
@@ -2081,7 +2088,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else if (host && lane < 2 && ((sp & 3u) == 0u || S.hwait != 0u)) {
                     hpoll = poll64_sys(&hctl_dev[lane == 0 ? kHctlInjTail : kHctlPkHead]);
                 }
-                if ((P.mode & MODE_TL) && lane == 0) {
+                if (TL_ON(P) && lane == 0) {
                     S.tl_clk[0] = (uint32_t)now_ticks();
                     if (BULK && S.tl_bfid) { tl_put(P, S.tl_bfid - 1u, TLC_NEXT, lr, S.tl_clk[0]); S.tl_bfid = 0; }
                 }

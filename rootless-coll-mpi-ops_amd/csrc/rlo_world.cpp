@@ -1192,6 +1192,9 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     w->tl_rows = 0;
     P.tl = nullptr;
     P.tl_rounds = 0;
+#ifndef RLO_DIAG
+    if (flags & RLO_FLAG_TIMELINE) return RLO_E_INVAL;  // (the diagnostics build's: make DIAG=1)
+#endif
     if (flags & RLO_FLAG_TIMELINE) {
         w->tl_rows = std::min<uint32_t>(rounds, rlo::kTlRoundsMax);
         if (w->d_tl.alloc((size_t)w->tl_rows * (rlo::kTlGlobal + rlo::kTlCols * (uint32_t)w->nl))) return RLO_E_HIP;

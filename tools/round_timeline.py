@@ -9,6 +9,7 @@ import sys
 
 import numpy as np
 
+os.environ.setdefault("RLO_DIAG_LIB", "1")  # RLO_FLAG_TIMELINE: the diagnostics build (make DIAG=1 -> lib_diag/)
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rootless-coll-mpi-ops_amd"))
 import rlo  # noqa: E402
