@@ -272,6 +272,8 @@ int rlo_host_running(rlo_world_t* w);
 int rlo_host_cmd_count(rlo_world_t* w, int rank, uint64_t* consumed, uint64_t* posted);
 /* number of HIP devices visible to this process (0 without a GPU) */
 int rlo_device_count(void);
+/* the NUMA node of HIP device `device` (its PCI function's numa_node in sysfs), -1 if unknown */
+int rlo_device_numa_node(int device);
 
 /* ---- bulk messages in the host-service program (the drop-in's RLO_bcast_gen beyond a slot).
  * rlo_host_bulk_stage: takes local rank `rank`'s next bulk sequence q, waits (RLO_E_AGAIN after

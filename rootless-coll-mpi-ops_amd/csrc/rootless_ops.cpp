@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <ctime>
 #include <cstring>
+#include <sched.h>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -565,6 +566,65 @@ void pump_loop() {
     }
 }
 
+// The rank processes onto the NUMA node of their part's GPU: the application thread, and the threads started from
+// here on (the pump; the leader's proxy) inherit the mask.  The shared segment's per-rank lines are written by
+// the rank's CPU and read by the GPU and the proxy, so a rank on the far socket pays remote-socket latency on every
+// command and pickup: 8 ranks unpinned ran the storm at 0.27-0.47 M bcast/s and the host-judge decisions at
+// 34.6-40.8 K/s from run to run, on the GPU's node 0.48-0.50 M and 41.3 K, on the other node 0.30 M and 34.6 K
+// (profiles/r4_dropin_numa_ab.txt).  Left alone: a process the launcher already placed within one node
+// (mpiexec -bind-to ..., taskset), RLO_NUMA_BIND=0, or a node that is unknown or has none of our CPUs
+static std::vector<int> node_cpus(int node) {
+    std::vector<int> out;
+    char path[96];
+    std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    FILE* f = std::fopen(path, "r");
+    if (!f) return out;
+    char buf[4096] = {0};
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    for (char* tok = std::strtok(buf, ",\n"); tok; tok = std::strtok(nullptr, ",\n")) {
+        int a = 0, b = 0;
+        if (std::sscanf(tok, "%d-%d", &a, &b) == 2) {
+            for (int c = a; c <= b; c++) out.push_back(c);
+        } else if (std::sscanf(tok, "%d", &a) == 1) {
+            out.push_back(a);
+        }
+    }
+    return out;
+}
+static int node_of_cpu(int cpu) {
+    for (int nd = 0; nd < 64; nd++) {
+        char path[96];
+        std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpu%d", nd, cpu);
+        if (access(path, F_OK) == 0) return nd;
+    }
+    return -1;
+}
+static void numa_bind(int node) {
+    if (node < 0) return;
+    if (const char* v = std::getenv("RLO_NUMA_BIND"))
+        if (std::strcmp(v, "0") == 0) return;
+    cpu_set_t cur;
+    CPU_ZERO(&cur);
+    if (sched_getaffinity(0, sizeof cur, &cur) != 0) return;
+    int first_node = -2;
+    bool one_node = true;
+    for (int c = 0; c < CPU_SETSIZE && one_node; c++) {
+        if (!CPU_ISSET(c, &cur)) continue;
+        const int nd = node_of_cpu(c);
+        if (first_node == -2) first_node = nd;
+        else if (nd != first_node) one_node = false;
+    }
+    if (one_node) return;  // placed by the launcher
+    cpu_set_t want;
+    CPU_ZERO(&want);
+    int k = 0;
+    for (int c : node_cpus(node))
+        if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &cur)) { CPU_SET(c, &want); k++; }
+    if (k) (void)sched_setaffinity(0, sizeof want, &want);
+}
+
 void pump_start() {
     if (g_pump.joinable() || std::getenv("RLO_NO_PUMP")) return;
     g_pump_stop = false;
@@ -831,6 +891,11 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     e->device = dev_of(part_begin[part]);  // a part's ranks share its leader's GPU
     e->leader = e->rank == part_begin[part];
     MPI_Comm_split(e->comm, part, e->rank, &e->group);
+    {  // every process of the part onto its GPU's NUMA node (the leader asks HIP; group rank 0 is the leader)
+        int numa = e->leader ? rlo_device_numa_node(e->device) : -1;
+        MPI_Bcast(&numa, 1, MPI_INT, 0, e->group);
+        numa_bind(numa);
+    }
     MPI_Comm leaders;
     MPI_Comm_split(e->comm, e->leader ? 0 : MPI_UNDEFINED, e->rank, &leaders);
     // extension: device judges -- the kinds must agree; ISP strings go to the part's leader

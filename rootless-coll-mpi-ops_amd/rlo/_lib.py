@@ -125,7 +125,7 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_last_kernel_ms", "rlo_stats", "rlo_log", "rlo_latencies", "rlo_round_ticks", "rlo_timeline", "rlo_strerror", "rlo_last_hip_error",
            "rlo_device_error", "rlo_bulk_debug",
            "rlo_program_host", "rlo_host_post", "rlo_host_poll", "rlo_host_running", "rlo_host_cmd_count",
-           "rlo_device_count", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan", "rlo_layout_plan",
+           "rlo_device_count", "rlo_device_numa_node", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan", "rlo_layout_plan",
            "rlo_storm_lengths", "rlo_host_share", "rlo_host_unlink", "rlo_host_proxy", "rlo_host_wait_started",
            "rlo_host_fail", "rlo_client_attach", "rlo_client_detach", "rlo_client_state", "rlo_client_post",
            "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_client_hdiag", "rlo_client_fwd", "rlo_host_device_judge"]
@@ -172,6 +172,7 @@ def load():
     L.rlo_host_running.argtypes = [vp]
     L.rlo_host_cmd_count.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.rlo_device_count.argtypes = []
+    L.rlo_device_numa_node.argtypes = [ctypes.c_int]
     L.rlo_host_bulk_stage.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32,
                                       ctypes.POINTER(ctypes.c_uint32)]
     L.rlo_host_bulk_copy.argtypes = [vp, ctypes.c_int, ctypes.POINTER(LogRec), vp]
