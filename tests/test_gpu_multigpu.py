@@ -220,3 +220,57 @@ def test_bench_two_parts_under_torchrun():
         _check_dump(dump, 2)  # against the oracle, not only step-to-step repeatability
     finally:
         shutil.rmtree(dump, ignore_errors=True)
+
+
+def _stale_part(part, tamper, blob_q, blobs_q, out_q, done_q):
+    """one part process of a 16-rank, 2-part world on this GPU; `tamper`: before connecting, change the creation
+    nonce the peer's blob carries (PartBlob.nonce, byte 480 of the blob), as a mapping of an earlier allocation
+    would show it"""
+    try:
+        import rlo
+
+        w = rlo.World.part(16, 2, part, part_begin=[0, 8, 16], max_payload=64, uncached=True)
+        blob_q.put((part, w.export()))
+        blobs = list(blobs_q.get(timeout=120))
+        if tamper:
+            b = bytearray(blobs[1 - part])
+            b[480] ^= 0x5A
+            blobs[1 - part] = bytes(b)
+        try:
+            w.connect(blobs)
+            out_q.put((part, "ok"))
+        except rlo.RloError as e:
+            out_q.put((part, str(e)))
+        done_q.get(timeout=120)  # the peer is done with its mapping of this part
+        w.close()
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        out_q.put((part, "error: %r" % e))
+
+
+def test_connect_detects_stale_mapping(rlo):
+    """rlo_part_connect reads every imported region's creation nonce back through its mapping: a blob whose
+    nonce the mapped memory does not show (what an IPC import of an earlier allocation looks like) fails the
+    connection with RLO_E_STALE, naming no wrong memory as a ring; the untampered peer connects"""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    blob_q, out_q = ctx.Queue(), ctx.Queue()
+    blobs_qs = [ctx.Queue(), ctx.Queue()]
+    done_qs = [ctx.Queue(), ctx.Queue()]
+    procs = [ctx.Process(target=_stale_part, args=(p, p == 1, blob_q, blobs_qs[p], out_q, done_qs[p])) for p in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(blob_q.get(timeout=180) for _ in range(2))
+        for q in blobs_qs:
+            q.put([got[0], got[1]])
+        res = dict(out_q.get(timeout=180) for _ in range(2))
+        for q in done_qs:
+            q.put(1)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert res[0] == "ok", res
+    assert "[-10]" in res[1] and "stale" in res[1], res
