@@ -829,6 +829,7 @@ __device__ __forceinline__ void flush_posts(BulkSh& B, const Params& P, int lane
         }
         j0 = rdl64(j0, 0);
         uint64_t* const jf = P.jfree + (size_t)cls * P.jslots;
+        const __amdgpu_buffer_rsrc_t rj = mk_rsrc(reinterpret_cast<void*>(P.jobs + (size_t)cls * P.jslots), P.jslots * (uint32_t)sizeof(BulkJob));
         const uint32_t parent = (uint32_t)(j0 & jm);
         for (uint32_t u = (uint32_t)lane; u < nsub; u += 64u) {
             const uint64_t j = j0 + u;
@@ -844,11 +845,14 @@ __device__ __forceinline__ void flush_posts(BulkSh& B, const Params& P, int lane
             if (!ok) break;
             u32x4* dst = reinterpret_cast<u32x4*>(P.jobs + (size_t)cls * P.jslots + (uint32_t)(j & jm));
             const uint32_t a = u * per, nt = min(per, ntiles - a);
+            // the body: one 8-B store and three 16-B sc1 stores (the job ring is part-local uncached memory,
+            // read by this part's movers only); the 8 bytes holding the sequence go last, after the drain
             __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + 1, (uint64_t)origin | ((uint64_t)lr << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            st_sys16(dst + 1, u32x4{slot_s, (uint32_t)uni((int)r.bid), len, nt});
-            st_sys16(dst + 2, u32x4{a, parent, (uint32_t)uni((int)r.from), (uint32_t)uni((int)r.logidx)});
-            st_sys16(dst + 3, u32x4{(uint32_t)uni((int)r.q), (uint32_t)uni((int)r.gen), ntiles, (uint32_t)j0});
+                               __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t jo = (uint32_t)(j & jm) * (uint32_t)sizeof(BulkJob);
+            st_sc1(rj, jo + 16u, u32x4{slot_s, (uint32_t)uni((int)r.bid), len, nt});
+            st_sc1(rj, jo + 32u, u32x4{a, parent, (uint32_t)uni((int)r.from), (uint32_t)uni((int)r.logidx)});
+            st_sc1(rj, jo + 48u, u32x4{(uint32_t)uni((int)r.q), (uint32_t)uni((int)r.gen), ntiles, (uint32_t)j0});
         }
     }
     VM_DRAIN();
@@ -924,8 +928,11 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
     BulkSh& S = SS.b;
     constexpr int kT = 64 * W;
     const uint32_t mi = blockIdx.x - P.n_local;
+    // chunked plans: class A the SCATTER and VERIFY jobs, class B the GATHERs (which wait), half the movers each.
+    // Direct plans (one GPU) post no GATHERs: every mover serves class A, VERIFYs in FIFO order with the scatters.
+    // (VERIFYs on a dedicated share of the movers -- 4, 7, 10 sixteenths -- cut a 64-MiB round to 160-214 us but
+    // left the verifications behind: 278-609 us of kernel per round against 267 us all in one class)
     const uint32_t na = (P.nmov + 1u) / 2u;
-    // (direct plans -- one GPU -- post no GATHER jobs: every mover serves class A)
     const uint32_t cls = (P.bulk_cross == 0u || mi < na) ? JCLS_A : JCLS_B;
     const bool sys = P.sys_scope != 0;
     const int n = P.n;

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "librlo_hip.so")
 if os.environ.get("RLO_DIAG_LIB") == "1":
     LIB_PATH = os.path.join(PKG_DIR, "lib_diag", "librlo_hip.so")
 _AB = os.environ.get("RLO_LIB_DIR", "")
-if re.fullmatch(r"lib_[a-z0-9]+", _AB):
+if re.fullmatch(r"lib_[a-z0-9_]+", _AB):
     LIB_PATH = os.path.join(PKG_DIR, _AB, "librlo_hip.so")
 
 RLO_OK = 0

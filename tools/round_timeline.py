@@ -36,7 +36,7 @@ for ln in sizes:
     with (rlo.World(a.n, max_payload=max(64, ln)) if ln <= 112 else
           rlo.World(a.n, max_payload=64, bulk_max=a.bulk_max)) as w:
         w.program_latency(a.rounds, ln, seed=0x7100 + ln, timeline=True)
-        w.run()
+        kms = w.run()
         st = w.stats()
         assert (st["error"] == 0).all(), (st["error"], st["error_aux"])
         tl = w.timeline()
@@ -95,6 +95,7 @@ for ln in sizes:
                 line += " [sent -> poll issued %5.2f, poll -> pass %5.2f, pass -> taken %5.2f (preamble %5.2f, to the ring loop %5.2f); %d]" % (
                     np.median(wait), np.median(rtt), np.median(pre), np.median(pa), np.median(pb), len(wait))
         line += " | last pickup %5.2f -> next origin +%5.2f | verified %5.2f" % (md(g["round"]), md(nxt), md(g["verified"]))
+        line += " | kernel %.2f us per round" % (kms * 1e3 / a.rounds)
         print(line, flush=True)
         for r in range(2, 2 + a.dump):
             print("    round %d: origin %d, posted %.2f claimed %.2f moved %.2f round %.2f" % (
