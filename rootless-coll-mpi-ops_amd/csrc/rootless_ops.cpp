@@ -593,14 +593,6 @@ static std::vector<int> node_cpus(int node) {
     }
     return out;
 }
-static int node_of_cpu(int cpu) {
-    for (int nd = 0; nd < 64; nd++) {
-        char path[96];
-        std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpu%d", nd, cpu);
-        if (access(path, F_OK) == 0) return nd;
-    }
-    return -1;
-}
 static void numa_bind(int node) {
     if (node < 0) return;
     if (const char* v = std::getenv("RLO_NUMA_BIND"))
@@ -608,15 +600,15 @@ static void numa_bind(int node) {
     cpu_set_t cur;
     CPU_ZERO(&cur);
     if (sched_getaffinity(0, sizeof cur, &cur) != 0) return;
-    int first_node = -2;
-    bool one_node = true;
-    for (int c = 0; c < CPU_SETSIZE && one_node; c++) {
-        if (!CPU_ISSET(c, &cur)) continue;
-        const int nd = node_of_cpu(c);
-        if (first_node == -2) first_node = nd;
-        else if (nd != first_node) one_node = false;
+    // the nodes my current mask touches (the node cpulists, read once)
+    int touched = 0;
+    for (int nd = 0; nd < 64 && touched < 2; nd++) {
+        bool any = false;
+        for (int c : node_cpus(nd))
+            if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &cur)) { any = true; break; }
+        touched += any ? 1 : 0;
     }
-    if (one_node) return;  // placed by the launcher
+    if (touched < 2) return;  // placed within one node by the launcher (or no node information)
     cpu_set_t want;
     CPU_ZERO(&want);
     int k = 0;
