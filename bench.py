@@ -237,7 +237,7 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
         # GPU leader process runs the application thread beside its pump and proxy threads
         rec = {"ranks": nr, "ours": {}, "reference_host_mpi": {}, "cores": nr, "cores_available": avail,
                "pinning": {"reference_host_mpi": "mpiexec -bind-to core: one core per rank (%d cores)" % nr,
-                           "ours": "none (%d cores available; the GPU does the engine's work)" % avail}}
+                           "ours": "RLO_NUMA_BIND=all: every thread of a rank process on the GPU's NUMA node (%d cores available)" % avail}}
         runs = {"ours": {}, "reference_host_mpi": {}}
         for rep in range(reps):
             for name, exe in (("ours", ours), ("reference_host_mpi", ref)):
@@ -248,7 +248,13 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
                     note("api n=%d %s %s (%d/%d)" % (nr, name, leg, rep + 1, reps))
                     try:
                         # iarpool: the proposal pool extension, 16 own proposals in flight per rank
-                        env = dict(os.environ, RLO_PROPOSAL_POOL="16") if leg == "iarpool" else None
+                        env = None
+                        if name == "ours":
+                            # the application opts in to having its own thread placed on the GPU's NUMA node
+                            # (the reference is placed by mpiexec -bind-to core)
+                            env = dict(os.environ, RLO_NUMA_BIND="all")
+                            if leg == "iarpool":
+                                env["RLO_PROPOSAL_POOL"] = "16"
                         bind = ["-bind-to", "core"] if name == "reference_host_mpi" else []
                         cmd = ["timeout", "-k", "5", str(timeout_s), mpiexec] + bind + ["-n", str(nr), exe] + args
                         r, seen = _run_sampled(cmd, timeout_s, env=env)

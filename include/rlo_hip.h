@@ -50,7 +50,9 @@ extern "C" {
 #define RLO_DERR_BAD_SLOT 6
 #define RLO_DERR_HOST_CMD 7      /* malformed / unexpected host-service command                */
 #define RLO_DERR_BULK 8          /* a bulk-message index / job field out of range (a bug: reported
-                                    instead of touching memory outside the heaps)                  */
+                                    instead of touching memory outside the heaps); site 14: a device
+                                    program's VERIFY read a granule that is not what the origin wrote
+                                    (aux value = receiver rank & 0xff << 16 | 16-KiB block of the message) */
 
 /* ------------------------------------------------------------------ topology (host only) */
 /* skip-ring overlay, restated from rootless_ops.c:1416-1579; usable without a GPU */
@@ -82,11 +84,13 @@ typedef struct {
 
 typedef struct {
     int32_t n_ranks, max_in_degree, max_fanout, edges;
-    uint32_t ring_slots, slot_stride, vote_slots, pad;
+    uint32_t ring_slots, slot_stride, vote_slots;
+    uint32_t peers;       /* RLO_PEER_*: where this part's peer parts are (set by rlo_part_connect)     */
     uint64_t fwd_bytes, vote_bytes, ctrl_bytes; /* this part's regions                    */
     int32_t cus, blocks_per_cu;
     int32_t part, n_parts, rank_begin, rank_end; /* ranks [rank_begin, rank_end) are local */
-    int32_t sys_scope;                           /* 1: parts span GPUs (system-scope stores) */
+    int32_t sys_scope;                           /* 1: system-scope remote stores and publishes: a peer part on
+                                                    another GPU or in another process (peers)              */
     int32_t waves;                               /* waves per rank-workgroup: 8 (512 messages per
                                                     iteration) or 4 (256), chosen at creation     */
     uint32_t bulk_slots, movers;                 /* bulk: heap slots per origin, mover workgroups   */
@@ -112,6 +116,8 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
  * part: same process = direct pointer, other process = hipIpc / dmabuf, xGMI across GPUs).
  * Every part must rlo_reset before ANY part launches (host barrier in between). */
 #define RLO_PART_BLOB_BYTES 512u
+#define RLO_PEER_OTHER_GPU 1u  /* rlo_world_info_t.peers: some peer part is on another GPU (xGMI; the chunked bulk plan) */
+#define RLO_PEER_IMPORTED 2u   /* ... some peer part is in another process (its regions hipIpc-imported)            */
 #define RLO_PART_UNCACHED 1u /* allocate the part's rings uncached (for peer GPUs writing over xGMI) */
 #define RLO_PART_PEND_HBM 4u /* the pending-proposal tables in HBM whatever the world size (the layout an 8-GPU
                                  * world takes, rehearsed at smaller N; every part must set it alike) */

@@ -32,6 +32,7 @@ constexpr int kHistBins = 128;    // latency histogram: 4 sub-bins per octave of
 constexpr int kMaxParts = 64;     // parts (processes x GPUs) of one world
 constexpr int kPoolMax = 16;      // own proposals in flight per rank (PROPOSAL_POOL_SIZE, rootless_ops.c:30)
 constexpr int kCtrlHdrWords = 16; // per-part control words before the rank blocks: [0] error flag
+// [15] the part's creation nonce (rlo_part_connect checks it through every peer's mapping; rlo_reset keeps it)
 constexpr int kCtrlNonceWord = 15;
 // MODE_TL timeline of a latency round: global events (the part where each happens writes it), then per local
 // rank the arrival of the round's message (or bulk announcement) and the completion of its bulk copy
@@ -43,7 +44,7 @@ enum TlCol : uint32_t { TLC_ARRIVE = 0, TLC_DONE = 1, TLC_PARENT = 2, TLC_ISSUE 
                         TLC_NEXT = 6,   // bulk announcement: the next spin of wave 0 began
                         TLC_P1 = 7, TLC_P2 = 8 };  // ring-slot message taken by the doorbell pass: probes in lone()
 enum TlEvent : uint32_t { TL_ORIGIN = 0, TL_POSTED = 1, TL_CLAIMED = 2, TL_MOVED = 3, TL_ROUND = 4, TL_VERIFIED = 5,
-                          TL_GEN = 6, TL_DRAINED = 7 };  // (the first sub-job's mover: origin copy written, copy drained)  // [15] the part's creation nonce (rlo_part_connect checks it; rlo_reset keeps it)
+                          TL_GEN = 6, TL_DRAINED = 7 };  // (the first sub-job's mover: origin copy written, copy drained)
 // latency program of a world split over parts: the round word and the per-round delivery counts are
 // one world-wide copy in part 0's control region (peer-mapped like the ring counters), after its rank
 // blocks: [round word, own 128-B line][counts: kLatCap x u32]
@@ -205,7 +206,7 @@ struct Params {
     uint64_t* lat_out;            // [lat_rounds] completion ticks
     uint32_t* lat_round;          // current round (global; part 0's control region when sharded)
     uint64_t* lat_obs;            // [lat_rounds] observer clock (world rank 0) when round i completed
-    uint32_t* tl;                 // MODE_TL: [tl_rounds][kTlGlobal + 2 n_local] low 32 bits of the 100-MHz clock
+    uint32_t* tl;                 // MODE_TL: [tl_rounds][kTlGlobal + kTlCols n_local] low 32 bits of the 100-MHz clock
     uint32_t tl_rounds;
     const uint32_t* lat_own_off;  // [n_local + 1] CSR of the rounds each local rank originates
     const uint32_t* lat_own;

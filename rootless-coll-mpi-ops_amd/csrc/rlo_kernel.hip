@@ -1175,6 +1175,13 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                                 const u32x4 w = {mask_bytes(v[uu].x, b0), mask_bytes(v[uu].y, b0 - 4),
                                                  mask_bytes(v[uu].z, b0 - 8), mask_bytes(v[uu].w, b0 - 12)};
                                 acc += chunk_mix(off >> 4, w);
+                                // the engine's own check of every delivered byte: a device program's bulk
+                                // message is the storm payload of (origin, bid), so a granule that is not
+                                // what the origin wrote -- a tile whose stores never became visible behind a
+                                // complete count -- is a device error, not a wrong sum
+                                const u32x4 x = storm_granule((uint32_t)o, jb.bid, len, off);
+                                if (w.x != x.x || w.y != x.y || w.z != x.z || w.w != x.w)
+                                    bulk_fault(P, 14, (uint32_t)(me & 0xff) << 16 | ((off >> 14) & 0xffffu));
                             }
                         }
                     };

@@ -359,7 +359,8 @@ struct rlo_world {
     uint32_t max_payload = 0, flags = 0;
     int cus = 0, blocks_per_cu = 0;
     bool connected = false;
-    int sys_scope = 0;
+    int sys_scope = 0;  // system-scope remote stores / publishes: some peer on another GPU or in another process
+    uint32_t peers = 0;  // RLO_PEER_*
     // local regions (the rings / counters this part consumes)
     uint8_t* fwd = nullptr;
     uint8_t* vote = nullptr;
@@ -855,6 +856,7 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
     HIPCHK(hipDeviceGetPCIBusId(mybus, sizeof mybus, w->device));
     const uint64_t tok = process_token();
     w->sys_scope = 0;
+    w->peers = 0;
     for (int q = 0; q < n_parts; q++) {
         PartBlob b;
         std::memcpy(&b, (const uint8_t*)blobs + (size_t)q * RLO_PART_BLOB_BYTES, sizeof b);
@@ -863,7 +865,13 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
             b.vote_bytes != L.vote_bytes[q] || b.ctrl_bytes != L.ctrl_words[q] * 8 || b.heap_bytes != L.heap_bytes[q] ||
             b.bflag_bytes != L.bflag_bytes[q])
             return RLO_E_INVAL;
-        if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->sys_scope = 1;
+        if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->peers |= RLO_PEER_OTHER_GPU;
+        // A peer in another process (its regions imported through hipIpc, on this GPU or another) gets the
+        // hand-off the 8-GPU world runs: system-scope (sc0 sc1) stores, system-scope counter publishes and
+        // flag adds, system-scope releases before the bulk flags (the round-4 churn
+        // failures).  Only the bulk PLAN follows the GPU layout (RLO_PEER_OTHER_GPU -> chunked).
+        if (q != w->part && b.token != tok) w->peers |= RLO_PEER_IMPORTED;
+        w->sys_scope = w->peers ? 1 : 0;
         // parts on other GPUs store into this part's rings and heaps over xGMI: a cached part's L2
         // could hold lines those system-scope stores do not invalidate (rlo_hip.h RLO_PART_UNCACHED)
         if (w->sys_scope && !(w->flags & RLO_PART_UNCACHED)) return RLO_E_INVAL;
@@ -1005,6 +1013,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->rank_begin = w->rb;
     o->rank_end = w->rb + w->nl;
     o->sys_scope = w->sys_scope;
+    o->peers = w->peers;
     o->waves = w->waves;
     o->bulk_slots = w->L.bslots;
     o->movers = w->nmov;
@@ -1033,6 +1042,9 @@ static uint32_t ll_mode(const rlo_world* w, uint32_t max_msg) {
 }
 
 static void base_params(rlo_world* w) {
+    // the previous program is gone from here on: a setup that fails below leaves no half-set program a later
+    // rlo_launch could run
+    w->have_program = false;
     rlo::Params& P = w->P;
     std::memset(&P, 0, sizeof P);
     P.n = w->L.n;
@@ -1071,7 +1083,7 @@ static void base_params(rlo_world* w) {
         P.bulk_slots = w->L.bslots;
         P.bulk_cap = w->L.bcap;
         P.nmov = w->nmov;
-        P.bulk_cross = (w->sys_scope || (w->flags & RLO_PART_CHUNKED)) ? 1u : 0u;  // the chunked plan (rlo_device.hpp)
+        P.bulk_cross = ((w->peers & RLO_PEER_OTHER_GPU) || (w->flags & RLO_PART_CHUNKED)) ? 1u : 0u;  // the chunked plan (rlo_device.hpp)
         P.bheap = w->d_bheap.p;
         P.bflag = w->d_bflag.p;
         P.part_of = w->d_part_of.p;
@@ -1151,6 +1163,9 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     if (!w->connected) return RLO_E_NOTCONNECTED;
     // sharded: the round word and counts are part 0's copy, peer-mapped (rlo_device.hpp kLatWords)
     if (w->L.nparts != 1 && rounds > (uint32_t)rlo::kLatCap) return RLO_E_INVAL;
+#ifndef RLO_DIAG
+    if (flags & RLO_FLAG_TIMELINE) return RLO_E_INVAL;  // (the diagnostics build's: make DIAG=1)
+#endif
     base_params(w);
     rlo::Params& P = w->P;
     const int n = w->L.n;
@@ -1193,9 +1208,6 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     w->tl_rows = 0;
     P.tl = nullptr;
     P.tl_rounds = 0;
-#ifndef RLO_DIAG
-    if (flags & RLO_FLAG_TIMELINE) return RLO_E_INVAL;  // (the diagnostics build's: make DIAG=1)
-#endif
     if (flags & RLO_FLAG_TIMELINE) {
         w->tl_rows = std::min<uint32_t>(rounds, rlo::kTlRoundsMax);
         if (w->d_tl.alloc((size_t)w->tl_rows * (rlo::kTlGlobal + rlo::kTlCols * (uint32_t)w->nl))) return RLO_E_HIP;

@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <ctime>
 #include <cstring>
+#include <pthread.h>
 #include <sched.h>
 #include <algorithm>
 #include <atomic>
@@ -79,6 +80,8 @@ struct progress_engine {
     MPI_Comm group = MPI_COMM_NULL;  // the ranks sharing my GPU (one part of the device world)
     int rank = 0, size = 0, id = 0, device = 0;
     bool leader = false;             // group rank 0: owns the part, its kernel and the proxy
+    bool caller_bound = false;       // RLO_NUMA_BIND=all moved the creating thread: its mask to restore at cleanup
+    cpu_set_t caller_mask;
     rlo_world_t* w = nullptr;        // leader only
     void* stream = nullptr;          // leader only
     rlo_client_t* cl = nullptr;      // every rank: its rank of the part, through the shared segment
@@ -566,13 +569,17 @@ void pump_loop() {
     }
 }
 
-// The rank processes onto the NUMA node of their part's GPU: the application thread, and the threads started from
-// here on (the pump; the leader's proxy) inherit the mask.  The shared segment's per-rank lines are written by
-// the rank's CPU and read by the GPU and the proxy, so a rank on the far socket pays remote-socket latency on every
-// command and pickup: 8 ranks unpinned ran the storm at 0.27-0.47 M bcast/s and the host-judge decisions at
+// The engine's own threads onto the NUMA node of their part's GPU.  The shared segment's per-rank lines are written
+// by the rank's CPU and read by the GPU and the proxy, so a thread on the far socket pays remote-socket latency on
+// every command and pickup: 8 ranks unpinned ran the storm at 0.27-0.47 M bcast/s and the host-judge decisions at
 // 34.6-40.8 K/s from run to run, on the GPU's node 0.48-0.50 M and 41.3 K, on the other node 0.30 M and 34.6 K
-// (profiles/r4_dropin_numa_ab.txt).  Left alone: a process the launcher already placed within one node
-// (mpiexec -bind-to ..., taskset), RLO_NUMA_BIND=0, or a node that is unknown or has none of our CPUs
+// (profiles/r4_dropin_numa_ab.txt).  RLO_NUMA_BIND:
+//   unset / 1  the pump and proxy threads this library starts, and nothing else: the application's threads keep
+//              the affinity the launcher gave them (the reference library changes no affinity at all);
+//   all        the calling application thread too, for the engine's lifetime (its mask is restored at cleanup);
+//   0          no thread.
+// A process the launcher already placed within one node (mpiexec -bind-to ..., taskset) is left alone, as is an
+// unknown node or one with none of the process's CPUs.
 static std::vector<int> node_cpus(int node) {
     std::vector<int> out;
     char path[96];
@@ -593,14 +600,17 @@ static std::vector<int> node_cpus(int node) {
     }
     return out;
 }
-static void numa_bind(int node) {
-    if (node < 0) return;
-    if (const char* v = std::getenv("RLO_NUMA_BIND"))
-        if (std::strcmp(v, "0") == 0) return;
-    cpu_set_t cur;
-    CPU_ZERO(&cur);
-    if (sched_getaffinity(0, sizeof cur, &cur) != 0) return;
-    // the nodes my current mask touches (the node cpulists, read once)
+enum NumaMode { kNumaOff = 0, kNumaEngine = 1, kNumaAll = 2 };
+static NumaMode numa_mode() {
+    const char* v = std::getenv("RLO_NUMA_BIND");
+    if (!v || !*v || std::strcmp(v, "1") == 0) return kNumaEngine;
+    if (std::strcmp(v, "all") == 0) return kNumaAll;
+    return kNumaOff;
+}
+// the CPUs of `node` within `cur`, or false when `cur` already lies within one node (the launcher placed the
+// process), the node is unknown or holds none of `cur`'s CPUs
+static bool numa_mask(int node, const cpu_set_t& cur, cpu_set_t* want) {
+    if (node < 0) return false;
     int touched = 0;
     for (int nd = 0; nd < 64 && touched < 2; nd++) {
         bool any = false;
@@ -608,19 +618,27 @@ static void numa_bind(int node) {
             if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &cur)) { any = true; break; }
         touched += any ? 1 : 0;
     }
-    if (touched < 2) return;  // placed within one node by the launcher (or no node information)
-    cpu_set_t want;
-    CPU_ZERO(&want);
+    if (touched < 2) return false;
+    CPU_ZERO(want);
     int k = 0;
     for (int c : node_cpus(node))
-        if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &cur)) { CPU_SET(c, &want); k++; }
-    if (k) (void)sched_setaffinity(0, sizeof want, &want);
+        if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &cur)) { CPU_SET(c, want); k++; }
+    return k > 0;
+}
+int g_numa_node = -1;        // the NUMA node of the latest engine's GPU (engine threads follow it)
+cpu_set_t g_proc_mask;       // the process's affinity before this library changed any thread's
+bool g_proc_mask_ok = false;
+static void bind_engine_thread(std::thread& t) {
+    if (!t.joinable() || !g_proc_mask_ok || numa_mode() == kNumaOff) return;
+    cpu_set_t want;
+    if (numa_mask(g_numa_node, g_proc_mask, &want)) (void)pthread_setaffinity_np(t.native_handle(), sizeof want, &want);
 }
 
 void pump_start() {
     if (g_pump.joinable() || std::getenv("RLO_NO_PUMP")) return;
     g_pump_stop = false;
     g_pump = std::thread(pump_loop);
+    bind_engine_thread(g_pump);
 }
 
 void pump_stop() {
@@ -701,6 +719,7 @@ void proxy_start() {
     if (g_proxy.joinable()) return;
     g_proxy_stop = false;
     g_proxy = std::thread(proxy_loop);
+    bind_engine_thread(g_proxy);
 }
 
 void proxy_stop() {
@@ -883,10 +902,22 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     e->device = dev_of(part_begin[part]);  // a part's ranks share its leader's GPU
     e->leader = e->rank == part_begin[part];
     MPI_Comm_split(e->comm, part, e->rank, &e->group);
-    {  // every process of the part onto its GPU's NUMA node (the leader asks HIP; group rank 0 is the leader)
+    {  // the engine's threads onto its GPU's NUMA node (the leader asks HIP; group rank 0 is the leader)
         int numa = e->leader ? rlo_device_numa_node(e->device) : -1;
         MPI_Bcast(&numa, 1, MPI_INT, 0, e->group);
-        numa_bind(numa);
+        if (!g_proc_mask_ok) {
+            CPU_ZERO(&g_proc_mask);
+            g_proc_mask_ok = sched_getaffinity(0, sizeof g_proc_mask, &g_proc_mask) == 0;
+        }
+        g_numa_node = numa;
+        bind_engine_thread(g_pump);  // already running for an earlier engine
+        bind_engine_thread(g_proxy);
+        cpu_set_t want, cur;
+        if (numa_mode() == kNumaAll && pthread_getaffinity_np(pthread_self(), sizeof cur, &cur) == 0 &&
+            numa_mask(numa, cur, &want) && pthread_setaffinity_np(pthread_self(), sizeof want, &want) == 0) {
+            e->caller_mask = cur;  // restored at cleanup
+            e->caller_bound = true;
+        }
     }
     MPI_Comm leaders;
     MPI_Comm_split(e->comm, e->leader ? 0 : MPI_UNDEFINED, e->rank, &leaders);
@@ -1174,6 +1205,7 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
     if (eng->leader) g_grave.push_back(std::make_pair(eng->w, eng->stream));
     if (!g_engines) bury();
     MPI_Comm_free(&eng->group);
+    if (eng->caller_bound) (void)pthread_setaffinity_np(pthread_self(), sizeof eng->caller_mask, &eng->caller_mask);
     delete eng;
     return 0;
 }

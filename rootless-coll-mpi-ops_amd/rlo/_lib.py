@@ -27,6 +27,7 @@ RLO_PART_BLOB_BYTES = 512
 RLO_PART_UNCACHED = 1
 RLO_PART_CHUNKED = 2
 RLO_PART_PEND_HBM = 4
+RLO_PEER_OTHER_GPU, RLO_PEER_IMPORTED = 1, 2  # rlo_world_info_t.peers
 RLO_LAUNCH_NO_RESET = 1
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF, RLO_FLAG_TIMELINE = 1, 2, 4, 8
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
@@ -50,7 +51,7 @@ class WorldCfg(ctypes.Structure):
 class WorldInfo(ctypes.Structure):
     _fields_ = [("n_ranks", ctypes.c_int32), ("max_in_degree", ctypes.c_int32), ("max_fanout", ctypes.c_int32),
                 ("edges", ctypes.c_int32), ("ring_slots", ctypes.c_uint32), ("slot_stride", ctypes.c_uint32),
-                ("vote_slots", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("fwd_bytes", ctypes.c_uint64),
+                ("vote_slots", ctypes.c_uint32), ("peers", ctypes.c_uint32), ("fwd_bytes", ctypes.c_uint64),
                 ("vote_bytes", ctypes.c_uint64), ("ctrl_bytes", ctypes.c_uint64), ("cus", ctypes.c_int32),
                 ("blocks_per_cu", ctypes.c_int32), ("part", ctypes.c_int32), ("n_parts", ctypes.c_int32),
                 ("rank_begin", ctypes.c_int32), ("rank_end", ctypes.c_int32), ("sys_scope", ctypes.c_int32),

@@ -53,6 +53,9 @@ def merge(results):
     st = {}
     for key in results[0]["stats"]:
         st[key] = np.concatenate([r["stats"][key] for r in results])
+    # per world rank: its part's rlo_world_info_t.peers / sys_scope (where that part's peers are)
+    for key in ("peers", "sys_scope"):
+        st["part_" + key] = np.concatenate([np.full(len(r["stats"]["error"]), r["info"][key]) for r in results])
     logs = {}
     for r in results:
         logs.update(r.get("logs", {}))

@@ -22,6 +22,7 @@ import numpy as np
 import pytest
 
 import pyoracle as orc
+from rlo import _lib as L
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -52,8 +53,8 @@ def test_cross_gpu_peer_switches_to_system_scope(rlo):
         b0, b1 = w0.export(), w1.export()
         w0.connect([b0, _forge_bus(b1)])  # part 1 "on another GPU"
         w1.connect([b0, b1])
-        assert w0.info["sys_scope"] == 1
-        assert w1.info["sys_scope"] == 0
+        assert w0.info["sys_scope"] == 1 and w0.info["peers"] == L.RLO_PEER_OTHER_GPU
+        assert w1.info["sys_scope"] == 0 and w1.info["peers"] == 0  # same GPU, same process
     finally:
         w0.close()
         w1.close()
@@ -108,6 +109,8 @@ def test_bulk_world_churn_processes(rlo):
     for it, ((st, _, _), rcs) in enumerate(runs):
         assert rcs == [0, 0], (it, st["error"], st["error_aux"])
         assert np.array_equal(st["bcast_sum"], want), it
+        # the peer is IPC-imported: both parts run the 8-GPU world's system-scope hand-off
+        assert (st["part_peers"] == L.RLO_PEER_IMPORTED).all() and (st["part_sys_scope"] == 1).all(), it
     k = 256
     runs = sharded.run_processes(16, [0, 8, 16], {"kind": "storm", "k": k, "len": 64, "seed": seed}, max_payload=64,
                                  uncached=True, repeat=6)
