@@ -1031,6 +1031,12 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
             auto recv = [&](int jj) { return bulk_rsrc_at(P, (o + 1 + jj) % n, o, s, off0, 16u * ngr); };
             if (sys) tile_copy<true, W>(rs, ngr, tid, n - 1, recv);
             else tile_copy<false, W>(rs, ngr, tid, n - 1, recv);
+#ifdef RLO_DIAG
+            if ((P.mode & MODE_CORRUPT) && jb.ti0 == 0u && tid == 0) {  // (the test that VERIFY's check fires)
+                VM_DRAIN();
+                st_ring(recv(0), 16u, u32x4{0u, 0u, 0u, 0u}, sys);
+            }
+#endif
             VM_DRAIN();
             __syncthreads();
             if (tid == 0 && jb.ti0 == 0u) tl_mark(P, jb.bid, TL_DRAINED);

@@ -1676,6 +1676,9 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     }();
     if (pipe) w->P.mode |= rlo::MODE_PIPE;
     else w->P.mode &= ~rlo::MODE_PIPE;
+    static const bool corrupt = diag_env("RLO_BULK_CORRUPT") != nullptr;  // test: VERIFY must catch a zeroed granule
+    if (corrupt) w->P.mode |= rlo::MODE_CORRUPT;
+    else w->P.mode &= ~rlo::MODE_CORRUPT;
     static const bool hdiag = diag_env("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
     if (hdiag) w->P.mode |= rlo::MODE_HDIAG;
     else w->P.mode &= ~rlo::MODE_HDIAG;

@@ -88,3 +88,32 @@ def test_timeline_rows_match_the_tree(n, ln):
             assert 0 < _rel(tl[i, 1], t0) <= _rel(tl[i, 2], t0) <= _rel(tl[i, 3], t0), (i, tl[i, :8])
             comp = tl[i, 8 + n:8 + 2 * n]
             assert (comp[others] != 0).all(), (i, comp)
+
+
+CORRUPT_CHILD = r'''
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import rlo
+with rlo.World(4, max_payload=64, bulk_max=1 << 20) as w:
+    w.program_latency(4, (64 << 10) + 48, seed=0x33)
+    w.launch()
+    rc = w.wait(raise_on_device_error=False)
+    print(json.dumps({"rc": rc, "err": list(w.device_error())}))
+'''
+
+
+def test_bulk_verify_catches_a_stale_granule():
+    """VERDICT r4 "next" 1: the bulk leg detects a corrupted tile itself.  The diagnostics build's RLO_BULK_CORRUPT
+    makes the first scatter of every message zero one granule of one receiver's copy after the copy (a tile store
+    that never became visible behind a complete count); the receiver's VERIFY compares every granule with the
+    origin's bytes and must stop the launch with RLO_DERR_BULK, site 14 -- not return rc 0 with a wrong sum"""
+    if not os.path.exists(os.path.join(PKG, "lib_diag", "librlo_hip.so")):
+        pytest.skip("diagnostics build (make DIAG=1) not built")
+    env = dict(os.environ, RLO_DIAG_LIB="1", RLO_BULK_CORRUPT="1")
+    r = subprocess.run([sys.executable, "-c", CORRUPT_CHILD, PKG], capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["rc"] == -4, d  # RLO_E_DEVICE
+    code, aux = d["err"]
+    assert code == 8 and aux >> 24 == 14, (code, hex(aux))  # RLO_DERR_BULK, the VERIFY site
+    assert (aux >> 16) & 0xff < 4 and aux & 0xffff == 0, hex(aux)  # a receiver, the message's first 16-KiB block
