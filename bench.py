@@ -841,8 +841,11 @@ def main():
             note("rank %d: bulk leg failed: %r" % (rank, e))
         if rank == 0:
             note("mixed-size leg (C5)")
+        # a one-GPU rehearsal of more than 2 parts (RLO_BENCH_DEVICE): every part's bulk rank-workgroups and
+        # movers (one per CU) must be resident on the one GPU at once -- 16 ranks + 4 movers per part
+        c5kw = {"per": 16, "movers": 4} if os.environ.get("RLO_BENCH_DEVICE") and world > 2 else {}
         try:
-            extras["c5_mixed"] = c5_leg(rlo, dist, world, rank, local, stream, red)
+            extras["c5_mixed"] = c5_leg(rlo, dist, world, rank, local, stream, red, **c5kw)
         except Exception as e:  # noqa: BLE001
             extras["c5_mixed"] = {"error": repr(e)[:300]}
             note("rank %d: C5 leg failed: %r" % (rank, e))

@@ -1245,13 +1245,24 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
 
 // ------------------------------------------------------------------ the kernel
 
+// program masks of the kernel instantiations (rlo_progress_kernel's PM): every mode bit but the program classes
+// it cannot run
+constexpr uint32_t kPmAll = 0xFFFFFFFFu;
+constexpr uint32_t kPmLat = ~(uint32_t)(MODE_STORM | MODE_IAR | MODE_HOST);
+constexpr uint32_t kPmIar = ~(uint32_t)(MODE_STORM | MODE_LAT | MODE_HOST);
+constexpr uint32_t kPmStorm = ~(uint32_t)(MODE_LAT | MODE_IAR | MODE_HOST);
+
 // PH: the pending-proposal tables live in HBM (Params.pend_hbm; worlds whose N x pool entries would crowd
 // the small copy path's stage out of LDS: the 8-GPU worlds), instantiated for the programs that hold
 // proposals (iar, host service).  Every other launch of such a world runs PH = false and never touches
 // the table.  All PendState traffic is the rank's own workgroup's, and every iteration that changed an
 // entry ends with a drain + barrier (the eager scheme) before any wave reads it again
-template <int W, bool BULK, bool LL, bool PH = false>
+template <int W, bool BULK, bool LL, bool PH = false, uint32_t PM = kPmAll>
 __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
+    // PM: the programs this instantiation can run (kPm*): a mode bit PM lacks is a compile-time 0, so the code of
+    // the other programs drops out of it (the latency and iar programs' doorbell kernels: fewer live values on the
+    // hop path).  rlo_launch_progress picks the instantiation by Params.mode
+#define PMODE(x) ((PM & (uint32_t)(x)) ? (P.mode & (uint32_t)(x)) : 0u)
     // pulled payloads (Params.pull) exist only in the 4-wave kernel without bulk messages (slots beyond
     // the small copy path); compiled out of the others
 #define PULL_ON (W == 4 && !BULK && P.pull != 0u)
@@ -1304,14 +1315,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1;
-    const bool host = (P.mode & MODE_HOST) != 0;
+    const bool host = (PMODE(MODE_HOST)) != 0;
     // counters are published at the end of the iteration whose stores they cover (all waves
     // drained), not after the next poll: one poll round trip less per hop (p50 -8%, decisions/s
     // +11%).  Not in the storm program: there the drain overlaps wave 0's bookkeeping and poll
     // instead (bcasts/s +4%)
-    const bool eager = host || !(P.mode & (MODE_LAZYPUB | MODE_STORM));
+    const bool eager = host || !(PMODE(MODE_LAZYPUB | MODE_STORM));
     const bool hjudge = host && P.host_judge != 0;  // host mode: the host's callbacks judge
-    const uint32_t my_mask = ((P.mode & MODE_IAR) && !hjudge && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
+    const uint32_t my_mask = ((PMODE(MODE_IAR)) && !hjudge && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
     // host-service mode: this rank's command ring (pinned host memory) and its counters
     const __amdgpu_buffer_rsrc_t rh =
         mk_rsrc(host ? P.hin + (size_t)lr * P.hin_cap * P.fwd_stride : P.fwd_region, host ? P.hin_cap * P.fwd_stride : 16u);
@@ -1351,12 +1362,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
             S.own_needed = 0; S.own_rr = 0; S.loc_nd = 0; S.loc_n = 0;
             S.own_iter = 0;
-            S.own_n = ((P.mode & MODE_IAR) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
+            S.own_n = ((PMODE(MODE_IAR)) && !host) ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
             S.lat_pos = 0;
             S.lat_seen = 0;
-            S.lat_pos_n = (P.mode & MODE_LAT) ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
+            S.lat_pos_n = (PMODE(MODE_LAT)) ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
             S.lat_own_next = S.lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
-            S.expect_dec = ((P.mode & MODE_IAR) && !host) ? P.expect_dec[lr] : 0;
+            S.expect_dec = ((PMODE(MODE_IAR)) && !host) ? P.expect_dec[lr] : 0;
             S.hbase = 0; S.nh = 0; S.ev_n = 0; S.quit = 0; S.hhead = 0; S.hin_head = 0; S.pk_tail = 0;
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
@@ -1376,7 +1387,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     BAR();
     if (host && tid == 0) pub64_sys(&hctl[kHctlState], 1ull);  // serving (rlo_host_wait_started)
     // a program that holds proposals in a PH world runs the PH instantiation (rlo_launch_progress)
-    if (!PH && P.pend_hbm && (P.mode & (MODE_IAR | MODE_HOST)) && tid == 0) set_error(S, P, ERR_HOST_CMD, 0x9E4Du);
+    if (!PH && P.pend_hbm && (PMODE(MODE_IAR | MODE_HOST)) && tid == 0) set_error(S, P, ERR_HOST_CMD, 0x9E4Du);
     const uint64_t t_start = now_ticks();
     unsigned long long acc_sum = 0;  // checksum of delivered bcast chunks (this thread's share)
 
@@ -1418,15 +1429,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint32_t p_lat = 0;
     // wave 0's own bookkeeping, kept in registers (LDS read-modify-writes by one lane are a serial
     // chain of LDS round trips on the critical path of every iteration)
-    const int64_t sched_base = (P.mode & MODE_STORM) ? P.sched_off[lr] : 0;
-    const int64_t sched_n = (P.mode & MODE_STORM) ? P.sched_off[lr + 1] - sched_base : 0;
-    const int64_t expect_bcast = (P.mode & (MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
+    const int64_t sched_base = (PMODE(MODE_STORM)) ? P.sched_off[lr] : 0;
+    const int64_t sched_n = (PMODE(MODE_STORM)) ? P.sched_off[lr + 1] - sched_base : 0;
+    const int64_t expect_bcast = (PMODE(MODE_STORM | MODE_LAT)) ? P.expect_bcast[lr] : 0;
     int64_t sched_next = 0;
     uint64_t n_iter = 0, n_busy = 0, n_stalls = 0;
     bool done_w0 = false;
     uint32_t rbase_r = 0, rtake_r = 0, noi_r = 0;  // lane g / oi: this iteration's selection, admitted counts
     // doorbells (rlo_device.hpp, MODE_LL): on in this launch unless it profiles phases or A/Bs the fast path
-    const bool llm = LL && (P.mode & MODE_LL) && !(P.mode & (MODE_PROF | MODE_NOFAST));
+    const bool llm = LL && (PMODE(MODE_LL)) && !(PMODE(MODE_PROF | MODE_NOFAST));
     // host mode with doorbells and command doorbells: the host's words (command tail, pickup head, the next
     // command's doorbell) are polled by wave 1 during phase A, so wave 0's spin is one VRAM round trip, not
     // a PCIe one (a host-service hop took twice the device program's: tools/host_latency.py)
@@ -1484,7 +1495,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const int fvote = (int)(int8_t)(fw0 >> 24);
         bool ok = ((fw2 >> 16) & 0xffu) == kSlotMark && forg < P.n && fnch <= nsmall &&
                   (ftag == TAG_BCAST || ftag == TAG_DECISION || ftag == TAG_PROPOSAL || (BULK && ftag == TAG_BULK)) &&
-                  !(ftag == TAG_BCAST && (P.mode & MODE_LAT) && fid >= P.lat_rounds);
+                  !(ftag == TAG_BCAST && (PMODE(MODE_LAT)) && fid >= P.lat_rounds);
         int fjudge = 1;
         uint32_t fkids = 0, fneed = 0;
         uint32_t flog = ~0u;
@@ -1545,7 +1556,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (lane == 0) {
                 tl_parent(P, fid, lr, ffrom);
                 atomicAdd(&S.bcast_delivered, 1ull);
-                if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
+                if (PMODE(MODE_HIST)) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
                 flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
                                (uint32_t)now_ticks() - ft0);
             }
@@ -1626,7 +1637,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
         if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
             st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
-        if (ftag == TAG_BCAST && (P.mode & MODE_LAT) && lane == 0) {  // the round's last pickup
+        if (ftag == TAG_BCAST && (PMODE(MODE_LAT)) && lane == 0) {  // the round's last pickup
             const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[fid], 1u, __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_SYSTEM)
                                      : atomicAdd(&P.lat_count[fid], 1u);
@@ -1774,15 +1785,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint32_t nv = (uint32_t)vp;  // votes to load from child j's vote ring (<= kLLVotes)
         // (a latency round of bulk messages is originated by the full path: its announcement, heap slot and
         // scatter job)
-        const bool lat_go = (P.mode & MODE_LAT) && (!BULK || P.len <= P.ring_cap) && S.lat_own_next != 0xffffffffu &&
+        const bool lat_go = (PMODE(MODE_LAT)) && (!BULK || P.len <= P.ring_cap) && S.lat_own_next != 0xffffffffu &&
                             rdl32(latr, 1) == S.lat_own_next;
-        const bool iar_dev = (P.mode & MODE_IAR) != 0;  // (host mode: decisions only -- its proposals are commands)
+        const bool iar_dev = (PMODE(MODE_IAR)) != 0;  // (host mode: decisions only -- its proposals are commands)
         const uint64_t nvm = __ballot(nv > 0u);
         // a bulk round of the latency program (its slot free by the release counts phase A last read): the
         // announcement by this pass too, and its scatter posted here -- not a full iteration per round
         [[maybe_unused]] bool blat = false;
         if constexpr (BULK) {
-            blat = (P.mode & MODE_LAT) && P.len > P.ring_cap && S.lat_own_next != 0xffffffffu &&
+            blat = (PMODE(MODE_LAT)) && P.len > P.ring_cap && S.lat_own_next != 0xffffffffu &&
                    rdl32(latr, 1) == S.lat_own_next &&
                    S.b.sdone[S.b.bulk_q & (bsl - 1u)] >= (uint64_t)(S.b.bulk_q / bsl) * (uint64_t)(P.n - 1);
         }
@@ -2124,10 +2135,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                   : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
-                if ((P.mode & MODE_LAT) && lane == 1)  // the round in progress (part 0's word when sharded)
+                if ((PMODE(MODE_LAT)) && lane == 1)  // the round in progress (part 0's word when sharded)
                     latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                : poll32(P.lat_round);
-                if ((P.mode & MODE_LAT) && me == 0) lat_observe(latr);  // every spin: doorbells keep wave 0 here
+                if ((PMODE(MODE_LAT)) && me == 0) lat_observe(latr);  // every spin: doorbells keep wave 0 here
                 if constexpr (LL) {
                     if (llm) {  // my doorbells beside the counters: lane (k, q) chunk q of in-edge k's, lane j child j's vote
                         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
@@ -2191,8 +2202,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if (lane < (int)bsl) S.b.sdone[lane] = dnw;
                 if (!bev) (void)bulk_eval();  // (else the spin's last evaluation stands: nothing was registered since)
             }
-            if ((P.mode & MODE_LAT) && me == 0) lat_observe(latr);
-            if ((P.mode & MODE_STORM) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
+            if ((PMODE(MODE_LAT)) && me == 0) lat_observe(latr);
+            if ((PMODE(MODE_STORM)) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
         } else if (hpw && w == 1) {
             // the host poller: until wave 0 ends its spin, the next command's doorbell (lanes 0-15, 16 B each,
@@ -2270,7 +2281,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint32_t own_ev = 2u * P.own_pool + 2u;
                 hblock = pk_free < own_ev + 4u;
                 hlim = hblock ? 0u : (pk_free - own_ev) / 2u;
-                if ((P.mode & MODE_HDIAG) && lane == 0) {
+                if ((PMODE(MODE_HDIAG)) && lane == 0) {
                     S.hd[3]++;
                     if (hblock) S.hd[2]++;
                 }
@@ -2313,7 +2324,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                                     log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
                                 queue_job(S.b, P, JCLS_A, JOB_VERIFY, o, lr, sl, pe.bid, pe.len,
                                          (pe.len + kVerifyTile - 1u) / kVerifyTile, pe.from, li, pe.q, 0u);
-                                if (P.mode & MODE_LAT) {  // the last of N-1 pickups completes the round
+                                if (PMODE(MODE_LAT)) {  // the last of N-1 pickups completes the round
                                     const uint32_t old =
                                         sys ? __hip_atomic_fetch_add(&P.lat_count[pe.bid], 1u, __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_SYSTEM)
@@ -2358,7 +2369,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             vin_head_r += vtake;  // merged by wave 1 before the next publish
             // in-rings: fair per-ring quotas
             const uint32_t ra = lane < n_in2 && in_tail_r > in_head_r ? (uint32_t)min(in_tail_r - in_head_r, (uint64_t)kMaxCand) : 0u;
-            const uint32_t reserve = host ? kPass + P.pend_slots : ((P.mode & MODE_IAR) ? P.pend_slots + 1u : 0u);  // host: stage block; the pool's originations
+            const uint32_t reserve = host ? kPass + P.pend_slots : ((PMODE(MODE_IAR)) ? P.pend_slots + 1u : 0u);  // host: stage block; the pool's originations
             const uint64_t ract = __ballot(ra > 0 && !hblock);
             const int nact = __popcll(ract);
             // max-min fair (water-filling) quotas: a ring's share that a short ring leaves unused goes
@@ -2404,7 +2415,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             uint32_t C = R, loc_kind = 0, nstorm = 0, storm_base = 0, lat_id = 0xffffffffu;
             int64_t prop_idx = -1;
             bool hprop_ok = false;  // host mode: a pool slot is free for one host proposal this iteration
-            if ((P.mode & MODE_IAR) && !hblock) {
+            if ((PMODE(MODE_IAR)) && !hblock) {
                 // the proposal pool: every decided slot originates its decision (:560-563, :908-917),
                 // then free slots (round-robin from own_rr) take the next proposals of my list, up to
                 // own_pool in flight (:876-906).  Lane k holds slot k
@@ -2445,7 +2456,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // active, and it ends the run)
                 // (a command doorbell may have run the head past the tail this poll saw)
                 const uint64_t pend_n = rdl64(hpoll, 0) > S.hin_head ? rdl64(hpoll, 0) - S.hin_head : 0ull;
-                if ((P.mode & MODE_HDIAG) && lane == 0) {  // how long seen commands wait here
+                if ((PMODE(MODE_HDIAG)) && lane == 0) {  // how long seen commands wait here
                     if (pend_n) {
                         S.hd[0]++;
                         if (!S.hd_t0) S.hd_t0 = now_ticks();
@@ -2515,7 +2526,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (pm) {
                         const uint32_t fp = (uint32_t)__builtin_ctzll(pm);
                         run = hprop_ok ? fp + 1u : fp;
-                        if ((P.mode & MODE_HDIAG) && lane == 0 && run == fp) S.hd[1]++;
+                        if ((PMODE(MODE_HDIAG)) && lane == 0 && run == fp) S.hd[1]++;
                     }
                     nh = run;
                     gap_lo = C;
@@ -2528,11 +2539,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if (nh) C = hbase + nh;
                 }
             }
-            if (!LL && (P.mode & MODE_STORM) && sched_next < sched_n) {  // (no storm runs with doorbells)
+            if (!LL && (PMODE(MODE_STORM)) && sched_next < sched_n) {  // (no storm runs with doorbells)
                 // throttle: originate only into shallow out-rings so forwarding never waits behind originations
                 const bool deep = lane < nout && (out_tail_r - out_head_r) * 2 >= P.fwd_cap;
                 const bool allow = !backlog && R < 2 * kPass && __ballot(deep) == 0;
-                if ((P.mode & MODE_PROF) && lane == 0) { if (!allow) S.dbg[5]++; else S.dbg[2]++; }
+                if ((PMODE(MODE_PROF)) && lane == 0) { if (!allow) S.dbg[5]++; else S.dbg[2]++; }
                 if (allow) {
                     const int64_t rem = sched_n - sched_next;
                     uint32_t ww = rem < (int64_t)P.window ? (uint32_t)rem : P.window;
@@ -2562,7 +2573,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     if ((uint32_t)lane < ww) S.storm_ids[lane] = sid;
                 }
             }
-            if ((P.mode & MODE_LAT) && C < kMaxCand) {
+            if ((PMODE(MODE_LAT)) && C < kMaxCand) {
                 // my next round (prefetched) starts when the previous round completed everywhere
                 bool lat_ok = true;
                 if constexpr (BULK) {
@@ -2583,7 +2594,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             uint32_t fastdone = 0;
             // (host-service mode too, for bcasts and decisions -- its proposals take the full path for
             // the host-judge hold and the JUDGED events -- when the pickup ring has room for their events)
-            if ((!host || hlim >= 2u) && R == 1u && C == 1u && vtot == 0u && !(P.mode & (MODE_PROF | MODE_NOFAST))) {
+            if ((!host || hlim >= 2u) && R == 1u && C == 1u && vtot == 0u && !(PMODE(MODE_PROF | MODE_NOFAST))) {
                 const int fg = __builtin_ctzll(__ballot(lane < n_in2 && take > 0u));
                 const uint64_t h0 = rdl64(in_head_r, fg);
                 const uint32_t fsrc = (uint32_t)uni((int)t.in_data[fg >> 1][fg & 1]) + (uint32_t)(h0 & fcap_m) * P.fwd_stride;
@@ -2612,7 +2623,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 S.lat_id = lat_id; S.prop_idx = prop_idx; S.nbig = 0; S.progressed = fastdone | (ll_prog ? 1u : 0u);
                 S.hbase = hbase; S.nh = nh; S.gap_lo = gap_lo; S.gap_hi = hbase; S.nchmax = 0;
                 S.exit_now = done_w0;
-                if (P.mode & MODE_PROF) S.dbg[0] += R;
+                if (PMODE(MODE_PROF)) S.dbg[0] += R;
             }
             ll_prog = false;
         }
@@ -2775,7 +2786,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     atomicAdd(&S.stale, 1ull);
                     set_error(S, P, ERR_BAD_SLOT, 0x57A1Eu);
                     kind = K_BAD;
-                } else if (origin >= P.n || (tag == TAG_BCAST && (P.mode & MODE_LAT) && id >= P.lat_rounds)) {
+                } else if (origin >= P.n || (tag == TAG_BCAST && (PMODE(MODE_LAT)) && id >= P.lat_rounds)) {
                     set_error(S, P, ERR_BAD_SLOT, w0);
                     kind = K_BAD;  // consumed, never forwarded, no side effects
                 } else if (tag == TAG_BCAST || tag == TAG_DECISION || (BULK && tag == TAG_BULK)) {
@@ -2945,7 +2956,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 const uint64_t b = __ballot(bit);
                 if (b && bit && (uint32_t)__popcll(b & lt_mask) >= rdl32(room_r, oi)) {
                     fits = false;
-                    if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) atomicAdd(&S.hist[oi], 1u);  // misfits per out-ring
+                    if ((PMODE(MODE_PROF | MODE_HIST)) == MODE_PROF) atomicAdd(&S.hist[oi], 1u);  // misfits per out-ring
                 }
             }
             if (active && !fits) atomicMin(&S.first_bad[group], c);
@@ -3001,10 +3012,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (admitted) {
                 if (kind == K_RING) {
                     if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
-                        if (P.mode & (MODE_HIST | MODE_LAT)) {
+                        if (PMODE(MODE_HIST | MODE_LAT)) {
                             const uint64_t tn = now_ticks();
-                            if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin((uint32_t)tn - t0)], 1u);
-                            if (P.mode & MODE_LAT) {  // round bookkeeping after the forwards are issued (G)
+                            if (PMODE(MODE_HIST)) atomicAdd(&S.hist[hist_bin((uint32_t)tn - t0)], 1u);
+                            if (PMODE(MODE_LAT)) {  // round bookkeeping after the forwards are issued (G)
                                 tl_mark(P, id, kTlGlobal + (uint32_t)lr);
                                 tl_parent(P, id, lr, from);
                                 lat_deliv = true;
@@ -3148,7 +3159,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const uint32_t rb = rb0 + (uint32_t)__popcll(bm & lt_mask), rfree = S.relay_free;
                     if (rl && rb < rfree) relay = t.orig_data + (uint32_t)((S.relay_tail + rb) & (P.relay_cap - 1u)) * P.fwd_stride;
                     if (lane == 0 && rb0 < rfree) S.ref_any = 1;
-                    if ((P.mode & MODE_PROF) && lane == 0 && rb0 + (uint32_t)__popcll(bm) > rfree)  // pushed: relay full
+                    if ((PMODE(MODE_PROF)) && lane == 0 && rb0 + (uint32_t)__popcll(bm) > rfree)  // pushed: relay full
                         atomicAdd((unsigned long long*)&S.dbg[4], (unsigned long long)(rb0 + (uint32_t)__popcll(bm) - max(rb0, rfree)));
                 }
             }
@@ -3173,7 +3184,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     bb = rdl32(bb, 0);
                     if (isbig) S.big[bb + (uint32_t)__popcll(bbig & lt_mask)] = (uint16_t)c;
                 }
-                if (P.mode & MODE_PROF) {
+                if (PMODE(MODE_PROF)) {
                     uint32_t tot;
                     wave_excl_scan(admitted ? (uint32_t)__builtin_popcount(kids) : 0u, &tot);
                     if (lane == 0) atomicAdd((unsigned long long*)&S.dbg[6], (unsigned long long)tot);
@@ -3191,7 +3202,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             const uint32_t nbig = (LL && W == 8) ? 0u : S.nbig;
             // staging rounds of all of stage2: load -> store -> wait.  (MODE_PIPE, A/B: two halves, round r+1's
             // loads in flight while round r is stored -- measured slower, the rounds halve)
-            const bool pipe = s2_units >= 2u * kSubMax && (P.mode & MODE_PIPE);
+            const bool pipe = s2_units >= 2u * kSubMax && (PMODE(MODE_PIPE));
             const uint32_t hu = pipe ? min(s2_units / 2u, 64u) : min(s2_units, 128u);  // units per round
             const uint32_t hg = pipe ? 64u : 128u;                                     // groups per round
             const uint32_t gsub = min(kSubMax, hu), gspan = 64u * gsub;                 // a group's units, chunks
@@ -3288,7 +3299,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             // MODE_PROF: wave 0's cycles waiting for a round's loads (and stores) in dbg[3], the rounds in
             // dbg[4] (push worlds: pull worlds count relay-full pushes there)
             auto big_drain = [&]() {
-                if ((P.mode & MODE_PROF) && tid == 0) {
+                if ((PMODE(MODE_PROF)) && tid == 0) {
                     const uint64_t c0 = __builtin_amdgcn_s_memtime();
                     VM_DRAIN();
                     S.dbg[3] += __builtin_amdgcn_s_memtime() - c0;
@@ -3506,7 +3517,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 in_head_r += adm;
                 if (adm < tk) win_r = max(adm + adm / 2u, 16u);
                 else if (adm == tk && tk == win_r) win_r = min(2u * win_r, (uint32_t)kMaxCand);
-                if (P.mode & MODE_PROF) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
+                if (PMODE(MODE_PROF)) atomicAdd((unsigned long long*)&S.dbg[1], (unsigned long long)adm);
             }
             PSX(4);
             if (eager) {
@@ -3541,11 +3552,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 // this iteration's stores are drained (see above): publish now, not after the next
                 // poll -- one poll round trip less per hop
                 if (eager && out_tail_r != PUB_OUT) { PUB_OUT = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
-                if ((P.mode & (MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
+                if ((PMODE(MODE_PROF | MODE_HIST)) == MODE_PROF) {  // per out-ring: admitted, free at start
                     S.hist[32 + lane] += noi_r;
                     S.hist[64 + lane] += S.ofree[lane] >> 4;
                 }
-                if (P.mode & MODE_PROF)
+                if (PMODE(MODE_PROF))
                     atomicMax((unsigned long long*)&S.dbg[7], (unsigned long long)(out_tail_r - S.out_tail0[lane] +
                                                                                    (P.fwd_cap - S.ofree[lane])));
             }
@@ -3591,10 +3602,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 }
                 if ((n_iter & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
                 bool done = true;
-                if (P.mode & MODE_STORM) done &= sched_next == sched_n;
-                if (P.mode & (MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == expect_bcast;
-                if (P.mode & MODE_LAT) done &= S.lat_pos >= S.lat_pos_n;
-                if ((P.mode & MODE_IAR) && !host) {
+                if (PMODE(MODE_STORM)) done &= sched_next == sched_n;
+                if (PMODE(MODE_STORM | MODE_LAT)) done &= (int64_t)S.bcast_delivered == expect_bcast;
+                if (PMODE(MODE_LAT)) done &= S.lat_pos >= S.lat_pos_n;
+                if ((PMODE(MODE_IAR)) && !host) {
                     bool idle = true;
                     for (uint32_t k = 0; k < P.pend_slots; k++) idle &= S.own_state[k] == 0u;
                     done &= (int64_t)S.own_iter == S.own_n && idle && (int64_t)S.dec_delivered == S.expect_dec;
@@ -3607,7 +3618,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             done_w0 = __builtin_amdgcn_readfirstlane((int)done_w0) != 0;  // lane 0 updated these
             sched_next = (int64_t)uni64((uint64_t)sched_next);
             // (BULK: pending receptions are polled in the spin, bulk_eval)
-            idle_prev = C == 0 && S.vtot == 0 && !done_w0 && !(P.mode & MODE_NOSPIN);
+            idle_prev = C == 0 && S.vtot == 0 && !done_w0 && !(PMODE(MODE_NOSPIN));
         }
         PROF_STAMP(6);
     }
@@ -3625,7 +3636,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
     // ---------------- flush statistics
     if constexpr (BULK) {
-        if (tid == 0 && !(P.mode & (MODE_PROF | MODE_TL))) {  // diagnostics in stats.dbg: pending receptions at exit
+        if (tid == 0 && !(PMODE(MODE_PROF | MODE_TL))) {  // diagnostics in stats.dbg: pending receptions at exit
             const uint32_t nb = S.b.nbact;
             S.dbg[0] = ((uint64_t)S.b.bulk_q << 32) | nb;
             for (uint32_t i = 0; i < 3 && i < nb; i++) {
@@ -3670,7 +3681,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         st.t_end = now_ticks();
         st.error = S.error;
         st.error_aux = S.error_aux;
-        if (host && (P.mode & MODE_HDIAG))
+        if (host && (PMODE(MODE_HDIAG)))
             for (int i = 0; i < 8; i++) pub64_sys(&hctl[kHctlDiag + i], S.hd[i]);
         if (host) pub64_sys(&hctl[kHctlState], 2ull);  // this rank stopped serving
     }
@@ -3682,11 +3693,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 // bulk messages (mover workgroups + mixed storm lengths); the Shared / LDS layout depends on it.  A
 // program with doorbells (MODE_LL: latency, IAR, host service) runs the doorbell instantiation of its
 // variant, the storm the one without (its registers untouched)
-template <int W, bool B, bool L, bool H>
+template <int W, bool B, bool L, bool H = false, uint32_t PM = rlo::kPmAll>
 static hipError_t grant_dyn_lds(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {  // > 64 KiB of dynamic LDS must be requested explicitly
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B, L, H>,
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_progress_kernel<W, B, L, H, PM>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
@@ -3694,11 +3705,11 @@ static hipError_t grant_dyn_lds(size_t dyn_lds) {
     return hipSuccess;
 }
 
-template <int W, bool B, bool L, bool H = false>
+template <int W, bool B, bool L, bool H = false, uint32_t PM = rlo::kPmAll>
 static hipError_t launch_v(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
-    hipError_t e = grant_dyn_lds<W, B, L, H>(dyn_lds);
+    hipError_t e = grant_dyn_lds<W, B, L, H, PM>(dyn_lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B, L, H>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
+    hipLaunchKernelGGL((rlo::rlo_progress_kernel<W, B, L, H, PM>), dim3(blocks), dim3(64 * W), dyn_lds, stream, *p);
     return hipGetLastError();
 }
 
@@ -3715,13 +3726,26 @@ static bool wants_ph(const rlo::Params* p) {
     return p->pend_hbm != nullptr && (p->mode & (rlo::MODE_IAR | rlo::MODE_HOST)) != 0;
 }
 
+// The 8-wave kernels of the three device programs the bench times are specialised by program (PM): the storm
+// (no doorbells), the latency program and the iar program (doorbells; the iar one with the LDS or the HBM
+// pending table).  Their register use never exceeds the general instantiation's, whose occupancy the host
+// checks (rlo_occupancy*); the Makefile guard holds every 8-wave instantiation to 2 waves per SIMD.
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
+    const uint32_t prog = p->mode & (rlo::MODE_STORM | rlo::MODE_LAT | rlo::MODE_IAR | rlo::MODE_HOST);
     if (wants_ph(p) && variant != 5) {
-        if (variant == 8) return ll ? launch_v<8, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false, true>(p, blocks, dyn_lds, stream);
+        if (variant == 8) {
+            if (ll && prog == rlo::MODE_IAR) return launch_v<8, false, true, true, rlo::kPmIar>(p, blocks, dyn_lds, stream);
+            return ll ? launch_v<8, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false, true>(p, blocks, dyn_lds, stream);
+        }
         return ll ? launch_v<4, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false, true>(p, blocks, dyn_lds, stream);
     }
-    if (variant == 8) return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
+    if (variant == 8) {
+        if (ll && prog == rlo::MODE_LAT) return launch_v<8, false, true, false, rlo::kPmLat>(p, blocks, dyn_lds, stream);
+        if (ll && prog == rlo::MODE_IAR) return launch_v<8, false, true, false, rlo::kPmIar>(p, blocks, dyn_lds, stream);
+        if (!ll && prog == rlo::MODE_STORM) return launch_v<8, false, false, false, rlo::kPmStorm>(p, blocks, dyn_lds, stream);
+        return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
+    }
     if (variant == 5) return ll ? launch_v<4, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, true, false>(p, blocks, dyn_lds, stream);
     return ll ? launch_v<4, false, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false>(p, blocks, dyn_lds, stream);
 }

@@ -116,17 +116,16 @@ def _run_iar(rlo, n, proposals, decline, pool=1, pend_hbm=False):
     return judge, actions, pickups, results
 
 
-@pytest.mark.parametrize("pend_hbm", [False, True])
-@pytest.mark.parametrize("n,origins,mask_ranks,per,pool", [(8, [1], [4], 1, 1), (8, [0, 3, 5, 6], [], 1, 1),
-                                                           (16, [0, 5, 9, 15], [6, 12], 1, 1),
-                                                           (64, list(range(0, 64, 5)), [7, 33], 1, 1),
-                                                           (256, [0, 77, 128, 255], [3], 1, 1),
-                                                           (8, [0, 3, 5, 6], [], 12, 4), (16, [0, 5, 9, 15], [6, 12], 20, 16),
-                                                           (64, list(range(0, 64, 7)), [7, 33], 6, 8)])
+_HOST_IAR_CASES = [(8, [1], [4], 1, 1), (8, [0, 3, 5, 6], [], 1, 1), (16, [0, 5, 9, 15], [6, 12], 1, 1),
+                   (64, list(range(0, 64, 5)), [7, 33], 1, 1), (256, [0, 77, 128, 255], [3], 1, 1),
+                   (8, [0, 3, 5, 6], [], 12, 4), (16, [0, 5, 9, 15], [6, 12], 20, 16), (64, list(range(0, 64, 7)), [7, 33], 6, 8)]
+
+
+# every case with the pending-proposal tables in LDS; the 16- and 256-rank ones also with them in HBM
+@pytest.mark.parametrize("n,origins,mask_ranks,per,pool,pend_hbm",
+                         [c + (False,) for c in _HOST_IAR_CASES] + [c + (True,) for c in _HOST_IAR_CASES if c[0] in (16, 256)])
 def test_host_iar_matches_oracle(rlo, n, origins, mask_ranks, per, pool, pend_hbm):
     """pend_hbm: the same with the pending-proposal tables in HBM (the 8-GPU world's layout)"""
-    if pend_hbm and n not in (16, 256):
-        pytest.skip("HBM tables: two worlds suffice")
     decline = np.zeros(n, dtype=np.uint8)
     decline[mask_ranks] = 1
     props = [(o, 1000 + i * n + o, ("proposal-%d-from-%d" % (i, o)).encode()) for i in range(per) for o in origins]
