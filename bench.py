@@ -807,6 +807,23 @@ def main():
         ok &= bool((ist["error"] == 0).all())
     w.close()
     if not args.no_extras and world == 1:
+        # VERDICT r4 "next" 4: C4 with the pending-proposal tables in HBM (the PH kernels an 8-GPU world's parts run:
+        # N x pool x 16 B per rank would crowd a 2048-rank world's LDS), beside the LDS-table number above
+        p = args.iar_p
+        with rlo.World(R, max_payload=max(64, length), device=local, pend_hbm=True) as wh:
+            assert wh.info["pend_hbm"] == 1
+            wh.program_iar([(r, it * R + r, b"0123456789abcdef") for it in range(p) for r in range(R)])
+            _step(wh, stream, None)
+            t1 = time.perf_counter()
+            rc, ims = _step(wh, stream, None)
+            idt = time.perf_counter() - t1
+            ist = wh.stats()
+        extras["decisions_per_s_pend_hbm"] = round(R * p / idt, 1)
+        extras["decisions_kernel_ms_pend_hbm"] = round(ims, 3)
+        if extras.get("decisions_per_s"):
+            extras["pend_hbm_cost"] = round(1.0 - extras["decisions_per_s_pend_hbm"] / extras["decisions_per_s"], 4)
+        ok &= rc == 0 and int(ist["own_decided"].sum()) == R * p and bool((ist["error"] == 0).all())
+    if not args.no_extras and world == 1:
         # the proposal pool at the C4 shape: every rank keeps 16 own proposals in flight (its own world:
         # the pending table is N x 16 entries of LDS, sized at creation)
         p = 4 * args.iar_p

@@ -138,6 +138,9 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out);
 int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap); /* returns RLO_PART_BLOB_BYTES */
 int rlo_part_connect(rlo_world_t* w, const void* blobs /* n_parts x RLO_PART_BLOB_BYTES, by part */, int n_parts);
 int rlo_world_destroy(rlo_world_t* w);
+/* close this part's hipIpc imports of its peers' regions (rlo_world_destroy does it too); the part can no longer
+ * launch.  Lets every part of a world drop its imports before any part frees the memory they map */
+int rlo_part_close_imports(rlo_world_t* w);
 int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 
 /* ------------------------------------------------------------------ programs */

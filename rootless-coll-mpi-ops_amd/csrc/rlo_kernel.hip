@@ -187,6 +187,7 @@ struct Shared {
     unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
     unsigned long long own_decided, own_approved, proposals_recv, log_count, stalls, stale;
     uint64_t prof[8], prof_t, dbg[8];
+    uint64_t hpt[9];     // MODE_HOPPROF: shader clocks at the points of the current doorbell hop
     uint32_t tl_clk[4];  // MODE_TL: when wave 0's spin issued its polls, when the doorbell pass began, its probes
     uint32_t tl_bfid;    // MODE_TL: a bulk announcement the doorbell pass took (+1), for its TLC_NEXT clock
     int64_t expect_dec;
@@ -308,6 +309,19 @@ __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { retu
     do {                                                      \
         if (TL_ON(P) && lane == 0) S.dbg[(k)]++;    \
     } while (0)
+// MODE_HOPPROF (diagnostics build): lane 0 of wave 0 stamps point k of a doorbell hop
+#ifdef RLO_DIAG
+// (the program-specialised doorbell kernels only: the general ones have no registers to spare)
+#define HP(k)                                                                                  \
+    do {                                                                                       \
+        if constexpr (PM == kPmLat || PM == kPmIar)                                            \
+            if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[(k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define HP(k) \
+    do {      \
+    } while (0)
+#endif
 // MODE_PROF: thread 0 charges the shader cycles since the last stamp to phase `ph`
 #define PROF_STAMP(ph)                                  \
     do {                                                \
@@ -397,6 +411,28 @@ __device__ __forceinline__ uint32_t need_of(uint32_t kids, int origin, int sll, 
     for (int j = 0; j < sll; j++)
         if ((kids >> j) & 1u) need |= 1u << (2 * j + ((int)rdl32(sl_r, j) < origin ? 1 : 0));
     return need;
+}
+
+// the same two for a wave-uniform message (the lone path): lane j tests send_list[j] at once -- three ballots
+// instead of two serial loops of v_readlane + compare over the send list
+__device__ __forceinline__ uint32_t spread_bits(uint32_t x) {  // bit j -> bit 2j (x < 2^16)
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
+__device__ __forceinline__ uint32_t kids_of_u(int me, int origin, int from, int level, int last_wall, int scc, int sll,
+                                              uint32_t sl_r, int lane) {
+    if (from < 0) return (1u << sll) - 1u;
+    if (level <= 0) return 0u;
+    if (from > last_wall) return (1u << (scc + 1)) - 1u;
+    return (uint32_t)__ballot(lane < scc && !passed_origin(me, origin, (int)sl_r));
+}
+__device__ __forceinline__ uint32_t need_of_u(uint32_t kids, int origin, int sll, uint32_t sl_r, int lane) {
+    const bool kid = lane < sll && ((kids >> lane) & 1u);
+    const uint32_t b1 = (uint32_t)__ballot(kid && (int)sl_r < origin);  // wrapped past rank N-1: vc 1
+    const uint32_t b0 = (uint32_t)__ballot(kid && !((int)sl_r < origin));
+    return spread_bits(b0) | (spread_bits(b1) << 1);
 }
 
 // latency histogram of 10 ns ticks: values < 4 exact, then 4 sub-bins per octave (to ~2^33 ticks)
@@ -1448,19 +1484,36 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
 
+    // the lone path's child set: lane-parallel in the program-specialised kernels (the general ones keep the serial
+    // form, which needs no extra registers)
+#define KIDS_U(o, f) (PM != kPmAll ? kids_of_u(me, (o), (f), level, last_wall, scc, sll, sl_r, lane) \
+                               : kids_of(me, (o), (f), level, last_wall, scc, sll, sl_r))
+#define NEED_U(k, o) (PM != kPmAll ? need_of_u((k), (o), sll, sl_r, lane) : need_of((k), (o), sll, sl_r))
     // a small message (lane q: slot chunk q, q < nch) into out-rings `need` at their tails: the ring slot,
     // and with bells the child's doorbell for the edge, tagged bell_tag(ring sequence) | vc << 31.  The
     // caller advances out_tail_r
     auto fwd_small = [&](u32x4 v, uint32_t nch, uint32_t need) {
         const uint32_t q = (uint32_t)lane;
+        // every out-ring's base (and its child's bell) read from LDS at once, lane oi holding ring oi's: one LDS
+        // round trip per forward, not two dependent ones per out-ring (program-specialised kernels: the general
+        // ones have no registers for it)
+        uint64_t obase = 0, bbase = 0;
+        if constexpr (PM != kPmAll) {
+            if (lane < nout) {
+                obase = t.out_ring[lane >> 1][lane & 1];
+                if (LL && llm) bbase = t.out_bell[lane >> 1];
+            }
+        }
         for (uint32_t m = need; m; m &= m - 1) {
             const int oi = __builtin_ctz(m);
             const uint64_t slot = rdl64(out_tail_r, oi);
-            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(ORING(oi)), oring_bytes);
+            const __amdgpu_buffer_rsrc_t ro =
+                mk_rsrc(reinterpret_cast<void*>(PM != kPmAll ? rdl64(obase, oi) : ORING(oi)), oring_bytes);
             if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
             if (LL && llm && nch <= kBellChunks && q < nch) {
                 const uint32_t T = bell_tag(slot) | ((uint32_t)(oi & 1) << 31);
-                const __amdgpu_buffer_rsrc_t rb = mk_rsrc(reinterpret_cast<void*>(uni64(t.out_bell[oi >> 1])), kBellWords * 8u);
+                const __amdgpu_buffer_rsrc_t rb = mk_rsrc(
+                    reinterpret_cast<void*>(PM != kPmAll ? rdl64(bbase, oi) : uni64(t.out_bell[oi >> 1])), kBellWords * 8u);
                 st_ring(rb, 32u * q, u32x4{v.x, T, v.y, T}, sys);
                 st_ring(rb, 32u * q + 16u, u32x4{v.z, T, v.w, T}, sys);
             }
@@ -1538,11 +1591,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         fjudge = judge_eval(P, rf, me, my_mask, (int32_t)fid, fsrc + kHdr + 16u, dl);
                     }
                 }
-                fkids = fjudge == 1 ? kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r) : 0u;
+                fkids = fjudge == 1 ? KIDS_U(forg, ffrom) : 0u;
             } else {
-                fkids = kids_of(me, forg, ffrom, level, last_wall, scc, sll, sl_r);
+                fkids = KIDS_U(forg, ffrom);
             }
-            fneed = need_of(fkids, forg, sll, sl_r);
+            fneed = NEED_U(fkids, forg);
             const bool full = lane < nout && ((fneed >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap;
             // a proposal whose pending entry still holds an earlier proposal of that pool slot
             // goes the full path (held there until that one's decision was applied); with host judges the
@@ -1551,6 +1604,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             ok = __ballot(full) == 0 && !held;
         }
         if (!ok) return ~0u;
+        HP(4);
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P1, lr, (uint32_t)now_ticks());
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
@@ -1627,7 +1681,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
+        HP(5);
         fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
+        HP(6);
         if constexpr (BULK) {
             if (TL_ON(P) && ftag == TAG_BULK && lane == 0) {
                 tl_put(P, fid, TLC_FWD, lr, (uint32_t)now_ticks());
@@ -1657,7 +1713,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     auto originate = [&](uint32_t kind, uint32_t w0, uint32_t id, uint32_t w2, uint32_t src, uint64_t out_head_r) -> bool {
         const uint32_t len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4;
         if (nch > nsmall || nch > kBellChunks) return false;
-        const uint32_t need = need_of((1u << sll) - 1u, me, sll, sl_r);  // the whole send_list (:1587)
+        const uint32_t need = NEED_U((1u << sll) - 1u, me);  // the whole send_list (:1587)
         if (__ballot(lane < nout && ((need >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap)) return false;
         const uint32_t q = (uint32_t)lane;
         const uint32_t hw2 = (w2 & 0xff00ffffu) | (kSlotMark << 16);
@@ -1724,6 +1780,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     auto ll_pass = [&](u32x4 ba, u32x4 bb, u32x4 vb, uint64_t in_tail_r, uint64_t vin_tail_r, uint64_t out_head_r,
                        uint64_t hpoll, uint32_t latr, uint32_t errf, bool& need_full) -> uint32_t {
         need_full = false;
+        HP(0);
+#ifdef RLO_DIAG
+        if constexpr (PM == kPmLat || PM == kPmIar)
+            if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[3] = 0;
+#endif
         if (__ballot(errf != 0)) return 0u;
         // the data words to LDS at once (registers are the kernel's scarcest resource): chunk q of in-edge
         // k's bell at kLLBell + 16 (8 k + q), child j's vote bell {word, pid} at kLLBellVote + 8 j
@@ -1751,6 +1812,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const bool ldr = lane < n_in2 && ip > 0ull && !rhit;  // a counter-visible head without its bell: load it
         const uint64_t ldm = __ballot(ldr);
         if (__ballot(ip > 2ull || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { need_full = true; return 0u; }
+        HP(1);
         uint32_t ncmd = 0;  // host commands to take (FIFO order, the first kLLCmds)
         bool cbell = false;  // ... the one in the command doorbell (already loaded, at kLLCmd)
         if (host) {  // too little room in the pickup ring: wait for the host
@@ -1914,6 +1976,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             done += c;
         }
         // ring heads: from the bell, or the loaded slot
+        HP(2);
         const uint64_t rhm = __ballot(rhit);
         for (uint64_t m = rhm | ldm; m; m &= m - 1) {
             const int g = __builtin_ctzll(m);
@@ -1926,6 +1989,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 continue;
             }
             if (TL_ON(P) && lane == 0) S.tl_clk[3] = (uint32_t)now_ticks();
+            HP(3);
             const uint32_t need = lone(v, g, 0u, true, out_head_r);
             if (need == kHeld || need == kAsked) {  // waits for the host's verdict (asked now: progress)
                 if (need == kAsked) done++;
@@ -2018,6 +2082,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (!done) return 0u;
         // every store of the pass drained, then the counters (the eager scheme's publish)
         VM_DRAIN();
+        HP(7);
         if (lane < nout && out_tail_r != PUB_OUT) { PUB_OUT = out_tail_r; pub64(OTPTR, out_tail_r, sys); }
         if (lane < n_in2 && in_head_r != PUB_IN) { PUB_IN = in_head_r; pub64(IHPTR, in_head_r, sys); }
         if (lane < sll && vin_head_r != PUB_VIN) { PUB_VIN = vin_head_r; pub64(VHPTR, vin_head_r, sys); }
@@ -2034,6 +2099,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
             }
         }
+        HP(8);
+#ifdef RLO_DIAG
+        if constexpr (PM == kPmLat || PM == kPmIar)
+            if ((P.mode & MODE_HOPPROF) && lane == 0 && done == 1u && S.hpt[3] != 0) {  // one ring message, nothing else
+                for (int k = 0; k < 8; k++) S.prof[k] += S.hpt[k + 1] - S.hpt[k];
+                S.dbg[0]++;
+            }
+#endif
         return done;
     };
 
@@ -3726,9 +3799,9 @@ static bool wants_ph(const rlo::Params* p) {
     return p->pend_hbm != nullptr && (p->mode & (rlo::MODE_IAR | rlo::MODE_HOST)) != 0;
 }
 
-// The 8-wave kernels of the three device programs the bench times are specialised by program (PM): the storm
+// The kernels of the device programs the bench times are specialised by program (PM): 8 waves -- the storm
 // (no doorbells), the latency program and the iar program (doorbells; the iar one with the LDS or the HBM
-// pending table).  Their register use never exceeds the general instantiation's, whose occupancy the host
+// pending table); bulk worlds -- the latency program (C3) and the storm (C5).  Their register use never exceeds the general instantiation's, whose occupancy the host
 // checks (rlo_occupancy*); the Makefile guard holds every 8-wave instantiation to 2 waves per SIMD.
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
@@ -3746,7 +3819,11 @@ extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size
         if (!ll && prog == rlo::MODE_STORM) return launch_v<8, false, false, false, rlo::kPmStorm>(p, blocks, dyn_lds, stream);
         return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
     }
-    if (variant == 5) return ll ? launch_v<4, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, true, false>(p, blocks, dyn_lds, stream);
+    if (variant == 5) {  // bulk worlds: the C3 leg's latency program (doorbells) and the C5 storm, specialised too
+        if (ll && prog == rlo::MODE_LAT) return launch_v<4, true, true, false, rlo::kPmLat>(p, blocks, dyn_lds, stream);
+        if (!ll && prog == rlo::MODE_STORM) return launch_v<4, true, false, false, rlo::kPmStorm>(p, blocks, dyn_lds, stream);
+        return ll ? launch_v<4, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, true, false>(p, blocks, dyn_lds, stream);
+    }
     return ll ? launch_v<4, false, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false>(p, blocks, dyn_lds, stream);
 }
 

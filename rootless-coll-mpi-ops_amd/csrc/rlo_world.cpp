@@ -878,6 +878,23 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
         if (q == w->part) {
             w->pf[q] = w->fwd; w->pv[q] = w->vote; w->pc[q] = w->ctrl;
             w->ph[q] = w->heap; w->pbf[q] = w->bflag;
+            // my own regions must still show the nonce rlo_part_create wrote (memory that changes under a part
+            // between its creation and its connection is not this part's to hand out)
+            const void* own[5] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, L.bulk_max ? w->heap : nullptr,
+                                  w->fwd + L.fwd_bytes[q], L.bulk_max ? w->bflag + L.bflag_bytes[q] : nullptr};
+            for (int i = 0; i < 5; i++) {
+                if (!own[i]) continue;
+                uint64_t got = 0;
+                HIPCHK(hipMemcpy(&got, own[i], 8, hipMemcpyDeviceToHost));
+                if (got != w->nonce) {
+                    static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
+                    std::fprintf(stderr, "rlo: part %d: its own %s region at %p (%llu bytes) shows %016llx since creation, "
+                                 "not its nonce %016llx\n", q, names[i], own[i],
+                                 (unsigned long long)(i == 2 ? L.heap_bytes[q] : 0), (unsigned long long)got,
+                                 (unsigned long long)w->nonce);
+                    return RLO_E_STALE;
+                }
+            }
         } else if (b.token == tok) {  // same process: the addresses are usable as they are
             if (b.device != w->device) {
                 hipError_t e = hipDeviceEnablePeerAccess(b.device, 0);
@@ -917,8 +934,16 @@ int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
                 HIPCHK(hipMemcpy(&got, regs[i], 8, hipMemcpyDeviceToHost));
                 if (got != b.nonce) {
                     static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
-                    std::fprintf(stderr, "rlo: part %d: the %s region of part %d, as mapped here, shows %016llx, not its nonce %016llx\n",
-                                 w->part, names[i], q, (unsigned long long)got, (unsigned long long)b.nonce);
+                    // (what the mapping shows: 0 = never written, another nonce = an earlier allocation of that part)
+                    std::fprintf(stderr, "rlo: part %d: the %s region of part %d, as mapped here at %p, shows %016llx, not its "
+                                 "nonce %016llx (its other regions' words:",
+                                 w->part, names[i], q, regs[i], (unsigned long long)got, (unsigned long long)b.nonce);
+                    for (int k = 0; k < 5; k++) {
+                        uint64_t g2 = 0;
+                        if (regs[k] && hipMemcpy(&g2, regs[k], 8, hipMemcpyDeviceToHost) == hipSuccess)
+                            std::fprintf(stderr, " %s %016llx", names[k], (unsigned long long)g2);
+                    }
+                    std::fprintf(stderr, ")\n");
                     return RLO_E_STALE;
                 }
             }
@@ -967,6 +992,15 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
 }
 
 static void host_free(rlo_world* w);
+
+int rlo_part_close_imports(rlo_world_t* w) {
+    if (!w) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
+    for (void* p : w->opened) (void)hipIpcCloseMemHandle(p);
+    w->opened.clear();
+    w->connected = false;
+    return RLO_OK;
+}
 
 int rlo_world_destroy(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
@@ -1676,6 +1710,9 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     }();
     if (pipe) w->P.mode |= rlo::MODE_PIPE;
     else w->P.mode &= ~rlo::MODE_PIPE;
+    static const bool hopprof = diag_env("RLO_HOP_PROF") != nullptr;  // diagnostic: clocks along a doorbell hop
+    if (hopprof) w->P.mode |= rlo::MODE_HOPPROF;
+    else w->P.mode &= ~rlo::MODE_HOPPROF;
     static const bool corrupt = diag_env("RLO_BULK_CORRUPT") != nullptr;  // test: VERIFY must catch a zeroed granule
     if (corrupt) w->P.mode |= rlo::MODE_CORRUPT;
     else w->P.mode &= ~rlo::MODE_CORRUPT;

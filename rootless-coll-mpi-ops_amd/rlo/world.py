@@ -80,6 +80,11 @@ class World:
     def reset(self, stream=None):
         check(self.lib.rlo_reset(self.h, stream), "rlo_reset")
 
+    def close_imports(self):
+        """rlo_part_close_imports: drop the hipIpc imports of the peers' regions (the part can no longer launch)"""
+        if self.h:
+            check(self.lib.rlo_part_close_imports(self.h), "rlo_part_close_imports")
+
     def close(self):
         if self.h:
             self.lib.rlo_world_destroy(self.h)
