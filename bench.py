@@ -381,6 +381,27 @@ def _agree(dist, world, err):
         raise RuntimeError("; ".join(bad))
 
 
+def _bcast_blob(dist):
+    """part k's blob to every part (World.staged_connect)"""
+    def f(blob, k):
+        obj = [blob]
+        dist.broadcast_object_list(obj, src=k)
+        return obj[0]
+    return f
+
+
+def _close(w, dist):
+    """tear a world down.  Sharded: every part first drops its hipIpc imports of its peers' regions, then -- after a
+    barrier -- frees its own.  A part that freed (and re-allocated, and exported) memory a peer still imported was
+    seen to hand that peer a mapping of its OLD memory for the new handle (tools/probe/part_churn.py)"""
+    if dist is not None and w.info.get("n_parts", 1) > 1:
+        try:
+            w.close_imports()
+        finally:
+            dist.barrier()
+    w.close()
+
+
 def _world(rlo, dist, R, world, rank, local, **kw):
     """one R-rank world: whole on this GPU (world == 1) or this process's part of it.  In the
     one-GPU rehearsal (RLO_BENCH_DEVICE) every part shares the GPU: bulk worlds then take few mover
@@ -405,7 +426,7 @@ def _world(rlo, dist, R, world, rank, local, **kw):
             w.close()
         raise RuntimeError("world part creation failed: " + "; ".join(errs))
     try:
-        w.connect([b for b, _ in blobs])
+        w.staged_connect([b for b, _ in blobs], dist.barrier, _bcast_blob(dist))  # one exporter at a time
     except Exception as e:  # noqa: BLE001
         err = "rank %d: connect: %r" % (rank, e)
     try:
@@ -487,7 +508,7 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
                     rec["ours_over_rccl"] = round(rec["rccl_ms"] / (rt * 1e3), 3)
             out.append(rec)
     finally:
-        w.close()
+        _close(w, dist)
     return {"ranks": G, "ranks_per_gpu": 1 if world > 1 else G, "movers_per_part": w.info.get("movers"),
             "algorithm": "rootless: announcement on the skip-ring tree, mover workgroups move the bytes between "
                          "per-rank heaps (rlo_kernel.hip mover_run): one GPU a fan-out from the origin's copy, "
@@ -542,7 +563,7 @@ def c5_leg(rlo, dist, world, rank, local, stream, red, per=64, k=2048, steps=3, 
                 "hbm_alg_GBps_per_gpu": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "verified": bool(ok),
                 "movers_per_part": w.info.get("movers"), "bulk_slots": w.info.get("bulk_slots")}
     finally:
-        w.close()
+        _close(w, dist)
 
 
 def small_n_legs(rlo, local, stream, sizes=(4, 8), rounds=2000, p=512):
@@ -690,7 +711,7 @@ def main():
             w = rlo.World.part(R, world, rank, max_payload=max(64, length), device=local, uncached=True)
             blobs = [None] * world
             dist.all_gather_object(blobs, w.export())
-            w.connect(blobs)
+            w.staged_connect(blobs, dist.barrier, _bcast_blob(dist))  # one exporter at a time (rlo_part_import)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line, never silent
             err = repr(e)[:300]
         errs = [None] * world
@@ -805,7 +826,7 @@ def main():
         extras["decisions_kernel_ms"] = round(max_over_ranks(ims), 3)
         ok &= rc == 0 and int(sum_over_ranks(float(ist["own_decided"].sum()))) == R * p * copies
         ok &= bool((ist["error"] == 0).all())
-    w.close()
+    _close(w, dist if mode == "sharded" else None)
     if not args.no_extras and world == 1:
         # VERDICT r4 "next" 4: C4 with the pending-proposal tables in HBM (the PH kernels an 8-GPU world's parts run:
         # N x pool x 16 B per rank would crowd a 2048-rank world's LDS), beside the LDS-table number above

@@ -114,7 +114,10 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
  * create (allocates the rings this part consumes) -> export a fixed-size blob -> exchange
  * blobs out of band (MPI_Allgather, torch.distributed, a file) -> connect (maps every peer
  * part: same process = direct pointer, other process = hipIpc / dmabuf, xGMI across GPUs).
- * Every part must rlo_reset before ANY part launches (host barrier in between). */
+ * Every part must rlo_reset before ANY part launches (host barrier in between), and every part must close its
+ * imports (rlo_part_close_imports) before ANY part destroys its world (host barrier in between): a part that frees
+ * and re-allocates memory a peer still imports can export, for its NEW allocation, a handle that maps the OLD one
+ * (seen on MI355X / ROCm 7.2 in 8-part worlds; rlo_part_connect's nonce check then fails with RLO_E_STALE). */
 #define RLO_PART_BLOB_BYTES 512u
 #define RLO_PEER_OTHER_GPU 1u  /* rlo_world_info_t.peers: some peer part is on another GPU (xGMI; the chunked bulk plan) */
 #define RLO_PEER_IMPORTED 2u   /* ... some peer part is in another process (its regions hipIpc-imported)            */
@@ -137,6 +140,11 @@ typedef struct {
 int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out);
 int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap); /* returns RLO_PART_BLOB_BYTES */
 int rlo_part_connect(rlo_world_t* w, const void* blobs /* n_parts x RLO_PART_BLOB_BYTES, by part */, int n_parts);
+/* map part q's regions now (rlo_part_connect then skips q).  Parts in several processes import one exporter at a
+ * time -- every part imports part k's regions while part k imports nothing, host barrier, next k: a part importing
+ * while its peers import its own regions was seen to hand them a mapping of ANOTHER part's region for its handle
+ * (8 parts on MI355X / ROCm 7.2) */
+int rlo_part_import(rlo_world_t* w, const void* blob /* RLO_PART_BLOB_BYTES */, int q);
 int rlo_world_destroy(rlo_world_t* w);
 /* close this part's hipIpc imports of its peers' regions (rlo_world_destroy does it too); the part can no longer
  * launch.  Lets every part of a world drop its imports before any part frees the memory they map */

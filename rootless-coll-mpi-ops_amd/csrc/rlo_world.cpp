@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cctype>
 #include <chrono>
+#include <mutex>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -369,6 +370,7 @@ struct rlo_world {
     std::vector<uint8_t*> pf, pv;
     std::vector<uint64_t*> pc;
     std::vector<void*> opened;  // hipIpc mappings to close
+    std::vector<uint8_t> peer_done;  // part q's regions are mapped (rlo_part_import / rlo_part_connect)
     std::vector<rlo::RankTopo> topo;
     DevBuf<rlo::RankTopo> d_topo;
     DevBuf<rlo::RankStats> d_stats;
@@ -432,13 +434,132 @@ struct rlo_world {
 namespace {
 
 constexpr uint64_t kNonceTail = 256;  // bytes past a region that hold its creation nonce (rlo_part_create)
+// the word region r (0 control, 1 vote, 2 heap, 3 forward, 4 bulk flags) of a part carries: different per region, so
+// an import that maps ANOTHER region of the same part fails the check too (one nonce for all five passed it)
+uint64_t region_nonce(uint64_t nonce, int r) { return nonce ^ (0x9E3779B97F4A7C15ull * (uint64_t)(r + 1)); }
+// ---- the region pool and the import cache.  A world's regions -- the memory its peers map --
+// are never handed back to HIP: a destroyed world's regions wait here, by (device, memory type, size class), for the
+// next world of this process, and a peer's import of a region stays open here for that peer's next world.  Freeing
+// exported memory and importing new handles world after world (bench.py's legs, the test suite's worlds) was seen on
+// MI355X / ROCm 7.2 to give importers mappings of OTHER memory for fresh handles (another part's heap, zeros) and
+// to make hipIpcGetMemHandle fail for fresh allocations; with the pool, a region a peer imported once is the same
+// memory at the same address in every later world (its handle names the same allocation), so no mapping goes stale.
+struct PoolEnt {
+    void* p;
+    uint64_t bytes;
+    int device;
+    bool uncached;
+};
+std::mutex g_pool_mu;
+std::vector<PoolEnt> g_pool;       // free regions
+std::vector<PoolEnt> g_pool_live;  // regions some world of this process holds
+constexpr uint64_t kPoolCapBytes = 96ull << 30;  // free regions kept per process (beyond: the oldest go back to HIP)
+// sizes rounded up to a class (>= 2 MiB: its own allocation, not a sub-allocation another region shares; then eighths
+// of the next power of two), so that worlds of similar sizes share regions
+uint64_t pool_class(uint64_t b) {
+    if (b <= (2ull << 20)) return 2ull << 20;
+    uint64_t p2 = 1;
+    while (p2 < b) p2 <<= 1;
+    const uint64_t step = p2 / 8;
+    return (b + step - 1) / step * step;
+}
+
 int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
-    if (bytes == 0) bytes = 256;
-    hipError_t e;
-    if (w->flags & RLO_PART_UNCACHED) e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
-    else e = hipMalloc(p, bytes);
+    const bool unc = (w->flags & RLO_PART_UNCACHED) != 0;
+    const uint64_t cls = pool_class(bytes ? bytes : 256);
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); i++)
+            if (g_pool[i].device == w->device && g_pool[i].uncached == unc && g_pool[i].bytes == cls) {
+                *p = g_pool[i].p;
+                g_pool_live.push_back(g_pool[i]);
+                g_pool.erase(g_pool.begin() + (long)i);
+                return RLO_OK;
+            }
+    }
+    hipError_t e = unc ? hipExtMallocWithFlags(p, cls, hipDeviceMallocUncached) : hipMalloc(p, cls);
     if (e != hipSuccess) { g_last_hip = (int)e; *p = nullptr; return RLO_E_HIP; }
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool_live.push_back(PoolEnt{*p, cls, w->device, unc});
     return RLO_OK;
+}
+
+// a destroyed world's region back to the pool (the oldest free ones go back to HIP beyond kPoolCapBytes)
+void release_region(void* p) {
+    if (!p) return;
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool_live.size(); i++)
+            if (g_pool_live[i].p == p) {
+                g_pool.push_back(g_pool_live[i]);
+                g_pool_live.erase(g_pool_live.begin() + (long)i);
+                break;
+            }
+        uint64_t tot = 0;
+        for (const PoolEnt& q : g_pool) tot += q.bytes;
+        while (tot > kPoolCapBytes && !g_pool.empty()) {
+            tot -= g_pool.front().bytes;
+            drop.push_back(g_pool.front().p);
+            g_pool.erase(g_pool.begin());
+        }
+    }
+    for (void* d : drop) (void)hipFree(d);
+}
+
+// imports of peers' regions, by the handle words that name the allocation (exporter address and pid, the
+// allocation's id, its size: the first 13 words; the handle's last words are not initialised)
+struct ImpEnt {
+    uint32_t key[13];
+    void* p;
+    int device;
+    int refs;
+};
+std::vector<ImpEnt> g_imports;  // [g_pool_mu]
+constexpr size_t kImportCap = 512;  // idle imports kept open (beyond: the idle ones are closed)
+
+hipError_t open_import(void** p, const hipIpcMemHandle_t& h, int device) {
+    uint32_t key[13];
+    std::memcpy(key, &h, sizeof key);
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (ImpEnt& e : g_imports)
+            if (e.device == device && std::memcmp(e.key, key, sizeof key) == 0) {
+                e.refs++;
+                *p = e.p;
+                return hipSuccess;
+            }
+    }
+    const hipError_t r = hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess);
+    if (r != hipSuccess) return r;
+    ImpEnt e;
+    std::memcpy(e.key, key, sizeof key);
+    e.p = *p;
+    e.device = device;
+    e.refs = 1;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_imports.push_back(e);
+    return hipSuccess;
+}
+
+void close_import(void* p) {
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (ImpEnt& e : g_imports)
+            if (e.p == p && e.refs > 0) { e.refs--; break; }
+        if (g_imports.size() > kImportCap) {
+            for (size_t i = 0; i < g_imports.size();) {
+                if (g_imports[i].refs == 0 && g_imports.size() > kImportCap / 2) {
+                    drop.push_back(g_imports[i].p);
+                    g_imports.erase(g_imports.begin() + (long)i);
+                } else {
+                    i++;
+                }
+            }
+        }
+    }
+    for (void* d : drop) (void)hipIpcCloseMemHandle(d);
 }
 
 // job-ring memory of a part (uncached, part-local): [jobs 2J x 64 B][jctl][jclaim 2J][jfree 2J][jdone 2J][jsum 2J]
@@ -793,8 +914,10 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         if (!w->nonce) w->nonce = 1;
         void* regs[5] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, w->heap, w->fwd + w->L.fwd_bytes[me],
                          w->bflag ? w->bflag + w->L.bflag_bytes[me] : nullptr};
-        for (void* r : regs)
-            if (r && hipMemcpy(r, &w->nonce, 8, hipMemcpyHostToDevice) != hipSuccess) { rlo_world_destroy(w); return RLO_E_HIP; }
+        for (int i = 0; i < 5; i++) {
+            const uint64_t rn = region_nonce(w->nonce, i);
+            if (regs[i] && hipMemcpy(regs[i], &rn, 8, hipMemcpyHostToDevice) != hipSuccess) { rlo_world_destroy(w); return RLO_E_HIP; }
+        }
     }
     // the null stream only: another part's persistent kernel may already run on this device
     // (a second engine in the process), and a device-wide sync would wait for it forever
@@ -807,6 +930,10 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
 
 int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap) {
     if (!w || !blob || cap < RLO_PART_BLOB_BYTES) return RLO_E_INVAL;
+    if (std::getenv("RLO_DEBUG_REGIONS"))  // (which addresses a part exports, world after world)
+        std::fprintf(stderr, "rlo: part %d exports ctrl %p vote %p fwd %p heap %p (%llu B) bflag %p nonce %016llx\n", w->part,
+                     (void*)w->ctrl, (void*)w->vote, (void*)w->fwd, (void*)w->heap,
+                     (unsigned long long)w->L.heap_bytes[w->part], (void*)w->bflag, (unsigned long long)w->nonce);
     PartBlob b;
     std::memset(&b, 0, sizeof b);
     b.magic = kBlobMagic;
@@ -843,111 +970,147 @@ int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap) {
     return (int)RLO_PART_BLOB_BYTES;
 }
 
-int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
-    if (!w || !blobs || n_parts != w->L.nparts || w->connected) return RLO_E_INVAL;
-    HIPCHK(hipSetDevice(w->device));
-    const Layout& L = w->L;
+// the peer tables of a part (sized once per connection attempt: rlo_part_import may fill some of them first)
+static void peer_tables(rlo_world* w, int n_parts) {
+    if ((int)w->pf.size() == n_parts) return;
     w->pf.assign(n_parts, nullptr);
     w->pv.assign(n_parts, nullptr);
     w->pc.assign(n_parts, nullptr);
     w->ph.assign(n_parts, nullptr);
     w->pbf.assign(n_parts, nullptr);
+    w->peer_done.assign(n_parts, 0);
+    w->sys_scope = 0;
+    w->peers = 0;
+}
+
+// part q's blob: checked against this part's layout
+static bool blob_ok(const rlo_world* w, const PartBlob& b, int q, int n_parts) {
+    const Layout& L = w->L;
+    return b.magic == kBlobMagic && b.part == q && b.nparts == n_parts && b.n == L.n && b.cap == L.cap &&
+           b.stride == L.stride && b.vote_cap == L.vote_cap && b.fwd_bytes == L.fwd_bytes[q] &&
+           b.vote_bytes == L.vote_bytes[q] && b.ctrl_bytes == L.ctrl_words[q] * 8 && b.heap_bytes == L.heap_bytes[q] &&
+           b.bflag_bytes == L.bflag_bytes[q];
+}
+
+// map part q's regions (my own: check them; same process: take the addresses; another process: hipIpc imports,
+// every one checked against the peer's creation nonce)
+static int import_peer(rlo_world* w, const PartBlob& b, int q) {
+    const Layout& L = w->L;
     char mybus[32] = {0};
     HIPCHK(hipDeviceGetPCIBusId(mybus, sizeof mybus, w->device));
     const uint64_t tok = process_token();
-    w->sys_scope = 0;
-    w->peers = 0;
+    if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->peers |= RLO_PEER_OTHER_GPU;
+    // A peer in another process (its regions imported through hipIpc, on this GPU or another) gets the
+    // hand-off the 8-GPU world runs: system-scope (sc0 sc1) stores, system-scope counter publishes and
+    // flag adds, system-scope releases before the bulk flags (the round-4 churn
+    // failures).  Only the bulk PLAN follows the GPU layout (RLO_PEER_OTHER_GPU -> chunked).
+    if (q != w->part && b.token != tok) w->peers |= RLO_PEER_IMPORTED;
+    w->sys_scope = w->peers ? 1 : 0;
+    // parts on other GPUs store into this part's rings and heaps over xGMI: a cached part's L2
+    // could hold lines those system-scope stores do not invalidate (rlo_hip.h RLO_PART_UNCACHED)
+    if (w->sys_scope && !(w->flags & RLO_PART_UNCACHED)) return RLO_E_INVAL;
+    if (q == w->part) {
+        w->pf[q] = w->fwd; w->pv[q] = w->vote; w->pc[q] = w->ctrl;
+        w->ph[q] = w->heap; w->pbf[q] = w->bflag;
+        // my own regions must still show the nonce rlo_part_create wrote (memory that changes under a part
+        // between its creation and its connection is not this part's to hand out)
+        const void* own[5] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, L.bulk_max ? w->heap : nullptr,
+                              w->fwd + L.fwd_bytes[q], L.bulk_max ? w->bflag + L.bflag_bytes[q] : nullptr};
+        for (int i = 0; i < 5; i++) {
+            if (!own[i]) continue;
+            uint64_t got = 0;
+            HIPCHK(hipMemcpy(&got, own[i], 8, hipMemcpyDeviceToHost));
+            if (got != region_nonce(w->nonce, i)) {
+                static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
+                std::fprintf(stderr, "rlo: part %d: its own %s region at %p (%llu bytes) shows %016llx since creation, "
+                             "not its nonce %016llx\n", q, names[i], own[i],
+                             (unsigned long long)(i == 2 ? L.heap_bytes[q] : 0), (unsigned long long)got,
+                             (unsigned long long)region_nonce(w->nonce, i));
+                return RLO_E_STALE;
+            }
+        }
+    } else if (b.token == tok) {  // same process: the addresses are usable as they are
+        if (b.device != w->device) {
+            hipError_t e = hipDeviceEnablePeerAccess(b.device, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { g_last_hip = (int)e; return RLO_E_HIP; }
+            (void)hipGetLastError();
+        }
+        w->pf[q] = (uint8_t*)(uintptr_t)b.fwd_ptr;
+        w->pv[q] = (uint8_t*)(uintptr_t)b.vote_ptr;
+        w->pc[q] = (uint64_t*)(uintptr_t)b.ctrl_ptr;
+        w->ph[q] = (uint8_t*)(uintptr_t)b.heap_ptr;
+        w->pbf[q] = (uint8_t*)(uintptr_t)b.bflag_ptr;
+    } else {  // another process: map its regions (dmabuf IPC; xGMI when on another GPU)
+        void* p = nullptr;
+        HIPCHK(open_import(&p, b.hf, w->device));
+        w->opened.push_back(p);
+        w->pf[q] = (uint8_t*)p;
+        HIPCHK(open_import(&p, b.hv, w->device));
+        w->opened.push_back(p);
+        w->pv[q] = (uint8_t*)p;
+        HIPCHK(open_import(&p, b.hc, w->device));
+        w->opened.push_back(p);
+        w->pc[q] = (uint64_t*)p;
+        if (L.bulk_max) {
+            HIPCHK(open_import(&p, b.hh, w->device));
+            w->opened.push_back(p);
+            w->ph[q] = (uint8_t*)p;
+            HIPCHK(open_import(&p, b.hb, w->device));
+            w->opened.push_back(p);
+            w->pbf[q] = (uint8_t*)p;
+        }
+        // every mapped region must show the peer's creation nonce (rlo_part_create)
+        const void* regs[5] = {w->pc[q] + rlo::kCtrlNonceWord, w->pv[q], L.bulk_max ? w->ph[q] : nullptr,
+                               w->pf[q] + L.fwd_bytes[q], L.bulk_max ? w->pbf[q] + L.bflag_bytes[q] : nullptr};
+        for (int i = 0; i < 5; i++) {
+            if (!regs[i]) continue;
+            uint64_t got = 0;
+            HIPCHK(hipMemcpy(&got, regs[i], 8, hipMemcpyDeviceToHost));
+            if (got != region_nonce(b.nonce, i)) {
+                static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
+                // (what the mapping shows: 0 = never written, another nonce = an earlier allocation of that part)
+                const uint64_t eva[5] = {b.ctrl_ptr, b.vote_ptr, b.heap_ptr, b.fwd_ptr, b.bflag_ptr};
+                std::fprintf(stderr, "rlo: part %d: the %s region of part %d (at %#llx there), as mapped here at %p, shows "
+                             "%016llx, not its nonce %016llx (its other regions' words:",
+                             w->part, names[i], q, (unsigned long long)eva[i], regs[i], (unsigned long long)got,
+                             (unsigned long long)region_nonce(b.nonce, i));
+                for (int k = 0; k < 5; k++) {
+                    uint64_t g2 = 0;
+                    if (regs[k] && hipMemcpy(&g2, regs[k], 8, hipMemcpyDeviceToHost) == hipSuccess)
+                        std::fprintf(stderr, " %s %016llx", names[k], (unsigned long long)g2);
+                }
+                std::fprintf(stderr, ")\n");
+                return RLO_E_STALE;
+            }
+        }
+    }
+    w->peer_done[q] = 1;
+    return RLO_OK;
+}
+
+int rlo_part_import(rlo_world_t* w, const void* blob, int q) {
+    if (!w || !blob || q < 0 || q >= w->L.nparts || w->connected) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
+    peer_tables(w, w->L.nparts);
+    PartBlob b;
+    std::memcpy(&b, blob, sizeof b);
+    if (!blob_ok(w, b, q, w->L.nparts)) return RLO_E_INVAL;
+    if (w->peer_done[q]) return RLO_OK;
+    return import_peer(w, b, q);
+}
+
+int rlo_part_connect(rlo_world_t* w, const void* blobs, int n_parts) {
+    if (!w || !blobs || n_parts != w->L.nparts || w->connected) return RLO_E_INVAL;
+    HIPCHK(hipSetDevice(w->device));
+    const Layout& L = w->L;
+    peer_tables(w, n_parts);
     for (int q = 0; q < n_parts; q++) {
         PartBlob b;
         std::memcpy(&b, (const uint8_t*)blobs + (size_t)q * RLO_PART_BLOB_BYTES, sizeof b);
-        if (b.magic != kBlobMagic || b.part != q || b.nparts != n_parts || b.n != L.n || b.cap != L.cap ||
-            b.stride != L.stride || b.vote_cap != L.vote_cap || b.fwd_bytes != L.fwd_bytes[q] ||
-            b.vote_bytes != L.vote_bytes[q] || b.ctrl_bytes != L.ctrl_words[q] * 8 || b.heap_bytes != L.heap_bytes[q] ||
-            b.bflag_bytes != L.bflag_bytes[q])
-            return RLO_E_INVAL;
-        if (std::strncmp(b.bus, mybus, sizeof mybus) != 0) w->peers |= RLO_PEER_OTHER_GPU;
-        // A peer in another process (its regions imported through hipIpc, on this GPU or another) gets the
-        // hand-off the 8-GPU world runs: system-scope (sc0 sc1) stores, system-scope counter publishes and
-        // flag adds, system-scope releases before the bulk flags (the round-4 churn
-        // failures).  Only the bulk PLAN follows the GPU layout (RLO_PEER_OTHER_GPU -> chunked).
-        if (q != w->part && b.token != tok) w->peers |= RLO_PEER_IMPORTED;
-        w->sys_scope = w->peers ? 1 : 0;
-        // parts on other GPUs store into this part's rings and heaps over xGMI: a cached part's L2
-        // could hold lines those system-scope stores do not invalidate (rlo_hip.h RLO_PART_UNCACHED)
-        if (w->sys_scope && !(w->flags & RLO_PART_UNCACHED)) return RLO_E_INVAL;
-        if (q == w->part) {
-            w->pf[q] = w->fwd; w->pv[q] = w->vote; w->pc[q] = w->ctrl;
-            w->ph[q] = w->heap; w->pbf[q] = w->bflag;
-            // my own regions must still show the nonce rlo_part_create wrote (memory that changes under a part
-            // between its creation and its connection is not this part's to hand out)
-            const void* own[5] = {w->ctrl + rlo::kCtrlNonceWord, w->vote, L.bulk_max ? w->heap : nullptr,
-                                  w->fwd + L.fwd_bytes[q], L.bulk_max ? w->bflag + L.bflag_bytes[q] : nullptr};
-            for (int i = 0; i < 5; i++) {
-                if (!own[i]) continue;
-                uint64_t got = 0;
-                HIPCHK(hipMemcpy(&got, own[i], 8, hipMemcpyDeviceToHost));
-                if (got != w->nonce) {
-                    static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
-                    std::fprintf(stderr, "rlo: part %d: its own %s region at %p (%llu bytes) shows %016llx since creation, "
-                                 "not its nonce %016llx\n", q, names[i], own[i],
-                                 (unsigned long long)(i == 2 ? L.heap_bytes[q] : 0), (unsigned long long)got,
-                                 (unsigned long long)w->nonce);
-                    return RLO_E_STALE;
-                }
-            }
-        } else if (b.token == tok) {  // same process: the addresses are usable as they are
-            if (b.device != w->device) {
-                hipError_t e = hipDeviceEnablePeerAccess(b.device, 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { g_last_hip = (int)e; return RLO_E_HIP; }
-                (void)hipGetLastError();
-            }
-            w->pf[q] = (uint8_t*)(uintptr_t)b.fwd_ptr;
-            w->pv[q] = (uint8_t*)(uintptr_t)b.vote_ptr;
-            w->pc[q] = (uint64_t*)(uintptr_t)b.ctrl_ptr;
-            w->ph[q] = (uint8_t*)(uintptr_t)b.heap_ptr;
-            w->pbf[q] = (uint8_t*)(uintptr_t)b.bflag_ptr;
-        } else {  // another process: map its regions (dmabuf IPC; xGMI when on another GPU)
-            void* p = nullptr;
-            HIPCHK(hipIpcOpenMemHandle(&p, b.hf, hipIpcMemLazyEnablePeerAccess));
-            w->opened.push_back(p);
-            w->pf[q] = (uint8_t*)p;
-            HIPCHK(hipIpcOpenMemHandle(&p, b.hv, hipIpcMemLazyEnablePeerAccess));
-            w->opened.push_back(p);
-            w->pv[q] = (uint8_t*)p;
-            HIPCHK(hipIpcOpenMemHandle(&p, b.hc, hipIpcMemLazyEnablePeerAccess));
-            w->opened.push_back(p);
-            w->pc[q] = (uint64_t*)p;
-            if (L.bulk_max) {
-                HIPCHK(hipIpcOpenMemHandle(&p, b.hh, hipIpcMemLazyEnablePeerAccess));
-                w->opened.push_back(p);
-                w->ph[q] = (uint8_t*)p;
-                HIPCHK(hipIpcOpenMemHandle(&p, b.hb, hipIpcMemLazyEnablePeerAccess));
-                w->opened.push_back(p);
-                w->pbf[q] = (uint8_t*)p;
-            }
-            // every mapped region must show the peer's creation nonce (rlo_part_create)
-            const void* regs[5] = {w->pc[q] + rlo::kCtrlNonceWord, w->pv[q], L.bulk_max ? w->ph[q] : nullptr,
-                                   w->pf[q] + L.fwd_bytes[q], L.bulk_max ? w->pbf[q] + L.bflag_bytes[q] : nullptr};
-            for (int i = 0; i < 5; i++) {
-                if (!regs[i]) continue;
-                uint64_t got = 0;
-                HIPCHK(hipMemcpy(&got, regs[i], 8, hipMemcpyDeviceToHost));
-                if (got != b.nonce) {
-                    static const char* const names[5] = {"control", "vote", "heap", "forward", "bulk-flag"};
-                    // (what the mapping shows: 0 = never written, another nonce = an earlier allocation of that part)
-                    std::fprintf(stderr, "rlo: part %d: the %s region of part %d, as mapped here at %p, shows %016llx, not its "
-                                 "nonce %016llx (its other regions' words:",
-                                 w->part, names[i], q, regs[i], (unsigned long long)got, (unsigned long long)b.nonce);
-                    for (int k = 0; k < 5; k++) {
-                        uint64_t g2 = 0;
-                        if (regs[k] && hipMemcpy(&g2, regs[k], 8, hipMemcpyDeviceToHost) == hipSuccess)
-                            std::fprintf(stderr, " %s %016llx", names[k], (unsigned long long)g2);
-                    }
-                    std::fprintf(stderr, ")\n");
-                    return RLO_E_STALE;
-                }
-            }
-        }
+        if (!blob_ok(w, b, q, n_parts)) return RLO_E_INVAL;
+        if (w->peer_done[q]) continue;  // (rlo_part_import did it)
+        const int rc = import_peer(w, b, q);
+        if (rc) return rc;
     }
     build_topo(w);
     if (w->d_topo.upload(w->topo)) return RLO_E_HIP;
@@ -996,23 +1159,21 @@ static void host_free(rlo_world* w);
 int rlo_part_close_imports(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
     HIPCHK(hipSetDevice(w->device));
-    for (void* p : w->opened) (void)hipIpcCloseMemHandle(p);
+    for (void* p : w->opened) close_import(p);
     w->opened.clear();
     w->connected = false;
+    w->pf.clear();  // (a new connection maps the peers again)
     return RLO_OK;
 }
 
 int rlo_world_destroy(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
     (void)hipSetDevice(w->device);
-    for (void* p : w->opened) (void)hipIpcCloseMemHandle(p);
-    if (w->fwd) (void)hipFree(w->fwd);
-    if (w->vote) (void)hipFree(w->vote);
-    if (w->ctrl) (void)hipFree(w->ctrl);
-    if (w->heap) (void)hipFree(w->heap);
-    if (w->bflag) (void)hipFree(w->bflag);
-    if (w->jmem) (void)hipFree(w->jmem);
-    if (w->pend_mem) (void)hipFree(w->pend_mem);
+    for (void* p : w->opened) close_import(p);
+    w->opened.clear();
+    for (void* r : {(void*)w->fwd, (void*)w->vote, (void*)w->ctrl, (void*)w->heap, (void*)w->bflag, (void*)w->jmem,
+                    (void*)w->pend_mem})
+        release_region(r);
     w->d_bheap.release(); w->d_bflag.release(); w->d_part_of.release(); w->d_part_begin.release();
     w->d_topo.release(); w->d_stats.release();
     w->d_sched_off.release(); w->d_expect_bcast.release(); w->d_prop_off.release(); w->d_expect_dec.release();

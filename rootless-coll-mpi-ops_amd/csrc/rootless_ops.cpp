@@ -1000,7 +1000,17 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
     ok = agree(rc == RLO_OK);
     if (ok && e->leader) {
         MPI_Allgather(blob.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, blobs.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, leaders);
-        rc = rlo_part_connect(e->w, blobs.data(), n_parts);
+        // the mappings in n_parts stages (rlo_hip.h rlo_part_import): in stage k part k exports its handles afresh
+        // and every other leader imports them while part k imports nothing -- a handle exported before its exporter
+        // imported anything (later imports by the exporter were seen to make an earlier handle map another region)
+        for (int k = 0; k < n_parts && n_parts > 1; k++) {
+            std::vector<uint8_t> bk(RLO_PART_BLOB_BYTES, 0);
+            if (k == part && rlo_part_export(e->w, bk.data(), RLO_PART_BLOB_BYTES) < 0 && rc == RLO_OK) rc = RLO_E_HIP;
+            MPI_Bcast(bk.data(), RLO_PART_BLOB_BYTES, MPI_BYTE, k, leaders);
+            if (k != part && rc == RLO_OK) rc = rlo_part_import(e->w, bk.data(), k);
+            MPI_Barrier(leaders);
+        }
+        if (rc == RLO_OK) rc = rlo_part_connect(e->w, blobs.data(), n_parts);
         setup_trace(e->rank, "connected");
         if (rc == RLO_OK) {
             std::snprintf(shm_name, sizeof shm_name, "/rlo.%d.%d.%d", (int)getpid(), g_engines_ever + 1, part);

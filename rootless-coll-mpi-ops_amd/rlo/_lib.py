@@ -119,7 +119,7 @@ class LogRec(ctypes.Structure):
 
 
 # every symbol include/rlo_hip.h declares (checked by tests/test_abi.py)
-EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destroy", "rlo_part_close_imports", "rlo_world_query",
+EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destroy", "rlo_part_close_imports", "rlo_part_import", "rlo_world_query",
            "rlo_part_create", "rlo_part_export", "rlo_part_connect", "rlo_reset", "rlo_launch_ex",
            "rlo_stream_create", "rlo_stream_destroy",
            "rlo_program_storm", "rlo_program_latency", "rlo_program_iar", "rlo_launch", "rlo_wait", "rlo_run",
@@ -148,6 +148,7 @@ def load():
     L.rlo_world_create.argtypes = [ctypes.POINTER(WorldCfg), ctypes.POINTER(vp)]
     L.rlo_world_destroy.argtypes = [vp]
     L.rlo_part_close_imports.argtypes = [vp]
+    L.rlo_part_import.argtypes = [vp, ctypes.c_char_p, ctypes.c_int]
     L.rlo_world_query.argtypes = [vp, ctypes.POINTER(WorldInfo)]
     L.rlo_program_storm.argtypes = [vp, ctypes.POINTER(StormCfg)]
     L.rlo_program_latency.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]

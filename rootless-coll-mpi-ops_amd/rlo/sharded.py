@@ -111,7 +111,14 @@ def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, bl
                            device=device, uncached=uncached, **world_kw)
             blob_q.put((part, w.export()))
             blobs = blobs_q.get(timeout=120)
-            w.connect(blobs)
+
+            def bcast(blob, k):  # part k's fresh blob, relayed by the parent
+                if blob is not None:
+                    blob_q.put((k, blob))
+                return blobs_q.get(timeout=120)
+
+            # one exporter at a time, its handles exported at its own stage (rlo_hip.h rlo_part_import)
+            w.staged_connect(blobs, lambda: barrier.wait(timeout=120), bcast)
             _program(w, spec)
             w.reset()
             barrier.wait(timeout=120)  # every part is reset before any part launches
@@ -119,6 +126,10 @@ def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, bl
             rc = w.wait(raise_on_device_error=False)
             res = _collect(w, spec)
             barrier.wait(timeout=120)  # no peer still stores into this part's rings
+            # every part drops its imports of its peers' regions before any part frees its own (a part that frees and
+            # re-exports memory a peer still imports can hand that peer its OLD memory for the new handle)
+            w.close_imports()
+            barrier.wait(timeout=120)
             w.close()
             out_q.put((part, rc, res, None))
     except Exception as e:  # report instead of hanging the parent
@@ -147,6 +158,11 @@ def run_processes(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
             blobs = [got[p] for p in range(parts)]
             for q in blobs_qs:
                 q.put(blobs)
+            for k in range(parts):  # staged connect: part k's fresh blob to every part
+                pk, bk = blob_q.get(timeout=timeout)
+                assert pk == k, (pk, k)
+                for q in blobs_qs:
+                    q.put(bk)
             outs = [out_q.get(timeout=timeout) for _ in range(parts)]
             errs = [(p, e) for p, rc, r, e in outs if e]
             if errs:

@@ -80,6 +80,31 @@ class World:
     def reset(self, stream=None):
         check(self.lib.rlo_reset(self.h, stream), "rlo_reset")
 
+    def import_part(self, blob, q):
+        """rlo_part_import: map part q's regions now (connect() then skips q)"""
+        check(self.lib.rlo_part_import(self.h, blob, q), "rlo_part_import")
+
+    def staged_connect(self, blobs, barrier, bcast=None):
+        """connect in n_parts stages: in stage k every other part imports part k's regions while part k imports
+        nothing, then barrier() (rlo_hip.h rlo_part_import).  bcast(blob or None, k) -> part k's blob: part k
+        exports its handles afresh at the start of its stage and every part imports those (a handle exported
+        before its exporter imported anything).  An import error is raised after the last stage, so every part
+        still joins every barrier"""
+        err = None
+        me = self.info["part"]
+        for k, b in enumerate(blobs):
+            if bcast is not None:
+                b = bcast(self.export() if k == me else None, k)
+            if k != me and err is None:
+                try:
+                    self.import_part(b, k)
+                except Exception as e:  # noqa: BLE001 - re-raised below
+                    err = e
+            barrier()
+        if err is not None:
+            raise err
+        self.connect(blobs)
+
     def close_imports(self):
         """rlo_part_close_imports: drop the hipIpc imports of the peers' regions (the part can no longer launch)"""
         if self.h:

@@ -17,7 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 class FakeWorld:
     def __init__(self, part, fail_export=False, fail_connect=False, fail_launch=False):
         self.part, self.fail_connect, self.fail_launch = part, fail_connect, fail_launch
-        self.info = {"part": part}
+        self.info = {"part": part, "n_parts": 2}
         self.closed = False
         if fail_export:
             raise RuntimeError("create failed on part %d" % part)
@@ -29,6 +29,17 @@ class FakeWorld:
         assert blobs == [b"blob0", b"blob1"]
         if self.fail_connect:
             raise RuntimeError("connect failed on part %d" % self.part)
+
+    def import_part(self, blob, k):
+        assert blob == b"blob%d" % k
+
+    def staged_connect(self, blobs, barrier, bcast=None):
+        from rlo.world import World  # the real staging logic over this fake's export / import_part / connect
+
+        World.staged_connect(self, blobs, barrier, bcast)
+
+    def close_imports(self):
+        pass
 
     def reset(self, stream=None):
         pass
