@@ -71,13 +71,32 @@ def dump_write(rank):
         json.dump(_DUMP["recs"], f)
 
 
-def cpu_baseline(n, length, seed, target_s):
+def cpu_baseline(n, length, seed, target_s, bulk=None):
     """The oracle's clean-room CPU restatement ("port") on the box's host cores: the same storm (n
     virtual ranks, length-byte payloads, random originators) with every tree edge copying the bytes,
     the ranks dealt to `threads` host threads (oracle/rlo_oracle.c orc_storm_mt), bounded sample.
-    Beside it: the compiled reference itself under host MPI at its own 4- and 8-rank worlds."""
+    Beside it: the compiled reference itself under host MPI at its own 4- and 8-rank worlds.
+    The oracle is also the checker of the bulk leg (`bulk`): every receiver's checksum of every round's bytes
+    against orc.msg_checksum of the oracle's payload (not launch-to-launch equality alone)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle as orc
+
+    if bulk:
+        for rec in bulk.get("sizes", []):
+            chk = rec.pop("_check", None)
+            if chk is None:
+                continue
+            got = chk["sum"]
+            g = len(got)
+            want = [0] * g
+            for i in range(chk["rounds"]):
+                o = orc.origin_of(chk["seed"], i, g)
+                cs = orc.msg_checksum(o, i, 0, orc.payload(o, i, chk["len"]))
+                for r in range(g):
+                    if r != o:
+                        want[r] = (want[r] + cs) & 0xFFFFFFFFFFFFFFFF
+            rec["verified_oracle"] = [int(x) for x in got] == want
+            rec["verified"] = bool(rec["verified"] and rec["verified_oracle"])
 
     threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU is 16
     t = time.perf_counter()
@@ -477,6 +496,8 @@ def bulk_leg(rlo, dist, world, rank, local, stream, red, sizes_mib=(1, 4, 16, 64
             ok = red(0.0 if ok else 1.0, "max") == 0.0
             rec = {"MiB": mib, "round_ms": round(rt * 1e3, 4), "kernel_ms_per_round": round(red(kms[1], "max") / rounds, 4),
                    "verified": bool(ok)}
+            if world == 1:  # per-receiver checksums, checked against the oracle in the cpu_baseline leg
+                rec["_check"] = {"seed": 0xB0 + mib, "rounds": rounds, "len": nbytes, "sum": sums[1].tolist()}
             rec["algbw_GBps"] = round(nbytes / rt / 1e9, 2) if rt > 0 else None
             if world == 1 and rt > 0:
                 # one GPU (direct plan): the origin's copy written at origination and read once by the
@@ -950,7 +971,11 @@ def main():
             line["c4_vs_reference"] = c4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         note("cpu baseline")
-        line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds, bulk=line.get("bulk"))
+        if line.get("bulk", {}).get("sizes"):
+            line["verified"] = bool(line["verified"] and all(s["verified"] for s in line["bulk"]["sizes"]))
+    for s in (line.get("bulk") or {}).get("sizes", []):
+        s.pop("_check", None)  # --no-cpu-baseline: unchecked against the oracle (launch-to-launch equality only)
     dump_write(rank)
     if rank == 0:
         print(json.dumps(line), flush=True)

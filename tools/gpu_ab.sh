@@ -1,10 +1,10 @@
-# round-5 A/B of this tree's library against a baseline build (tools/ab_libs/<base>, lib_<base>/):
+# A/B of this tree's library against a baseline build (tools/ab_libs/<base>, lib_<base>/):
 # latency + one-proposal decisions (tools/lat_ab.py), the 256-rank storms (tools/storm_ab.py) and the 8-rank
 # bulk rounds (tools/bulk_probe.py), interleaved
 set -o pipefail
 base=${1:-r5base}; tag=${2:-ab}
-mkdir -p gpurun_out/r5
-out=gpurun_out/r5/ab_$tag.txt
+mkdir -p gpurun_out/${RLO_OUT:-r5}
+out=gpurun_out/${RLO_OUT:-r5}/ab_$tag.txt
 : > $out
 timeout -k 10 300 python3 -u tools/lat_ab.py $base 8 256 >> $out 2>&1 || exit $?
 for rep in 1 2; do
