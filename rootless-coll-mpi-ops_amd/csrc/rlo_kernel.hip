@@ -314,7 +314,7 @@ __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { retu
 // (the program-specialised doorbell kernels only: the general ones have no registers to spare)
 #define HP(k)                                                                                  \
     do {                                                                                       \
-        if constexpr (PM == kPmLat || PM == kPmIar)                                            \
+        if constexpr (PM == kPmLat || PM == kPmIar || PM == kPmHost)                           \
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[(k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
@@ -1287,6 +1287,7 @@ constexpr uint32_t kPmAll = 0xFFFFFFFFu;
 constexpr uint32_t kPmLat = ~(uint32_t)(MODE_STORM | MODE_IAR | MODE_HOST);
 constexpr uint32_t kPmIar = ~(uint32_t)(MODE_STORM | MODE_LAT | MODE_HOST);
 constexpr uint32_t kPmStorm = ~(uint32_t)(MODE_LAT | MODE_IAR | MODE_HOST);
+constexpr uint32_t kPmHost = ~(uint32_t)(MODE_STORM | MODE_LAT | MODE_IAR);  // the drop-in's host service
 
 // PH: the pending-proposal tables live in HBM (Params.pend_hbm; worlds whose N x pool entries would crowd
 // the small copy path's stage out of LDS: the 8-GPU worlds), instantiated for the programs that hold
@@ -1351,7 +1352,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1;
-    const bool host = (PMODE(MODE_HOST)) != 0;
+    const bool host = PM == kPmHost || (PMODE(MODE_HOST)) != 0;  // (kPmHost: launched for host mode only)
     // counters are published at the end of the iteration whose stores they cover (all waves
     // drained), not after the next poll: one poll round trip less per hop (p50 -8%, decisions/s
     // +11%).  Not in the storm program: there the drain overlaps wave 0's bookkeeping and poll
@@ -1782,7 +1783,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         need_full = false;
         HP(0);
 #ifdef RLO_DIAG
-        if constexpr (PM == kPmLat || PM == kPmIar)
+        if constexpr (PM == kPmLat || PM == kPmIar || PM == kPmHost)
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[3] = 0;
 #endif
         if (__ballot(errf != 0)) return 0u;
@@ -2101,7 +2102,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
         HP(8);
 #ifdef RLO_DIAG
-        if constexpr (PM == kPmLat || PM == kPmIar)
+        if constexpr (PM == kPmLat || PM == kPmIar || PM == kPmHost)
             if ((P.mode & MODE_HOPPROF) && lane == 0 && done == 1u && S.hpt[3] != 0) {  // one ring message, nothing else
                 for (int k = 0; k < 8; k++) S.prof[k] += S.hpt[k + 1] - S.hpt[k];
                 S.dbg[0]++;
@@ -3801,29 +3802,36 @@ static bool wants_ph(const rlo::Params* p) {
 
 // The kernels of the device programs the bench times are specialised by program (PM): 8 waves -- the storm
 // (no doorbells), the latency program and the iar program (doorbells; the iar one with the LDS or the HBM
-// pending table); bulk worlds -- the latency program (C3) and the storm (C5).  Their register use never exceeds the general instantiation's, whose occupancy the host
+// pending table); bulk worlds -- the latency program (C3) and the storm (C5); and the host service the drop-in
+// runs (doorbells; every variant, LDS or HBM tables).  Their register use never exceeds the general instantiation's, whose occupancy the host
 // checks (rlo_occupancy*); the Makefile guard holds every 8-wave instantiation to 2 waves per SIMD.
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
     const uint32_t prog = p->mode & (rlo::MODE_STORM | rlo::MODE_LAT | rlo::MODE_IAR | rlo::MODE_HOST);
+    const bool hll = ll && prog == rlo::MODE_HOST;  // the drop-in's host service with doorbells
     if (wants_ph(p) && variant != 5) {
         if (variant == 8) {
             if (ll && prog == rlo::MODE_IAR) return launch_v<8, false, true, true, rlo::kPmIar>(p, blocks, dyn_lds, stream);
+            if (hll) return launch_v<8, false, true, true, rlo::kPmHost>(p, blocks, dyn_lds, stream);
             return ll ? launch_v<8, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false, true>(p, blocks, dyn_lds, stream);
         }
+        if (hll) return launch_v<4, false, true, true, rlo::kPmHost>(p, blocks, dyn_lds, stream);
         return ll ? launch_v<4, false, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false, true>(p, blocks, dyn_lds, stream);
     }
     if (variant == 8) {
         if (ll && prog == rlo::MODE_LAT) return launch_v<8, false, true, false, rlo::kPmLat>(p, blocks, dyn_lds, stream);
         if (ll && prog == rlo::MODE_IAR) return launch_v<8, false, true, false, rlo::kPmIar>(p, blocks, dyn_lds, stream);
         if (!ll && prog == rlo::MODE_STORM) return launch_v<8, false, false, false, rlo::kPmStorm>(p, blocks, dyn_lds, stream);
+        if (hll) return launch_v<8, false, true, false, rlo::kPmHost>(p, blocks, dyn_lds, stream);
         return ll ? launch_v<8, false, true>(p, blocks, dyn_lds, stream) : launch_v<8, false, false>(p, blocks, dyn_lds, stream);
     }
     if (variant == 5) {  // bulk worlds: the C3 leg's latency program (doorbells) and the C5 storm, specialised too
         if (ll && prog == rlo::MODE_LAT) return launch_v<4, true, true, false, rlo::kPmLat>(p, blocks, dyn_lds, stream);
         if (!ll && prog == rlo::MODE_STORM) return launch_v<4, true, false, false, rlo::kPmStorm>(p, blocks, dyn_lds, stream);
+        if (hll) return launch_v<4, true, true, false, rlo::kPmHost>(p, blocks, dyn_lds, stream);
         return ll ? launch_v<4, true, true>(p, blocks, dyn_lds, stream) : launch_v<4, true, false>(p, blocks, dyn_lds, stream);
     }
+    if (hll) return launch_v<4, false, true, false, rlo::kPmHost>(p, blocks, dyn_lds, stream);
     return ll ? launch_v<4, false, true>(p, blocks, dyn_lds, stream) : launch_v<4, false, false>(p, blocks, dyn_lds, stream);
 }
 

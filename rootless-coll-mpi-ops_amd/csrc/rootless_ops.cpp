@@ -71,6 +71,19 @@ struct Cmd {  // a command waiting for room in the command ring
 struct RawEv {  // a pickup-ring event pulled off the device, not yet handled on the app thread
     rlo_log_rec_t ev;
     std::vector<uint8_t> payload;
+    int64_t t_seen = 0;  // RLO_TRACE_DIR: when the pump took it off the pickup ring
+};
+
+// RLO_TRACE_DIR=dir (diagnostics): every command posted, every event taken off the pickup ring and handled,
+// and every advance of the kernel's command head, with the host clock (CLOCK_MONOTONIC: one clock for every rank
+// process of the node), written to dir/trace_rank<R>_e<id>.txt at cleanup; tools/dropin_legs.py splits a bcast's
+// and a host-judged proposal's time into legs from them
+struct TraceRec {
+    int64_t t;
+    char what;  // 'P' command posted, 'S' event seen (pump), 'H' event handled (app thread), 'C' commands consumed
+    uint32_t kind;
+    int32_t origin, id, from;
+    uint32_t aux;
 };
 
 }  // namespace
@@ -125,6 +138,9 @@ struct progress_engine {
     int64_t d_cons_ns = 0, d_fwd_ns = 0;
     uint32_t d_hist[2][5] = {}, d_fh[2][5] = {};  // d_fh: submit -> forwarded by the proxy, forwarded -> consumed
     int64_t t_moved = 0, t_dump = 0;  // RLO_WATCHDOG: last event / last state dump
+    std::vector<TraceRec> tr;         // RLO_TRACE_DIR (the app and pump threads both append: tr_mu)
+    std::mutex tr_mu;
+    uint64_t tr_consumed = 0;
     progress_engine* next = nullptr;
 };
 
@@ -137,6 +153,29 @@ std::vector<RLO_msg_t*> g_pool;         // recycled received messages
 
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+const char* trace_dir() {
+    static const char* d = std::getenv("RLO_TRACE_DIR");
+    return d && *d ? d : nullptr;
+}
+
+void trace(progress_engine* e, char what, uint32_t kind, int32_t origin, int32_t id, int32_t from, uint32_t aux,
+           int64_t t = 0) {
+    std::lock_guard<std::mutex> lk(e->tr_mu);
+    if (e->tr.size() >= (1u << 22)) return;
+    e->tr.push_back(TraceRec{t ? t : now_ns(), what, kind, origin, id, from, aux});
+}
+
+void trace_write(progress_engine* e) {
+    char path[4096];
+    std::snprintf(path, sizeof path, "%s/trace_rank%d_e%d.txt", trace_dir(), e->rank, e->id);
+    FILE* f = std::fopen(path, "w");
+    if (!f) return;
+    std::fprintf(f, "# rank %d size %d engine %d\n", e->rank, e->size, e->id);
+    for (const TraceRec& r : e->tr)
+        std::fprintf(f, "%lld %c %u %d %d %d %u\n", (long long)r.t, r.what, r.kind, r.origin, r.id, r.from, r.aux);
+    std::fclose(f);
 }
 
 // RLO_TRACE_SETUP=1: engine construction steps with timestamps on stderr (diagnostics)
@@ -204,6 +243,7 @@ size_t pbuf_put(char* out, RLO_ID pid, RLO_Vote vote, uint64_t len, const void* 
 
 int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t len, RLO_msg_t* msg) {
     std::lock_guard<std::mutex> lk(e->mu);
+    if (trace_dir()) trace(e, 'P', c.kind, c.origin, c.id, -1, c.pseq);
     if (e->backlog.empty()) {
         int rc = rlo_client_post(e->cl, &c, payload, len);
         if (rc == RLO_OK) {
@@ -459,6 +499,7 @@ bool pump(progress_engine* e) {
         if (r != 1) break;
         RawEv q;
         q.ev = ev;
+        if (trace_dir()) q.t_seen = now_ns();
         if (ev.payload_idx != 0xffffffffu) {
             const uint32_t n = ev.len < (uint32_t)e->evbuf.size() ? ev.len : (uint32_t)e->evbuf.size();
             q.payload.assign(e->evbuf.data(), e->evbuf.data() + n);
@@ -466,6 +507,12 @@ bool pump(progress_engine* e) {
         e->evq.push_back(std::move(q));
     }
     if (got) flush_backlog(e);
+    if (trace_dir()) {
+        uint64_t consumed = 0;
+        rlo_client_cmd_count(e->cl, &consumed, nullptr);
+        if (consumed != e->tr_consumed) trace(e, 'C', 0, -1, (int32_t)consumed, -1, 0);
+        e->tr_consumed = consumed;
+    }
     return got || e->backlog.size() != backlog0;
 }
 
@@ -535,7 +582,13 @@ void progress(progress_engine* e) {
     }
     e->n_progress++;
     e->n_events += local.size();
-    for (const RawEv& q : local) handle_event(e, q.ev, q.payload.data());
+    for (const RawEv& q : local) {
+        if (trace_dir()) {
+            trace(e, 'S', q.ev.kind, q.ev.origin, (int32_t)q.ev.id, q.ev.from, q.ev.aux, q.t_seen);
+            trace(e, 'H', q.ev.kind, q.ev.origin, (int32_t)q.ev.id, q.ev.from, q.ev.aux);
+        }
+        handle_event(e, q.ev, q.payload.data());
+    }
     if (local.empty() && (++e->poll_tick & 255u) == 0) check_alive(e);
     static const double wd = std::getenv("RLO_WATCHDOG") ? std::atof(std::getenv("RLO_WATCHDOG")) : 0.0;
     if (wd > 0) watchdog(e, !local.empty(), (int64_t)(wd * 1e9));
@@ -1146,6 +1199,7 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
         std::fprintf(stderr, "rlo trace rank %d split: submit->forwarded %u %u %u %u %u | forwarded->consumed %u %u %u %u %u\n",
                      eng->rank, eng->d_fh[0][0], eng->d_fh[0][1], eng->d_fh[0][2], eng->d_fh[0][3], eng->d_fh[0][4],
                      eng->d_fh[1][0], eng->d_fh[1][1], eng->d_fh[1][2], eng->d_fh[1][3], eng->d_fh[1][4]);
+    if (trace_dir()) trace_write(eng);
     // collective quiescence (:1607-1627): every bcast and decision sent anywhere has arrived here
     int sent = (int)eng->sent_bcast, total = 0, done = 0;
     MPI_Request req;

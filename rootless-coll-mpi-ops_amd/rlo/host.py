@@ -27,11 +27,12 @@ def pbuf(pid, vote, data):
 
 class HostWorld:
     def __init__(self, n, max_payload=256, device=-1, cmd_slots=0, pickup_slots=0, idle_timeout_s=60, pool=1,
-                 pend_hbm=False):
+                 pend_hbm=False, **world_kw):
         """pool: own proposals a rank may keep in flight (the proposal pool; 1 = my_own_proposal);
-        pend_hbm: the pending-proposal tables in HBM (the 8-GPU layout, rehearsed)"""
+        pend_hbm: the pending-proposal tables in HBM (the 8-GPU layout, rehearsed); world_kw: World's other
+        arguments (bulk_max, movers, ring_slots ... -- the drop-in's world shape)"""
         self.world = World(n, max_payload=max_payload, device=device, proposal_pool=max(2, 1 << (pool - 1).bit_length()),
-                           pend_hbm=pend_hbm)
+                           pend_hbm=pend_hbm, **world_kw)
         self.lib = self.world.lib
         self.h = self.world.h
         self.n = n
