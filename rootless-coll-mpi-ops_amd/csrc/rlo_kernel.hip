@@ -314,12 +314,21 @@ __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { retu
 // (the program-specialised doorbell kernels only: the general ones have no registers to spare)
 #define HP(k)                                                                                  \
     do {                                                                                       \
-        if constexpr (PM == kPmLat || PM == kPmIar || PM == kPmHost)                           \
+        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))                           \
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[(k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+// ... and S.dbg[k] counts why a doorbell pass handed over to the full iteration (hop_prof.py prints them)
+#define HPC(k)                                                                                 \
+    do {                                                                                       \
+        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))                           \
+            if ((P.mode & MODE_HOPPROF) && lane == 0) S.dbg[(k)]++;                            \
     } while (0)
 #else
 #define HP(k) \
     do {      \
+    } while (0)
+#define HPC(k) \
+    do {       \
     } while (0)
 #endif
 // MODE_PROF: thread 0 charges the shader cycles since the last stamp to phase `ph`
@@ -1287,7 +1296,7 @@ constexpr uint32_t kPmAll = 0xFFFFFFFFu;
 constexpr uint32_t kPmLat = ~(uint32_t)(MODE_STORM | MODE_IAR | MODE_HOST);
 constexpr uint32_t kPmIar = ~(uint32_t)(MODE_STORM | MODE_LAT | MODE_HOST);
 constexpr uint32_t kPmStorm = ~(uint32_t)(MODE_LAT | MODE_IAR | MODE_HOST);
-constexpr uint32_t kPmHost = ~(uint32_t)(MODE_STORM | MODE_LAT | MODE_IAR);  // the drop-in's host service
+constexpr uint32_t kPmHost = ~(uint32_t)(MODE_STORM | MODE_LAT);  // the drop-in's host service (MODE_HOST | MODE_IAR)
 
 // PH: the pending-proposal tables live in HBM (Params.pend_hbm; worlds whose N x pool entries would crowd
 // the small copy path's stage out of LDS: the 8-GPU worlds), instantiated for the programs that hold
@@ -1783,7 +1792,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         need_full = false;
         HP(0);
 #ifdef RLO_DIAG
-        if constexpr (PM == kPmLat || PM == kPmIar || PM == kPmHost)
+        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[3] = 0;
 #endif
         if (__ballot(errf != 0)) return 0u;
@@ -1812,13 +1821,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
         const bool ldr = lane < n_in2 && ip > 0ull && !rhit;  // a counter-visible head without its bell: load it
         const uint64_t ldm = __ballot(ldr);
-        if (__ballot(ip > 2ull || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { need_full = true; return 0u; }
+        if (__ballot(ip > 2ull || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { HPC(1); need_full = true; return 0u; }
         HP(1);
         uint32_t ncmd = 0;  // host commands to take (FIFO order, the first kLLCmds)
         bool cbell = false;  // ... the one in the command doorbell (already loaded, at kLLCmd)
         if (host) {  // too little room in the pickup ring: wait for the host
             const uint32_t pk_free = P.log_cap - (uint32_t)(S.pk_tail - rdl64(hpoll, 1));
-            if (pk_free < 2u * (uint32_t)__popcll(__ballot(rhit || ldr)) + 2u * P.own_pool + 8u) return 0u;
+            if (pk_free < 2u * (uint32_t)__popcll(__ballot(rhit || ldr)) + 2u * P.own_pool + 8u) { HPC(7); return 0u; }
             if (ll_cmds) {
                 const uint64_t ct = rdl64(hpoll, 0), hh = S.hin_head;
                 ncmd = ct > hh ? (uint32_t)min(ct - hh, (uint64_t)kLLCmds) : 0u;
@@ -1924,7 +1933,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     }
                 } else if (htag == TAG_BCAST || htag == TAG_PROPOSAL) {  // RLO_bcast_gen :1581 / RLO_submit_proposal :876
                     const uint32_t len = hd.z & 0xffffu;
-                    if (((kHdr + len + 15u) >> 4) > lcap || sll == 0) { need_full = true; break; }
+                    if (((kHdr + len + 15u) >> 4) > lcap || sll == 0) { HPC(2); need_full = true; break; }
                     if (htag == TAG_BCAST) {
                         if (!originate(K_HOST, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), hd.y, len,
                                        kLLCmd + 128u * taken, out_head_r))
@@ -1949,6 +1958,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         }
                     }
                 } else {  // quit, bulk: the full iteration's
+                    HPC(2);
                     need_full = true;
                     break;
                 }
@@ -1992,11 +2002,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (TL_ON(P) && lane == 0) S.tl_clk[3] = (uint32_t)now_ticks();
             HP(3);
             const uint32_t need = lone(v, g, 0u, true, out_head_r);
+            if (need == kHeld) HPC(6);
             if (need == kHeld || need == kAsked) {  // waits for the host's verdict (asked now: progress)
                 if (need == kAsked) done++;
                 continue;
             }
             if (need == ~0u) {  // the full path takes it, through its counter
+                HPC(3);
                 if (!fromb) need_full = true;
                 continue;
             }
@@ -2081,6 +2093,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
         }
         if (!done) return 0u;
+        HPC(4);
         // every store of the pass drained, then the counters (the eager scheme's publish)
         VM_DRAIN();
         HP(7);
@@ -2102,7 +2115,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
         HP(8);
 #ifdef RLO_DIAG
-        if constexpr (PM == kPmLat || PM == kPmIar || PM == kPmHost)
+        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))
             if ((P.mode & MODE_HOPPROF) && lane == 0 && done == 1u && S.hpt[3] != 0) {  // one ring message, nothing else
                 for (int k = 0; k < 8; k++) S.prof[k] += S.hpt[k + 1] - S.hpt[k];
                 S.dbg[0]++;
@@ -3710,7 +3723,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
 
     // ---------------- flush statistics
     if constexpr (BULK) {
-        if (tid == 0 && !(PMODE(MODE_PROF | MODE_TL))) {  // diagnostics in stats.dbg: pending receptions at exit
+        if (tid == 0 && !(P.mode & (MODE_PROF | MODE_TL | MODE_HOPPROF))) {  // diagnostics in stats.dbg: pending receptions at exit
             const uint32_t nb = S.b.nbact;
             S.dbg[0] = ((uint64_t)S.b.bulk_q << 32) | nb;
             for (uint32_t i = 0; i < 3 && i < nb; i++) {
@@ -3808,7 +3821,7 @@ static bool wants_ph(const rlo::Params* p) {
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
     const uint32_t prog = p->mode & (rlo::MODE_STORM | rlo::MODE_LAT | rlo::MODE_IAR | rlo::MODE_HOST);
-    const bool hll = ll && prog == rlo::MODE_HOST;  // the drop-in's host service with doorbells
+    const bool hll = ll && (prog & rlo::MODE_HOST) != 0;  // the drop-in's host service (HOST | IAR) with doorbells
     if (wants_ph(p) && variant != 5) {
         if (variant == 8) {
             if (ll && prog == rlo::MODE_IAR) return launch_v<8, false, true, true, rlo::kPmIar>(p, blocks, dyn_lds, stream);

@@ -243,7 +243,11 @@ size_t pbuf_put(char* out, RLO_ID pid, RLO_Vote vote, uint64_t len, const void* 
 
 int post(progress_engine* e, const rlo_cmd_t& c, const void* payload, uint32_t len, RLO_msg_t* msg) {
     std::lock_guard<std::mutex> lk(e->mu);
-    if (trace_dir()) trace(e, 'P', c.kind, c.origin, c.id, -1, c.pseq);
+    if (trace_dir()) {  // with the command's index in this rank's command stream (the kernel's head passes it)
+        uint64_t posted = 0;
+        rlo_client_cmd_count(e->cl, nullptr, &posted);
+        trace(e, 'P', c.kind, c.origin, c.id, (int32_t)(posted + e->backlog.size() + 1), c.pseq);
+    }
     if (e->backlog.empty()) {
         int rc = rlo_client_post(e->cl, &c, payload, len);
         if (rc == RLO_OK) {
@@ -1244,6 +1248,27 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
         int rc = rlo_wait(eng->w);
         if (rc != RLO_OK && !eng->failed)
             std::fprintf(stderr, "rlo: rank %d engine %d: kernel ended with %s\n", eng->rank, eng->id, rlo_strerror(rc));
+        if (std::getenv("RLO_HOP_PROF")) {  // diagnostics build: the part's doorbell-pass profile (tools/hop_prof.py)
+            rlo_world_info_t wi;
+            if (rlo_world_query(eng->w, &wi) == RLO_OK) {
+                const int nl = wi.rank_end - wi.rank_begin;
+                std::vector<rlo_rank_stats_t> st((size_t)nl);
+                if (rlo_stats(eng->w, st.data(), nl) == RLO_OK) {
+                    uint64_t pr[8] = {}, db[8] = {}, it = 0, busy = 0;
+                    for (const auto& x : st) {
+                        for (int k = 0; k < 8; k++) { pr[k] += x.prof[k]; db[k] += x.dbg[k]; }
+                        it += x.iterations;
+                        busy += x.busy_iterations;
+                    }
+                    std::fprintf(stderr, "rlo hopprof part %d: hops %llu, cycles per hop", wi.part, (unsigned long long)db[0]);
+                    for (int k = 0; k < 8; k++) std::fprintf(stderr, " %.0f", db[0] ? (double)pr[k] / db[0] : 0.0);
+                    std::fprintf(stderr, " | passes %llu, to full: busy %llu cmd %llu lone %llu | held %llu pk-room %llu | "
+                                 "iterations %llu busy %llu\n", (unsigned long long)db[4], (unsigned long long)db[1],
+                                 (unsigned long long)db[2], (unsigned long long)db[3], (unsigned long long)db[6],
+                                 (unsigned long long)db[7], (unsigned long long)it, (unsigned long long)busy);
+                }
+            }
+        }
     }
     MPI_Barrier(eng->comm);
     for (RLO_msg_t* m : eng->pickup) msg_release(m);

@@ -41,9 +41,26 @@ def test_bench_world_parts_layout(rlo, n, parts):
 
 
 def test_c5_world_part_at_8_gpus(rlo):
-    """bench.py's C5 leg at 8 GPUs: 512 ranks, bulk messages to 1 MiB (was refused: N x B > 256)"""
-    with rlo.World.part(512, 8, 3, max_payload=4096, device=0, uncached=True, bulk_max=1 << 20) as w:
-        assert w.info["bulk_slots"] == 2 and w.info["nsmall"] == 5 and w.info["waves"] == 4
+    """bench.py's C5 leg at 8 GPUs: 512 ranks, bulk messages to 1 MiB (was refused: N x B > 256); the host plan
+    (rlo_layout_plan) agrees with what the part got on the GPU (the bulk variant's model)"""
+    kw = dict(max_payload=4096, bulk_max=1 << 20)
+    with rlo.World.part(512, 8, 3, device=0, uncached=True, **kw) as w:
+        got = {k: w.info[k] for k in KEYS + ("bulk_slots",)}
+    assert got["bulk_slots"] == 2 and got["nsmall"] == 5 and got["waves"] == 4
+    plan = rlo.layout_plan(512, 8, 3, cus=w.info["cus"], **kw)
+    assert got == {k: plan[k] for k in got}, (got, plan)
+
+
+@pytest.mark.parametrize("n,payload,pend_hbm", [(320, 256, False), (384, 1024, False), (300, 64, True)])
+def test_four_wave_parts_plan_matches(rlo, n, payload, pend_hbm):
+    """4-wave parts with more local ranks than CUs (two rank-workgroups per CU: doorbells only where the 4-wave
+    LL instantiation keeps 2 waves per SIMD), medium and large slots, LDS and HBM tables: the host plan agrees
+    with the part the GPU built (waves, staged chunks, doorbells, table placement)"""
+    with rlo.World(n, max_payload=payload, device=0, pend_hbm=pend_hbm) as w:
+        got = {k: w.info[k] for k in KEYS}
+    plan = rlo.layout_plan(n, max_payload=payload, pend_hbm=pend_hbm, cus=w.info["cus"])
+    assert got == {k: plan[k] for k in KEYS}, (got, plan)
+    assert got["waves"] == 4 and (got["pend_hbm"] == 1 or not pend_hbm)
 
 
 @pytest.mark.parametrize("n,p,ppm,pool", [(256, 4, 201, 1), (256, 8, 201, 16), (64, 16, 50000, 4), (8, 64, 20000, 16),

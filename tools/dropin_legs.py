@@ -105,6 +105,20 @@ def proposals(recs):
                 dec[(o, i)].append(t)
     if not sub:
         return
+    # command in: a verdict posted -> the first time this rank saw the kernel's command head past it
+    cin = []
+    for r, rows in recs.items():
+        cons = [(t, i) for t, w, k, o, i, fr, aux in rows if w == "C"]  # time order, counts non-decreasing
+        ci = 0
+        for t, w, k, o, i, fr, aux in rows:
+            if w == "P" and k == CMD_JUDGE and fr > 0:
+                while ci < len(cons) and cons[ci][0] < t:
+                    ci += 1
+                cj = ci
+                while cj < len(cons) and cons[cj][1] < fr:
+                    cj += 1
+                if cj < len(cons):
+                    cin.append((cons[cj][0] - t) / 1e3)
     hop, queue, cb, up, ownsvc, decl, resl, total, down = [], [], [], [], [], [], [], [], []
     for (o, pid), ts in sub.items():
         if (o, pid) not in res:
@@ -139,6 +153,7 @@ def proposals(recs):
     summary("submit -> result seen (total)", total)
     summary("submit -> last judge request seen (down)", down)
     summary("one hop: parent's verdict/submit -> request seen", hop)
+    summary("verdict posted -> command head past it (seen)", cin)
     summary("request seen -> handled (app thread queue)", queue)
     summary("handled -> verdict posted (judge callback)", cb)
     summary("last verdict posted -> own judge(NULL) seen (up)", up)
