@@ -1615,6 +1615,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
         if (!ok) return ~0u;
         HP(4);
+        // the forwards first: a child's copy does not wait for this rank's own effects (its pickup record and
+        // payload -- PCIe writes in host mode --, counters, pending state), as the reference forwards before it
+        // queues the pickup (rootless_ops.c:583-589)
+        fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
+        HP(5);
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P1, lr, (uint32_t)now_ticks());
         if (ftag == TAG_BCAST) {
             if (lane == 0) {
@@ -1691,8 +1696,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
-        HP(5);
-        fwd_small(v, fnch, fneed);  // the same slot bytes into every needed out-ring (phase G)
         HP(6);
         if constexpr (BULK) {
             if (TL_ON(P) && ftag == TAG_BULK && lane == 0) {

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "rootless-coll-mpi-ops_amd"))
 import rlo  # noqa: E402
 
 SEG = ["pass entry -> bells checked", "-> votes / commands done", "-> ring loop at the message", "-> lone(): checks",
-       "-> effects", "-> forwards (fwd_small)", "-> pass drained", "-> counters published"]
+       "-> forwards (fwd_small)", "-> effects", "-> pass drained", "-> counters published"]
 HOST = "--host" in sys.argv  # the drop-in's host service instead: its world shape, one bcast at a time, polled here
 
 
