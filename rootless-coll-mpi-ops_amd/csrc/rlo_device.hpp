@@ -72,6 +72,7 @@ enum Mode : uint32_t {
     MODE_LL = 16384u,     // doorbells (below): lone messages and originations hop without a counter round trip
     MODE_TL = 32768u,     // latency program: per-round event clocks into Params.tl (RLO_FLAG_TIMELINE; no path changes)
     MODE_HOPPROF = 131072u,  // diagnostics build: shader clocks at points of a doorbell hop into stats.prof (tools/hop_prof.py)
+    MODE_NOHPW = 262144u,   // diagnostics build, host mode A/B: no wave-1 host poller (wave 0 polls the host words itself)
     MODE_CORRUPT = 65536u,  // diagnostics build, test of the VERIFY check: a direct scatter zeroes one granule of one copy
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)

@@ -263,6 +263,27 @@ __device__ __forceinline__ u32x4 ld_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 __device__ __forceinline__ uint64_t poll64_sys(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// The host service's wave-1 poller reads pinned host memory through the SCALAR data path (s_load ... glc: a miss in
+// the scalar cache every time, so each poll sees the host's latest stores); only a command longer than 16 payload
+// bytes, once seen, has its other chunks read with vector loads.  Its vector loads to host memory held up
+// the other waves' VRAM loads on the CU: a wave timing dependent 16-B uncached VRAM loads saw 0.134 us per load
+// beside an idle wave, 0.672 us beside one polling host memory with vector loads, 0.136 us beside one polling it with
+// scalar loads (tools/probe/poll_interference.hip, profiles/r5_poll_interference.txt) -- and wave 0's doorbell polls
+// are such loads.  Loads only: nothing is ever written through the scalar cache.
+typedef uint32_t su16 __attribute__((ext_vector_type(16)));
+// the first 64 B of a command doorbell (chunks 0-1: a verdict, a judge(NULL) verdict, the header of any command)
+// and two host words (command tail, pickup head), one round trip
+__device__ __forceinline__ void spoll_cmd(const uint8_t* slot, const uint64_t* w0, const uint64_t* w1, su16& a,
+                                          uint64_t& x0, uint64_t& x1) {
+    asm volatile(
+        "s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+        "s_load_dwordx2 %1, %4, 0x0 glc\n\t"
+        "s_load_dwordx2 %2, %5, 0x0 glc\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(a), "=&s"(x0), "=&s"(x1)
+        : "s"(slot), "s"(w0), "s"(w1)
+        : "memory");
+}
 __device__ __forceinline__ void pub64_sys(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1488,7 +1509,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // command's doorbell) are polled by wave 1 during phase A, so wave 0's spin is one VRAM round trip, not
     // a PCIe one (a host-service hop took twice the device program's: tools/host_latency.py)
     // (4-wave kernels only -- the drop-in's large-slot worlds: the 8-wave doorbell kernel has no registers for it)
-    const bool hpw = W == 4 && host && llm && ll_cmds && P.hll != nullptr;
+    const bool hpw = W == 4 && host && llm && ll_cmds && P.hll != nullptr && !(P.mode & MODE_NOHPW);
     uint32_t a_it = 0;  // phase-A rounds (every wave counts them alike)
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);  // my part's ctrl region (my bells)
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
@@ -2296,17 +2317,31 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if ((PMODE(MODE_STORM)) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
         } else if (hpw && w == 1) {
-            // the host poller: until wave 0 ends its spin, the next command's doorbell (lanes 0-15, 16 B each,
-            // to LDS at kLLCmdBell: the doorbell pass checks its tags) and the command tail / pickup head
-            // (lanes 16, 17 -> S.hp).  Every load of a round is waited for before the stop word is read, so
-            // the last round's values are in LDS before the barrier
+            // the host poller: until wave 0 ends its spin, the next command's doorbell (16 B to each of lanes 0-15,
+            // to LDS at kLLCmdBell: the doorbell pass checks its tags) and the command tail / pickup head (-> S.hp),
+            // all through scalar loads (spoll_cmd).  Every load of a round is waited for before the stop word is
+            // read, so the last round's values are in LDS before the barrier
             for (;;) {
                 const uint64_t hh = uni64(S.hin_head);
+                // scalar loads (spoll_cmd): the doorbell's first two chunks, the command tail and the pickup head in
+                // one round trip; a longer command's other chunks (its header whole and tagged for hh) with vector
+                // loads, once
+                const uint8_t* slot = reinterpret_cast<const uint8_t*>(
+                    uni64(reinterpret_cast<uint64_t>(P.hll + ((uint64_t)lr * P.hin_cap + (hh & hcap_m)) * kLLCmdSlotB)));
+                su16 sa;
+                uint64_t ht = 0, hk = 0;
+                spoll_cmd(slot, &hctl_dev[kHctlInjTail], &hctl_dev[kHctlPkHead], sa, ht, hk);
+                if (lane == 0) { S.hp[0] = ht; S.hp[1] = hk; }
                 u32x4 cv = {0u, 0u, 0u, 0u};
-                uint64_t hv = 0;
-                if (lane < 16) cv = ld_sys(rll, (uint32_t)(hh & hcap_m) * kLLCmdSlotB + 16u * (uint32_t)lane);
-                if (lane == 16 || lane == 17) hv = poll64_sys(&hctl_dev[lane == 16 ? kHctlInjTail : kHctlPkHead]);
-                if (lane == 16 || lane == 17) S.hp[lane - 16] = hv;
+#pragma unroll
+                for (int p = 0; p < 4; p++)
+                    if (lane == p) cv = u32x4{sa[4 * p], sa[4 * p + 1], sa[4 * p + 2], sa[4 * p + 3]};
+                {
+                    const uint32_t T0 = bell_tag(hh);
+                    const bool head_ok = sa[1] == T0 && sa[3] == T0 && sa[5] == T0 && sa[7] == T0;
+                    if (head_ok && ((kHdr + (sa[4] & 0xffffu) + 15u) >> 4) > 2u && lane >= 4 && lane < 16)
+                        cv = ld_sys(rll, (uint32_t)(hh & hcap_m) * kLLCmdSlotB + 16u * (uint32_t)lane);
+                }
                 // whole: every 8-byte half of its chunks (lanes 2q, 2q + 1 = chunk q) carries hh + 1.  Then its
                 // words go to LDS under the seqlock S.cseq (0 while they are rewritten), once per command
                 const uint32_t T = bell_tag(hh);

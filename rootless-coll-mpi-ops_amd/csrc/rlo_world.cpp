@@ -1877,6 +1877,9 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool corrupt = diag_env("RLO_BULK_CORRUPT") != nullptr;  // test: VERIFY must catch a zeroed granule
     if (corrupt) w->P.mode |= rlo::MODE_CORRUPT;
     else w->P.mode &= ~rlo::MODE_CORRUPT;
+    static const bool nohpw = diag_env("RLO_NO_HPOLLER") != nullptr;  // A/B: no wave-1 host poller
+    if (nohpw) w->P.mode |= rlo::MODE_NOHPW;
+    else w->P.mode &= ~rlo::MODE_NOHPW;
     static const bool hdiag = diag_env("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
     if (hdiag) w->P.mode |= rlo::MODE_HDIAG;
     else w->P.mode &= ~rlo::MODE_HDIAG;

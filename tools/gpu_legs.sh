@@ -3,7 +3,7 @@ set -o pipefail
 tag=${1:-legs}
 O=gpurun_out/${RLO_OUT:-r5}/$tag
 mkdir -p $O
-B=rootless-coll-mpi-ops_amd/lib/rlo_api_bench
+B=${BENCH:-rootless-coll-mpi-ops_amd/lib/rlo_api_bench}
 export RLO_NUMA_BIND=all
 for n in ${NS:-4 8}; do
   for leg in "lat 500 64" "iar 2000"; do
