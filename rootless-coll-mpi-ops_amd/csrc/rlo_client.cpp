@@ -21,7 +21,7 @@ struct rlo_client {
     const rlo::ShmHdr* h = nullptr;
     int rank = 0, lr = 0;
     uint64_t* hctl = nullptr;       // this rank's device-written counters
-    const rlo::LogRec* ev = nullptr;
+    const uint8_t* ev = nullptr;   // tagged pickup records of my rank (kPkRecBytes each)
     const uint8_t* evp = nullptr;
     rlo::ClientBox* box = nullptr;
     uint8_t* cmd = nullptr;
@@ -86,7 +86,7 @@ int rlo_client_attach(const char* name, int rank, rlo_client_t** out) {
     c->lr = rank - (int)h.rb;
     const uint64_t lr = (uint64_t)c->lr;
     c->hctl = (uint64_t*)(c->base + h.off_hctl) + lr * rlo::kHctlWords;
-    c->ev = (const rlo::LogRec*)(c->base + h.off_ev) + lr * h.pk_cap;
+    c->ev = c->base + h.off_ev + (uint64_t)lr * h.pk_cap * rlo::kPkRecBytes;
     c->evp = c->base + h.off_evp + lr * h.pk_cap * h.max_payload;
     c->box = (rlo::ClientBox*)(c->base + h.off_cli) + lr;
     c->cmd = c->base + h.off_cmd + lr * h.cmd_cap * h.stride;
@@ -137,14 +137,10 @@ int rlo_client_post(rlo_client_t* c, const rlo_cmd_t* cmd, const void* payload, 
 int rlo_client_poll(rlo_client_t* c, rlo_log_rec_t* ev, void* payload, uint32_t cap) {
     if (!c || !ev) return RLO_E_INVAL;
     const rlo::ShmHdr& h = *c->h;
-    const uint64_t tail = ld_acq(&c->hctl[rlo::kHctlPkTail]);
-    if (c->pk_head == tail) return 0;
-    const uint32_t i = (uint32_t)(c->pk_head & (h.pk_cap - 1));
-    std::memcpy(ev, &c->ev[i], sizeof *ev);
-    if (payload && cap && ev->payload_idx != 0xffffffffu) {
-        const uint32_t n = std::min(std::min(ev->len, cap), h.max_payload);
-        std::memcpy(payload, c->evp + (uint64_t)i * h.max_payload, n);
-    }
+    // the next event as soon as its tagged units landed (rlo_shm.hpp pk_take), not after the published tail
+    if (!rlo::pk_take(c->ev, c->evp, h.pk_cap, h.max_payload, __atomic_load_n(&h.pk_epoch, __ATOMIC_ACQUIRE), c->pk_head,
+                      &c->hctl[rlo::kHctlPkTail], reinterpret_cast<rlo::LogRec*>(ev), payload, cap))
+        return 0;
     c->pk_head++;
     __atomic_store_n(&c->box->mpk, c->pk_head, __ATOMIC_RELEASE);
     return 1;

@@ -171,6 +171,20 @@ struct RankStats {
     uint64_t unmarked_slots;               // staged ring slots whose header lacked the slot mark (an error)
 };
 
+// Host mode's pickup ring carries self-validating records (the LL idea): the record's four 8-byte units -- each
+// lands whole -- and the units of a payload the doorbell pass writes carry a tag derived from the event's sequence and
+// the launch epoch, so the host takes an event as soon as its units have landed instead of after the kernel drained
+// its stores and then published the pickup tail (two PCIe crossings later).  The record keeps LogRec's 32 bytes with
+// a 16-bit tag in the spare upper half of one word of each unit: kind (16 bits used), from + 1 (a rank or -1),
+// vote (-1 / 0 / 1), and the payload slot (< kPkMaxSlots; kPkNoPayload = none, | kPkTaggedPayload = the tagged
+// form: payload byte 4k + j in the low half of 8-byte unit k, pk_tag in the high half).  A plain payload (the full
+// path's, large messages) is read once the published tail covers the event.
+constexpr uint32_t kPkRecBytes = 32, kPkMaxSlots = 16384, kPkNoPayload = 0xffffu, kPkTaggedPayload = 0x8000u;
+__host__ __device__ inline uint32_t pk_tag(uint64_t seq, uint32_t epoch) { return (((uint32_t)seq << 1) | 1u) ^ epoch; }
+__host__ __device__ inline uint32_t pk_tag16(uint64_t seq, uint32_t epoch) { return pk_tag(seq, epoch) & 0xffffu; }
+// the pickup payload stride: room for a doorbell-pass payload (<= 7 chunks, 112 B) in the tagged form (224 B)
+__host__ __device__ inline uint32_t pk_payload_stride(uint32_t max_payload) { return max_payload >= 256u ? max_payload : 256u; }
+
 struct LogRec {            // 32 bytes
     uint32_t kind;         // LogKind | tag << 8
     int32_t origin;
@@ -258,6 +272,7 @@ struct Params {
     uint8_t* hin;                 // command slots [n_local][hin_cap] x fwd_stride (forward-slot layout),
                                   //   uncached VRAM written by the CPU through the BAR
     uint32_t hin_cap;
+    uint32_t pk_epoch;            // host mode: this launch's pickup-tag epoch (even; pk_tag), in hin_cap's padding
     uint64_t* hctl;               // [n_local][kHctlWords] counters the DEVICE writes (pinned host memory)
     uint64_t* hctl_dev;           // [n_local][kHctlWords] counters the HOST writes (uncached VRAM:
                                   //   the CPU stores through the BAR, the kernel polls locally)

@@ -521,13 +521,22 @@ __device__ __forceinline__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_
 // one event record: the parity log (MODE_LOG, linear) or the host pickup ring (MODE_HOST, the
 // slot after this iteration's earlier events; the selection phase guaranteed the room).  Returns the
 // record's payload index (~0u: no payload), or with want_rec the record index itself
-template <class SH>
+template <uint32_t PMK, class SH>  // PMK: the kernel's program mask (no host-mode code where it has none)
 __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint32_t kind, int origin, int from,
-                                            uint32_t id, uint32_t len, int vote, uint32_t aux, bool want_rec = false) {
+                                            uint32_t id, uint32_t len, int vote, uint32_t aux, bool want_rec = false,
+                                            bool tagged_payload = false) {
     if (!(P.mode & (MODE_LOG | MODE_HOST))) return ~0u;
     uint32_t i;
-    if (P.mode & MODE_HOST) {
-        i = (uint32_t)((S.pk_tail + atomicAdd(&S.ev_n, 1u)) & (uint64_t)(P.log_cap - 1u));
+    if ((PMK & MODE_HOST) && (P.mode & MODE_HOST)) {  // the tagged record (rlo_device.hpp kPkRecBytes): no drain
+        const uint64_t seq = S.pk_tail + atomicAdd(&S.ev_n, 1u);              // and no tail publish before the host
+        i = (uint32_t)(seq & (uint64_t)(P.log_cap - 1u));
+        const uint32_t t16 = pk_tag16(seq, P.pk_epoch) << 16;
+        const bool pl = P.log_payload && (kind == (LOG_DELIVER | (TAG_BCAST << 8)) || kind == LOG_JREQ || kind == LOG_JUDGED);
+        const uint32_t pidx = pl ? (i | (tagged_payload ? kPkTaggedPayload : 0u)) : kPkNoPayload;
+        u32x4* dst = reinterpret_cast<u32x4*>(&P.log[(size_t)lr * P.log_cap + i]);
+        st_sys16(dst, u32x4{kind | t16, (uint32_t)origin, ((uint32_t)(from + 1) & 0xffffu) | t16, id});
+        st_sys16(dst + 1, u32x4{len, ((uint32_t)vote & 0xffffu) | t16, aux, pidx | t16});
+        return want_rec ? i : (pl ? i : ~0u);
     } else {
         i = (uint32_t)atomicAdd(&S.log_count, 1ull);
         if (i >= P.log_cap) {
@@ -548,6 +557,18 @@ __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint
     st_sys16(dst, u32x4{r.kind, (uint32_t)r.origin, (uint32_t)r.from, r.id});
     st_sys16(dst + 1, u32x4{r.len, (uint32_t)r.vote, r.aux, r.payload_idx});
     return want_rec ? i : r.payload_idx;
+}
+
+// chunk q >= 1 of a doorbell-pass event's payload (v: the message's 16-B chunk q) into pickup slot `slot` of my
+// ring, in the tagged form (two 8-B units per 8 payload bytes); host mode only
+template <class SH>
+__device__ __forceinline__ void pk_payload_tagged(const SH& S, const Params& P, int lr, uint32_t slot, uint32_t q, u32x4 v) {
+    const uint64_t seq = S.pk_tail + ((slot - (uint32_t)S.pk_tail) & (P.log_cap - 1u));
+    const uint32_t tg = pk_tag(seq, P.pk_epoch);
+    const __amdgpu_buffer_rsrc_t rp =
+        mk_rsrc(P.log_payload + (size_t)lr * P.log_cap * P.log_stride, P.log_cap * P.log_stride);
+    st_ring(rp, slot * P.log_stride + 32u * (q - 1u), u32x4{v.x, tg, v.y, tg}, true);
+    st_ring(rp, slot * P.log_stride + 32u * (q - 1u) + 16u, u32x4{v.z, tg, v.w, tg}, true);
 }
 
 // a received proposal carries one of my own in-flight pids (the reference checks its one
@@ -1569,6 +1590,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const int forg = (int)(fw0 & 0xffffu);
         const uint32_t ftag = (fw0 >> 16) & 0xffu, flen = fw2 & 0xffffu, fnch = (kHdr + flen + 15u) >> 4;
         const uint32_t fpseq = fw2 >> 24;
+        // this event's payload in the pickup ring's tagged form (host-service kernels, when it fits the slot's
+        // stride at 2x); else plain, read by the host once the published tail covers it
+        const bool tagp = PM == kPmHost && 32u * (fnch - 1u) <= P.log_stride;
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) {
             tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
             tl_put(P, fid, TLC_ISSUE, lr, S.tl_clk[0]);
@@ -1600,12 +1624,17 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     PendState* pw = &PEND(forg, fpseq);
                     pw->pid = (int32_t)fid;
                     pw->valid = PS_JREQ;
-                    flog = log_put(S, P, lr, LOG_JREQ, forg, ffrom, fid, flen, -1, fpseq);
+                    flog = log_put<PM>(S, P, lr, LOG_JREQ, forg, ffrom, fid, flen, -1, fpseq, false, tagp);
                     atomicAdd(&S.hwait, 1u);
                 }
                 flog = rdl32(flog, 0);
-                if (q >= 1u && q < fnch && 16u * q <= P.log_stride)
-                    st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+                if (q >= 1u && q < fnch) {
+                    if (tagp) {
+                        pk_payload_tagged(S, P, lr, flog, q, v);
+                    } else if (16u * q <= P.log_stride) {  // (plain: the host reads it once the tail covers it)
+                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+                    }
+                }
                 return kAsked;
             }
         }
@@ -1647,8 +1676,8 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 tl_parent(P, fid, lr, ffrom);
                 atomicAdd(&S.bcast_delivered, 1ull);
                 if (PMODE(MODE_HIST)) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
-                flog = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
-                               (uint32_t)now_ticks() - ft0);
+                flog = log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
+                               (uint32_t)now_ticks() - ft0, false, tagp);
             }
             flog = rdl32(flog, 0);
             if (q < fnch)
@@ -1662,9 +1691,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 } else {
                     const uint32_t k = (uint32_t)fg >> 1;
                     atomicAdd(&S.judge_calls, 1ull);
-                    if (!host) log_put(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
+                    if (!host) log_put<PM>(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
                     else if (!hjudge)  // device judge in host mode: the verdict + PBuf for action() (phase F)
-                        flog = log_put(S, P, lr, LOG_JUDGED, forg, ffrom, fid, flen, fjudge, fpseq);
+                        flog = log_put<PM>(S, P, lr, LOG_JUDGED, forg, ffrom, fid, flen, fjudge, fpseq, false, tagp);
                     PendState* ps = &PEND(forg, fpseq);
                     if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                         ps->valid = PS_NONE;
@@ -1708,13 +1737,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
                 if (fvote != 0) {
                     atomicAdd(&S.actions, 1ull);
-                    log_put(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8);
+                    log_put<PM>(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8);
                 }
                 ps->valid = PS_NONE;
             }
             atomicAdd(&S.dec_delivered, 1ull);
             if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
-            log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
+            log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
         HP(6);
@@ -1725,8 +1754,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             }
         }
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
-        if (flog != ~0u && q >= 1u && q < fnch && 16u * q <= P.log_stride)
-            st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+        if (flog != ~0u && q >= 1u && q < fnch) {
+            if (tagp) {  // the pickup ring's tagged form (no drain and no tail publish stand before the host)
+                pk_payload_tagged(S, P, lr, flog, q, v);
+            } else if (16u * q <= P.log_stride) {  // (the parity log, a host-mode general kernel, a long payload: plain)
+                st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+            }
+        }
         if (ftag == TAG_BCAST && (PMODE(MODE_LAT)) && lane == 0) {  // the round's last pickup
             const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[fid], 1u, __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_SYSTEM)
@@ -1775,13 +1809,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if ((nw & 0xffffu) == S.own_needed) {
                     const int d = (nw >> 16) == 0 ? 1 : 0;
                     if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback (phase B1)
-                        log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
+                        log_put<PM>(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
                         atomicAdd(&S.hwait, 1u);
                         S.own_state[k] = 3;
                     } else {
                         if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
                             atomicAdd(&S.judge_calls, 1ull);
-                            if (!host) log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                            if (!host) log_put<PM>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
                         }
                         S.own_decision[k] = (uint32_t)d;
                         S.own_state[k] = 2;
@@ -2053,7 +2087,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if (lane == 0) {
                     atomicAdd(&S.own_decided, 1ull);
                     if (dec) atomicAdd(&S.own_approved, 1ull);
-                    log_put(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, k);
+                    log_put<PM>(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, k);
                     S.own_state[k] = 0;
                     S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
                 }
@@ -2441,12 +2475,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             if (!((ob >> (e & 31u)) & 1u) || pe.pad0 != (0x5A000000u | ((uint32_t)o << 8) | sl))
                                 bulk_fault(P, 11, (e << 8) | (pe.pad0 & 0xffu));
                             if (host) {
-                                log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, sl);
+                                log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, sl);
                             } else {
                                 tl_mark(P, pe.bid, kTlGlobal + P.n_local + (uint32_t)lr);
                                 atomicAdd(&S.bcast_delivered, 1ull);
                                 const uint32_t li =
-                                    log_put(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
+                                    log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_BULK << 8), o, pe.from, pe.bid, pe.len, -1, 0, true);
                                 queue_job(S.b, P, JCLS_A, JOB_VERIFY, o, lr, sl, pe.bid, pe.len,
                                          (pe.len + kVerifyTile - 1u) / kVerifyTile, pe.from, li, pe.q, 0u);
                                 if (PMODE(MODE_LAT)) {  // the last of N-1 pickups completes the round
@@ -2860,13 +2894,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             if ((nw & 0xffffu) == S.own_needed) {
                                 const int d = (nw >> 16) == 0 ? 1 : 0;
                                 if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback
-                                    log_put(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
+                                    log_put<PM>(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
                                     atomicAdd(&S.hwait, 1u);
                                     S.own_state[k] = 3;
                                 } else {
                                     if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
                                         atomicAdd(&S.judge_calls, 1ull);
-                                        if (!host) log_put(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                                        if (!host) log_put<PM>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
                                     }
                                     S.own_decision[k] = (uint32_t)d;
                                     S.own_state[k] = 2;
@@ -3040,7 +3074,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     PendState* ps = &PEND(lorg, lw2 >> 24);
                     ps->pid = (int32_t)lid;
                     ps->valid = PS_JREQ;
-                    slot = log_put(S, P, lr, LOG_JREQ, lorg, lfrom, lid, plen, -1, lw2 >> 24);
+                    slot = log_put<PM>(S, P, lr, LOG_JREQ, lorg, lfrom, lid, plen, -1, lw2 >> 24);
                     atomicAdd(&S.hwait, 1u);  // (lane 0 of several waves)
                 }
                 slot = rdl32(slot, 0);
@@ -3148,7 +3182,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             }
                         }
                         // aux: device ticks (10 ns) from origination to this pickup (latency diagnostics)
-                        logidx = log_put(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1,
+                        logidx = log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1,
                                          (uint32_t)now_ticks() - t0);
                     } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler (:668-726)
                         const int32_t pid = (int32_t)id;
@@ -3158,10 +3192,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                             set_error(S, P, ERR_PID_COLLISION, (uint32_t)pid);  // :690-692 (the reference never votes)
                         } else {
                             atomicAdd(&S.judge_calls, 1ull);
-                            if (!host) log_put(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
+                            if (!host) log_put<PM>(S, P, lr, LOG_JUDGE, origin, from, (uint32_t)pid, len, judge, 0);
                             else if (!hjudge) {  // device judge in host mode: the host learns the verdict and keeps
                                                  // the PBuf for action() (rootless_ops.c:842), no round trip
-                                const uint32_t slot = log_put(S, P, lr, LOG_JUDGED, origin, from, (uint32_t)pid, len, judge,
+                                const uint32_t slot = log_put<PM>(S, P, lr, LOG_JUDGED, origin, from, (uint32_t)pid, len, judge,
                                                               pseq);
                                 uint8_t* dst = P.log_payload + ((size_t)lr * P.log_cap + slot) * P.log_stride;
                                 for (uint32_t q = 0; 16u * q < len && 16u * q < P.log_stride; q++)
@@ -3187,13 +3221,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)id) {
                             if (vote != 0) {
                                 atomicAdd(&S.actions, 1ull);
-                                log_put(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, ps->pseq >> 8);
+                                log_put<PM>(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, ps->pseq >> 8);
                             }
                             ps->valid = PS_NONE;
                         }
                         atomicAdd(&S.dec_delivered, 1ull);
                         if (vote != 0) atomicAdd(&S.dec_approved, 1ull);
-                        log_put(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+                        log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
                     } else if constexpr (BULK) {
                       if (tag == TAG_BULK) {
                         // a bulk announcement: pending until my copy is complete; my movers push my
@@ -3244,7 +3278,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     const uint32_t k = pseq & (P.pend_slots - 1u);
                     atomicAdd(&S.own_decided, 1ull);
                     if (vote) atomicAdd(&S.own_approved, 1ull);
-                    log_put(S, P, lr, LOG_RESULT, me, -1, id, 0, vote, k);
+                    log_put<PM>(S, P, lr, LOG_RESULT, me, -1, id, 0, vote, k);
                     S.own_state[k] = 0;
                     S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
                 } else if (kind == K_LAT) {

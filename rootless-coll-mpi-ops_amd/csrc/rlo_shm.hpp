@@ -10,8 +10,8 @@
 // service exactly one process per GPU holds queues, whatever the rank count.
 //
 // Segment layout (page-aligned regions, sizes in the header so a client derives them):
-//   header page | hctl [nl][kHctlWords] (device-written counters) | ev [nl][pk_cap] LogRec |
-//   evp [nl][pk_cap][max_payload] | cli [nl] ClientBox | cmd [nl][cmd_cap][stride] |
+//   header page | hctl [nl][kHctlWords] (device-written counters) | ev [nl][pk_cap] tagged records (kPkRecBytes) |
+//   evp [nl][pk_cap][pickup payload stride] | cli [nl] ClientBox | cmd [nl][cmd_cap][stride] |
 //   stage [nl][stage_bytes]
 // The leader registers the whole segment with HIP (the kernel writes hctl / ev / evp; the proxy
 // DMAs bulk bytes through stage).  A client writes its commands into `cmd` and its counters into
@@ -19,15 +19,17 @@
 // ring and the pickup head into the VRAM counter the kernel polls, and runs bulk copies between
 // `stage` and the heap on the client's behalf.
 #pragma once
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 
 #include "rlo_device.hpp"
 
 namespace rlo {
 
 constexpr uint32_t kShmMagic = 0x534f4c52u;  // "RLOS"
-constexpr uint32_t kShmVersion = 4;
+constexpr uint32_t kShmVersion = 5;
 
 // a bulk origination: ACQUIRE (the next bulk sequence q, once its heap slot is free; q is not taken
 // yet), PUT the bytes window by window, COMMIT q (taken: the announcement carries it).  A failed PUT
@@ -39,11 +41,12 @@ struct ShmHdr {
     uint32_t nl, rb;                 // local ranks of the part, first world rank
     uint32_t n, bslots;              // world size, bulk heap slots per (receiver, origin)
     uint32_t cmd_cap, pk_cap;        // ring capacities per rank
-    uint32_t stride, max_payload;    // command slot stride, pickup payload stride
+    uint32_t stride, max_payload;    // command slot stride, pickup payload stride (pk_payload_stride)
     uint64_t bulk_max, stage_bytes;  // bulk message cap; staging window per rank
     uint64_t off_hctl, off_ev, off_evp, off_cli, off_cmd, off_stage, total;
     uint64_t off_llc;                // command doorbells [nl][cmd_cap] x kLLCmdSlot (ll_cmd_put)
-    uint32_t leader_failed, pad;     // the leader gave up (its kernel could not start / ended early)
+    uint32_t leader_failed;          // the leader gave up (its kernel could not start / ended early)
+    uint32_t pk_epoch;               // the running launch's pickup-tag epoch (rlo_device.hpp pk_tag)
 };
 
 // one per local rank; the two sides' words on separate 128-byte lines.  The kernel polls mtail and
@@ -91,12 +94,55 @@ inline void ll_cmd_put(uint8_t* slot, uint64_t seq, const uint32_t hdr[4], const
 
 inline uint64_t shm_page(uint64_t x) { return (x + 4095u) & ~uint64_t(4095); }
 
+// Take pickup event `seq` of one rank's ring (records `evs`, payloads `evp` at `stride`, `cap` slots) if it is whole:
+// each of its record's four units carries pk_tag16(seq, epoch) (rlo_device.hpp kPkRecBytes), so does every unit of a
+// tagged payload (pk_tag); a plain payload (the full path's) is read only once the published tail covers the event.
+// Returns 1 (ev / payload filled, the record decoded to rlo_log_rec_t's form), 0 (not yet).
+inline int pk_take(const uint8_t* evs, const uint8_t* evp, uint32_t cap, uint32_t stride, uint32_t epoch, uint64_t seq,
+                   const uint64_t* pk_tail, LogRec* ev, void* payload, uint32_t pcap) {
+    const uint32_t i = (uint32_t)(seq & (cap - 1));
+    const uint32_t t16 = pk_tag16(seq, epoch);
+    const uint64_t* r = reinterpret_cast<const uint64_t*>(evs + (uint64_t)i * kPkRecBytes);
+    uint64_t u[4];
+    for (int k = 0; k < 4; k++) u[k] = __atomic_load_n(r + k, __ATOMIC_ACQUIRE);
+    const uint32_t w0 = (uint32_t)u[0], w2 = (uint32_t)u[1], w5 = (uint32_t)(u[2] >> 32), w7 = (uint32_t)(u[3] >> 32);
+    if ((w0 >> 16) != t16 || (w2 >> 16) != t16 || (w5 >> 16) != t16 || (w7 >> 16) != t16) return 0;
+    ev->kind = w0 & 0xffffu;
+    ev->origin = (int32_t)(uint32_t)(u[0] >> 32);
+    ev->from = (int32_t)(w2 & 0xffffu) - 1;
+    ev->id = (uint32_t)(u[1] >> 32);
+    ev->len = (uint32_t)u[2];
+    ev->vote = (int32_t)(int16_t)(w5 & 0xffffu);
+    ev->aux = (uint32_t)u[3];
+    const uint32_t pidx = w7 & 0xffffu;
+    ev->payload_idx = pidx == kPkNoPayload ? 0xffffffffu : (pidx & ~kPkTaggedPayload);
+    if (pidx != kPkNoPayload) {
+        const uint32_t n = payload && pcap ? std::min(std::min(ev->len, pcap), stride) : 0u;
+        const uint8_t* src = evp + (uint64_t)i * stride;
+        if (pidx & kPkTaggedPayload) {
+            const uint32_t tg = pk_tag(seq, epoch);
+            const uint64_t* pu = reinterpret_cast<const uint64_t*>(src);
+            uint8_t* out = static_cast<uint8_t*>(payload);
+            for (uint32_t k = 0; 4 * k < n; k++) {
+                const uint64_t x = __atomic_load_n(pu + k, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(x >> 32) != tg) return 0;
+                const uint32_t d = (uint32_t)x;
+                std::memcpy(out + 4 * k, &d, std::min(4u, n - 4 * k));
+            }
+        } else {
+            if (__atomic_load_n(pk_tail, __ATOMIC_ACQUIRE) <= seq) return 0;
+            if (n) std::memcpy(payload, src, n);
+        }
+    }
+    return 1;
+}
+
 inline ShmLayout shm_layout(uint32_t nl, uint32_t cmd_cap, uint32_t pk_cap, uint32_t stride, uint32_t max_payload,
                             uint64_t stage_bytes) {
     ShmLayout L;
     uint64_t o = 4096;  // header page
     L.hctl = o; o = shm_page(o + (uint64_t)nl * kHctlWords * 8);
-    L.ev = o; o = shm_page(o + (uint64_t)nl * pk_cap * sizeof(LogRec));
+    L.ev = o; o = shm_page(o + (uint64_t)nl * pk_cap * kPkRecBytes);  // tagged records (rlo_device.hpp pk_tag16)
     L.evp = o; o = shm_page(o + (uint64_t)nl * pk_cap * max_payload);
     L.cli = o; o = shm_page(o + (uint64_t)nl * sizeof(ClientBox));
     L.cmd = o; o = shm_page(o + (uint64_t)nl * cmd_cap * stride);

@@ -396,7 +396,9 @@ struct rlo_world {
     volatile uint32_t* hdp = nullptr;  // the GPU's HDP_MEM_COHERENCY_FLUSH_CNTL register (see hdp_flush)
     bool cmd_host = false;          // the command ring + host counters in pinned host memory (default)
     rlo::LogRec* h_ev = nullptr;    // [nl][pk_cap]
-    uint8_t* h_evp = nullptr;       // [nl][pk_cap][max_payload]
+    uint8_t* h_evp = nullptr;       // [nl][pk_cap][pk_stride]
+    uint32_t pk_stride = 0;         // pickup payload stride (rlo_device.hpp pk_payload_stride)
+    uint32_t pk_epoch = 0;          // pickup-tag epoch of the latest host-mode launch (pk_tag)
     uint32_t cmd_cap = 0, pk_cap = 0;
     std::vector<uint64_t> cmd_tail, pk_head;  // host-side copies of the counters it owns
     // shared host service (rlo_host_share): h_ctl / h_ev / h_evp live in a POSIX shared-memory
@@ -1567,7 +1569,7 @@ static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec*
                      uint8_t** dev_cmd, uint64_t** dev_cli, uint8_t** dev_llc) {
     const uint32_t nl = (uint32_t)w->nl;
     const uint64_t stage = w->L.bulk_max ? w->share_stage : 0;
-    const rlo::ShmLayout L = rlo::shm_layout(nl, w->cmd_cap, w->pk_cap, w->L.stride, w->max_payload, stage);
+    const rlo::ShmLayout L = rlo::shm_layout(nl, w->cmd_cap, w->pk_cap, w->L.stride, w->pk_stride, stage);
     const char* name = w->shm_name.c_str();
     const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0) return RLO_E_INVAL;
@@ -1611,7 +1613,7 @@ static int shm_build(rlo_world* w, const uint64_t** dev_hctl, const rlo::LogRec*
     h->cmd_cap = w->cmd_cap;
     h->pk_cap = w->pk_cap;
     h->stride = w->L.stride;
-    h->max_payload = w->max_payload;
+    h->max_payload = w->pk_stride;  // (the pickup payload stride)
     h->bulk_max = w->L.bulk_max;
     h->stage_bytes = stage;
     h->off_hctl = L.hctl; h->off_ev = L.ev; h->off_evp = L.evp; h->off_cli = L.cli; h->off_cmd = L.cmd;
@@ -1625,7 +1627,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     if (!w->connected) return RLO_E_NOTCONNECTED;
     const uint32_t cc = cfg && cfg->cmd_slots ? pow2_ceil(cfg->cmd_slots) : 256u;
     const uint32_t pc = cfg && cfg->pickup_slots ? pow2_ceil(cfg->pickup_slots) : 1024u;
-    if (pc < 64 || cc < 4 || (uint64_t)cc * w->L.stride > 0xFFFF0000ull) return RLO_E_INVAL;
+    if (pc < 64 || pc > rlo::kPkMaxSlots || cc < 4 || (uint64_t)cc * w->L.stride > 0xFFFF0000ull) return RLO_E_INVAL;
     const uint32_t pool = cfg && cfg->pool ? cfg->pool : 1u;
     if (pool > w->L.pend_slots) return RLO_E_INVAL;
     HIPCHK(hipSetDevice(w->device));
@@ -1659,12 +1661,13 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     uint8_t* dev_cmd = nullptr;
     uint64_t* dev_cli = nullptr;
     uint8_t* dev_llc = nullptr;
+    w->pk_stride = rlo::pk_payload_stride(w->max_payload);
     if (!w->shm_name.empty()) {  // rlo_host_share: the host-side rings in the shared segment
         int rc = shm_build(w, &dev_hctl, &dev_ev, &dev_evp, &dev_cmd, &dev_cli, &dev_llc);
         if (rc) { host_free(w); return rc; }
     } else if (host_alloc((void**)&w->h_ctl, nl * rlo::kHctlWords * 8) ||
-               host_alloc((void**)&w->h_ev, nl * pc * sizeof(rlo::LogRec)) ||
-               host_alloc((void**)&w->h_evp, nl * pc * w->max_payload) ||
+               host_alloc((void**)&w->h_ev, nl * pc * rlo::kPkRecBytes) ||
+               host_alloc((void**)&w->h_evp, nl * pc * w->pk_stride) ||
                (w->cmd_host && host_alloc((void**)&w->h_llc, nl * cc * rlo::kLLCmdSlot))) {
         host_free(w);
         return RLO_E_HIP;
@@ -1679,7 +1682,7 @@ int rlo_program_host(rlo_world_t* w, const rlo_host_cfg_t* cfg) {
     P.log = dev_ev ? const_cast<rlo::LogRec*>(dev_ev) : w->h_ev;
     P.log_cap = pc;
     P.log_payload = dev_evp ? const_cast<uint8_t*>(dev_evp) : w->h_evp;
-    P.log_stride = w->max_payload;
+    P.log_stride = w->pk_stride;
     // shared service, commands in host memory: the kernel reads the clients' own rings and counters in
     // the segment (the proxy then only serves bulk requests)
     const bool direct = w->cmd_host && dev_cmd;
@@ -1737,14 +1740,11 @@ int rlo_host_poll(rlo_world_t* w, int rank, rlo_log_rec_t* ev, void* payload, ui
     const int lr = rank - w->rb;
     uint64_t* ctl = w->h_ctl + (size_t)lr * rlo::kHctlWords;
     const uint64_t head = w->pk_head[lr];
-    const uint64_t tail = __atomic_load_n(&ctl[rlo::kHctlPkTail], __ATOMIC_ACQUIRE);
-    if (head == tail) return 0;
-    const uint32_t i = (uint32_t)(head & (w->pk_cap - 1));
-    std::memcpy(ev, &w->h_ev[(size_t)lr * w->pk_cap + i], sizeof *ev);
-    if (payload && cap && ev->payload_idx != 0xffffffffu) {
-        const uint32_t n = std::min(std::min(ev->len, cap), w->max_payload);
-        std::memcpy(payload, w->h_evp + ((size_t)lr * w->pk_cap + i) * w->max_payload, n);
-    }
+    // the next event as soon as its tagged units landed (rlo_shm.hpp pk_take)
+    if (!rlo::pk_take(reinterpret_cast<const uint8_t*>(w->h_ev) + (size_t)lr * w->pk_cap * rlo::kPkRecBytes,
+                      w->h_evp + (size_t)lr * w->pk_cap * w->pk_stride, w->pk_cap, w->pk_stride, w->pk_epoch, head,
+                      &ctl[rlo::kHctlPkTail], reinterpret_cast<rlo::LogRec*>(ev), payload, cap))
+        return 0;
     w->pk_head[lr] = head + 1;
     if (w->shm && w->cmd_host) {  // direct mode: the kernel polls the pickup head in the rank's ClientBox
         __atomic_store_n(&((rlo::ClientBox*)(w->shm + w->SL.cli) + lr)->mpk, head + 1, __ATOMIC_RELEASE);
@@ -1847,6 +1847,13 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     if (!(flags & RLO_LAUNCH_NO_RESET)) {
         int rc = rlo_reset(w, stream);
         if (rc) return rc;
+        if (w->P.mode & rlo::MODE_HOST) {
+            // a new pickup-tag epoch: the rings restart at sequence 0, and a record or payload unit an earlier
+            // launch left in a slot carries another epoch's tag, so it never passes for this launch's event
+            w->pk_epoch += 0x9E3779B8u;  // (even: tags stay odd, never the 0 of fresh memory)
+            w->P.pk_epoch = w->pk_epoch;
+            if (w->shm) __atomic_store_n(&((rlo::ShmHdr*)w->shm)->pk_epoch, w->pk_epoch, __ATOMIC_RELEASE);
+        }
     }
     HIPCHK(hipEventRecord(w->ev0, s));
     // diagnostic A/B switch: publish producer counters after the next poll instead of at the end

@@ -157,6 +157,25 @@ def test_bulk_world_config_rejected_without_gpu_or_bad_slots():
         rlo.World(8, bulk_max=1 << 20, bulk_slots=3)
 
 
+EPOCH = 0x9E3779B8  # the segment's pickup-tag epoch (rlo_shm.hpp ShmHdr.pk_epoch)
+
+
+def _pk_tag(seq, epoch=EPOCH):
+    """rlo_device.hpp pk_tag"""
+    return (((seq << 1) | 1) & 0xFFFFFFFF) ^ epoch
+
+
+def _pk_record(seq, kind, origin, frm, ident, length, vote, aux, slot, tagged, epoch=EPOCH):
+    """a pickup record as the kernel writes it in host mode (rlo_device.hpp kPkRecBytes): LogRec's eight words with
+    the 16-bit tag in the upper half of kind, from + 1, vote and the payload slot"""
+    import struct
+
+    t = (_pk_tag(seq, epoch) & 0xFFFF) << 16
+    pidx = 0xFFFF if slot is None else (slot | (0x8000 if tagged else 0))
+    return struct.pack("<8I", kind | t, origin & 0xFFFFFFFF, ((frm + 1) & 0xFFFF) | t, ident, length, (vote & 0xFFFF) | t,
+                       aux, pidx | t)
+
+
 def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
     """a shared-host-service segment as rlo_program_host + rlo_host_share lay it out (rlo_shm.hpp),
     built here without a GPU so the client side can be exercised on CPU"""
@@ -178,8 +197,8 @@ def _fake_segment(name, nl=2, rb=4, n=8, cc=4, pc=64, stride=80, maxp=64):
     os.ftruncate(fd, total)
     m = mmap.mmap(fd, total)
     os.close(fd)
-    hdr = struct.pack("<10I10Q2I", 0, 4, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
-                      off["cli"], off["cmd"], off["stage"], total, off["llc"], 0, 0)
+    hdr = struct.pack("<10I10Q2I", 0, 5, nl, rb, n, 2, cc, pc, stride, maxp, 0, 0, off["hctl"], off["ev"], off["evp"],
+                      off["cli"], off["cmd"], off["stage"], total, off["llc"], 0, EPOCH)
     m[:len(hdr)] = hdr
     m[0:4] = struct.pack("<I", 0x534F4C52)  # magic last
     return m, off, rec
@@ -227,21 +246,33 @@ def test_shared_service_client_protocol_without_gpu():
         lib.rlo_client_cmd_count(c, ctypes.byref(consumed), ctypes.byref(posted))
         assert (consumed.value, posted.value) == (3, 4)
         assert lib.rlo_client_post(c, ctypes.byref(cmd), payload, len(payload)) == 0
-        # two pickup events written "by the kernel": records + payload, then the pickup tail
-        ev = L.LogRec()
+        # pickup events written "by the kernel" as tagged records (rlo_device.hpp kPkRecBytes): event 0 with a
+        # tagged payload is taken as soon as its units are there, no tail; event 1's plain payload (the full path's)
+        # only once the published tail covers it; a unit with a stale tag is not taken
         got = L.LogRec()
         buf = ctypes.create_string_buffer(64)
         assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0
-        for i in range(2):
-            ev.kind, ev.origin, ev.len, ev.payload_idx = 1, i, 4, i
-            at = off["ev"] + (1 * 64 + i) * rec
-            m[at:at + rec] = bytes(ev)
-            pat = off["evp"] + (1 * 64 + i) * 64
-            m[pat:pat + 4] = b"ev%02d" % i
+        at0, at1 = off["ev"] + (1 * 64 + 0) * rec, off["ev"] + (1 * 64 + 1) * rec
+        pat0, pat1 = off["evp"] + (1 * 64 + 0) * 64, off["evp"] + (1 * 64 + 1) * 64
+        m[at0:at0 + rec] = _pk_record(0, 1, 0, 6, 11, 6, -1, 77, 0, True)
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0  # its payload units are not there yet
+        m[pat0:pat0 + 16] = struct.pack("<2I2I", struct.unpack("<I", b"ev00")[0], _pk_tag(0),
+                                        struct.unpack("<I", b"ab\0\0")[0], _pk_tag(0))
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 1
+        assert (got.kind, got.origin, got.from_, got.id, got.len, got.vote, got.aux, got.payload_idx) == (1, 0, 6, 11, 6, -1, 77, 0)
+        assert buf.raw[:6] == b"ev00ab"
+        stale = bytearray(_pk_record(1, 1, 1, -1, 12, 4, -1, 0, 1, False))
+        stale[28:32] = struct.pack("<I", (struct.unpack_from("<I", stale, 28)[0] & 0xFFFF) | ((_pk_tag(1 + 64) & 0xFFFF) << 16))
+        m[at1:at1 + rec] = bytes(stale)
+        m[pat1:pat1 + 4] = b"ev01"
         m[hctl + 32 * 8:hctl + 33 * 8] = struct.pack("<Q", 2)
-        for i in range(2):
-            assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 1
-            assert (got.origin, buf.raw[:4]) == (i, b"ev%02d" % i)
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0  # one unit carries another sequence's tag
+        m[at1:at1 + rec] = _pk_record(1, 1, 1, -1, 12, 4, -1, 0, 1, False)
+        m[hctl + 32 * 8:hctl + 33 * 8] = struct.pack("<Q", 1)
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0  # plain payload: the tail does not cover it
+        m[hctl + 32 * 8:hctl + 33 * 8] = struct.pack("<Q", 2)
+        assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 1
+        assert (got.origin, got.from_, buf.raw[:4]) == (1, -1, b"ev01")
         assert lib.rlo_client_poll(c, ctypes.byref(got), buf, 64) == 0
         # mpk: the kernel polls it here, at its pickup-head word (kHctlPkHead = 48)
         assert struct.unpack_from("<Q", m, box + 48 * 8)[0] == 2
