@@ -271,6 +271,22 @@ __device__ __forceinline__ uint64_t poll64_sys(uint64_t* p) {
 // scalar loads (tools/probe/poll_interference.hip, profiles/r5_poll_interference.txt) -- and wave 0's doorbell polls
 // are such loads.  Loads only: nothing is ever written through the scalar cache.
 typedef uint32_t su16 __attribute__((ext_vector_type(16)));
+// host-service kernels: the doorbell's first 160 B (chunks 0-4: a command with <= 64 payload bytes -- the drop-in's
+// small bcasts and proposals -- in one round trip) and the two host words
+typedef uint32_t su8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void spoll_cmd5(const uint8_t* slot, const uint64_t* w0, const uint64_t* w1, su16& a, su16& b,
+                                           su8& c, uint64_t& x0, uint64_t& x1) {
+    asm volatile(
+        "s_load_dwordx16 %0, %5, 0x0 glc\n\t"
+        "s_load_dwordx16 %1, %5, 0x40 glc\n\t"
+        "s_load_dwordx8 %2, %5, 0x80 glc\n\t"
+        "s_load_dwordx2 %3, %6, 0x0 glc\n\t"
+        "s_load_dwordx2 %4, %7, 0x0 glc\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(a), "=&s"(b), "=&s"(c), "=&s"(x0), "=&s"(x1)
+        : "s"(slot), "s"(w0), "s"(w1)
+        : "memory");
+}
 // the first 64 B of a command doorbell (chunks 0-1: a verdict, a judge(NULL) verdict, the header of any command)
 // and two host words (command tail, pickup head), one round trip
 __device__ __forceinline__ void spoll_cmd(const uint8_t* slot, const uint64_t* w0, const uint64_t* w1, su16& a,
@@ -2364,16 +2380,31 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     uni64(reinterpret_cast<uint64_t>(P.hll + ((uint64_t)lr * P.hin_cap + (hh & hcap_m)) * kLLCmdSlotB)));
                 su16 sa;
                 uint64_t ht = 0, hk = 0;
-                spoll_cmd(slot, &hctl_dev[kHctlInjTail], &hctl_dev[kHctlPkHead], sa, ht, hk);
-                if (lane == 0) { S.hp[0] = ht; S.hp[1] = hk; }
                 u32x4 cv = {0u, 0u, 0u, 0u};
+                uint32_t scov = 2u;  // chunks the scalar loads covered
+                if constexpr (PM == kPmHost) {
+                    su16 sb;
+                    su8 sc;
+                    spoll_cmd5(slot, &hctl_dev[kHctlInjTail], &hctl_dev[kHctlPkHead], sa, sb, sc, ht, hk);
 #pragma unroll
-                for (int p = 0; p < 4; p++)
-                    if (lane == p) cv = u32x4{sa[4 * p], sa[4 * p + 1], sa[4 * p + 2], sa[4 * p + 3]};
+                    for (int p = 0; p < 4; p++) {
+                        if (lane == p) cv = u32x4{sa[4 * p], sa[4 * p + 1], sa[4 * p + 2], sa[4 * p + 3]};
+                        if (lane == 4 + p) cv = u32x4{sb[4 * p], sb[4 * p + 1], sb[4 * p + 2], sb[4 * p + 3]};
+                    }
+                    if (lane == 8) cv = u32x4{sc[0], sc[1], sc[2], sc[3]};
+                    if (lane == 9) cv = u32x4{sc[4], sc[5], sc[6], sc[7]};
+                    scov = 5u;
+                } else {
+                    spoll_cmd(slot, &hctl_dev[kHctlInjTail], &hctl_dev[kHctlPkHead], sa, ht, hk);
+#pragma unroll
+                    for (int p = 0; p < 4; p++)
+                        if (lane == p) cv = u32x4{sa[4 * p], sa[4 * p + 1], sa[4 * p + 2], sa[4 * p + 3]};
+                }
+                if (lane == 0) { S.hp[0] = ht; S.hp[1] = hk; }
                 {
                     const uint32_t T0 = bell_tag(hh);
                     const bool head_ok = sa[1] == T0 && sa[3] == T0 && sa[5] == T0 && sa[7] == T0;
-                    if (head_ok && ((kHdr + (sa[4] & 0xffffu) + 15u) >> 4) > 2u && lane >= 4 && lane < 16)
+                    if (head_ok && ((kHdr + (sa[4] & 0xffffu) + 15u) >> 4) > scov && lane >= (int)(2u * scov) && lane < 16)
                         cv = ld_sys(rll, (uint32_t)(hh & hcap_m) * kLLCmdSlotB + 16u * (uint32_t)lane);
                 }
                 // whole: every 8-byte half of its chunks (lanes 2q, 2q + 1 = chunk q) carries hh + 1.  Then its
