@@ -234,7 +234,7 @@ typedef struct {
  * (:698, :773, :842), which the host layer (librootless_ops.so) invokes on pickup events. */
 typedef struct {
     uint32_t cmd_slots;      /* command ring capacity per rank (power of two), 0 = 256       */
-    uint32_t pickup_slots;   /* pickup ring capacity per rank (power of two, >= 64), 0 = 1024 */
+    uint32_t pickup_slots;   /* pickup ring capacity per rank (power of two, 64 .. 16384), 0 = 1024 */
     uint32_t idle_timeout_s; /* kernel stops (RLO_DERR_TIMEOUT) after this long without any
                                 progress; 0 = never                                          */
     uint32_t flags;
