@@ -1018,7 +1018,11 @@ RLO_engine_t* engine_new(MPI_Comm mpi_comm, size_t msg_size_max, void* approv_cb
         MPI_Allreduce(&mine, &depth, 1, MPI_INT, MPI_MAX, e->comm);
         e->pool_depth = depth;
     }
-    e->bulk_max = 64ull << 20;  // extension: bcasts beyond the data area up to RLO_BULK_MAX bytes (0: off)
+    // extension, opt-in: bcasts beyond the data area up to RLO_BULK_MAX bytes.  Off by default, as the reference
+    // caps a bcast at its data area (:295): a world without bulk messages runs the host-service kernel without the
+    // bulk code and its mover workgroups -- the drop-in's 8-rank p50 20.0 vs 21.9 us with it
+    // (profiles/r5_dropin_legs_bulk_ab.txt)
+    e->bulk_max = 0;
     if (const char* bm = std::getenv("RLO_BULK_MAX")) e->bulk_max = std::strtoull(bm, nullptr, 10);
     int rc = RLO_OK;
     char shm_name[96] = {0};

@@ -50,6 +50,11 @@ def run(harness, n, *args, timeout=80):
     return capture.run(harness, n, *args, timeout=timeout)
 
 
+def _bulk_env(base=None):
+    """bulk messages are an opt-in extension of the drop-in (RLO_BULK_MAX)"""
+    return dict(base if base is not None else os.environ, RLO_BULK_MAX=str(64 << 20))
+
+
 @pytest.mark.parametrize("n", [4, 5, 8, 9, 12, 13])
 def test_parents_match_reference(harness, n):
     fx = load("parents.json")
@@ -78,7 +83,7 @@ def test_bulk_bcast_through_dropin(harness, n, k):
     import pyoracle as orc
 
     seed, lo, hi = 21, 64, 1 << 20
-    recs = run(harness, n, "bulkstream", seed, k, lo, hi, timeout=120)
+    recs = capture.run(harness, n, "bulkstream", seed, k, lo, hi, timeout=120, env=_bulk_env())
     par = orc.storm(n, seed, k, lo, want_parent=True, len_max=hi, order=1)["parent"]
     want = []
     for b in range(k):
@@ -268,7 +273,7 @@ def test_multi_part_engine_bulk(harness):
     import pyoracle as orc
 
     n, k, seed, lo, hi = 8, 24, 21, 64, 1 << 20
-    recs = capture.run(harness, n, "bulkstream", seed, k, lo, hi, timeout=120, env=_parts_env(2))
+    recs = capture.run(harness, n, "bulkstream", seed, k, lo, hi, timeout=120, env=_bulk_env(_parts_env(2)))
     par = orc.storm(n, seed, k, lo, want_parent=True, len_max=hi, order=1)["parent"]
     want = []
     for b in range(k):
