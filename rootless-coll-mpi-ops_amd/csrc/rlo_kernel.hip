@@ -351,13 +351,13 @@ __device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t magic) { retu
 // (the program-specialised doorbell kernels only: the general ones have no registers to spare)
 #define HP(k)                                                                                  \
     do {                                                                                       \
-        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))                           \
+        if constexpr (PM == kPmLat || PM == kPmIar)                           \
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[(k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 // ... and S.dbg[k] counts why a doorbell pass handed over to the full iteration (hop_prof.py prints them)
 #define HPC(k)                                                                                 \
     do {                                                                                       \
-        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))                           \
+        if constexpr (PM == kPmLat || PM == kPmIar)                           \
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.dbg[(k)]++;                            \
     } while (0)
 #else
@@ -1866,7 +1866,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         need_full = false;
         HP(0);
 #ifdef RLO_DIAG
-        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))
+        if constexpr (PM == kPmLat || PM == kPmIar)
             if ((P.mode & MODE_HOPPROF) && lane == 0) S.hpt[3] = 0;
 #endif
         if (__ballot(errf != 0)) return 0u;
@@ -2189,7 +2189,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         }
         HP(8);
 #ifdef RLO_DIAG
-        if constexpr (PM == kPmLat || PM == kPmIar || (PM == kPmHost && W == 4))
+        if constexpr (PM == kPmLat || PM == kPmIar)
             if ((P.mode & MODE_HOPPROF) && lane == 0 && done == 1u && S.hpt[3] != 0) {  // one ring message, nothing else
                 for (int k = 0; k < 8; k++) S.prof[k] += S.hpt[k + 1] - S.hpt[k];
                 S.dbg[0]++;

@@ -1,7 +1,9 @@
 """Where a doorbell hop's instructions go (diagnostics build, RLO_HOP_PROF): shader clocks (s_memtime) at points
 of every doorbell pass that took exactly one ring message, summed per segment over the latency program's hops.
     python tools/hop_prof.py [n ...] [--host]   (RLO_DIAG_LIB=1 and RLO_HOP_PROF=1 are set here; --host: the drop-in's
-    host service, one bcast at a time)"""
+    host service, one bcast at a time).  The host kernels carried the stamps during round 5's analysis (DESIGN.md
+    section 4.1.1); with the scalar doorbell poll they no longer fit the host kernel's registers, so --host now reports
+    no profiled hops unless the kPmHost condition is put back into the kernel's HP macro (diagnostics build)."""
 import os
 import sys
 
