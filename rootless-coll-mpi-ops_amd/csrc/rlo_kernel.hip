@@ -1895,7 +1895,10 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
         const bool ldr = lane < n_in2 && ip > 0ull && !rhit;  // a counter-visible head without its bell: load it
         const uint64_t ldm = __ballot(ldr);
-        if (__ballot(ip > 2ull || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { HPC(1); need_full = true; return 0u; }
+        // a backlog is the full iteration's; the host service (proposals held for verdicts queue behind a ring's
+        // head) lets deeper rings stay on the doorbell pass
+        constexpr uint64_t kBacklog = PM == kPmHost ? 4ull : 2ull;
+        if (__ballot(ip > kBacklog || vp > (uint64_t)kLLVotes) || __popcll(ldm) > 8) { HPC(1); need_full = true; return 0u; }
         HP(1);
         uint32_t ncmd = 0;  // host commands to take (FIFO order, the first kLLCmds)
         bool cbell = false;  // ... the one in the command doorbell (already loaded, at kLLCmd)
