@@ -48,6 +48,9 @@ def percentile(a, p):
 
 
 _DUMP = {"dir": "", "recs": {}}
+# storm legs (the headline and the payload-size legs) whose per-rank results the cpu_baseline leg checks against the
+# oracle: each a record dict carrying "verified" and a "_check" {n, seed, k, len, count, sum}
+_STORM_CHECKS = []
 _DUMP_FIELDS = ("bcast_delivered", "bcast_sum", "originated", "own_decided", "own_approved", "actions", "judge_calls",
                 "dec_delivered", "error")
 
@@ -80,6 +83,17 @@ def cpu_baseline(n, length, seed, target_s, bulk=None):
     against orc.msg_checksum of the oracle's payload (not launch-to-launch equality alone)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle as orc
+    import numpy as np
+
+    # every storm leg's per-rank delivery counts and checksums against the oracle's analytic expectation of the same
+    # (n, seed, k, length) storm (VERDICT r5 weak 1: the headline's `verified` was step-to-step equality only)
+    for rec in _STORM_CHECKS:
+        chk = rec.pop("_check")
+        want = orc.storm_expected(chk["n"], chk["seed"], chk["k"], chk["len"])
+        rec["verified_oracle"] = bool(np.array_equal(np.asarray(chk["count"], dtype=np.int64), want["count"]) and
+                                      np.array_equal(np.asarray(chk["sum"], dtype=np.uint64), want["sum"]))
+        rec["verified"] = bool(rec["verified"] and rec["verified_oracle"])
+    _STORM_CHECKS.clear()
 
     if bulk:
         for rec in bulk.get("sizes", []):
@@ -353,10 +367,14 @@ def size_legs(rlo, R, device, stream, sizes=(256, 1024, 4096), k=1 << 16, steps=
             ok &= all(np.array_equal(sums[0], x) for x in sums[1:])
             kernel_ms = float(np.mean(kms))
             gbs = k * 2.0 * (R - 1) * (s + 16) / (kernel_ms * 1e-3) / 1e9
-            out.append({"payload_bytes": s, "bcasts": k, "bcast_per_s": round(k / dt, 1),
-                        "deliveries_per_s": round(k * (R - 1) / dt, 1), "kernel_ms": round(kernel_ms, 3),
-                        "alg_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                        "payloads": "pulled" if w.info["pull"] else "pushed", "verified": ok})
+            rec = {"payload_bytes": s, "bcasts": k, "bcast_per_s": round(k / dt, 1),
+                   "deliveries_per_s": round(k * (R - 1) / dt, 1), "kernel_ms": round(kernel_ms, 3),
+                   "alg_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                   "payloads": "pulled" if w.info["pull"] else "pushed", "verified": ok,
+                   "_check": {"n": R, "seed": 0x5EED, "k": k, "len": s, "count": st["bcast_delivered"].tolist(),
+                              "sum": st["bcast_sum"].tolist()}}
+            _STORM_CHECKS.append(rec)
+            out.append(rec)
     return out
 
 
@@ -419,6 +437,19 @@ def _close(w, dist):
         finally:
             dist.barrier()
     w.close()
+    if dist is not None:
+        import rlo
+        import torch
+
+        # the world-wide close (rlo_hip.h rlo_pool_trim): regions a peer imported leave the pool only once every part
+        # dropped its idle imports -- needed only when some part has retired regions (beyond RLO_POOL_CAP_BYTES)
+        t = torch.tensor([float(rlo.pool_stats()["retired"])], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if t.item() > 0:
+            rlo.pool_trim(rlo.abi.RLO_TRIM_IMPORTS | rlo.abi.RLO_TRIM_FREE)
+            dist.barrier()
+            rlo.pool_trim(rlo.abi.RLO_TRIM_RETIRED)
+            dist.barrier()
 
 
 def _world(rlo, dist, R, world, rank, local, **kw):
@@ -937,6 +968,12 @@ def main():
                      "alg_bytes_per_launch": alg_bytes},
         "verified": ok,
     }
+    if world == 1 or mode == "replicas":
+        # the timed storm's per-rank delivery counts and checksums, checked against the oracle in the cpu_baseline leg
+        line["verified_oracle"] = None
+        line["_check"] = {"n": R, "seed": seed, "k": k, "len": length, "count": st["bcast_delivered"].tolist(),
+                          "sum": st["bcast_sum"].tolist()}
+        _STORM_CHECKS.insert(0, line)
     line.update(extras)
     if rank == 0:
         note("storm timed: %.3f ms/step" % (elapsed / args.steps * 1e3))
@@ -974,8 +1011,12 @@ def main():
         line["cpu_baseline"] = cpu_baseline(R, length, seed, args.cpu_seconds, bulk=line.get("bulk"))
         if line.get("bulk", {}).get("sizes"):
             line["verified"] = bool(line["verified"] and all(s["verified"] for s in line["bulk"]["sizes"]))
-    for s in (line.get("bulk") or {}).get("sizes", []):
-        s.pop("_check", None)  # --no-cpu-baseline: unchecked against the oracle (launch-to-launch equality only)
+        if line.get("payload_sizes"):
+            line["verified"] = bool(line["verified"] and all(s["verified"] for s in line["payload_sizes"]))
+    # --no-cpu-baseline: unchecked against the oracle (launch-to-launch equality only)
+    for s in (line.get("bulk") or {}).get("sizes", []) + (line.get("payload_sizes") or []) + [line]:
+        s.pop("_check", None)
+    _STORM_CHECKS.clear()
     dump_write(rank)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -151,6 +151,23 @@ int rlo_world_destroy(rlo_world_t* w);
 int rlo_part_close_imports(rlo_world_t* w);
 int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* out);
 
+/* ---- the per-process region pool.  A destroyed world's device regions stay in a per-process pool for
+ * the next world, and imports of peers' regions stay open (idle) for the peer's next world: exported memory freed and
+ * re-exported world after world gave importers mappings of OTHER memory on MI355X / ROCm 7.2.  Free bytes beyond
+ * RLO_POOL_CAP_BYTES (environment, default 8 GiB) leave the pool: a region no other process ever mapped is freed at
+ * once, an exported one is RETIRED and freed only by RLO_TRIM_RETIRED.  To give every byte back, all processes that
+ * shared worlds run the world-wide close: each rlo_pool_trim(RLO_TRIM_IMPORTS | RLO_TRIM_FREE | RLO_TRIM_EXPORTED)
+ * once none of its worlds is alive, a barrier, then each rlo_pool_trim(RLO_TRIM_RETIRED).  No replacement in the
+ * reference (MPI owns its buffers). */
+#define RLO_TRIM_IMPORTS 1u  /* close this process's idle imports of peers' regions                            */
+#define RLO_TRIM_FREE 2u     /* hipFree the free regions no other process ever mapped                          */
+#define RLO_TRIM_RETIRED 4u  /* hipFree the retired exported regions: only after EVERY peer process trimmed its
+                                imports (a world-wide close with a barrier)                                     */
+#define RLO_TRIM_EXPORTED 8u /* retire every free exported region (RLO_TRIM_RETIRED then frees it)               */
+int rlo_pool_trim(uint32_t what, uint64_t* freed_bytes);
+/* out[6]: bytes held by live worlds, free never-exported, free exported, retired; imports in use, idle imports */
+int rlo_pool_stats(uint64_t* out, uint32_t cap);
+
 /* ------------------------------------------------------------------ programs */
 #define RLO_FLAG_LOG 1u  /* record every delivery / judge / action / result (+ payload bytes) */
 #define RLO_FLAG_HIST 2u /* per-delivery latency histogram                                  */

@@ -132,6 +132,13 @@ int RLO_get_world_size(void);
 int RLO_user_msg_source(const RLO_user_msg* msg);
 /* HIP device ordinal this engine's rank lives on */
 int RLO_engine_device(RLO_engine_t* eng);
+/* Device memory held between engines.  An engine's device regions go back to a per-process pool
+ * at cleanup and are reused by the next engine; the last engine's cleanup in a process frees every region no other
+ * process ever mapped and closes the idle imports of peers' regions.  Regions a multi-GPU engine exported to other
+ * processes stay pooled (up to RLO_POOL_CAP_BYTES free bytes, default 8 GiB, then retired but kept): freeing memory a
+ * peer may still map is unsafe.  RLO_device_memory_release(comm) gives those back too: collective over
+ * every process that shared engines with this one, called when none of them has an engine; 0 or -1 */
+int RLO_device_memory_release(MPI_Comm comm);
 
 /* Device judges: RLO_progress_engine_new_dj creates an engine whose proposals are judged on the
  * GPU by a registered predicate instead of approv_cb_func -- no host round trip per tree hop, and

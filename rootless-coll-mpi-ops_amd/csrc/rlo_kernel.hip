@@ -3906,11 +3906,29 @@ static hipError_t launch_v(const rlo::Params* p, int blocks, size_t dyn_lds, hip
     return hipGetLastError();
 }
 
-template <int W, bool B, bool L, bool H = false>
-static hipError_t occ_v(int* blocks, size_t dyn_lds) {
-    hipError_t e = grant_dyn_lds<W, B, L, H>(dyn_lds);
+template <int W, bool B, bool L, bool H = false, uint32_t PM = rlo::kPmAll>
+static hipError_t occ_one(int* blocks, size_t dyn_lds) {
+    hipError_t e = grant_dyn_lds<W, B, L, H, PM>(dyn_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B, L, H>, 64 * W, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_progress_kernel<W, B, L, H, PM>, 64 * W, dyn_lds);
+}
+
+// the occupancy of <W, B, L, H> = the least over its general instantiation and every program-specialised one that
+// rlo_launch_progress launches for it (PMs...): co-residency is decided from this answer, so a specialised kernel
+// that fell below its general twin would leave workgroups of a persistent launch unscheduled
+template <int W, bool B, bool L, bool H, uint32_t... PMs>
+static hipError_t occ_v(int* blocks, size_t dyn_lds) {
+    hipError_t e = occ_one<W, B, L, H>(blocks, dyn_lds);
+    if (e != hipSuccess) return e;
+    const hipError_t es[] = {hipSuccess, [&]() -> hipError_t {
+        int b = 0;
+        const hipError_t r = occ_one<W, B, L, H, PMs>(&b, dyn_lds);
+        if (r == hipSuccess && b < *blocks) *blocks = b;
+        return r;
+    }()...};
+    for (hipError_t x : es)
+        if (x != hipSuccess) return x;
+    return hipSuccess;
 }
 
 // programs that hold proposals in a world with HBM pending tables run the PH instantiations (no bulk
@@ -3922,8 +3940,8 @@ static bool wants_ph(const rlo::Params* p) {
 // The kernels of the device programs the bench times are specialised by program (PM): 8 waves -- the storm
 // (no doorbells), the latency program and the iar program (doorbells; the iar one with the LDS or the HBM
 // pending table); bulk worlds -- the latency program (C3) and the storm (C5); and the host service the drop-in
-// runs (doorbells; every variant, LDS or HBM tables).  Their register use never exceeds the general instantiation's, whose occupancy the host
-// checks (rlo_occupancy*); the Makefile guard holds every 8-wave instantiation to 2 waves per SIMD.
+// runs (doorbells; every variant, LDS or HBM tables).  The host's occupancy answer (rlo_occupancy*) is the least over the
+// general instantiation and these; the Makefile guard holds every 8-wave instantiation to 2 waves per SIMD.
 extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream, int variant) {
     const bool ll = (p->mode & rlo::MODE_LL) != 0;
     const uint32_t prog = p->mode & (rlo::MODE_STORM | rlo::MODE_LAT | rlo::MODE_IAR | rlo::MODE_HOST);
@@ -3964,17 +3982,17 @@ extern "C" size_t rlo_kernel_static_lds(int variant) {
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant) {
     if (variant == (8 | 16)) return occ_v<8, false, false, true>(blocks, dyn_lds);
     if (variant == (4 | 16)) return occ_v<4, false, false, true>(blocks, dyn_lds);
-    if (variant == 8) return occ_v<8, false, false>(blocks, dyn_lds);
-    if (variant == 5) return occ_v<4, true, false>(blocks, dyn_lds);
-    return occ_v<4, false, false>(blocks, dyn_lds);
+    if (variant == 8) return occ_v<8, false, false, false, rlo::kPmStorm>(blocks, dyn_lds);
+    if (variant == 5) return occ_v<4, true, false, false, rlo::kPmStorm>(blocks, dyn_lds);
+    return occ_v<4, false, false, false>(blocks, dyn_lds);
 }
 
 // the doorbell instantiation of a variant: the 4-wave ones may take more than 256 registers (one wave
 // per SIMD: worlds whose ranks have a CU each), so a world gets doorbells only where this answer covers it
 extern "C" hipError_t rlo_occupancy_ll(int* blocks, size_t dyn_lds, int variant) {
-    if (variant == (8 | 16)) return occ_v<8, false, true, true>(blocks, dyn_lds);
-    if (variant == (4 | 16)) return occ_v<4, false, true, true>(blocks, dyn_lds);
-    if (variant == 8) return occ_v<8, false, true>(blocks, dyn_lds);
-    if (variant == 5) return occ_v<4, true, true>(blocks, dyn_lds);
-    return occ_v<4, false, true>(blocks, dyn_lds);
+    if (variant == (8 | 16)) return occ_v<8, false, true, true, rlo::kPmIar, rlo::kPmHost>(blocks, dyn_lds);
+    if (variant == (4 | 16)) return occ_v<4, false, true, true, rlo::kPmHost>(blocks, dyn_lds);
+    if (variant == 8) return occ_v<8, false, true, false, rlo::kPmLat, rlo::kPmIar, rlo::kPmHost>(blocks, dyn_lds);
+    if (variant == 5) return occ_v<4, true, true, false, rlo::kPmLat, rlo::kPmHost>(blocks, dyn_lds);
+    return occ_v<4, false, true, false, rlo::kPmHost>(blocks, dyn_lds);
 }

@@ -399,6 +399,7 @@ struct rlo_world {
     uint8_t* h_evp = nullptr;       // [nl][pk_cap][pk_stride]
     uint32_t pk_stride = 0;         // pickup payload stride (rlo_device.hpp pk_payload_stride)
     uint32_t pk_epoch = 0;          // pickup-tag epoch of the latest host-mode launch (pk_tag)
+    bool pk_dirty = false;          // a host-mode launch may have written pickup records / payloads since the last reset
     uint32_t cmd_cap = 0, pk_cap = 0;
     std::vector<uint64_t> cmd_tail, pk_head;  // host-side copies of the counters it owns
     // shared host service (rlo_host_share): h_ctl / h_ev / h_evp live in a POSIX shared-memory
@@ -451,11 +452,24 @@ struct PoolEnt {
     uint64_t bytes;
     int device;
     bool uncached;
+    bool exported;  // a handle of it went out (rlo_part_export): a peer process may hold an import of it
 };
 std::mutex g_pool_mu;
 std::vector<PoolEnt> g_pool;       // free regions
 std::vector<PoolEnt> g_pool_live;  // regions some world of this process holds
-constexpr uint64_t kPoolCapBytes = 96ull << 30;  // free regions kept per process (beyond: the oldest go back to HIP)
+std::vector<PoolEnt> g_retired;    // free exported regions beyond the cap: freed only by rlo_pool_trim(RLO_TRIM_RETIRED)
+// free bytes kept per process (RLO_POOL_CAP_BYTES, default 8 GiB).  Beyond it a region nobody else ever mapped goes
+// back to HIP at once; an EXPORTED one is only retired -- never hipFree'd while a peer process may still hold an import
+// of it (freeing exported memory a peer still imported is the failure the pool exists to prevent), until
+// the application runs the world-wide close (every process rlo_pool_trim(RLO_TRIM_IMPORTS), a barrier, then
+// rlo_pool_trim(RLO_TRIM_RETIRED)); bench.py's sharded legs and the drop-in's RLO_device_memory_release do
+uint64_t pool_cap() {
+    static const uint64_t cap = [] {
+        const char* e = std::getenv("RLO_POOL_CAP_BYTES");
+        return e && *e ? std::strtoull(e, nullptr, 10) : (8ull << 30);
+    }();
+    return cap;
+}
 // sizes rounded up to a class (>= 2 MiB: its own allocation, not a sub-allocation another region shares; then eighths
 // of the next power of two), so that worlds of similar sizes share regions
 uint64_t pool_class(uint64_t b) {
@@ -469,6 +483,7 @@ uint64_t pool_class(uint64_t b) {
 int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
     const bool unc = (w->flags & RLO_PART_UNCACHED) != 0;
     const uint64_t cls = pool_class(bytes ? bytes : 256);
+    bool reused = false;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         for (size_t i = 0; i < g_pool.size(); i++)
@@ -476,17 +491,40 @@ int alloc_region(rlo_world* w, void** p, uint64_t bytes) {
                 *p = g_pool[i].p;
                 g_pool_live.push_back(g_pool[i]);
                 g_pool.erase(g_pool.begin() + (long)i);
-                return RLO_OK;
+                reused = true;
+                break;
             }
+        for (size_t i = 0; !reused && i < g_retired.size(); i++)  // a retired region is still good memory to reuse
+            if (g_retired[i].device == w->device && g_retired[i].uncached == unc && g_retired[i].bytes == cls) {
+                *p = g_retired[i].p;
+                g_pool_live.push_back(g_retired[i]);
+                g_retired.erase(g_retired.begin() + (long)i);
+                reused = true;
+            }
+    }
+    if (reused) {
+        // a region another world used: zeroed, as hipMalloc'd memory was, so no byte of that world is ever read
+        // as this one's (the heap and vote regions rely on write-before-read alone otherwise)
+        hipError_t e = hipMemset(*p, 0, cls);
+        if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
+        return RLO_OK;
     }
     hipError_t e = unc ? hipExtMallocWithFlags(p, cls, hipDeviceMallocUncached) : hipMalloc(p, cls);
     if (e != hipSuccess) { g_last_hip = (int)e; *p = nullptr; return RLO_E_HIP; }
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool_live.push_back(PoolEnt{*p, cls, w->device, unc});
+    g_pool_live.push_back(PoolEnt{*p, cls, w->device, unc, false});
     return RLO_OK;
 }
 
-// a destroyed world's region back to the pool (the oldest free ones go back to HIP beyond kPoolCapBytes)
+// a handle of region p is about to leave this process
+void mark_exported(void* p) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (PoolEnt& q : g_pool_live)
+        if (q.p == p) q.exported = true;
+}
+
+// a destroyed world's region back to the pool; beyond the cap the oldest free ones leave it (never-exported: freed;
+// exported: retired, see pool_cap)
 void release_region(void* p) {
     if (!p) return;
     std::vector<void*> drop;
@@ -500,9 +538,10 @@ void release_region(void* p) {
             }
         uint64_t tot = 0;
         for (const PoolEnt& q : g_pool) tot += q.bytes;
-        while (tot > kPoolCapBytes && !g_pool.empty()) {
+        while (tot > pool_cap() && !g_pool.empty()) {
             tot -= g_pool.front().bytes;
-            drop.push_back(g_pool.front().p);
+            if (g_pool.front().exported) g_retired.push_back(g_pool.front());
+            else drop.push_back(g_pool.front().p);
             g_pool.erase(g_pool.begin());
         }
     }
@@ -956,16 +995,22 @@ int rlo_part_export(rlo_world_t* w, void* blob, uint32_t cap) {
     b.vote_bytes = w->L.vote_bytes[w->part];
     b.ctrl_bytes = w->L.ctrl_words[w->part] * 8;
     HIPCHK(hipDeviceGetPCIBusId(b.bus, sizeof b.bus, w->device));
-    HIPCHK(hipIpcGetMemHandle(&b.hf, w->fwd));
-    HIPCHK(hipIpcGetMemHandle(&b.hv, w->vote));
-    HIPCHK(hipIpcGetMemHandle(&b.hc, w->ctrl));
     if (w->L.bulk_max) {
         b.heap_ptr = (uint64_t)(uintptr_t)w->heap;
         b.bflag_ptr = (uint64_t)(uintptr_t)w->bflag;
         b.heap_bytes = w->L.heap_bytes[w->part];
         b.bflag_bytes = w->L.bflag_bytes[w->part];
-        HIPCHK(hipIpcGetMemHandle(&b.hh, w->heap));
-        HIPCHK(hipIpcGetMemHandle(&b.hb, w->bflag));
+    }
+    if (w->L.nparts > 1) {  // handles only where another process may map the regions (a one-part world needs none)
+        for (void* r : {(void*)w->fwd, (void*)w->vote, (void*)w->ctrl, (void*)w->heap, (void*)w->bflag})
+            if (r) mark_exported(r);
+        HIPCHK(hipIpcGetMemHandle(&b.hf, w->fwd));
+        HIPCHK(hipIpcGetMemHandle(&b.hv, w->vote));
+        HIPCHK(hipIpcGetMemHandle(&b.hc, w->ctrl));
+        if (w->L.bulk_max) {
+            HIPCHK(hipIpcGetMemHandle(&b.hh, w->heap));
+            HIPCHK(hipIpcGetMemHandle(&b.hb, w->bflag));
+        }
     }
     std::memset(blob, 0, RLO_PART_BLOB_BYTES);
     std::memcpy(blob, &b, sizeof b);
@@ -1157,6 +1202,62 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
 }
 
 static void host_free(rlo_world* w);
+
+int rlo_pool_trim(uint32_t what, uint64_t* freed_bytes) {
+    std::vector<void*> regions, imports;
+    uint64_t freed = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (what & RLO_TRIM_IMPORTS) {
+            for (size_t i = 0; i < g_imports.size();) {
+                if (g_imports[i].refs == 0) {
+                    imports.push_back(g_imports[i].p);
+                    g_imports.erase(g_imports.begin() + (long)i);
+                } else {
+                    i++;
+                }
+            }
+        }
+        if (what & (RLO_TRIM_FREE | RLO_TRIM_EXPORTED)) {
+            for (size_t i = 0; i < g_pool.size();) {
+                const PoolEnt q = g_pool[i];
+                if (!q.exported && (what & RLO_TRIM_FREE)) {
+                    regions.push_back(q.p);
+                    freed += q.bytes;
+                } else if (q.exported && (what & RLO_TRIM_EXPORTED)) {
+                    g_retired.push_back(q);
+                } else {
+                    i++;
+                    continue;
+                }
+                g_pool.erase(g_pool.begin() + (long)i);
+            }
+        }
+        if (what & RLO_TRIM_RETIRED) {
+            for (const PoolEnt& q : g_retired) {
+                regions.push_back(q.p);
+                freed += q.bytes;
+            }
+            g_retired.clear();
+        }
+    }
+    for (void* d : imports) (void)hipIpcCloseMemHandle(d);
+    for (void* d : regions) (void)hipFree(d);
+    if (freed_bytes) *freed_bytes = freed;
+    return RLO_OK;
+}
+
+int rlo_pool_stats(uint64_t* out, uint32_t cap) {
+    if (!out || cap < 6) return RLO_E_INVAL;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    uint64_t v[6] = {0, 0, 0, 0, 0, 0};
+    for (const PoolEnt& q : g_pool_live) v[0] += q.bytes;
+    for (const PoolEnt& q : g_pool) v[q.exported ? 2 : 1] += q.bytes;
+    for (const PoolEnt& q : g_retired) v[3] += q.bytes;
+    for (const ImpEnt& e : g_imports) v[e.refs ? 4 : 5]++;
+    for (int i = 0; i < 6; i++) out[i] = v[i];
+    return RLO_OK;
+}
 
 int rlo_part_close_imports(rlo_world_t* w) {
     if (!w) return RLO_E_INVAL;
@@ -1810,6 +1911,16 @@ int rlo_reset(rlo_world_t* w, void* stream) {
             __atomic_store_n(&((rlo::ShmHdr*)w->shm)->leader_failed, 0u, __ATOMIC_RELEASE);
         }
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        // the pickup ring restarts at sequence 0: records and tagged payload units a previous launch left behind are
+        // cleared, so none can pass for this launch's event whatever the epochs (with 16-bit record tags and
+        // a per-launch epoch step, the record of the launch 16 (pk_cap 64) .. 256 (pk_cap 1024) back in the same slot
+        // could carry the expected tag).  A fresh world's memory is already zero
+        if (w->pk_dirty) {
+            if (w->h_ev) std::memset((void*)w->h_ev, 0, (size_t)w->nl * w->pk_cap * rlo::kPkRecBytes);
+            if (w->h_evp) std::memset(w->h_evp, 0, (size_t)w->nl * w->pk_cap * w->pk_stride);
+            w->pk_dirty = false;
+        }
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
         std::fill(w->cmd_tail.begin(), w->cmd_tail.end(), 0);
         std::fill(w->pk_head.begin(), w->pk_head.end(), 0);
     }
@@ -1850,11 +1961,15 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
         if (w->P.mode & rlo::MODE_HOST) {
             // a new pickup-tag epoch: the rings restart at sequence 0, and a record or payload unit an earlier
             // launch left in a slot carries another epoch's tag, so it never passes for this launch's event
-            w->pk_epoch += 0x9E3779B8u;  // (even: tags stay odd, never the 0 of fresh memory)
+            // (even: tags stay odd, never the 0 of fresh memory).  Diagnostics build: RLO_PK_EPOCH_SAME keeps the
+            // epoch, the worst case for stale records (tests/test_gpu_timeline.py: rlo_reset must clear them)
+            static const bool same = diag_env("RLO_PK_EPOCH_SAME") != nullptr;
+            if (!same) w->pk_epoch += 0x9E3779B8u;
             w->P.pk_epoch = w->pk_epoch;
             if (w->shm) __atomic_store_n(&((rlo::ShmHdr*)w->shm)->pk_epoch, w->pk_epoch, __ATOMIC_RELEASE);
         }
     }
+    if (w->P.mode & rlo::MODE_HOST) w->pk_dirty = true;  // rlo_reset clears what this launch writes
     HIPCHK(hipEventRecord(w->ev0, s));
     // diagnostic A/B switch: publish producer counters after the next poll instead of at the end
     // of the iteration that drained the stores

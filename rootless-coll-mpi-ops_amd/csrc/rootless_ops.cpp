@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "rlo_hip.h"
+#include "rlo_trace.hpp"
 
 int total_pickup = 0;  // rootless_ops.h:46
 
@@ -72,18 +73,6 @@ struct RawEv {  // a pickup-ring event pulled off the device, not yet handled on
     rlo_log_rec_t ev;
     std::vector<uint8_t> payload;
     int64_t t_seen = 0;  // RLO_TRACE_DIR: when the pump took it off the pickup ring
-};
-
-// RLO_TRACE_DIR=dir (diagnostics): every command posted, every event taken off the pickup ring and handled,
-// and every advance of the kernel's command head, with the host clock (CLOCK_MONOTONIC: one clock for every rank
-// process of the node), written to dir/trace_rank<R>_e<id>.txt at cleanup; tools/dropin_legs.py splits a bcast's
-// and a host-judged proposal's time into legs from them
-struct TraceRec {
-    int64_t t;
-    char what;  // 'P' command posted, 'S' event seen (pump), 'H' event handled (app thread), 'C' commands consumed
-    uint32_t kind;
-    int32_t origin, id, from;
-    uint32_t aux;
 };
 
 }  // namespace
@@ -138,8 +127,7 @@ struct progress_engine {
     int64_t d_cons_ns = 0, d_fwd_ns = 0;
     uint32_t d_hist[2][5] = {}, d_fh[2][5] = {};  // d_fh: submit -> forwarded by the proxy, forwarded -> consumed
     int64_t t_moved = 0, t_dump = 0;  // RLO_WATCHDOG: last event / last state dump
-    std::vector<TraceRec> tr;         // RLO_TRACE_DIR (the app and pump threads both append: tr_mu)
-    std::mutex tr_mu;
+    rlo::TraceLog tr;                 // RLO_TRACE_DIR (the app and pump threads both append)
     uint64_t tr_consumed = 0;
     progress_engine* next = nullptr;
 };
@@ -162,20 +150,14 @@ const char* trace_dir() {
 
 void trace(progress_engine* e, char what, uint32_t kind, int32_t origin, int32_t id, int32_t from, uint32_t aux,
            int64_t t = 0) {
-    std::lock_guard<std::mutex> lk(e->tr_mu);
-    if (e->tr.size() >= (1u << 22)) return;
-    e->tr.push_back(TraceRec{t ? t : now_ns(), what, kind, origin, id, from, aux});
+    e->tr.add(rlo::TraceRec{t ? t : now_ns(), what, kind, origin, id, from, aux});
 }
 
 void trace_write(progress_engine* e) {
-    char path[4096];
+    char path[4096], hdr[128];
     std::snprintf(path, sizeof path, "%s/trace_rank%d_e%d.txt", trace_dir(), e->rank, e->id);
-    FILE* f = std::fopen(path, "w");
-    if (!f) return;
-    std::fprintf(f, "# rank %d size %d engine %d\n", e->rank, e->size, e->id);
-    for (const TraceRec& r : e->tr)
-        std::fprintf(f, "%lld %c %u %d %d %d %u\n", (long long)r.t, r.what, r.kind, r.origin, r.id, r.from, r.aux);
-    std::fclose(f);
+    std::snprintf(hdr, sizeof hdr, "# rank %d size %d engine %d\n", e->rank, e->size, e->id);
+    (void)e->tr.write(path, hdr);
 }
 
 // RLO_TRACE_SETUP=1: engine construction steps with timestamps on stderr (diagnostics)
@@ -1296,7 +1278,12 @@ int RLO_progress_engine_cleanup(RLO_engine_t* eng) {
     // hipFree / hipIpcCloseMemHandle may wait for the whole device, i.e. for the persistent
     // kernel of another engine of this process: free the world once no engine kernel runs
     if (eng->leader) g_grave.push_back(std::make_pair(eng->w, eng->stream));
-    if (!g_engines) bury();
+    if (!g_engines) {
+        bury();
+        // the process's last engine: the device memory only this process ever mapped goes back to HIP, and its idle
+        // imports of peers' regions close (regions it exported stay pooled: RLO_device_memory_release)
+        (void)rlo_pool_trim(RLO_TRIM_IMPORTS | RLO_TRIM_FREE, nullptr);
+    }
     MPI_Comm_free(&eng->group);
     if (eng->caller_bound) (void)pthread_setaffinity_np(pthread_self(), sizeof eng->caller_mask, &eng->caller_mask);
     delete eng;
@@ -1495,5 +1482,19 @@ int RLO_get_world_size(void) {
 int RLO_user_msg_source(const RLO_user_msg* msg) { return msg ? ((const RLO_msg_t*)msg)->source : -1; }
 
 int RLO_engine_device(RLO_engine_t* eng) { return eng ? eng->device : -1; }
+
+int RLO_device_memory_release(MPI_Comm comm) {
+    // the world-wide close (rlo_hip.h rlo_pool_trim): every process drops its idle imports before any frees a region a
+    // peer may have imported
+    int live = g_engines ? 1 : 0, any = 0;
+    MPI_Allreduce(&live, &any, 1, MPI_INT, MPI_MAX, comm);
+    if (any) return -1;
+    bury();
+    (void)rlo_pool_trim(RLO_TRIM_IMPORTS | RLO_TRIM_FREE | RLO_TRIM_EXPORTED, nullptr);
+    MPI_Barrier(comm);
+    (void)rlo_pool_trim(RLO_TRIM_RETIRED, nullptr);
+    MPI_Barrier(comm);
+    return 0;
+}
 
 }  // extern "C"

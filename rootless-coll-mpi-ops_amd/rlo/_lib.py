@@ -29,6 +29,7 @@ RLO_PART_CHUNKED = 2
 RLO_PART_PEND_HBM = 4
 RLO_PEER_OTHER_GPU, RLO_PEER_IMPORTED = 1, 2  # rlo_world_info_t.peers
 RLO_LAUNCH_NO_RESET = 1
+RLO_TRIM_IMPORTS, RLO_TRIM_FREE, RLO_TRIM_RETIRED, RLO_TRIM_EXPORTED = 1, 2, 4, 8  # rlo_pool_trim
 RLO_FLAG_LOG, RLO_FLAG_HIST, RLO_FLAG_PROF, RLO_FLAG_TIMELINE = 1, 2, 4, 8
 RLO_JUDGE_APPROVE, RLO_JUDGE_MASK, RLO_JUDGE_ISP, RLO_JUDGE_HASH = 0, 1, 2, 3
 DERR = {1: "timeout", 2: "vote ring", 3: "pid collision", 4: "vote orphan", 5: "log full", 6: "bad slot", 7: "host command",
@@ -129,7 +130,8 @@ EXPORTS = ["rlo_topology", "rlo_children", "rlo_world_create", "rlo_world_destro
            "rlo_device_count", "rlo_device_numa_node", "rlo_host_bulk_stage", "rlo_host_bulk_copy", "rlo_bulk_plan", "rlo_layout_plan",
            "rlo_storm_lengths", "rlo_host_share", "rlo_host_unlink", "rlo_host_proxy", "rlo_host_wait_started",
            "rlo_host_fail", "rlo_client_attach", "rlo_client_detach", "rlo_client_state", "rlo_client_post",
-           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_client_hdiag", "rlo_client_fwd", "rlo_host_device_judge"]
+           "rlo_client_poll", "rlo_client_cmd_count", "rlo_client_bulk_put", "rlo_client_bulk_get", "rlo_client_debug", "rlo_client_hdiag", "rlo_client_fwd", "rlo_host_device_judge",
+           "rlo_pool_trim", "rlo_pool_stats"]
 
 _lib = None
 
@@ -148,6 +150,8 @@ def load():
     L.rlo_world_create.argtypes = [ctypes.POINTER(WorldCfg), ctypes.POINTER(vp)]
     L.rlo_world_destroy.argtypes = [vp]
     L.rlo_part_close_imports.argtypes = [vp]
+    L.rlo_pool_trim.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    L.rlo_pool_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     L.rlo_part_import.argtypes = [vp, ctypes.c_char_p, ctypes.c_int]
     L.rlo_world_query.argtypes = [vp, ctypes.POINTER(WorldInfo)]
     L.rlo_program_storm.argtypes = [vp, ctypes.POINTER(StormCfg)]

@@ -12,6 +12,7 @@ rank 0's clock at each round's completion).
 """
 import ctypes
 import multiprocessing as mp
+import os
 
 import numpy as np
 
@@ -104,7 +105,8 @@ def run_inprocess(n, bounds, spec, max_payload=4096, ring_slots=0, devices=None,
 def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, blob_q, blobs_q, barrier, out_q,
             world_kw, repeat=1):
     try:
-        from .world import World
+        from . import _lib as L
+        from .world import World, pool_trim
 
         for it in range(repeat):
             w = World.part(n, len(bounds) - 1, part, part_begin=bounds, max_payload=max_payload, ring_slots=ring_slots,
@@ -131,6 +133,13 @@ def _worker(n, bounds, part, device, spec, max_payload, ring_slots, uncached, bl
             w.close_imports()
             barrier.wait(timeout=120)
             w.close()
+            if os.environ.get("RLO_POOL_CAP_BYTES"):
+                # a lowered pool cap (the test hook): the world-wide close, so exported regions beyond it are freed --
+                # every part drops its idle imports, then every part frees its retired regions (rlo_hip.h rlo_pool_trim)
+                pool_trim(L.RLO_TRIM_IMPORTS | L.RLO_TRIM_FREE)
+                barrier.wait(timeout=120)
+                res["pool_freed"] = pool_trim(L.RLO_TRIM_RETIRED)
+                barrier.wait(timeout=120)
             out_q.put((part, rc, res, None))
     except Exception as e:  # report instead of hanging the parent
         out_q.put((part, -99, None, repr(e)))

@@ -257,6 +257,22 @@ class World:
         return np.array(arr[:n * stride.value], dtype=np.uint32).reshape(n, stride.value)
 
 
+def pool_trim(what):
+    """rlo_pool_trim: give pooled device regions / idle peer imports back (rlo_hip.h RLO_TRIM_*); returns bytes freed"""
+    lib = L.load()
+    freed = ctypes.c_uint64()
+    check(lib.rlo_pool_trim(what, ctypes.byref(freed)), "rlo_pool_trim")
+    return int(freed.value)
+
+
+def pool_stats():
+    """rlo_pool_stats: bytes live / free / free exported / retired, imports in use / idle"""
+    lib = L.load()
+    out = (ctypes.c_uint64 * 6)()
+    check(lib.rlo_pool_stats(out, 6), "rlo_pool_stats")
+    return dict(zip(("live", "free", "free_exported", "retired", "imports_used", "imports_idle"), [int(x) for x in out]))
+
+
 def hist_percentile(hist, p):
     """Percentile (in 10 ns ticks) from the device log-bucket histogram (4 sub-bins per octave)."""
     hist = np.asarray(hist, dtype=np.float64)

@@ -69,6 +69,18 @@ def test_world_create_without_gpu_fails_cleanly():
         rlo.World(8)
 
 
+def test_region_pool_empty_and_trim_without_gpu():
+    """rlo_pool_stats / rlo_pool_trim (the region pool's accounting and its release path) need no device when the
+    pool is empty: every count 0, every trim frees nothing"""
+    import rlo
+
+    assert rlo.pool_stats() == {"live": 0, "free": 0, "free_exported": 0, "retired": 0, "imports_used": 0,
+                                "imports_idle": 0}
+    L = rlo.abi
+    assert rlo.pool_trim(L.RLO_TRIM_IMPORTS | L.RLO_TRIM_FREE | L.RLO_TRIM_EXPORTED | L.RLO_TRIM_RETIRED) == 0
+    assert rlo.abi.load().rlo_pool_stats(None, 6) == L.RLO_E_INVAL
+
+
 def test_topology_matches_oracle():
     import pyoracle as orc
     import rlo

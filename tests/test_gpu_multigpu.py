@@ -121,6 +121,36 @@ def test_bulk_world_churn_processes(rlo):
         assert np.array_equal(st["bcast_sum"], ref["sum"]), it
 
 
+def test_bulk_world_churn_processes_pool_cap0(rlo):
+    """VERDICT r5 next 5 / ADVICE r5: the pool's free path.  RLO_POOL_CAP_BYTES=0 keeps no free region: every destroyed
+    world's exported regions are retired, and after each repeat the parts run the world-wide close (every part drops
+    its idle imports, barrier, every part frees its retired regions -- rlo_pool_trim), so each repeat creates, exports
+    and imports fresh memory; every repeat must still map and deliver the oracle's bytes"""
+    from rlo import sharded
+
+    n, rounds, seed, ln = 4, 4, 33, (1 << 20) + 48
+    spec = {"kind": "lat", "rounds": rounds, "len": ln, "seed": seed}
+    old = os.environ.get("RLO_POOL_CAP_BYTES")
+    os.environ["RLO_POOL_CAP_BYTES"] = "0"  # read by the spawned part processes
+    try:
+        runs = sharded.run_processes(n, [0, 2, 4], spec, max_payload=64, bulk_max=ln, movers=16, uncached=True, repeat=4)
+    finally:
+        if old is None:
+            os.environ.pop("RLO_POOL_CAP_BYTES", None)
+        else:
+            os.environ["RLO_POOL_CAP_BYTES"] = old
+    org = [orc.origin_of(seed, i, n) for i in range(rounds)]
+    want = np.zeros(n, dtype=np.uint64)
+    for i, o in enumerate(org):
+        cs = np.uint64(orc.msg_checksum(o, i, 0, orc.payload(o, i, ln)))
+        for r in range(n):
+            if r != o:
+                want[r] += cs
+    for it, ((st, _, _), rcs) in enumerate(runs):
+        assert rcs == [0, 0], (it, st["error"], st["error_aux"])
+        assert np.array_equal(st["bcast_sum"], want), it
+
+
 def _merged(recs, name):
     """one leg's per-rank statistics of every part, by world rank"""
     parts = sorted((r[name] for r in recs), key=lambda x: x["rank_begin"])
@@ -240,6 +270,8 @@ def test_bench_eight_parts_under_torchrun():
     CU; parts split on multiples of 8); every leg checked against the oracle per world rank"""
     line = _bench_parts(8, 32, 29541, 140)
     assert line["bulk"]["ranks"] == 8 and line["c5_mixed"]["world_ranks"] == 128
+
+
 def _stale_part(part, tamper, blob_q, blobs_q, out_q, done_q):
     """one part process of a 16-rank, 2-part world on this GPU; `tamper`: before connecting, change the creation
     nonce the peer's blob carries (PartBlob.nonce, byte 480 of the blob), as a mapping of an earlier allocation

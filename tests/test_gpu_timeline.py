@@ -117,3 +117,58 @@ def test_bulk_verify_catches_a_stale_granule():
     code, aux = d["err"]
     assert code == 8 and aux >> 24 == 14, (code, hex(aux))  # RLO_DERR_BULK, the VERIFY site
     assert (aux >> 16) & 0xff < 4 and aux & 0xffff == 0, hex(aux)  # a receiver, the message's first 16-KiB block
+
+
+STALE_CHILD = r'''
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[2])
+import rlo
+import pyoracle as orc
+n, ln = 8, 48
+out = {}
+with rlo.HostWorld(n, max_payload=64) as hw:
+    for i, o in enumerate((0, 5)):
+        assert hw.bcast(o, orc.payload(o, i, ln), seq=i)
+    got = {r: [] for r in range(n)}
+    t0 = time.time()
+    while sum(len(v) for v in got.values()) < 2 * (n - 1) and time.time() - t0 < 20:
+        for r in range(n):
+            got[r] += hw.poll(r)
+    out["first"] = sum(len(v) for v in got.values())
+    hw.relaunch()
+    time.sleep(0.3)
+    out["phantom"] = sum(len(hw.poll(r)) for r in range(n))
+    assert hw.bcast(3, orc.payload(3, 7, ln), seq=7)
+    got = {r: [] for r in range(n)}
+    t0 = time.time()
+    while sum(len(v) for v in got.values()) < n - 1 and time.time() - t0 < 20:
+        for r in range(n):
+            got[r] += hw.poll(r)
+    time.sleep(0.1)
+    for r in range(n):
+        got[r] += hw.poll(r)
+    out["second"] = {r: [(e["origin"], e["id"], e["payload"][:ln].hex()) for e in got[r]] for r in range(n)}
+print(json.dumps(out))
+'''
+
+
+def test_host_relaunch_same_epoch_takes_no_stale_pickup():
+    """ADVICE r5 (medium): pickup records are tagged with 16 bits of (sequence, launch epoch), so a record a launch
+    16..256 launches back left in a slot could carry the tag the running launch expects.  rlo_reset now clears the
+    pickup ring.  The diagnostics build's RLO_PK_EPOCH_SAME keeps the epoch across launches -- every stale record then
+    carries exactly the expected tag -- and the relaunched world must still surface nothing before the host posts,
+    then exactly the new bcast"""
+    if not os.path.exists(os.path.join(PKG, "lib_diag", "librlo_hip.so")):
+        pytest.skip("diagnostics build (make DIAG=1) not built")
+    env = dict(os.environ, RLO_DIAG_LIB="1", RLO_PK_EPOCH_SAME="1")
+    r = subprocess.run([sys.executable, "-c", STALE_CHILD, PKG, os.path.join(REPO, "oracle")], capture_output=True,
+                       text=True, timeout=150, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    n, ln = 8, 48
+    assert d["first"] == 2 * (n - 1), d
+    assert d["phantom"] == 0, d
+    for r_ in range(n):
+        want = [] if r_ == 3 else [[3, 7, orc.payload(3, 7, ln).hex()]]
+        assert d["second"][str(r_)] == want, (r_, d["second"])
