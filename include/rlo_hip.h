@@ -104,6 +104,9 @@ typedef struct {
     uint32_t ll_ok;        /* 1: the latency / iar / host programs run with doorbells                 */
     uint32_t pend_hbm;     /* 1: the pending-proposal tables live in HBM, not LDS (large N x pool)     */
     uint32_t dyn_lds, static_lds; /* bytes of LDS per rank-workgroup                                  */
+    uint32_t last_kernel;  /* the latest launch ran: 0 the progress kernel, 1 the hop kernel (the latency / iar
+                              programs with doorbells: one wave per rank)                  */
+    uint32_t info_pad;
 } rlo_world_info_t;
 
 /* single-part world: all N ranks on one GPU (replaces RLO_progress_engine_new :467-522

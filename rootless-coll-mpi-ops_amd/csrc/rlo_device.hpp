@@ -298,6 +298,7 @@ struct Params {
     uint64_t* jsum;                 // [2][jslots] VERIFY checksum accumulator
     uint32_t storm_order;           // RLO_ORDER_SLOTS: bcast b originates at b mod N
     uint32_t host_judge;            // host mode: 1 = judges are the host's callbacks, 0 = the device registry
+    uint32_t hop_chunks;            // the hop kernel (rlo_hop.hip): 16-B chunks of the program's longest message
 };
 
 // ---- bulk messages (longer than a ring slot; SURVEY §8(f)1, BASELINE configs[2], [4]).

@@ -1,0 +1,587 @@
+// rlo_hop.hip -- the hop kernel (gfx950 / CDNA4): the latency and iar programs on ONE wave per rank.
+//
+// The programs that move one message at a time -- the latency program (one bcast in flight, rootless_ops.c
+// testcases.c:59-108 at scale) and the iar program (proposal / vote / decision rounds with device judges,
+// rootless_ops.c:668-917) -- spend their time on the HOP: a message's arrival, its checks, its forwards.  The
+// progress kernel (rlo_kernel.hip) serves them with its doorbell pass, but that pass lives inside a 4 / 8-wave
+// kernel built for batched storms: 200-256 VGPRs and 240-360 SGPRs spilled to VGPR lanes, so a hop's checks were
+// ~800 instructions.  This kernel restates only what these programs need, in one wave, and
+// handles every message the way the reference does -- one received message at a time, in per-edge FIFO order
+// (make_progress_gen :551-641 surfaces one per call) -- with no batched iteration at all:
+//
+//   poll   : one round trip for every counter of the rank (in-ring tails, vote-in tails, out-ring heads, vote-out
+//            heads), its forward and vote DOORBELLS (rlo_device.hpp), the part's error word and the latency round
+//            word.  The previous round's counters are published right after it returns: its wait covered the
+//            previous round's stores (vmcnt counts loads and stores in issue order), so no separate drain
+//   load   : the ring messages and votes the counters show beyond what the bells carried, one round trip
+//   votes  : _iar_vote_handler :743-812 / _vote_merge :1056-1070, a completed merge votes up (_vote_back :728-741)
+//   rings  : per in-ring, its messages in order: _bc_forward :1104-1225 (children relative to the dynamic origin,
+//            forwarded into every child's ring and doorbell), then the delivery / proposal / decision effects
+//            (:583-615, :668-726, :814-859); a message whose out-rings are full waits (the ring stops there)
+//   own    : the pool's decisions (_iar_decision_bcast :908-917), then its next proposals (RLO_submit_proposal
+//            :876-906), or this rank's next latency round (RLO_bcast_gen :1581-1604)
+//
+// Rings, doorbells, counters, pending tables, logs and statistics are the world's own (rlo_world.cpp builds them
+// for both kernels): parts of one world may run either kernel, and every test of these programs runs this one.
+// Memory ordering as in rlo_kernel.hip: every handed-off byte stored sc1 (system scope across GPUs) and loaded
+// sc1 behind the counter that covers it; a counter is stored after its stores drained.
+#include "rlo_kernel_common.hpp"
+
+namespace rlo {
+
+constexpr uint32_t kHopScratch = 64u * 16u;  // one batch of 16-B chunks (64 lanes x 16 B)
+constexpr uint32_t kHopLoads = 4;            // ring-message loads per lane per round trip (256 chunks)
+constexpr uint32_t kPmHop = ~(uint32_t)MODE_HOST;  // log_put: no host-mode code here
+
+struct HopShared {
+    RankTopo t;
+    uint64_t vout_tail[kMaxIn], vout_head[kMaxIn];  // vote rings towards my parents (emit_vote)
+    // own proposals: the pool (rootless_ops.c:30, :159-165, :1251-1366), slot k named by the pseq byte
+    int32_t own_pid[kPoolMax];
+    uint32_t own_word[kPoolMax], own_state[kPoolMax], own_decision[kPoolMax];
+    uint32_t own_needed, own_rr;
+    unsigned long long own_iter;
+    int64_t own_n;
+    uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen;
+    uint32_t error, error_aux;
+    unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
+    unsigned long long own_decided, own_approved, proposals_recv, log_count, stale;
+    uint64_t pk_tail;  // (log_put's host-mode fields: this kernel runs no host mode)
+    uint32_t ev_n;
+    uint32_t hist[kHistBins];
+    alignas(16) uint8_t bell[kHopScratch];   // in-edge k's doorbell, chunk q at 16 (8 k + q)
+    alignas(16) uint8_t msg[kHopLoads * kHopScratch];  // loaded ring messages, message m chunk q at 16 (m mch + q)
+    alignas(16) uint8_t vote[kHopScratch];   // loaded votes, one 16-B slot per lane
+};
+
+template <bool PH>
+__global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    __shared__ HopShared S;
+    const int lr = blockIdx.x, me = P.rank_begin + lr;
+    const int lane = (int)threadIdx.x;
+    PendState* pend;  // [n][pend_slots]: dynamic LDS, or (PH) this rank's table in HBM
+    if constexpr (PH)
+        pend = (PendState*)(__attribute__((address_space(1))) PendState*)(P.pend_hbm + (size_t)blockIdx.x * (uint32_t)P.n * P.pend_slots);
+    else
+        pend = reinterpret_cast<PendState*>(dyn_lds);
+#define PEND(o, q) pend[(uint32_t)(o) * P.pend_slots + ((uint32_t)(q) & (P.pend_slots - 1u))]
+    const bool lat = (P.mode & MODE_LAT) != 0, iar = (P.mode & MODE_IAR) != 0;
+    const uint32_t mch = P.hop_chunks;  // 16-B chunks of the program's longest message (<= 64)
+
+    // ---------------- init
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&P.topo[lr]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&S.t);
+        for (int i = lane; i < (int)(sizeof(RankTopo) / 4); i += 64) dst[i] = src[i];
+        for (int i = lane; i < P.n * (int)P.pend_slots; i += 64) pend[i] = PendState{0, 0, 0, 0, 0, 0};
+        for (int i = lane; i < kHistBins; i += 64) S.hist[i] = 0;
+        if (lane < kMaxIn) { S.vout_tail[lane] = 0; S.vout_head[lane] = 0; }
+        if (lane < kPoolMax) { S.own_pid[lane] = -1; S.own_word[lane] = 0; S.own_state[lane] = 0; S.own_decision[lane] = 0; }
+        if (lane == 0) {
+            S.own_needed = 0; S.own_rr = 0; S.own_iter = 0;
+            S.own_n = iar ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
+            S.lat_pos = 0; S.lat_seen = 0;
+            S.lat_pos_n = lat ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
+            S.lat_own_next = S.lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
+            S.error = 0; S.error_aux = 0;
+            S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
+            S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stale = 0;
+            S.pk_tail = 0; S.ev_n = 0;
+        }
+    }
+    if constexpr (PH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the table's zeros land before any read
+    __syncthreads();
+    const uint64_t t_start = now_ticks();
+    unsigned long long acc_sum = 0;  // checksum of delivered bcast chunks (this lane's share)
+    const int64_t expect_bcast = lat ? P.expect_bcast[lr] : 0;
+    const int64_t expect_dec = iar ? P.expect_dec[lr] : 0;
+    const uint32_t my_mask = (iar && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
+
+    // topology: wave-uniform scalars + lane-distributed send list
+    const RankTopo& t = S.t;
+    const int level = uni(t.level), last_wall = uni(t.last_wall), scc = uni(t.scc), sll = uni(t.sll);
+    const int n_in = uni(t.n_in), n_in2 = 2 * n_in, nout = 2 * sll;
+    const uint32_t inbox = (uint32_t)uni((int)t.inbox_ctrl), outbox = (uint32_t)uni((int)t.outbox_ctrl);
+    const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
+    const uint32_t sl_r = lane < sll ? (uint32_t)t.send_list[lane] : 0u;
+    const bool sys = P.sys_scope != 0;
+    const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
+    const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
+    const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);
+    const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1, oring_bytes = P.fwd_cap * P.fwd_stride;
+    // lane-distributed ring state: lane g = in-ring g (k*2 + vc), lane oi = out-ring oi (j*2 + vc), lane j = vote
+    // ring from child j, lane k = vote ring to the parent of in-edge k; published values beside them
+    uint64_t in_head_r = 0, out_tail_r = 0, vin_head_r = 0;
+    uint64_t pub_in = 0, pub_out = 0, pub_vin = 0, pub_vout = 0;
+    // this lane's out-ring (lane oi < nout): its base in the child's part and the child's doorbell for the edge
+    const uint64_t obase_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;
+    const uint64_t bbase_r = lane < nout ? t.out_bell[lane >> 1] : 0ull;
+    uint64_t n_iter = 0, n_busy = 0, idle_since = 0;
+    uint32_t idle_n = 0;
+    bool done = false;
+
+    // a message (lane q holds slot chunk q, q < nch) into out-rings `need` at their tails, and into each child's
+    // doorbell for the edge when it fits one (tag bell_tag(ring sequence) | vc << 31).  The caller advances out_tail_r
+    auto forward = [&](u32x4 v, uint32_t nch, uint32_t need) {
+        const uint32_t q = (uint32_t)lane;
+        for (uint32_t m = need; m; m &= m - 1) {
+            const int oi = __builtin_ctz(m);
+            const uint64_t slot = rdl64(out_tail_r, oi);
+            const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(obase_r, oi)), oring_bytes);
+            if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+            if (nch <= kBellChunks && q < nch) {
+                const uint32_t T = bell_tag(slot) | ((uint32_t)(oi & 1) << 31);
+                const __amdgpu_buffer_rsrc_t rb = mk_rsrc(reinterpret_cast<void*>(rdl64(bbase_r, oi)), kBellWords * 8u);
+                st_ring(rb, 32u * q, u32x4{v.x, T, v.y, T}, sys);
+                st_ring(rb, 32u * q + 16u, u32x4{v.z, T, v.w, T}, sys);
+            }
+        }
+    };
+    // out-rings of `need` that have no free slot (uniform)
+    auto full_of = [&](uint32_t need, uint64_t out_head_r) -> bool {
+        return __ballot(lane < nout && ((need >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap) != 0ull;
+    };
+
+    // one vote from child j (lane 0): _iar_vote_handler :743-812, _vote_merge :1056-1070
+    auto merge_vote = [&](int origin, int32_t pid, uint32_t pseq, int vote, uint32_t vw) {
+        const uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
+        if (origin >= P.n) {
+            set_error(S, P, ERR_BAD_SLOT, vw);
+        } else if (origin == me) {  // a vote for my own proposal (:756-783)
+            const uint32_t k = pseq & (P.pend_slots - 1u);
+            if (S.own_state[k] != 1 || pid != S.own_pid[k]) {
+                set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+            } else {
+                const uint32_t nw = (S.own_word[k] += inc);
+                if ((nw & 0xffffu) == S.own_needed) {
+                    const int d = (nw >> 16) == 0 ? 1 : 0;
+                    if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
+                        S.judge_calls++;
+                        log_put<kPmHop>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                    }
+                    S.own_decision[k] = (uint32_t)d;
+                    S.own_state[k] = 2;
+                }
+            }
+        } else {
+            PendState* ps = &PEND(origin, pseq);
+            if (ps->valid != PS_ACTIVE || ps->pid != pid) {
+                set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+            } else {
+                const uint32_t nw = (ps->word += inc);
+                if ((nw & 0xffffu) == ps->needed)
+                    emit_vote<true>(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+            }
+        }
+    };
+
+    // one ring message from in-ring g, lane q holding slot chunk q (q < nch): checks, forwards, effects.  Returns
+    // false when it cannot go now (an out-ring it needs is full, or its pending entry still holds the previous
+    // proposal of that pool slot): nothing changed, the ring waits
+    auto take = [&](u32x4 v, int g, uint64_t out_head_r) -> bool {
+        const uint32_t q = (uint32_t)lane;
+        const int from = uni(t.in_src[g >> 1]);
+        const uint32_t w0 = rdl32(v.x, 0), id = rdl32(v.y, 0), w2 = rdl32(v.z, 0), t0 = rdl32(v.w, 0);
+        const int origin = (int)(w0 & 0xffffu);
+        const uint32_t tag = (w0 >> 16) & 0xffu, len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4, pseq = w2 >> 24;
+        const int vote = (int)(int8_t)(w0 >> 24);
+        if (((w2 >> 16) & 0xffu) != kSlotMark) {  // bytes not visible behind the published tail: a protocol violation
+            if (lane == 0) {
+                S.stale++;
+                set_error(S, P, ERR_BAD_SLOT, 0x57A1Eu);
+            }
+            return true;  // consumed, never forwarded
+        }
+        if (origin >= P.n || nch > mch || !(tag == TAG_BCAST || tag == TAG_DECISION || tag == TAG_PROPOSAL) ||
+            (tag == TAG_BCAST && lat && id >= P.lat_rounds)) {
+            if (lane == 0) set_error(S, P, ERR_BAD_SLOT, w0);
+            return true;
+        }
+        int judge = 1;
+        if (tag == TAG_PROPOSAL) {
+            if (PEND(origin, pseq).valid != PS_NONE) return false;  // the decision ahead of it first
+            // device judge on the PBuf data [pid][vote][data_len u64][data] at slot + 16 (:1402-1410): chunk 1's
+            // word 2 is data_len, the data from chunk 2 on (LDS copy of this lane's chunk)
+            uint32_t dl = rdl32(v.z, 1);
+            if (dl > len - 16u) dl = len > 16u ? len - 16u : 0u;
+            if (P.judge_kind == JUDGE_ISP) {
+                if (q < nch) *reinterpret_cast<u32x4*>(S.vote + 16u * q) = v;  // (scratch: votes are merged already)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint8_t* d = S.vote + kHdr + 16u;
+                judge = judge_eval_f(P, me, my_mask, (int32_t)id, [&](uint32_t i) { return d[i]; }, dl);
+            } else {
+                judge = judge_eval_f(P, me, my_mask, (int32_t)id, [&](uint32_t) { return (uint8_t)0; }, dl);
+            }
+        }
+        const uint32_t kids = judge == 1 ? kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane) : 0u;
+        const uint32_t need = need_of_u(kids, origin, sll, sl_r, lane);
+        if (full_of(need, out_head_r)) return false;
+        forward(v, nch, need);  // before the effects, as the reference forwards before queueing the pickup (:583-589)
+        if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
+        if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
+            uint32_t li = ~0u;
+            if (lane == 0) {
+                S.bcast_delivered++;
+                const uint32_t tn = (uint32_t)now_ticks();
+                if (P.mode & MODE_HIST) S.hist[hist_bin(tn - t0)]++;
+                li = log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, tn - t0);
+            }
+            li = rdl32(li, 0);
+            if (q < nch) {
+                acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, id, TAG_BCAST, len}) : chunk_mix(q - 1u, v);
+                if (li != ~0u && q >= 1u && 16u * q <= P.log_stride)
+                    st_sys16(P.log_payload + ((size_t)lr * P.log_cap + li) * P.log_stride + 16u * (q - 1u), v);
+            }
+            if (lat && lane == 0) {  // the round's last pickup completes it
+                const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                         : atomicAdd(&P.lat_count[id], 1u);
+                if (old + 1u == (uint32_t)(P.n - 1)) {
+                    P.lat_out[id] = (uint64_t)((uint32_t)now_ticks() - t0);
+                    if (sys) __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    else __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
+            if (lane == 0) {
+                S.proposals_recv++;
+                if (own_has(S, P, (int32_t)id)) {
+                    set_error(S, P, ERR_PID_COLLISION, id);  // :690-692
+                } else {
+                    const uint32_t k = (uint32_t)g >> 1;
+                    S.judge_calls++;
+                    log_put<kPmHop>(S, P, lr, LOG_JUDGE, origin, from, id, len, judge, 0);
+                    PendState* ps = &PEND(origin, pseq);
+                    if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
+                        ps->valid = PS_NONE;
+                        emit_vote<true>(S, P, me, k, origin, (int32_t)id, pseq, 0);
+                    } else {
+                        const uint32_t nk = (uint32_t)__builtin_popcount(kids);
+                        ps->pid = (int32_t)id;
+                        ps->word = 0;
+                        ps->parent_k = (uint16_t)k;
+                        ps->needed = (uint8_t)nk;
+                        ps->pseq = pseq | ((len - 16u) << 8);
+                        ps->valid = PS_ACTIVE;
+                        if (nk == 0) emit_vote<true>(S, P, me, k, origin, (int32_t)id, pseq, 1);
+                    }
+                }
+            }
+        } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
+            PendState* ps = &PEND(origin, pseq);
+            if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)id) {
+                if (vote != 0) {
+                    S.actions++;
+                    log_put<kPmHop>(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, ps->pseq >> 8);
+                }
+                ps->valid = PS_NONE;
+            }
+            S.dec_delivered++;
+            if (vote != 0) S.dec_approved++;
+            log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+        }
+        return true;
+    };
+
+    // a local origination to the whole send list (:1587): header + generated chunks; false (nothing changed) when
+    // an out-ring is full
+    auto originate = [&](uint32_t kind, uint32_t w0, uint32_t id, uint32_t w2, uint32_t src, uint64_t out_head_r) -> bool {
+        const uint32_t len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4;
+        const uint32_t need = need_of_u((1u << sll) - 1u, me, sll, sl_r, lane);
+        if (full_of(need, out_head_r)) return false;
+        const uint32_t q = (uint32_t)lane;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (q == 0) v = u32x4{w0, id, (w2 & 0xff00ffffu) | (kSlotMark << 16), (uint32_t)now_ticks()};
+        else if (q < nch) v = gen_chunk(P, kind, me, id, len, src, (int)(int8_t)(w0 >> 24), q);
+        forward(v, nch, need);
+        if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
+        return true;
+    };
+
+    for (;;) {
+        // ---------------- poll: counters, doorbells, error word, round word -- one round trip
+        uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
+        uint32_t errf = 0, latr = 0;
+        if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
+        if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
+        if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
+        if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
+        if (lane == 0) errf = poll32(P.error_flag);
+        if (lat && lane == 1) latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : poll32(P.lat_round);
+        const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
+        u32x4 ba = {0u, 0u, 0u, 0u}, bb = {0u, 0u, 0u, 0u}, vb = {0u, 0u, 0u, 0u};
+        if ((int)bk < n_in) {
+            const uint32_t o = (in_bell + bk * kBellWords) * 8u + 32u * bq;
+            ba = ld_sc1(rc, o);
+            bb = ld_sc1(rc, o + 16u);
+        }
+        if (lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (also the previous round's stores: in-order counter)
+        n_iter++;
+        // ---- the previous round's counters: its stores have drained
+        if (lane < nout && out_tail_r != pub_out) { pub_out = out_tail_r; pub64(t.out_tail[lane >> 1][lane & 1], out_tail_r, sys); }
+        if (lane < n_in2 && in_head_r != pub_in) { pub_in = in_head_r; pub64(t.in_head[lane >> 1][lane & 1], in_head_r, sys); }
+        if (lane < sll && vin_head_r != pub_vin) { pub_vin = vin_head_r; pub64(t.vin_head[lane], vin_head_r, sys); }
+        if (lane < n_in) {
+            const uint64_t vt = S.vout_tail[lane];
+            if (vt != pub_vout) { pub_vout = vt; pub64(t.vout_tail[lane], vt, sys); }
+            S.vout_head[lane] = vout_head_r;
+        }
+        if (done) break;  // (the final counters are out)
+        if (__builtin_amdgcn_readfirstlane(errf) != 0) break;  // another rank failed: stop everyone
+        if (lat && me == 0) {  // world rank 0 observes round completions on its own clock
+            const uint32_t done_r = rdl32(latr, 1), seen = S.lat_seen;
+            if (done_r > seen) {
+                const uint64_t tn = now_ticks();
+                for (uint32_t k = seen + (uint32_t)lane; k < done_r && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
+                if (lane == 0) S.lat_seen = done_r;
+            }
+        }
+
+        // ---- what the doorbells hold: in-edge k's bell is whole for (k, vc) when every half of its header's chunks
+        // carries bell_tag(in-ring head) | vc << 31; a vote bell when it carries bell_tag(vote head)
+        *reinterpret_cast<u32x4*>(S.bell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
+        const uint32_t e0 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk)));
+        const uint32_t e1 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk + 1u))) | 0x80000000u;
+        const bool inb = (int)bk < n_in;
+        const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
+        const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
+        const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;
+        const uint64_t gm = hn <= kBellChunks ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
+        const uint64_t fh = __ballot(bq == 0u && gm && ((B0 & gm) == gm || (B1 & gm) == gm));
+        const uint64_t fv = __ballot(bq == 0u && gm && (B1 & gm) == gm);
+        const int rk = lane >> 1;
+        // lane g: its head is in the bell; the messages the counter shows beyond it
+        const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
+        const uint64_t ip = lane < n_in2 && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
+        const uint32_t vbh = lane < sll && vb.y == bell_tag(vin_head_r) && vb.w == bell_tag(vin_head_r) ? 1u : 0u;
+        const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
+
+        // ---- load what the counters show beyond the bells: ring messages (lane (m, q): chunk q of the m-th message
+        // to load) and votes (one slot per lane), one round trip
+        const uint32_t mmax = min(kHopLoads * 64u / mch, 64u);
+        uint32_t mtot = 0;
+        const uint32_t want = (uint32_t)min(ip > (rhit ? 1ull : 0ull) ? ip - (rhit ? 1ull : 0ull) : 0ull, (uint64_t)mmax);
+        const uint32_t mb = wave_excl_scan(want, &mtot);
+        const uint32_t mtake = mb >= mmax ? 0u : min(want, mmax - mb);  // lane g: slot messages loaded this round
+        const uint32_t mload = min(mtot, mmax);
+        uint32_t vtot = 0;
+        const uint32_t vwant = (uint32_t)min(vp > vbh ? vp - vbh : 0ull, (uint64_t)64);
+        const uint32_t vbase = wave_excl_scan(vwant, &vtot);
+        const uint32_t vtake = vbase >= 64u ? 0u : min(vwant, 64u - vbase);  // lane j: vote slots loaded
+        if (mtot | vtot) {
+            u32x4 lm[kHopLoads], lw = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (uint32_t u = 0; u < kHopLoads; u++) {  // item u 64 + lane = (message m, chunk qq)
+                lm[u] = u32x4{0u, 0u, 0u, 0u};
+                if (u * 64u >= mload * mch) continue;  // (uniform)
+                const uint32_t i = u * 64u + (uint32_t)lane, m = i / mch, qq = i - m * mch;
+                uint32_t src = 0;
+                bool any = false;
+                for (uint64_t gs = __ballot(mtake > 0u); gs; gs &= gs - 1) {  // uniform loop over rings with loads
+                    const int g = __builtin_ctzll(gs);
+                    const uint32_t b0 = rdl32(mb, g), n0 = rdl32(mtake, g);
+                    if (m >= b0 && m < b0 + n0) {
+                        const uint64_t seq = rdl64(in_head_r, g) + (rdl32(rhit ? 1u : 0u, g)) + (m - b0);
+                        src = t.in_data[g >> 1][g & 1] + (uint32_t)(seq & fcap_m) * P.fwd_stride + 16u * qq;
+                        any = true;
+                    }
+                }
+                if (any) lm[u] = ld_sc1(rf, src);
+            }
+            {
+                bool any = false;
+                uint32_t src = 0;
+                for (uint64_t js = __ballot(vtake > 0u); js; js &= js - 1) {
+                    const int j = __builtin_ctzll(js);
+                    const uint32_t b0 = rdl32(vbase, j), n0 = rdl32(vtake, j);
+                    if ((uint32_t)lane >= b0 && (uint32_t)lane < b0 + n0) {
+                        const uint64_t seq = rdl64(vin_head_r, j) + rdl32(vbh, j) + ((uint32_t)lane - b0);
+                        src = t.vin_data[j] + (uint32_t)(seq & vcap_m) * kVoteSlot;
+                        any = true;
+                    }
+                }
+                if (any) lw = ld_sc1(rv, src);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kHopLoads; u++)
+                if (u * 64u < mload * mch) *reinterpret_cast<u32x4*>(S.msg + 16u * (u * 64u + (uint32_t)lane)) = lm[u];
+            *reinterpret_cast<u32x4*>(S.vote + 16u * (uint32_t)lane) = lw;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        bool progressed = false;
+
+        // ---------------- votes: child j's head from its bell, then its loaded slots, in order
+        for (uint64_t js = __ballot(vbh || vtake); js; js &= js - 1) {
+            const int j = __builtin_ctzll(js);
+            const uint32_t hb = rdl32(vbh, j), nv = rdl32(vtake, j), b0 = rdl32(vbase, j);
+            if (lane == 0) {
+                if (hb) {  // vote bell {origin | pseq << 16 | vote << 24, pid}
+                    const uint32_t x = rdl32(vb.x, j), pid = rdl32(vb.z, j);
+                    merge_vote((int)(x & 0xffffu), (int32_t)pid, (x >> 16) & 0xffu, (int)(int8_t)(x >> 24), x);
+                }
+                for (uint32_t i = 0; i < nv; i++) {  // vote slot {origin | vote << 24, pid, pseq, voter}
+                    const u32x4 vs = *reinterpret_cast<const u32x4*>(S.vote + 16u * (b0 + i));
+                    merge_vote((int)(vs.x & 0xffffu), (int32_t)vs.y, vs.z & 0xffu, (int)(int8_t)(vs.x >> 24), vs.x);
+                }
+            }
+            if (lane == j) vin_head_r += hb + nv;
+            progressed = true;
+        }
+
+        // ---------------- ring messages: per in-ring its head (bell or slot), then its loaded slots, in order
+        for (uint64_t gs = __ballot(rhit || mtake); gs; gs &= gs - 1) {
+            const int g = __builtin_ctzll(gs);
+            const uint32_t hb = rdl32(rhit ? 1u : 0u, g), nm = rdl32(mtake, g), b0 = rdl32(mb, g);
+            uint32_t taken = 0;
+            for (uint32_t i = 0; i < hb + nm; i++) {  // uniform
+                const bool bell = i < hb;
+                const uint32_t at = bell ? 16u * (8u * (uint32_t)(g >> 1)) : 16u * ((b0 + i - hb) * mch);
+                u32x4 v = {0u, 0u, 0u, 0u};
+                if ((uint32_t)lane < (bell ? kBellChunks : mch)) v = *reinterpret_cast<const u32x4*>((bell ? S.bell : S.msg) + at + 16u * (uint32_t)lane);
+                // a bell holds at most kBellChunks chunks (its header says how many); a longer message comes by slot
+                if (!take(v, g, out_head_r)) break;
+                taken++;
+            }
+            if (lane == g) in_head_r += taken;
+            if (taken) progressed = true;
+        }
+
+        // ---------------- my own originations
+        if (iar) {
+            for (;;) {  // the pool's decided slots (_iar_decision_bcast :908-917)
+                const uint32_t ps_ = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
+                const uint64_t dm = __ballot(ps_ == 2u);
+                if (!dm) break;
+                const uint32_t k = (uint32_t)__builtin_ctzll(dm);
+                const uint32_t id = (uint32_t)S.own_pid[k], dec = S.own_decision[k];
+                if (!originate(K_DEC, (uint32_t)me | (TAG_DECISION << 16) | ((dec & 0xffu) << 24), id, 23u | (k << 24), 0u,
+                               out_head_r))
+                    break;
+                if (lane == 0) {
+                    S.own_decided++;
+                    if (dec) S.own_approved++;
+                    log_put<kPmHop>(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, k);
+                    S.own_state[k] = 0;
+                    S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
+                }
+                progressed = true;
+            }
+            for (;;) {  // RLO_submit_proposal :876-906, up to own_pool in flight
+                const uint32_t ps2 = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
+                const uint64_t busy = __ballot(ps2 != 0u);
+                if (S.own_iter >= (unsigned long long)S.own_n || (uint32_t)__popcll(busy) >= P.own_pool) break;
+                uint32_t k = S.own_rr;
+                while ((busy >> k) & 1ull) k = (k + 1u) & (P.pend_slots - 1u);
+                const int64_t pi = P.prop_off[lr] + (int64_t)S.own_iter;
+                const uint32_t id = (uint32_t)P.prop_pid[pi];
+                if (!originate(K_PROP, (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id,
+                               (16u + P.prop_data_len[pi]) | (k << 24), (uint32_t)pi, out_head_r))
+                    break;
+                if (lane == 0) {  // proposalPool_proposal_add (:1253-1279)
+                    S.own_pid[k] = (int32_t)id;
+                    S.own_word[k] = 0;
+                    S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
+                    S.own_state[k] = 1;
+                    S.own_iter++;
+                    S.own_rr = (k + 1u) & (P.pend_slots - 1u);
+                }
+                progressed = true;
+            }
+        }
+        if (lat && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next &&
+            originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), S.lat_own_next, P.len, 0u, out_head_r)) {
+            if (lane == 0) {
+                S.originated++;
+                const uint32_t np = S.lat_pos + 1u;
+                S.lat_pos = np;
+                S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
+            }
+            progressed = true;
+        }
+
+        // ---------------- bookkeeping (lane 0 decides, every lane follows)
+        if (lane == 0) {
+            if (progressed) {
+                n_busy++;
+                idle_n = 0;
+            } else if ((++idle_n & 63u) == 1u) {  // the clock on the 1st and every 64th idle round only
+                const uint64_t tn = now_ticks();
+                if (idle_n == 1) idle_since = tn;
+                else if (tn - idle_since > P.timeout_ticks) set_error(S, P, ERR_TIMEOUT, 0);
+            }
+            if ((n_iter & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
+            bool d = true;
+            if (lat) d &= S.lat_pos >= S.lat_pos_n && (int64_t)S.bcast_delivered == expect_bcast;
+            if (iar) {
+                bool idle = true;
+                for (uint32_t k = 0; k < P.pend_slots; k++) idle &= S.own_state[k] == 0u;
+                d &= (int64_t)S.own_iter == S.own_n && idle && (int64_t)S.dec_delivered == expect_dec;
+            }
+            if (S.error == ERR_TIMEOUT) d = true;
+            done = d;
+        }
+        done = __builtin_amdgcn_readfirstlane((int)done) != 0;
+        // (done: one more poll round publishes this round's counters behind its drain, then the loop ends)
+    }
+#undef PEND
+
+    // ---------------- statistics
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
+    for (int i = lane; i < kHistBins; i += 64) P.stats[lr].hist[i] = S.hist[i];
+    if (lane < 8) { P.stats[lr].prof[lane] = 0; P.stats[lr].dbg[lane] = 0; }
+    if (lane == 0) {
+        RankStats& st = P.stats[lr];
+        st.bcast_delivered = S.bcast_delivered;
+        st.originated = S.originated;
+        st.dec_delivered = S.dec_delivered;
+        st.dec_approved = S.dec_approved;
+        st.actions = S.actions;
+        st.judge_calls = S.judge_calls;
+        st.own_decided = S.own_decided;
+        st.own_approved = S.own_approved;
+        st.proposals_recv = S.proposals_recv;
+        st.iterations = n_iter;
+        st.busy_iterations = n_busy;
+        st.stalls = 0;
+        st.unmarked_slots = S.stale;
+        st.log_count = S.log_count;
+        st.t_start = t_start;
+        st.t_end = now_ticks();
+        st.error = S.error;
+        st.error_aux = S.error_aux;
+    }
+}
+
+}  // namespace rlo
+
+// C-ABI launch shims (rlo_world.cpp): one 64-thread workgroup per local rank, the pending table in dynamic LDS
+// (dyn_lds bytes) or, with Params.pend_hbm, in HBM (the PH instantiation)
+template <bool PH>
+static hipError_t hop_grant(size_t dyn_lds) {
+    static size_t granted = 0;
+    if (dyn_lds > granted) {
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_hop_kernel<PH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)dyn_lds);
+        if (e != hipSuccess) return e;
+        granted = dyn_lds;
+    }
+    return hipSuccess;
+}
+
+extern "C" hipError_t rlo_launch_hop(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
+    const bool ph = p->pend_hbm != nullptr;
+    hipError_t e = ph ? hop_grant<true>(dyn_lds) : hop_grant<false>(dyn_lds);
+    if (e != hipSuccess) return e;
+    if (ph) hipLaunchKernelGGL((rlo::rlo_hop_kernel<true>), dim3(blocks), dim3(64), dyn_lds, stream, *p);
+    else hipLaunchKernelGGL((rlo::rlo_hop_kernel<false>), dim3(blocks), dim3(64), dyn_lds, stream, *p);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rlo_occupancy_hop(int* blocks, size_t dyn_lds, int ph) {
+    hipError_t e = ph ? hop_grant<true>(dyn_lds) : hop_grant<false>(dyn_lds);
+    if (e != hipSuccess) return e;
+    return ph ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<true>, 64, dyn_lds)
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<false>, 64, dyn_lds);
+}

@@ -31,6 +31,8 @@ extern "C" hipError_t rlo_launch_progress(const rlo::Params* p, int blocks, size
 extern "C" size_t rlo_kernel_static_lds(int variant);
 extern "C" hipError_t rlo_occupancy(int* blocks, size_t dyn_lds, int variant);
 extern "C" hipError_t rlo_occupancy_ll(int* blocks, size_t dyn_lds, int variant);
+extern "C" hipError_t rlo_launch_hop(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream);
+extern "C" hipError_t rlo_occupancy_hop(int* blocks, size_t dyn_lds, int ph);
 
 static_assert(sizeof(rlo_rank_stats_t) == sizeof(rlo::RankStats), "stats ABI");
 static_assert(sizeof(rlo_log_rec_t) == sizeof(rlo::LogRec), "log ABI");
@@ -400,6 +402,7 @@ struct rlo_world {
     uint32_t pk_stride = 0;         // pickup payload stride (rlo_device.hpp pk_payload_stride)
     uint32_t pk_epoch = 0;          // pickup-tag epoch of the latest host-mode launch (pk_tag)
     bool pk_dirty = false;          // a host-mode launch may have written pickup records / payloads since the last reset
+    bool last_hop = false;          // the latest launch ran the hop kernel (rlo_hop.hip), not the progress kernel
     uint32_t cmd_cap = 0, pk_cap = 0;
     std::vector<uint64_t> cmd_tail, pk_head;  // host-side copies of the counters it owns
     // shared host service (rlo_host_share): h_ctl / h_ev / h_evp live in a POSIX shared-memory
@@ -1324,6 +1327,7 @@ int rlo_world_query(const rlo_world_t* w, rlo_world_info_t* o) {
     o->ll_ok = w->ll_ok ? 1u : 0u;
     o->pend_hbm = w->pend_hbm ? 1u : 0u;
     o->dyn_lds = (uint32_t)w->dyn_lds;
+    o->last_kernel = w->last_hop ? 1u : 0u;
     o->static_lds = (uint32_t)rlo_kernel_static_lds(w->variant);
     return RLO_OK;
 }
@@ -1489,6 +1493,7 @@ int rlo_program_latency(rlo_world_t* w, uint32_t rounds, uint32_t len, uint64_t 
     P.len = len;
     P.seed = seed;
     P.lat_rounds = rounds;
+    P.hop_chunks = (rlo::kHdr + len + 15u) / 16u;
     P.lat_origin = w->d_lat_origin.p;
     P.lat_count = w->d_lat_count.p;
     P.lat_out = w->d_lat_out.p;
@@ -1594,6 +1599,7 @@ int rlo_program_iar(rlo_world_t* w, const rlo_iar_cfg_t* cfg, int64_t nprop, con
     uint32_t max_msg = 23;  // a decision's PBuf (:908-917); a proposal's is 16 B + its data
     for (int64_t i = 0; i < nprop; i++) max_msg = std::max<uint32_t>(max_msg, 16u + data_len[i]);
     P.mode = rlo::MODE_IAR | ((cfg->flags & RLO_FLAG_PROF) ? rlo::MODE_PROF : 0u) | ll_mode(w, max_msg);
+    P.hop_chunks = (rlo::kHdr + max_msg + 15u) / 16u;
     {
         const int jrc = set_judge(w, cfg);
         if (jrc) return jrc;
@@ -1949,6 +1955,28 @@ int rlo_reset(rlo_world_t* w, void* stream) {
     return RLO_OK;
 }
 
+// The hop kernel (rlo_hop.hip: one wave per rank, one message at a time) runs the latency and iar programs with
+// doorbells (device judges, no host service, no bulk messages) whenever every rank-wave of the part is co-resident;
+// the diagnostics modes that instrument the progress kernel's doorbell pass (phase profile, timeline, hop profile, the
+// no-fast-path A/B) keep that kernel, and so does RLO_NO_HOP (diagnostics build: A/B of the two kernels)
+static size_t hop_lds(const rlo_world* w) {
+    return w->P.pend_hbm ? 0 : (size_t)16u * (uint32_t)w->L.n * w->P.pend_slots;
+}
+static bool hop_eligible(rlo_world* w) {
+    const rlo::Params& P = w->P;
+    if (!(P.mode & rlo::MODE_LL) || !(P.mode & (rlo::MODE_LAT | rlo::MODE_IAR))) return false;
+    if (P.mode & (rlo::MODE_HOST | rlo::MODE_STORM | rlo::MODE_PROF | rlo::MODE_TL | rlo::MODE_HOPPROF | rlo::MODE_NOFAST))
+        return false;
+    if (w->L.bulk_max || P.hop_chunks == 0 || P.hop_chunks > 64u) return false;
+    static const bool off = diag_env("RLO_NO_HOP") != nullptr;
+    if (off) return false;
+    const size_t lds = hop_lds(w);
+    if (lds > 64u * 1024u) return false;
+    int b = 0;
+    if (rlo_occupancy_hop(&b, lds, P.pend_hbm ? 1 : 0) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return b > 0 && (int64_t)b * w->cus >= (int64_t)w->nl;
+}
+
 int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     if (!w) return RLO_E_INVAL;
     if (!w->connected) return RLO_E_NOTCONNECTED;
@@ -2005,7 +2033,14 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     static const bool hdiag = diag_env("RLO_HOST_DIAG") != nullptr;  // diagnostic: command-wait counters
     if (hdiag) w->P.mode |= rlo::MODE_HDIAG;
     else w->P.mode &= ~rlo::MODE_HDIAG;
-    hipError_t e = rlo_launch_progress(&w->P, w->nl + (w->L.bulk_max ? (int)w->nmov : 0), w->dyn_lds, s, w->variant);
+    hipError_t e;
+    if (hop_eligible(w)) {
+        w->last_hop = true;
+        e = rlo_launch_hop(&w->P, w->nl, hop_lds(w), s);
+    } else {
+        w->last_hop = false;
+        e = rlo_launch_progress(&w->P, w->nl + (w->L.bulk_max ? (int)w->nmov : 0), w->dyn_lds, s, w->variant);
+    }
     if (e != hipSuccess) { g_last_hip = (int)e; return RLO_E_HIP; }
     HIPCHK(hipEventRecord(w->ev1, s));
     return RLO_OK;

@@ -60,7 +60,7 @@ class WorldInfo(ctypes.Structure):
                 ("bulk_max", ctypes.c_uint64), ("heap_bytes", ctypes.c_uint64), ("proposal_pool", ctypes.c_uint32),
                 ("pull", ctypes.c_uint32), ("nsmall", ctypes.c_uint32), ("stage2_bytes", ctypes.c_uint32),
                 ("ll_ok", ctypes.c_uint32), ("pend_hbm", ctypes.c_uint32), ("dyn_lds", ctypes.c_uint32),
-                ("static_lds", ctypes.c_uint32)]
+                ("static_lds", ctypes.c_uint32), ("last_kernel", ctypes.c_uint32), ("info_pad", ctypes.c_uint32)]
 
 
 class PlanCfg(ctypes.Structure):

@@ -67,6 +67,11 @@ class World:
         self.rank_begin, self.rank_end = self.info["rank_begin"], self.info["rank_end"]
         self.n_local = self.rank_end - self.rank_begin
 
+    def info_now(self):
+        """rlo_world_query now (self.info is the answer at creation / connection): e.g. last_kernel after a launch"""
+        self._query()
+        return self.info
+
     def export(self):
         buf = ctypes.create_string_buffer(L.RLO_PART_BLOB_BYTES)
         check(self.lib.rlo_part_export(self.h, buf, L.RLO_PART_BLOB_BYTES), "rlo_part_export")

@@ -3,8 +3,8 @@
 # bulk rounds (tools/bulk_probe.py), interleaved
 set -o pipefail
 base=${1:-r5base}; tag=${2:-ab}
-mkdir -p gpurun_out/${RLO_OUT:-r5}
-out=gpurun_out/${RLO_OUT:-r5}/ab_$tag.txt
+mkdir -p gpurun_out/${RLO_OUT:-r6}
+out=gpurun_out/${RLO_OUT:-r6}/ab_$tag.txt
 : > $out
 timeout -k 10 300 python3 -u tools/lat_ab.py $base 8 256 >> $out 2>&1 || exit $?
 for rep in 1 2; do

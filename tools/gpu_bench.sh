@@ -1,10 +1,10 @@
 # the default bench line (python bench.py), stderr progress kept
 set -o pipefail
 tag=${1:-bench}
-mkdir -p gpurun_out/${RLO_OUT:-r5}
-timeout -k 10 900 python3 -u bench.py > gpurun_out/${RLO_OUT:-r5}/$tag.json 2> gpurun_out/${RLO_OUT:-r5}/$tag.err || { tail -20 gpurun_out/${RLO_OUT:-r5}/$tag.err; exit 1; }
-tail -3 gpurun_out/${RLO_OUT:-r5}/$tag.err
-python3 - gpurun_out/${RLO_OUT:-r5}/$tag.json <<'PY'
+mkdir -p gpurun_out/${RLO_OUT:-r6}
+timeout -k 10 900 python3 -u bench.py > gpurun_out/${RLO_OUT:-r6}/$tag.json 2> gpurun_out/${RLO_OUT:-r6}/$tag.err || { tail -20 gpurun_out/${RLO_OUT:-r6}/$tag.err; exit 1; }
+tail -3 gpurun_out/${RLO_OUT:-r6}/$tag.err
+python3 - gpurun_out/${RLO_OUT:-r6}/$tag.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 keys = ["value", "ms_per_step", "p50_us", "p99_us", "decisions_per_s", "decisions_per_s_pend_hbm", "pend_hbm_cost",

@@ -2,7 +2,7 @@
 # (tools/hop_prof.py --host), then the drop-in's lat / iar / iardj legs at 8 ranks, whose leader prints the part's
 # pass profile and why passes handed over to the full iteration
 set -o pipefail
-O=gpurun_out/${RLO_OUT:-r5}/hostprof; mkdir -p $O
+O=gpurun_out/${RLO_OUT:-r6}/hostprof; mkdir -p $O
 timeout -k 10 200 python3 -u tools/hop_prof.py 8 --host 2>&1 | tee $O/hop_host.txt || exit 1
 B=rootless-coll-mpi-ops_amd/lib_diag/rlo_api_bench
 for leg in "lat 500 64" "iar 2000" "iardj 2000"; do

@@ -1,7 +1,7 @@
 # the drop-in's legs: api_bench lat / iar under RLO_TRACE_DIR, split by tools/dropin_legs.py
 set -o pipefail
 tag=${1:-legs}
-O=gpurun_out/${RLO_OUT:-r5}/$tag
+O=gpurun_out/${RLO_OUT:-r6}/$tag
 mkdir -p $O
 B=${BENCH:-rootless-coll-mpi-ops_amd/lib/rlo_api_bench}
 export RLO_NUMA_BIND=all
