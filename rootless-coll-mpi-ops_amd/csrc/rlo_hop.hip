@@ -117,6 +117,8 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     // this lane's out-ring (lane oi < nout): its base in the child's part and the child's doorbell for the edge
     const uint64_t obase_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;
     const uint64_t bbase_r = lane < nout ? t.out_bell[lane >> 1] : 0ull;
+    // MODE_TL (diagnostics build): this round's poll issued / returned, counters published, ring loop entered
+    uint32_t tl_iss = 0, tl_back = 0, tl_pub = 0, tl_loop = 0;
     uint64_t n_iter = 0, n_busy = 0, idle_since = 0;
     uint32_t idle_n = 0;
     bool done = false;
@@ -180,6 +182,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     // false when it cannot go now (an out-ring it needs is full, or its pending entry still holds the previous
     // proposal of that pool slot): nothing changed, the ring waits
     auto take = [&](u32x4 v, int g, uint64_t out_head_r) -> bool {
+        const uint32_t tl_take = TL_ON(P) ? (uint32_t)now_ticks() : 0u;
         const uint32_t q = (uint32_t)lane;
         const int from = uni(t.in_src[g >> 1]);
         const uint32_t w0 = rdl32(v.x, 0), id = rdl32(v.y, 0), w2 = rdl32(v.z, 0), t0 = rdl32(v.w, 0);
@@ -217,7 +220,17 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         const uint32_t kids = judge == 1 ? kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane) : 0u;
         const uint32_t need = need_of_u(kids, origin, sll, sl_r, lane);
         if (full_of(need, out_head_r)) return false;
+        if (TL_ON(P) && tag == TAG_BCAST && lane == 0) {  // the hop's clocks (tools/round_timeline.py)
+            tl_put(P, id, TLC_ARRIVE, lr, tl_take);
+            tl_put(P, id, TLC_ISSUE, lr, tl_iss);
+            tl_put(P, id, TLC_PASS, lr, tl_back);
+            tl_put(P, id, TLC_FWD, lr, tl_pub);
+            tl_put(P, id, TLC_NEXT, lr, tl_loop);
+            tl_put(P, id, TLC_P1, lr, (uint32_t)now_ticks());
+            tl_parent(P, id, lr, from);
+        }
         forward(v, nch, need);  // before the effects, as the reference forwards before queueing the pickup (:583-589)
+        if (TL_ON(P) && tag == TAG_BCAST && lane == 0) tl_put(P, id, TLC_P2, lr, (uint32_t)now_ticks());
         if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
         if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
             uint32_t li = ~0u;
@@ -237,11 +250,13 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : atomicAdd(&P.lat_count[id], 1u);
                 if (old + 1u == (uint32_t)(P.n - 1)) {
+                    tl_mark(P, id, TL_ROUND);
                     P.lat_out[id] = (uint64_t)((uint32_t)now_ticks() - t0);
                     if (sys) __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     else __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            if (TL_ON(P) && lane == 0) tl_mark(P, id, kTlGlobal + P.n_local + (uint32_t)lr);
         } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
             if (lane == 0) {
                 S.proposals_recv++;
@@ -300,23 +315,21 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
 
     for (;;) {
         // ---------------- poll: counters, doorbells, error word, round word -- one round trip
-        uint64_t in_tail_r = 0, out_head_r = 0, vin_tail_r = 0, vout_head_r = 0;
-        uint32_t errf = 0, latr = 0;
-        if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
-        if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
-        if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
-        if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
-        if (lane == 0) errf = poll32(P.error_flag);
-        if (lat && lane == 1) latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : poll32(P.lat_round);
+        // (branch-free: rlo_kernel_common.hpp kOob)
+        if (TL_ON(P)) tl_iss = (uint32_t)now_ticks();
+        const uint64_t in_tail_r = ld64_sc1(rc, lane < n_in2 ? (inbox + (uint32_t)lane) * 8u : kOob);
+        const uint64_t vin_tail_r = ld64_sc1(rc, lane < sll ? (inbox + (uint32_t)(n_in2 + lane)) * 8u : kOob);
+        const uint64_t out_head_r = ld64_sc1(rc, lane < nout ? (outbox + (uint32_t)lane) * 8u : kOob);
+        const uint64_t vout_head_r = ld64_sc1(rc, lane < n_in ? (outbox + (uint32_t)(nout + lane)) * 8u : kOob);
+        const uint32_t errf = ld32_sc1(rc, 0u);  // (the part's error word is its ctrl word 0)
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
-        u32x4 ba = {0u, 0u, 0u, 0u}, bb = {0u, 0u, 0u, 0u}, vb = {0u, 0u, 0u, 0u};
-        if ((int)bk < n_in) {
-            const uint32_t o = (in_bell + bk * kBellWords) * 8u + 32u * bq;
-            ba = ld_sc1(rc, o);
-            bb = ld_sc1(rc, o + 16u);
-        }
-        if (lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (also the previous round's stores: in-order counter)
+        const uint32_t bo = (int)bk < n_in ? (in_bell + bk * kBellWords) * 8u + 32u * bq : kOob;
+        const u32x4 ba = ld_sc1(rc, bo), bb = ld_sc1(rc, bo == kOob ? kOob : bo + 16u);
+        const u32x4 vb = ld_sc1(rc, lane < sll ? (vin_bell + 2u * (uint32_t)lane) * 8u : kOob);
+        // the latency round word (part 0's when sharded; system scope covers both)
+        const uint32_t latr = __hip_atomic_load(lat ? P.lat_round : P.error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler (also the previous round's stores)
+        if (TL_ON(P)) tl_back = (uint32_t)now_ticks();
         n_iter++;
         // ---- the previous round's counters: its stores have drained
         if (lane < nout && out_tail_r != pub_out) { pub_out = out_tail_r; pub64(t.out_tail[lane >> 1][lane & 1], out_tail_r, sys); }
@@ -327,10 +340,11 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             if (vt != pub_vout) { pub_vout = vt; pub64(t.vout_tail[lane], vt, sys); }
             S.vout_head[lane] = vout_head_r;
         }
+        if (TL_ON(P)) tl_pub = (uint32_t)now_ticks();
         if (done) break;  // (the final counters are out)
         if (__builtin_amdgcn_readfirstlane(errf) != 0) break;  // another rank failed: stop everyone
         if (lat && me == 0) {  // world rank 0 observes round completions on its own clock
-            const uint32_t done_r = rdl32(latr, 1), seen = S.lat_seen;
+            const uint32_t done_r = latr, seen = S.lat_seen;
             if (done_r > seen) {
                 const uint64_t tn = now_ticks();
                 for (uint32_t k = seen + (uint32_t)lane; k < done_r && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
@@ -370,7 +384,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         const uint32_t vbase = wave_excl_scan(vwant, &vtot);
         const uint32_t vtake = vbase >= 64u ? 0u : min(vwant, 64u - vbase);  // lane j: vote slots loaded
         if (mtot | vtot) {
-            u32x4 lm[kHopLoads], lw = {0u, 0u, 0u, 0u};
+            u32x4 lm[kHopLoads], lw;
 #pragma unroll
             for (uint32_t u = 0; u < kHopLoads; u++) {  // item u 64 + lane = (message m, chunk qq)
                 lm[u] = u32x4{0u, 0u, 0u, 0u};
@@ -387,7 +401,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                         any = true;
                     }
                 }
-                if (any) lm[u] = ld_sc1(rf, src);
+                lm[u] = ld_sc1(rf, any ? src : kOob);  // (branch-free: rlo_kernel_common.hpp kOob)
             }
             {
                 bool any = false;
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                         any = true;
                     }
                 }
-                if (any) lw = ld_sc1(rv, src);
+                lw = ld_sc1(rv, any ? src : kOob);
             }
 #pragma unroll
             for (uint32_t u = 0; u < kHopLoads; u++)
@@ -429,6 +443,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             progressed = true;
         }
 
+        if (TL_ON(P)) tl_loop = (uint32_t)now_ticks();
         // ---------------- ring messages: per in-ring its head (bell or slot), then its loaded slots, in order
         for (uint64_t gs = __ballot(rhit || mtake); gs; gs &= gs - 1) {
             const int g = __builtin_ctzll(gs);
@@ -489,9 +504,10 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 progressed = true;
             }
         }
-        if (lat && S.lat_own_next != 0xffffffffu && rdl32(latr, 1) == S.lat_own_next &&
+        if (lat && S.lat_own_next != 0xffffffffu && latr == S.lat_own_next &&
             originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), S.lat_own_next, P.len, 0u, out_head_r)) {
             if (lane == 0) {
+                tl_mark(P, S.lat_own_next, TL_ORIGIN);
                 S.originated++;
                 const uint32_t np = S.lat_pos + 1u;
                 S.lat_pos = np;

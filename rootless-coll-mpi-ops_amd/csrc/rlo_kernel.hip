@@ -1415,13 +1415,14 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             const uint32_t vj = (uint32_t)lane / kLLVotes, vi = (uint32_t)lane % kLLVotes;
             const uint32_t nvj = (uint32_t)__shfl((int)nv, (int)vj), vhj = (uint32_t)__shfl((int)(uint32_t)vin_head_r, (int)vj);
             const uint32_t vdat = (int)vj < sll ? t.vin_data[vj] : 0u;
-            u32x4 lv = {0u, 0u, 0u, 0u}, lw = {0u, 0u, 0u, 0u};
-            if (gsel >= 0 && q < lcap) lv = ld_sc1(rf, dsel + (hsel & fcap_m) * P.fwd_stride + 16u * q);
-            if ((int)vj < sll && vi < nvj) lw = ld_sc1(rv, vdat + ((vhj + vi) & vcap_m) * kVoteSlot);
+            // (branch-free, kOob: the three loads leave back to back, one wait)
+            const u32x4 lv = ld_sc1(rf, gsel >= 0 && q < lcap ? dsel + (hsel & fcap_m) * P.fwd_stride + 16u * q : kOob);
+            const u32x4 lw = ld_sc1(rv, (int)vj < sll && vi < nvj ? vdat + ((vhj + vi) & vcap_m) * kVoteSlot : kOob);
             // host commands: lane 8 s + q chunk q of command s, from the command ring in host memory
             // (system-scope loads behind the tail poll, as the full path's command DMA)
             u32x4 lc = {0u, 0u, 0u, 0u};
-            if (!cbell && sl < ncmd && q < lcap) lc = ld_sys(rh, (uint32_t)((S.hin_head + sl) & hcap_m) * P.fwd_stride + 16u * q);
+            if (ncmd && !cbell)
+                lc = ld_sys(rh, sl < ncmd && q < lcap ? (uint32_t)((S.hin_head + sl) & hcap_m) * P.fwd_stride + 16u * q : kOob);
             *reinterpret_cast<u32x4*>(stage + kLLRing + 16u * (uint32_t)lane) = lv;
             *reinterpret_cast<u32x4*>(stage + kLLVote + 16u * (uint32_t)lane) = lw;
             if (ncmd && !cbell) *reinterpret_cast<u32x4*>(stage + kLLCmd + 16u * (uint32_t)lane) = lc;
@@ -1738,32 +1739,34 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     S.tl_clk[0] = (uint32_t)now_ticks();
                     if (BULK && S.tl_bfid) { tl_put(P, S.tl_bfid - 1u, TLC_NEXT, lr, S.tl_clk[0]); S.tl_bfid = 0; }
                 }
-                if (lane < n_in2) in_tail_r = poll64(&P.ctrl[inbox + lane]);
-                if (lane < sll) vin_tail_r = poll64(&P.ctrl[inbox + n_in2 + lane]);
-                if (lane < nout) out_head_r = poll64(&P.ctrl[outbox + lane]);
-                if (lane < n_in) vout_head_r = poll64(&P.ctrl[outbox + nout + lane]);
-                if (lane == 0) errf = poll32(P.error_flag);
-                if constexpr (BULK) {
-                    if (lane < (int)bsl) {
-                        uint64_t* d = reinterpret_cast<uint64_t*>(uni64(S.b.dbase) + (uint64_t)lane * kBulkLine);
-                        dnw = sys ? __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                  : __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
+                // branch-free: every lane issues every load of the poll (rlo_kernel_common.hpp kOob), one wait for all.
+                // The doorbells first (LL instantiations; a launch without bells reads kOob): nothing that uses a loaded
+                // value may stand between the loads, or the compiler waits there
+                [[maybe_unused]] u32x4 ba, bb, vb;
+                if constexpr (LL) {
+                    const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
+                    const uint32_t bo = llm && (int)bk < n_in ? (in_bell + bk * kBellWords) * 8u + 32u * bq : kOob;
+                    ba = ld_sc1(rc, bo);
+                    bb = ld_sc1(rc, bo == kOob ? kOob : bo + 16u);
+                    vb = ld_sc1(rc, llm && lane < sll ? (vin_bell + 2u * (uint32_t)lane) * 8u : kOob);
                 }
-                if ((PMODE(MODE_LAT)) && lane == 1)  // the round in progress (part 0's word when sharded)
-                    latr = sys ? __hip_atomic_load(P.lat_round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                               : poll32(P.lat_round);
-                if ((PMODE(MODE_LAT)) && me == 0) lat_observe(latr);  // every spin: doorbells keep wave 0 here
+                in_tail_r = ld64_sc1(rc, lane < n_in2 ? (inbox + (uint32_t)lane) * 8u : kOob);
+                vin_tail_r = ld64_sc1(rc, lane < sll ? (inbox + (uint32_t)(n_in2 + lane)) * 8u : kOob);
+                out_head_r = ld64_sc1(rc, lane < nout ? (outbox + (uint32_t)lane) * 8u : kOob);
+                vout_head_r = ld64_sc1(rc, lane < n_in ? (outbox + (uint32_t)(nout + lane)) * 8u : kOob);
+                errf = ld32_sc1(rc, 0u);  // (the part's error word is its ctrl word 0)
+                if constexpr (BULK) {  // my heap slots' release counts (lane s < B), system scope (covers agent scope)
+                    const __amdgpu_buffer_rsrc_t rd = mk_rsrc(reinterpret_cast<void*>(uni64(S.b.dbase)), bsl * kBulkLine);
+                    dnw = ld64_sys(rd, lane < (int)bsl ? (uint32_t)lane * kBulkLine : kOob);
+                }
+                // the round in progress (part 0's word when sharded; system scope covers both), every lane; a launch of
+                // another program reads its own error word there (never a round: it stops on it anyway)
+                if constexpr ((PM & MODE_LAT) != 0u)
+                    latr = __hip_atomic_load((PMODE(MODE_LAT)) ? P.lat_round : P.error_flag, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
                 if constexpr (LL) {
                     if (llm) {  // my doorbells beside the counters: lane (k, q) chunk q of in-edge k's, lane j child j's vote
-                        const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
-                        u32x4 ba = {0u, 0u, 0u, 0u}, bb = {0u, 0u, 0u, 0u}, vb = {0u, 0u, 0u, 0u};
-                        if ((int)bk < n_in) {
-                            const uint32_t o = (in_bell + bk * kBellWords) * 8u + 32u * bq;
-                            ba = ld_sc1(rc, o);
-                            bb = ld_sc1(rc, o + 16u);
-                        }
-                        if (lane < sll) vb = ld_sc1(rc, (vin_bell + 2u * (uint32_t)lane) * 8u);
+                        if ((PMODE(MODE_LAT)) && me == 0) lat_observe(latr);  // every spin: doorbells keep wave 0 here
                         bool need_full = false;
                         const uint32_t nb0 = nact_of(S.b);
                         const uint32_t nll = ll_pass(ba, bb, vb, in_tail_r, vin_tail_r, out_head_r, hpoll, latr, errf, need_full);
@@ -1780,6 +1783,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                         }
                     }
                 }
+                if ((PMODE(MODE_LAT)) && me == 0 && !(LL && llm)) lat_observe(latr);  // (with bells: above)
                 if (!idle_prev || sp >= kIdleSpin) { SPIN_WHY(idle_prev ? 1 : 0); break; }
                 // pending receptions: their completion counts are polled here, every spin, and the first complete
                 // one ends the spin (phase C delivers it) -- not a full iteration per poll.  Queued job posts (a

@@ -69,6 +69,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(void* base, uint32_t b
 __device__ __forceinline__ u32x4 ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1);
 }
+// Branch-free polls.  A poll written as `x = 0; if (lane < k) x = load(...)` makes the compiler copy the loaded value
+// into x's register at the join -- behind a vmcnt wait -- so a poll of several such loads became two or three round
+// trips in a row (counters, then bells, then vote bells: rlo_kernel.isa, VERDICT r5 "next" 1).  Here every lane
+// issues the load; a lane with nothing to poll reads at kOob, past the resource's end, where the hardware's range
+// check returns zeros.  The loads of a poll then leave back to back and one wait covers them all
+constexpr uint32_t kOob = 0xFFFFFFF0u;
+__device__ __forceinline__ uint64_t ld64_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1);
+    return (uint64_t)v.x | ((uint64_t)v.y << 32);
+}
+__device__ __forceinline__ uint64_t ld64_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) {  // system scope (sc0 sc1)
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1 | 1);
+    return (uint64_t)v.x | ((uint64_t)v.y << 32);
+}
+__device__ __forceinline__ uint32_t ld32_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kAuxSc1);
+}
 __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1);
 }

@@ -1957,16 +1957,18 @@ int rlo_reset(rlo_world_t* w, void* stream) {
 
 // The hop kernel (rlo_hop.hip: one wave per rank, one message at a time) runs the latency and iar programs with
 // doorbells (device judges, no host service, no bulk messages) whenever every rank-wave of the part is co-resident;
-// the diagnostics modes that instrument the progress kernel's doorbell pass (phase profile, timeline, hop profile, the
-// no-fast-path A/B) keep that kernel, and so does RLO_NO_HOP (diagnostics build: A/B of the two kernels)
+// the diagnostics modes that instrument the progress kernel's doorbell pass (phase profile, hop profile, the no-fast-path
+// A/B) keep that kernel, and so does RLO_NO_HOP (diagnostics build: A/B of the two kernels)
 static size_t hop_lds(const rlo_world* w) {
     return w->P.pend_hbm ? 0 : (size_t)16u * (uint32_t)w->L.n * w->P.pend_slots;
 }
 static bool hop_eligible(rlo_world* w) {
     const rlo::Params& P = w->P;
     if (!(P.mode & rlo::MODE_LL) || !(P.mode & (rlo::MODE_LAT | rlo::MODE_IAR))) return false;
-    if (P.mode & (rlo::MODE_HOST | rlo::MODE_STORM | rlo::MODE_PROF | rlo::MODE_TL | rlo::MODE_HOPPROF | rlo::MODE_NOFAST))
-        return false;
+    if (P.mode & (rlo::MODE_HOST | rlo::MODE_STORM | rlo::MODE_PROF | rlo::MODE_HOPPROF | rlo::MODE_NOFAST)) return false;
+    // the timeline (diagnostics build) is the hop kernel's too unless RLO_TL_FULL asks for the progress kernel's
+    static const bool tl_full = diag_env("RLO_TL_FULL") != nullptr;
+    if ((P.mode & rlo::MODE_TL) && tl_full) return false;
     if (w->L.bulk_max || P.hop_chunks == 0 || P.hop_chunks > 64u) return false;
     static const bool off = diag_env("RLO_NO_HOP") != nullptr;
     if (off) return false;

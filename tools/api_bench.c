@@ -307,6 +307,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[1], "iarpool")) iarpool(atoi(argv[2]));
 #endif
     fflush(g_out);
+#ifdef RLO_HAVE_DEVICE_JUDGE
+    /* the drop-in's extension: every engine is gone -- the device memory the engines pooled goes back (world-wide) */
+    if (RLO_device_memory_release(MPI_COMM_WORLD) != 0 && g_rank == 0) fprintf(stderr, "api_bench: device memory release refused\n");
+#endif
     MPI_Finalize();
     return 0;
 }
