@@ -104,10 +104,16 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t* dst, ui
 __device__ __forceinline__ uint64_t poll64(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Stores through addresses the kernel loads from memory (the topology's remote counters and bells, the vote rings) are
+// made through GLOBAL pointers: a generic (flat) store counts in lgkmcnt as well as vmcnt, so every later LDS wait of
+// the wave -- s_waitcnt lgkmcnt(0) before the next LDS read -- waited for the store to reach memory (a counter publish
+// or a vote held the next hop's LDS work up for a whole memory round trip)
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ gu64* gptr64(uint64_t addr) { return (gu64*)addr; }
 // a counter store into a (possibly peer) part: agent scope inside one GPU, system scope when
 // the world spans GPUs (the store then crosses xGMI into the peer's HBM)
 __device__ __forceinline__ void pub64(uint64_t addr, uint64_t v, bool sys) {
-    uint64_t* p = reinterpret_cast<uint64_t*>(addr);
+    gu64* p = gptr64(addr);
     if (sys) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -121,7 +127,7 @@ __device__ __forceinline__ void st_sys16(void* p, u32x4 v) {
     // two 8-B system-scope stores (sc0 sc1: write-through to host memory / visible to every XCD).
     // Not inline asm: the compiler cannot see an asm store's pending reads of its address and data
     // registers and may reuse them at once -- job records were seen with a neighbour's words in them
-    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    gu64* q = gptr64(reinterpret_cast<uint64_t>(p));  // (global, not flat: see gu64)
     __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -170,7 +176,7 @@ __device__ __forceinline__ void spoll_cmd(const uint8_t* slot, const uint64_t* w
         : "memory");
 }
 __device__ __forceinline__ void pub64_sys(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(gptr64(reinterpret_cast<uint64_t>(p)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint32_t poll32(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -477,7 +483,7 @@ __device__ __forceinline__ void emit_vote(SH& S, const Params& P, int me, uint32
     }
     if (LLB && (P.mode & MODE_LL)) {  // {origin | pseq << 16 | vote << 24, T, pid, T}: every 8-B half tagged
         const uint32_t T = bell_tag(p);
-        uint64_t* b = reinterpret_cast<uint64_t*>(S.t.vout_bell[k]);
+        gu64* b = gptr64(S.t.vout_bell[k]);
         const uint64_t w0 = (uint64_t)(((uint32_t)origin & 0xffffu) | ((pseq & 0xffu) << 16) | ((uint32_t)(vote & 0xff) << 24)) |
                             ((uint64_t)T << 32);
         const uint64_t w1 = (uint64_t)(uint32_t)pid | ((uint64_t)T << 32);
@@ -491,7 +497,7 @@ __device__ __forceinline__ void emit_vote(SH& S, const Params& P, int me, uint32
     }
     const uint64_t lo = (uint64_t)((uint32_t)origin | ((uint32_t)(vote & 0xff) << 24)) | ((uint64_t)(uint32_t)pid << 32);
     const uint64_t hi = (uint64_t)(pseq & 0xffu) | ((uint64_t)(uint32_t)me << 32);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(S.t.vout_ring[k] + (uint64_t)(p & (P.vote_cap - 1)) * kVoteSlot);
+    gu64* dst = gptr64(S.t.vout_ring[k] + (uint64_t)(p & (P.vote_cap - 1)) * kVoteSlot);
     if (P.sys_scope) {
         __hip_atomic_store(dst, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(dst + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
