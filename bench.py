@@ -22,6 +22,7 @@ import argparse
 import json
 import os
 import subprocess
+import resource
 import sys
 import tempfile
 import time
@@ -230,12 +231,23 @@ def _run_sampled(cmd, timeout_s, env=None, period=0.05):
 
     th = threading.Thread(target=sample, daemon=True)
     t0 = cpu_throttle()
+    ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
+    w0 = time.perf_counter()
     th.start()
     try:
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=timeout_s + 20, env=env)
     finally:
         stop.set()
         th.join(timeout=2)
+    wall = time.perf_counter() - w0
+    ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+    # core accounting: CPU seconds of every process of the run (mpiexec, its proxies, the rank processes and all
+    # their threads: waited-for descendants accumulate into RUSAGE_CHILDREN), and that over the run's wall time =
+    # the cores the run kept busy on average (init and teardown included)
+    cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    seen["cpu_s"] = round(cpu, 2)
+    seen["wall_s"] = round(wall, 2)
+    seen["cores_busy"] = round(cpu / wall, 2) if wall > 0 else None
     t1 = cpu_throttle()
     if t0 and t1:
         seen["cpu_throttled_periods"] = t1[0] - t0[0]
@@ -297,6 +309,7 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
                             res["kfd"] = seen
                         else:
                             res["cpu_throttled_ms"] = seen.get("cpu_throttled_ms")
+                        res["cpu"] = {k: seen.get(k) for k in ("cpu_s", "wall_s", "cores_busy")}
                     except Exception as e:  # noqa: BLE001 - informative leg, never fails the bench
                         res = {"error": str(e)[:200]}
                     runs[name].setdefault(leg, []).append(res)
@@ -314,6 +327,7 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
                 med["runs_" + key] = vals
                 if "seconds" in good[0]:
                     med["runs_seconds"] = [x.get("seconds") for x in good]
+                med["runs_cores_busy"] = [x.get("cpu", {}).get("cores_busy") for x in good]
                 if name == "ours":
                     # the census of the GPU our rank processes used: processes holding queues on it at once
                     # (ours: one leader per GPU), the other processes among them, the CPU quota's throttling
@@ -324,6 +338,15 @@ def dropin_api_leg(ranks=(4, 8), timeout_s=150, reps=3):
                 else:
                     med["runs_cpu_throttled_ms"] = [x.get("cpu_throttled_ms") for x in good]
                 rec[name][leg] = med
+        # the CPU each side spent: average cores kept busy over a run (CPU seconds of all the
+        # run's processes and threads / wall), median over the runs, per leg -- ours spins an application thread and a
+        # pump per rank plus the leader's proxy; the reference one pinned core per rank
+        rec["cores_busy"] = {}
+        for name in ("ours", "reference_host_mpi"):
+            for leg, rs in runs[name].items():
+                cb = sorted(x["cpu"]["cores_busy"] for x in rs if x.get("cpu", {}).get("cores_busy") is not None)
+                if cb:
+                    rec["cores_busy"].setdefault(leg, {})[name] = cb[len(cb) // 2]
         try:
             o, f = rec["ours"], rec["reference_host_mpi"]
             rec["ratio_vs_reference"] = {

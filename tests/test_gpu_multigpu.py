@@ -212,10 +212,14 @@ def _check_dump(d, parts):
     assert np.array_equal(c5["bcast_sum"], exp["sum"])
 
 
-def _bench_parts(parts, per, port, limit):
+def _bench_parts(parts, per, port, limit, pool_cap=None):
     """bench.py --gpus `parts` under torch.distributed.run, every part on this GPU (RLO_BENCH_DEVICE): one world of
-    parts x per ranks, every leg's per-rank statistics (--dump) checked against the oracle"""
+    parts x per ranks, every leg's per-rank statistics (--dump) checked against the oracle.  pool_cap: the parts'
+    RLO_POOL_CAP_BYTES (0: every destroyed world's exported regions retire, and bench.py runs the world-wide close
+    after every leg, so each leg exports and imports fresh memory)"""
     env = dict(os.environ, RLO_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    if pool_cap is not None:
+        env["RLO_POOL_CAP_BYTES"] = str(pool_cap)
     dump = tempfile.mkdtemp(prefix="rlo_dump")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(parts), "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"), "--gpus", str(parts), "--steps", "2",
@@ -270,6 +274,14 @@ def test_bench_eight_parts_under_torchrun():
     CU; parts split on multiples of 8); every leg checked against the oracle per world rank"""
     line = _bench_parts(8, 32, 29541, 140)
     assert line["bulk"]["ranks"] == 8 and line["c5_mixed"]["world_ranks"] == 128
+
+
+def test_bench_eight_parts_pool_cap0():
+    """the 8-part rehearsal with the pool's free path -- no free region kept, so every leg's
+    destroyed world retires its exported regions and the world-wide close (rlo_pool_trim: imports dropped, barrier,
+    retired regions freed) runs between legs; the next leg's fresh exports must map right in all 8 parts"""
+    line = _bench_parts(8, 32, 29547, 140, pool_cap=0)
+    assert line["bulk"]["ranks"] == 8
 
 
 def _stale_part(part, tamper, blob_q, blobs_q, out_q, done_q):
