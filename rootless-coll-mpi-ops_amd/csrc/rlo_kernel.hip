@@ -1002,7 +1002,11 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     uint32_t a_it = 0;  // phase-A rounds (every wave counts them alike)
     // ... and wave 2 is the pickup writer (rlo_kernel_common.hpp wq_put): the doorbell pass hands it its stores to host
     // memory through a queue in the stage2 area (free in the spin).  The host-service kernels only
+#ifdef RLO_NO_WQ
+    constexpr bool kWqK = false;  // (A/B build: make AB=nowq ABFLAGS=-DRLO_NO_WQ)
+#else
     constexpr bool kWqK = PM == kPmHost && W == 4;
+#endif
     const bool wqon = kWqK && hpw && P.stage2_bytes >= kWqBytes;
     const uint32_t wqb = wqon ? (uint32_t)(stage2 - dyn_lds) : 0u;  // (its offset in dynamic LDS; 0: no writer)
     // (a doorbell-pass payload too long for the tagged form is plain: the writer drains before the tail covering it)

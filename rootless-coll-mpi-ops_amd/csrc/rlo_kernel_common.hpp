@@ -190,13 +190,17 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 #define TL_ON(P) false
 #endif
 // MODE_TL: the clock of event `ev` of latency round r (rlo_device.hpp kTlGlobal; the latest writer wins)
+// (global pointers: a generic store counts in lgkmcnt, and the next clock read -- s_memrealtime, an lgkmcnt wait --
+// then waited for the store to reach memory: the probes read ~0.8 us of their own stores into the hop)
+typedef __attribute__((address_space(1))) uint32_t gu32;
 __device__ __forceinline__ void tl_mark(const Params& P, uint32_t r, uint32_t ev) {
     if (TL_ON(P) && r < P.tl_rounds)
-        atomicMax(&P.tl[r * (kTlGlobal + kTlCols * P.n_local) + ev], (uint32_t)now_ticks());
+        __hip_atomic_fetch_max((gu32*)(P.tl + r * (kTlGlobal + kTlCols * P.n_local) + ev), (uint32_t)now_ticks(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // MODE_TL: per-rank column col (rlo_device.hpp TlCol) of local rank lr for round r := v
 __device__ __forceinline__ void tl_put(const Params& P, uint32_t r, uint32_t col, int lr, uint32_t v) {
-    if (TL_ON(P) && r < P.tl_rounds) P.tl[r * (kTlGlobal + kTlCols * P.n_local) + kTlGlobal + col * P.n_local + lr] = v;
+    if (TL_ON(P) && r < P.tl_rounds) ((gu32*)P.tl)[r * (kTlGlobal + kTlCols * P.n_local) + kTlGlobal + col * P.n_local + lr] = v;
 }
 __device__ __forceinline__ void tl_parent(const Params& P, uint32_t r, int lr, int from) {
     tl_put(P, r, TLC_PARENT, lr, (uint32_t)(from + 1));

@@ -1970,6 +1970,11 @@ static bool hop_eligible(rlo_world* w) {
     static const bool tl_full = diag_env("RLO_TL_FULL") != nullptr;
     if ((P.mode & rlo::MODE_TL) && tl_full) return false;
     if (w->L.bulk_max || P.hop_chunks == 0 || P.hop_chunks > 64u) return false;
+    // iar: one own proposal in flight per rank in small worlds only.  The hop kernel takes one message at a time per
+    // rank; with many proposals in flight per rank (the pool, or N of them reaching every rank of a large world) the
+    // progress kernel's batches win: decisions/s 4 / 8 ranks 153 K / 148 K vs 113 K / 118 K, but 64 / 256 ranks 158 K /
+    // 140 K vs 254 K / 618 K and pool 16 at 8 ranks 186 K vs 686 K (profiles/r6_hop_ab.txt)
+    if ((P.mode & rlo::MODE_IAR) && (P.own_pool > 1 || w->L.n > 16)) return false;
     static const bool off = diag_env("RLO_NO_HOP") != nullptr;
     if (off) return false;
     const size_t lds = hop_lds(w);

@@ -42,7 +42,9 @@ def main():
                         continue
                     if not os.path.exists(exe):
                         continue
-                    v = run(exe, nr, args, bind=(b == "reference")).get(key)
+                    # ours as bench.py runs it (the application thread on the GPU's NUMA node too)
+                    env = None if b == "reference" else dict(os.environ, RLO_NUMA_BIND="all")
+                    v = run(exe, nr, args, bind=(b == "reference"), env=env).get(key)
                     res.setdefault((nr, leg, b), []).append(v)
     for (nr, leg, b), vs in sorted(res.items()):
         ok = [v for v in vs if isinstance(v, (int, float))]
