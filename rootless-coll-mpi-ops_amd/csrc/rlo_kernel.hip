@@ -140,7 +140,6 @@ struct Shared {
     // the command tail / pickup head it saw last, and the phase-A round wave 0 finished (wave 1 stops)
     uint64_t hp[2];
     uint32_t a_done, cseq;
-    uint32_t wq_tail, wq_head;  // host mode: the pickup writer's queue (rlo_kernel_common.hpp wq_put), entries taken / issued
     uint64_t hd[8], hd_t0;  // MODE_HDIAG counters (host mode)
     // pull worlds: my relay ring (slots taken / released), this iteration's allocations, and the release
     // records: relay count rq_relay[e] is released once every out-ring's consumer passed rq_out[e][oi]
@@ -928,7 +927,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
             S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stalls = S.stale = 0;
             S.error = 0; S.error_aux = 0; S.exit_now = 0; S.progressed = 0; S.hd_t0 = 0; S.hwait = 0;
-            S.hp[0] = 0; S.hp[1] = 0; S.a_done = 0; S.cseq = 0; S.wq_tail = 0; S.wq_head = 0;
+            S.hp[0] = 0; S.hp[1] = 0; S.a_done = 0; S.cseq = 0;
             S.relay_tail = 0; S.relay_rel = 0; S.relay_n = 0; S.ref_any = 0; S.rq_n = 0; S.rq_h = 0; S.relay_free = 0;
             if constexpr (BULK) {
                 S.b.nbact = 0; S.b.ncomp = 0; S.b.bulk_q = 0; S.b.nstable = 0; S.b.npost = 0;
@@ -1000,17 +999,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
     // (4-wave kernels only -- the drop-in's large-slot worlds: the 8-wave doorbell kernel has no registers for it)
     const bool hpw = W == 4 && host && llm && ll_cmds && P.hll != nullptr && !(P.mode & MODE_NOHPW);
     uint32_t a_it = 0;  // phase-A rounds (every wave counts them alike)
-    // ... and wave 2 is the pickup writer (rlo_kernel_common.hpp wq_put): the doorbell pass hands it its stores to host
-    // memory through a queue in the stage2 area (free in the spin).  The host-service kernels only
-#ifdef RLO_NO_WQ
-    constexpr bool kWqK = false;  // (A/B build: make AB=nowq ABFLAGS=-DRLO_NO_WQ)
-#else
-    constexpr bool kWqK = PM == kPmHost && W == 4;
-#endif
-    const bool wqon = kWqK && hpw && P.stage2_bytes >= kWqBytes;
-    const uint32_t wqb = wqon ? (uint32_t)(stage2 - dyn_lds) : 0u;  // (its offset in dynamic LDS; 0: no writer)
-    // (a doorbell-pass payload too long for the tagged form is plain: the writer drains before the tail covering it)
-    const uint32_t wq_tail_kind = P.log_stride >= 32u * (kBellChunks - 1u) ? WQ_ST8 : WQ_ST8_DRAIN;
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);  // my part's ctrl region (my bells)
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     bool ll_prog = false;  // the doorbell pass handled something since the last bookkeeping (progress)
@@ -1072,7 +1060,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         // this event's payload in the pickup ring's tagged form (host-service kernels, when it fits the slot's
         // stride at 2x); else plain, read by the host once the published tail covers it
         const bool tagp = PM == kPmHost && 32u * (fnch - 1u) <= P.log_stride;
-        const uint32_t lwq = from_bell ? wqb : 0u;  // the doorbell pass: host-memory stores by the pickup writer
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) {
             tl_mark(P, fid, kTlGlobal + (uint32_t)lr);
             tl_put(P, fid, TLC_ISSUE, lr, S.tl_clk[0]);
@@ -1104,15 +1091,15 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     PendState* pw = &PEND(forg, fpseq);
                     pw->pid = (int32_t)fid;
                     pw->valid = PS_JREQ;
-                    flog = log_put<PM>(S, P, lr, LOG_JREQ, forg, ffrom, fid, flen, -1, fpseq, false, tagp, lwq);
+                    flog = log_put<PM>(S, P, lr, LOG_JREQ, forg, ffrom, fid, flen, -1, fpseq, false, tagp);
                     atomicAdd(&S.hwait, 1u);
                 }
                 flog = rdl32(flog, 0);
                 if (q >= 1u && q < fnch) {
                     if (tagp) {
-                        pk_payload_tagged(S, P, lr, flog, q, v, lwq);
+                        pk_payload_tagged(S, P, lr, flog, q, v);
                     } else if (16u * q <= P.log_stride) {  // (plain: the host reads it once the tail covers it)
-                        hst16(S, lwq, P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+                        st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
                     }
                 }
                 return kAsked;
@@ -1157,7 +1144,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 atomicAdd(&S.bcast_delivered, 1ull);
                 if (PMODE(MODE_HIST)) atomicAdd(&S.hist[hist_bin((uint32_t)now_ticks() - ft0)], 1u);
                 flog = log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), forg, ffrom, fid, flen, -1,
-                               (uint32_t)now_ticks() - ft0, false, tagp, lwq);
+                               (uint32_t)now_ticks() - ft0, false, tagp);
             }
             flog = rdl32(flog, 0);
             if (q < fnch)
@@ -1173,7 +1160,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                     atomicAdd(&S.judge_calls, 1ull);
                     if (!host) log_put<PM>(S, P, lr, LOG_JUDGE, forg, ffrom, fid, flen, fjudge, 0);
                     else if (!hjudge)  // device judge in host mode: the verdict + PBuf for action() (phase F)
-                        flog = log_put<PM>(S, P, lr, LOG_JUDGED, forg, ffrom, fid, flen, fjudge, fpseq, false, tagp, lwq);
+                        flog = log_put<PM>(S, P, lr, LOG_JUDGED, forg, ffrom, fid, flen, fjudge, fpseq, false, tagp);
                     PendState* ps = &PEND(forg, fpseq);
                     if (!fjudge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                         ps->valid = PS_NONE;
@@ -1217,13 +1204,13 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)fid) {
                 if (fvote != 0) {
                     atomicAdd(&S.actions, 1ull);
-                    log_put<PM>(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8, false, false, lwq);
+                    log_put<PM>(S, P, lr, LOG_ACTION, forg, ffrom, fid, 0, 1, ps->pseq >> 8);
                 }
                 ps->valid = PS_NONE;
             }
             atomicAdd(&S.dec_delivered, 1ull);
             if (fvote != 0) atomicAdd(&S.dec_approved, 1ull);
-            log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0, false, false, lwq);
+            log_put<PM>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), forg, ffrom, fid, 7, fvote, 0);
         }
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_put(P, fid, TLC_P2, lr, (uint32_t)now_ticks());
         HP(6);
@@ -1236,9 +1223,9 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
         if (TL_ON(P) && ftag == TAG_BCAST && lane == 0) tl_mark(P, fid, kTlGlobal + P.n_local + (uint32_t)lr);
         if (flog != ~0u && q >= 1u && q < fnch) {
             if (tagp) {  // the pickup ring's tagged form (no drain and no tail publish stand before the host)
-                pk_payload_tagged(S, P, lr, flog, q, v, lwq);
+                pk_payload_tagged(S, P, lr, flog, q, v);
             } else if (16u * q <= P.log_stride) {  // (the parity log, a host-mode general kernel, a long payload: plain)
-                hst16(S, lwq, P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
+                st_sys16(P.log_payload + ((size_t)lr * P.log_cap + flog) * P.log_stride + 16u * (q - 1u), v);
             }
         }
         if (ftag == TAG_BCAST && (PMODE(MODE_LAT)) && lane == 0) {  // the round's last pickup
@@ -1289,7 +1276,7 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
                 if ((nw & 0xffffu) == S.own_needed) {
                     const int d = (nw >> 16) == 0 ? 1 : 0;
                     if (d && hjudge) {  // final judge(NULL) (:770-775) is the host's callback (phase B1)
-                        log_put<PM>(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k, false, false, wqb);
+                        log_put<PM>(S, P, lr, LOG_OWN_JREQ, me, -1, (uint32_t)pid, 0, -1, k);
                         atomicAdd(&S.hwait, 1u);
                         S.own_state[k] = 3;
                     } else {
@@ -1647,18 +1634,12 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if (vt != PUB_VOUT) { PUB_VOUT = vt; pub64(VTPTR, vt, sys); }
         }
         if (host && lane == 0) {
-            const uint64_t hh = S.hin_head;
-            if (ncmd) {  // the commands taken (the host's sends complete)
-                if (wqb) wq_put(S, wqb, &hctl[kHctlInjHead], WQ_ST8, u32x4{(uint32_t)hh, (uint32_t)(hh >> 32), 0u, 0u});
-                else pub64_sys(&hctl[kHctlInjHead], hh);
-            }
+            if (ncmd) pub64_sys(&hctl[kHctlInjHead], S.hin_head);  // the commands taken (the host's sends complete)
             if (S.ev_n) {
                 S.pk_tail += S.ev_n;
                 S.log_count += S.ev_n;
                 S.ev_n = 0;
-                const uint64_t pt = S.pk_tail;
-                if (wqb) wq_put(S, wqb, &hctl[kHctlPkTail], wq_tail_kind, u32x4{(uint32_t)pt, (uint32_t)(pt >> 32), 0u, 0u});
-                else pub64_sys(&hctl[kHctlPkTail], pt);
+                pub64_sys(&hctl[kHctlPkTail], S.pk_tail);
             }
         }
         HP(8);
@@ -1843,43 +1824,6 @@ __global__ __launch_bounds__(64 * W) void rlo_progress_kernel(Params P) {
             if ((PMODE(MODE_LAT)) && me == 0) lat_observe(latr);
             if ((PMODE(MODE_STORM)) && sched_next + lane < sched_n && (uint32_t)lane < P.window)
                 sid = P.sched_ids[sched_base + sched_next + lane];
-        } else if (kWqK && wqon && w == 2) {
-            // the pickup writer: until wave 0 ends its spin, the stores the doorbell pass queued, in queue order (a
-            // drain before an entry that asks for one: the tail publish that covers plain payloads).  a_done is read
-            // before the tail, so once it shows this round every entry of the round is in the range taken
-            uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.wq_head);
-            for (;;) {
-                const uint32_t ad = (uint32_t)__builtin_amdgcn_readfirstlane((int)*lds_word(&S.a_done));
-                const uint32_t tq = (uint32_t)__builtin_amdgcn_readfirstlane((int)*lds_word(&S.wq_tail));
-                while (h != tq) {
-                    const uint32_t nn = min(tq - h, 64u);
-                    u32x4 e0 = {0u, 0u, 0u, 0u}, e1 = {0u, 0u, 0u, 0u};
-                    if ((uint32_t)lane < nn) {
-                        const __attribute__((address_space(3))) u32x4* e =
-                            (const __attribute__((address_space(3))) u32x4*)(stage2 + ((h + (uint32_t)lane) & (kWq - 1u)) * 32u);
-                        e0 = e[0];
-                        e1 = e[1];
-                    }
-                    const uint32_t kd = e0.x & 7u;
-                    const uint64_t ea = ((uint64_t)e0.x | ((uint64_t)e0.y << 32)) & ~7ull;
-                    const uint64_t dm = __ballot((uint32_t)lane < nn && kd == WQ_ST8_DRAIN);
-                    const uint32_t run = dm ? (uint32_t)__builtin_ctzll(dm) : nn;
-                    if ((uint32_t)lane < run) {
-                        if (kd == WQ_ST16) st_sys16(reinterpret_cast<void*>(ea), e1);
-                        else pub64_sys(reinterpret_cast<uint64_t*>(ea), (uint64_t)e1.x | ((uint64_t)e1.y << 32));
-                    }
-                    h += run;
-                    if (dm) {
-                        VM_DRAIN();
-                        if ((uint32_t)lane == run) pub64_sys(reinterpret_cast<uint64_t*>(ea), (uint64_t)e1.x | ((uint64_t)e1.y << 32));
-                        h++;
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the entries read: their slots may be reused)
-                    if (lane == 0) *lds_word(&S.wq_head) = h;
-                }
-                if (ad == a_it) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
         } else if (hpw && w == 1) {
             // the host poller: until wave 0 ends its spin, the next command's doorbell (16 B to each of lanes 0-15,
             // to LDS at kLLCmdBell: the doorbell pass checks its tags) and the command tail / pickup head (-> S.hp),

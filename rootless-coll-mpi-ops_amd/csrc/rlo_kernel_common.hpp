@@ -413,46 +413,12 @@ __device__ __forceinline__ int judge_eval(const Params& P, __amdgpu_buffer_rsrc_
     return judge_eval_f(P, me, my_mask, pid, [&](uint32_t i) { return ld8_sc1(rf, arg_off + i); }, data_len);
 }
 
-// ---- the pickup writer (host-service kernels with the wave-1 host poller, rlo_kernel.hip): during phase A's spin,
-// wave 0's stores to host memory -- pickup records and tagged payloads, the command head and pickup tail it publishes --
-// go to wave 2 through an LDS queue (the stage2 area, which nothing uses in the spin) instead of being made by wave 0.
-// A PCIe store takes ~1-2 us to complete and vmcnt retires in issue order, so every later wait of wave 0 (its next
-// poll's, its next pass's drain) waited for them; wave 2's stores count in its own vmcnt.
-// Entries of 32 B: {address | kind, 0, 0} then the data.  The queue is named by its offset in dynamic LDS (0: no
-// writer, the store is made where it is asked for): an LDS pointer selected against a null one would be a generic
-// pointer, and generic LDS accesses count in vmcnt -- the very wait the writer exists to take off wave 0
-extern __shared__ __attribute__((aligned(16))) uint8_t rlo_dyn_lds[];  // (every extern __shared__ array is the same)
-constexpr uint32_t kWq = 128;
-constexpr uint32_t kWqBytes = kWq * 32u;
-enum : uint32_t { WQ_ST16 = 0u, WQ_ST8 = 1u, WQ_ST8_DRAIN = 2u };  // (kind in the 8-B aligned address's low bits)
-// a volatile LDS word through an LDS-typed pointer (ds_read / ds_write: a generic one is a flat access, counted in vmcnt)
+// a volatile LDS word through an LDS-typed pointer (ds_read / ds_write: a generic one is a flat access, counted in
+// vmcnt as well as lgkmcnt -- every wait for it also waited for the wave's stores in flight, PCIe ones included)
 typedef volatile __attribute__((address_space(3))) uint32_t lds_vu32;
 __device__ __forceinline__ lds_vu32* lds_word(uint32_t* p) { return (lds_vu32*)(p); }
 typedef volatile __attribute__((address_space(3))) uint64_t lds_vu64;
 __device__ __forceinline__ lds_vu64* lds_dword(uint8_t* p) { return (lds_vu64*)(p); }
-// by the active lanes of wave 0 (any subset): one entry each, in lane order
-template <class SH>
-__device__ __forceinline__ void wq_put(SH& S, uint32_t wq, const void* p, uint32_t kind, u32x4 v) {
-    const uint32_t lane = __lane_id();
-    const uint64_t m = __ballot(1);
-    const uint32_t n = (uint32_t)__popcll(m), k = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)*lds_word(&S.wq_tail));
-    while (t + n - (uint32_t)__builtin_amdgcn_readfirstlane((int)*lds_word(&S.wq_head)) > kWq)
-        __builtin_amdgcn_s_sleep(1);  // full: the writer frees entries as it issues their stores
-    __attribute__((address_space(3))) u32x4* e =
-        (__attribute__((address_space(3))) u32x4*)(rlo_dyn_lds + wq + ((t + k) & (kWq - 1u)) * 32u);
-    const uint64_t a = reinterpret_cast<uint64_t>(p) | kind;
-    e[0] = u32x4{(uint32_t)a, (uint32_t)(a >> 32), 0u, 0u};
-    e[1] = v;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entries land before the tail that hands them over
-    if (k == 0) *lds_word(&S.wq_tail) = t + n;
-}
-// a 16-B system-scope store to host memory: made here (wq null) or handed to the pickup writer
-template <class SH>
-__device__ __forceinline__ void hst16(SH& S, uint32_t wq, void* p, u32x4 v) {
-    if (wq) wq_put(S, wq, p, WQ_ST16, v);
-    else st_sys16(p, v);
-}
 
 // one event record: the parity log (MODE_LOG, linear) or the host pickup ring (MODE_HOST, the
 // slot after this iteration's earlier events; the selection phase guaranteed the room).  Returns the
@@ -460,7 +426,7 @@ __device__ __forceinline__ void hst16(SH& S, uint32_t wq, void* p, u32x4 v) {
 template <uint32_t PMK, class SH>  // PMK: the kernel's program mask (no host-mode code where it has none)
 __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint32_t kind, int origin, int from,
                                             uint32_t id, uint32_t len, int vote, uint32_t aux, bool want_rec = false,
-                                            bool tagged_payload = false, uint32_t wq = 0u) {
+                                            bool tagged_payload = false) {
     if (!(P.mode & (MODE_LOG | MODE_HOST))) return ~0u;
     uint32_t i;
     if ((PMK & MODE_HOST) && (P.mode & MODE_HOST)) {  // the tagged record (rlo_device.hpp kPkRecBytes): no drain
@@ -470,17 +436,8 @@ __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint
         const bool pl = P.log_payload && (kind == (LOG_DELIVER | (TAG_BCAST << 8)) || kind == LOG_JREQ || kind == LOG_JUDGED);
         const uint32_t pidx = pl ? (i | (tagged_payload ? kPkTaggedPayload : 0u)) : kPkNoPayload;
         u32x4* dst = reinterpret_cast<u32x4*>(&P.log[(size_t)lr * P.log_cap + i]);
-        const u32x4 r0 = u32x4{kind | t16, (uint32_t)origin, ((uint32_t)(from + 1) & 0xffffu) | t16, id};
-        const u32x4 r1 = u32x4{len, ((uint32_t)vote & 0xffffu) | t16, aux, pidx | t16};
-        if constexpr ((PMK & MODE_HOST) != 0u) {
-            if (wq) {  // the pickup writer's (rlo_kernel.hip, phase A)
-                wq_put(S, wq, dst, WQ_ST16, r0);
-                wq_put(S, wq, dst + 1, WQ_ST16, r1);
-                return want_rec ? i : (pl ? i : ~0u);
-            }
-        }
-        st_sys16(dst, r0);
-        st_sys16(dst + 1, r1);
+        st_sys16(dst, u32x4{kind | t16, (uint32_t)origin, ((uint32_t)(from + 1) & 0xffffu) | t16, id});
+        st_sys16(dst + 1, u32x4{len, ((uint32_t)vote & 0xffffu) | t16, aux, pidx | t16});
         return want_rec ? i : (pl ? i : ~0u);
     } else {
         i = (uint32_t)atomicAdd(&S.log_count, 1ull);
@@ -507,16 +464,9 @@ __device__ __forceinline__ uint32_t log_put(SH& S, const Params& P, int lr, uint
 // chunk q >= 1 of a doorbell-pass event's payload (v: the message's 16-B chunk q) into pickup slot `slot` of my
 // ring, in the tagged form (two 8-B units per 8 payload bytes); host mode only
 template <class SH>
-__device__ __forceinline__ void pk_payload_tagged(SH& S, const Params& P, int lr, uint32_t slot, uint32_t q, u32x4 v,
-                                                  uint32_t wq = 0u) {
+__device__ __forceinline__ void pk_payload_tagged(const SH& S, const Params& P, int lr, uint32_t slot, uint32_t q, u32x4 v) {
     const uint64_t seq = S.pk_tail + ((slot - (uint32_t)S.pk_tail) & (P.log_cap - 1u));
     const uint32_t tg = pk_tag(seq, P.pk_epoch);
-    if (wq) {  // (every 8-B unit carries its tag: two 8-B stores per 16 B are as good as one 16-B store)
-        uint8_t* d = P.log_payload + ((size_t)lr * P.log_cap + slot) * P.log_stride + 32u * (q - 1u);
-        wq_put(S, wq, d, WQ_ST16, u32x4{v.x, tg, v.y, tg});
-        wq_put(S, wq, d + 16, WQ_ST16, u32x4{v.z, tg, v.w, tg});
-        return;
-    }
     const __amdgpu_buffer_rsrc_t rp =
         mk_rsrc(P.log_payload + (size_t)lr * P.log_cap * P.log_stride, P.log_cap * P.log_stride);
     st_ring(rp, slot * P.log_stride + 32u * (q - 1u), u32x4{v.x, tg, v.y, tg}, true);

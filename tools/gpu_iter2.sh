@@ -4,9 +4,9 @@ set -o pipefail
 tag=${1:-it2}
 d=gpurun_out/${RLO_OUT:-r6}
 mkdir -p $d
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $d/gpu_tests_$tag.log 2>&1
+[ -n "$SKIP_SUITE" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $d/gpu_tests_$tag.log 2>&1
 rc=$?; grep -E "FAILED|ERROR|passed|failed" $d/gpu_tests_$tag.log | tail -8; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python3 -u tools/api_ab.py --reps 3 --ranks 4 8 rootless-coll-mpi-ops_amd/lib rootless-coll-mpi-ops_amd/lib_nowq > $d/api_ab_$tag.txt 2>&1 || exit $?
+timeout -k 10 400 python3 -u tools/api_ab.py --reps 3 --ranks 4 8 -- rootless-coll-mpi-ops_amd/lib rootless-coll-mpi-ops_amd/lib_nowq > $d/api_ab_$tag.txt 2>&1 || exit $?
 cat $d/api_ab_$tag.txt
 timeout -k 10 120 python3 -u tools/round_timeline.py --n 8 --sizes 64 --rounds 64 > $d/tl_hop_$tag.txt 2>&1 || exit $?
 RLO_NO_HOP=1 timeout -k 10 120 python3 -u tools/round_timeline.py --n 8 --sizes 64 --rounds 64 > $d/tl_full_$tag.txt 2>&1 || exit $?
