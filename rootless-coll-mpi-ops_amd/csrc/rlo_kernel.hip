@@ -218,13 +218,17 @@ __device__ __forceinline__ uint64_t* bulk_done(const Params& P, int o, uint32_t 
     return reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(P.bflag[p]) +
                                        (nlp * (uint64_t)P.n * P.bulk_slots + lr * P.bulk_slots + s) * kBulkLine);
 }
+// (flag words through global pointers: a generic access counts in lgkmcnt too, so the next LDS wait of the wave
+// waited for it to reach memory)
 __device__ __forceinline__ uint32_t bflag_ld(uint32_t* p, bool sys) {
-    return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-               : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gu32* g = (gu32*)p;
+    return sys ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+               : __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void bflag_add(uint32_t* p, uint32_t v, bool sys) {
-    if (sys) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gu32* g = (gu32*)p;
+    if (sys) __hip_atomic_fetch_add(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_fetch_add(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // a receiver's completion count (tiles landed in its copy).  Direct plans (one GPU) keep it in 16 shards
 // -- the line's words 0..15, which only the scatter -> gather hand-off of chunked plans uses -- each mover
@@ -267,9 +271,9 @@ __device__ __forceinline__ void bulk_slot_release(const Params& P, int r, int o,
                                        (want & 0xfffu)) == 0ull)
             bulk_fault(P, 13, ((uint32_t)r << 12) | ((uint32_t)o & 0xfffu));
     }
-    for (int i = 0; i <= (int)kBulkTflag; i++) __hip_atomic_store(f + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i <= (int)kBulkTflag; i++) __hip_atomic_store((gu32*)f + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bulk_release(sys);
-    uint64_t* d = bulk_done(P, o, s);
+    gu64* d = gptr64(reinterpret_cast<uint64_t>(bulk_done(P, o, s)));
     if (sys) __hip_atomic_fetch_add(d, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else __hip_atomic_fetch_add(d, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
