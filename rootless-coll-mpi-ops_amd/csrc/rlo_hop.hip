@@ -32,6 +32,14 @@ namespace rlo {
 constexpr uint32_t kHopScratch = 64u * 16u;  // one batch of 16-B chunks (64 lanes x 16 B)
 constexpr uint32_t kHopLoads = 4;            // ring-message loads per lane per round trip (256 chunks)
 constexpr uint32_t kPmHop = ~(uint32_t)MODE_HOST;  // log_put: no host-mode code here
+constexpr uint32_t kHopSpin = 64;            // re-polls of an idle rank before a whole round runs again
+// the diagnostics build's section profile (tools/hop_anatomy.py): shader clocks per section of a round into
+// stats.prof[0..7] and event counts into stats.dbg[0..7]; the product kernel carries none of it
+#ifdef RLO_DIAG
+constexpr bool kHopProf = true;
+#else
+constexpr bool kHopProf = false;
+#endif
 
 struct HopShared {
     RankTopo t;
@@ -233,12 +241,12 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         if (TL_ON(P) && tag == TAG_BCAST && lane == 0) tl_put(P, id, TLC_P2, lr, (uint32_t)now_ticks());
         if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
         if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
-            uint32_t li = ~0u;
+            uint32_t li = ~0u, li_tn = 0;
             if (lane == 0) {
                 S.bcast_delivered++;
-                const uint32_t tn = (uint32_t)now_ticks();
-                if (P.mode & MODE_HIST) S.hist[hist_bin(tn - t0)]++;
-                li = log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, tn - t0);
+                li_tn = (uint32_t)now_ticks();  // this rank's pickup
+                if (P.mode & MODE_HIST) S.hist[hist_bin(li_tn - t0)]++;
+                li = log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, li_tn - t0);
             }
             li = rdl32(li, 0);
             if (q < nch) {
@@ -247,11 +255,14 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                     st_sys16(P.log_payload + ((size_t)lr * P.log_cap + li) * P.log_stride + 16u * (q - 1u), v);
             }
             if (lat && lane == 0) {  // the round's last pickup completes it
+                // the round's one-way latency: origination -> the LAST receiver's pickup, each receiver's own pickup
+                // clock (the reference harness's t_recv, ref_harness.c mode_lat), so the completion count's round
+                // trip below is not part of it (non-returning max; lat_out is zeroed at every launch)
+                __hip_atomic_fetch_max(&P.lat_out[id], (uint64_t)(li_tn - t0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : atomicAdd(&P.lat_count[id], 1u);
                 if (old + 1u == (uint32_t)(P.n - 1)) {
                     tl_mark(P, id, TL_ROUND);
-                    P.lat_out[id] = (uint64_t)((uint32_t)now_ticks() - t0);
                     if (sys) __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     else __hip_atomic_store(P.lat_round, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
@@ -313,36 +324,123 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         return true;
     };
 
+    // what the last poll saw (lane-distributed, as the counters): an idle rank re-polls until one of them moves
+    uint64_t snap_in = 0, snap_vin = 0, snap_out = 0;
+    uint32_t snap_lat = 0;
+    bool idle_prev = false, room_wait = false;
+    // kHopProf: clocks per section (0 poll + spin, 1 bells, 2 publish, 3 loads, 4 votes, 5 loaded messages,
+    // 6 originations, 7 bookkeeping) and counts (0 rounds, 1 re-polls, 2 bell takes, 3 slot takes, 4 votes merged,
+    // 5 refusals, 6 originations, 7 busy rounds)
+    uint64_t hpc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hpn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t hpt = kHopProf ? __builtin_amdgcn_s_memtime() : 0;
+#define HP_MARK(i)                                               \
+    do {                                                         \
+        if constexpr (kHopProf) {                                \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+            hpc[i] += t_ - hpt;                                  \
+            hpt = t_;                                            \
+        }                                                        \
+    } while (0)
+#define HP_CNT(i, v)                       \
+    do {                                   \
+        if constexpr (kHopProf) hpn[i] += (v); \
+    } while (0)
     for (;;) {
         // ---------------- poll: counters, doorbells, error word, round word -- one round trip
-        // (branch-free: rlo_kernel_common.hpp kOob)
-        if (TL_ON(P)) tl_iss = (uint32_t)now_ticks();
-        const uint64_t in_tail_r = ld64_sc1(rc, lane < n_in2 ? (inbox + (uint32_t)lane) * 8u : kOob);
-        const uint64_t vin_tail_r = ld64_sc1(rc, lane < sll ? (inbox + (uint32_t)(n_in2 + lane)) * 8u : kOob);
-        const uint64_t out_head_r = ld64_sc1(rc, lane < nout ? (outbox + (uint32_t)lane) * 8u : kOob);
-        const uint64_t vout_head_r = ld64_sc1(rc, lane < n_in ? (outbox + (uint32_t)(nout + lane)) * 8u : kOob);
-        const uint32_t errf = ld32_sc1(rc, 0u);  // (the part's error word is its ctrl word 0)
+        // (branch-free: rlo_kernel_common.hpp kOob).  After a round that did nothing the poll repeats right away, with
+        // no round around it, until a polled word moves: a message landing at an idle rank waits for at most one poll
+        // period of one round trip, not of a whole round (bounded, so the idle clock and the deadline still tick)
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
-        const uint32_t bo = (int)bk < n_in ? (in_bell + bk * kBellWords) * 8u + 32u * bq : kOob;
-        const u32x4 ba = ld_sc1(rc, bo), bb = ld_sc1(rc, bo == kOob ? kOob : bo + 16u);
-        const u32x4 vb = ld_sc1(rc, lane < sll ? (vin_bell + 2u * (uint32_t)lane) * 8u : kOob);
-        // the latency round word (part 0's when sharded; system scope covers both)
-        const uint32_t latr = __hip_atomic_load(lat ? P.lat_round : P.error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler (also the previous round's stores)
-        if (TL_ON(P)) tl_back = (uint32_t)now_ticks();
-        n_iter++;
-        // ---- the previous round's counters: its stores have drained
-        if (lane < nout && out_tail_r != pub_out) { pub_out = out_tail_r; pub64(t.out_tail[lane >> 1][lane & 1], out_tail_r, sys); }
-        if (lane < n_in2 && in_head_r != pub_in) { pub_in = in_head_r; pub64(t.in_head[lane >> 1][lane & 1], in_head_r, sys); }
-        if (lane < sll && vin_head_r != pub_vin) { pub_vin = vin_head_r; pub64(t.vin_head[lane], vin_head_r, sys); }
-        if (lane < n_in) {
-            const uint64_t vt = S.vout_tail[lane];
-            if (vt != pub_vout) { pub_vout = vt; pub64(t.vout_tail[lane], vt, sys); }
-            S.vout_head[lane] = vout_head_r;
+        const bool inb = (int)bk < n_in;
+        const uint32_t bo = inb ? (in_bell + bk * kBellWords) * 8u + 32u * bq : kOob;
+        const uint32_t own_next = lat ? (uint32_t)uni((int)S.lat_own_next) : 0xffffffffu;
+        uint64_t in_tail_r, vin_tail_r, out_head_r, vout_head_r;
+        uint32_t errf, latr;
+        u32x4 ba, bb, vb;
+        // the tags that make in-edge k's bell whole for its ring heads (vc 0 / vc 1), and child j's vote bell
+        const uint32_t e0 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk)));
+        const uint32_t e1 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk + 1u))) | 0x80000000u;
+        const uint32_t ve = bell_tag(vin_head_r);
+        for (uint32_t sp = 0;; sp++) {
+            if (TL_ON(P)) tl_iss = (uint32_t)now_ticks();
+            in_tail_r = ld64_sc1(rc, lane < n_in2 ? (inbox + (uint32_t)lane) * 8u : kOob);
+            vin_tail_r = ld64_sc1(rc, lane < sll ? (inbox + (uint32_t)(n_in2 + lane)) * 8u : kOob);
+            out_head_r = ld64_sc1(rc, lane < nout ? (outbox + (uint32_t)lane) * 8u : kOob);
+            vout_head_r = ld64_sc1(rc, lane < n_in ? (outbox + (uint32_t)(nout + lane)) * 8u : kOob);
+            errf = ld32_sc1(rc, 0u);  // (the part's error word is its ctrl word 0)
+            ba = ld_sc1(rc, bo);
+            bb = ld_sc1(rc, bo == kOob ? kOob : bo + 16u);
+            vb = ld_sc1(rc, lane < sll ? (vin_bell + 2u * (uint32_t)lane) * 8u : kOob);
+            // the latency round word (part 0's when sharded; system scope covers both)
+            latr = __hip_atomic_load(lat ? P.lat_round : P.error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler (also the previous round's stores)
+            if (TL_ON(P)) tl_back = (uint32_t)now_ticks();
+            if (!idle_prev || sp >= kHopSpin) break;
+            HP_CNT(1, 1);
+            // new work: a bell's first half tagged for a ring head or a vote head (the round checks it is whole), a
+            // counter beyond what was taken that moved since the last round, freed out-ring slots when something waits
+            // for room, the round word when it concerns this rank, an error
+            const bool moved = (inb && bq == 0u && (ba.y == e0 || ba.y == e1)) || (lane < sll && vb.y == ve) ||
+                               (lane < n_in2 && in_tail_r > in_head_r && in_tail_r != snap_in) ||
+                               (lane < sll && vin_tail_r > vin_head_r && vin_tail_r != snap_vin) ||
+                               (room_wait && lane < nout && out_head_r != snap_out) ||
+                               (latr != snap_lat && (me == 0 || latr == own_next)) || errf != 0u;
+            if (__ballot(moved)) break;
         }
-        if (TL_ON(P)) tl_pub = (uint32_t)now_ticks();
+        snap_in = in_tail_r; snap_vin = vin_tail_r; snap_out = out_head_r; snap_lat = latr;
+        n_iter++;
+        HP_MARK(0);
+        HP_CNT(0, 1);
+        // the previous round's counters (its stores have drained: the wait above covered them), taken before this
+        // round's first forwards move them
+        const uint64_t out_pub = out_tail_r, in_pub = in_head_r, vin_pub = vin_head_r;
+        const uint64_t vt_pub = lane < n_in ? S.vout_tail[lane] : 0ull;
+        if (lane < n_in) S.vout_head[lane] = vout_head_r;
+        bool progressed = false;
+        room_wait = false;
+        const bool go = !done && __builtin_amdgcn_readfirstlane(errf) == 0;
+
+        // ---------------- whole doorbells first (forward-first): in-edge k's bell is whole for (k, vc) when every half of
+        // its header's chunks carries bell_tag(in-ring head) | vc << 31.  Its message is the ring's head: taken straight
+        // from the bell registers (lane q <- chunk q of edge k), forwarded before this rank publishes, merges or loads
+        // anything -- the reference forwards on receipt too (_bc_forward from make_progress_gen :583-589)
+        const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
+        const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
+        const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;
+        const uint64_t gm = hn <= kBellChunks ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
+        const uint64_t fh = __ballot(bq == 0u && gm && ((B0 & gm) == gm || (B1 & gm) == gm));
+        const uint64_t fv = __ballot(bq == 0u && gm && (B1 & gm) == gm);
+        const int rk = lane >> 1;
+        const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
+        uint64_t blocked = 0;  // rings whose head cannot go this round (full out-ring, pending entry busy): they wait
+        if (go) {
+            if (TL_ON(P)) tl_pub = tl_loop = (uint32_t)now_ticks();
+            for (uint64_t gs = __ballot(rhit); gs; gs &= gs - 1) {  // (uniform)
+                const int g = __builtin_ctzll(gs);
+                const int sl = 8 * (g >> 1) + (lane & 7);
+                u32x4 v = {(uint32_t)__shfl((int)ba.x, sl), (uint32_t)__shfl((int)ba.z, sl), (uint32_t)__shfl((int)bb.x, sl),
+                           (uint32_t)__shfl((int)bb.z, sl)};
+                if ((uint32_t)lane >= kBellChunks) v = u32x4{0u, 0u, 0u, 0u};
+                if (take(v, g, out_head_r)) {
+                    if (lane == g) in_head_r++;
+                    progressed = true;
+                    HP_CNT(2, 1);
+                } else {
+                    blocked |= 1ull << g;
+                    room_wait = true;
+                    HP_CNT(5, 1);
+                }
+            }
+        }
+        HP_MARK(1);
+
+        // ---- publish what the previous round left (before this round's forwards)
+        if (lane < nout && out_pub != pub_out) { pub_out = out_pub; pub64(t.out_tail[lane >> 1][lane & 1], out_pub, sys); }
+        if (lane < n_in2 && in_pub != pub_in) { pub_in = in_pub; pub64(t.in_head[lane >> 1][lane & 1], in_pub, sys); }
+        if (lane < sll && vin_pub != pub_vin) { pub_vin = vin_pub; pub64(t.vin_head[lane], vin_pub, sys); }
+        if (lane < n_in && vt_pub != pub_vout) { pub_vout = vt_pub; pub64(t.vout_tail[lane], vt_pub, sys); }
         if (done) break;  // (the final counters are out)
-        if (__builtin_amdgcn_readfirstlane(errf) != 0) break;  // another rank failed: stop everyone
+        if (!go) break;   // another rank failed: stop everyone
         if (lat && me == 0) {  // world rank 0 observes round completions on its own clock
             const uint32_t done_r = latr, seen = S.lat_seen;
             if (done_r > seen) {
@@ -352,30 +450,18 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             }
         }
 
-        // ---- what the doorbells hold: in-edge k's bell is whole for (k, vc) when every half of its header's chunks
-        // carries bell_tag(in-ring head) | vc << 31; a vote bell when it carries bell_tag(vote head)
-        *reinterpret_cast<u32x4*>(S.bell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
-        const uint32_t e0 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk)));
-        const uint32_t e1 = bell_tag((uint32_t)__shfl((int)(uint32_t)in_head_r, (int)(2u * bk + 1u))) | 0x80000000u;
-        const bool inb = (int)bk < n_in;
-        const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
-        const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
-        const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;
-        const uint64_t gm = hn <= kBellChunks ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
-        const uint64_t fh = __ballot(bq == 0u && gm && ((B0 & gm) == gm || (B1 & gm) == gm));
-        const uint64_t fv = __ballot(bq == 0u && gm && (B1 & gm) == gm);
-        const int rk = lane >> 1;
-        // lane g: its head is in the bell; the messages the counter shows beyond it
-        const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
-        const uint64_t ip = lane < n_in2 && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
-        const uint32_t vbh = lane < sll && vb.y == bell_tag(vin_head_r) && vb.w == bell_tag(vin_head_r) ? 1u : 0u;
+        HP_MARK(2);
+        // ---- the messages the counters show beyond what was taken (ring g: from its head, unless the head waits),
+        // and the vote slots beyond child j's vote bell
+        const uint64_t ip = lane < n_in2 && !((blocked >> lane) & 1ull) && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
+        const uint32_t vbh = lane < sll && vb.y == ve && vb.w == ve ? 1u : 0u;
         const uint64_t vp = lane < sll && vin_tail_r > vin_head_r ? vin_tail_r - vin_head_r : 0ull;
 
-        // ---- load what the counters show beyond the bells: ring messages (lane (m, q): chunk q of the m-th message
-        // to load) and votes (one slot per lane), one round trip
+        // ---- load them: ring messages (lane (m, q): chunk q of the m-th message to load) and votes (one slot per
+        // lane), one round trip
         const uint32_t mmax = min(kHopLoads * 64u / mch, 64u);
         uint32_t mtot = 0;
-        const uint32_t want = (uint32_t)min(ip > (rhit ? 1ull : 0ull) ? ip - (rhit ? 1ull : 0ull) : 0ull, (uint64_t)mmax);
+        const uint32_t want = (uint32_t)min(ip, (uint64_t)mmax);
         const uint32_t mb = wave_excl_scan(want, &mtot);
         const uint32_t mtake = mb >= mmax ? 0u : min(want, mmax - mb);  // lane g: slot messages loaded this round
         const uint32_t mload = min(mtot, mmax);
@@ -396,7 +482,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                     const int g = __builtin_ctzll(gs);
                     const uint32_t b0 = rdl32(mb, g), n0 = rdl32(mtake, g);
                     if (m >= b0 && m < b0 + n0) {
-                        const uint64_t seq = rdl64(in_head_r, g) + (rdl32(rhit ? 1u : 0u, g)) + (m - b0);
+                        const uint64_t seq = rdl64(in_head_r, g) + (m - b0);
                         src = t.in_data[g >> 1][g & 1] + (uint32_t)(seq & fcap_m) * P.fwd_stride + 16u * qq;
                         any = true;
                     }
@@ -423,7 +509,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             *reinterpret_cast<u32x4*>(S.vote + 16u * (uint32_t)lane) = lw;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-        bool progressed = false;
+        HP_MARK(3);
 
         // ---------------- votes: child j's head from its bell, then its loaded slots, in order
         for (uint64_t js = __ballot(vbh || vtake); js; js &= js - 1) {
@@ -441,27 +527,30 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             }
             if (lane == j) vin_head_r += hb + nv;
             progressed = true;
+            HP_CNT(4, hb + nv);
         }
+        HP_MARK(4);
 
-        if (TL_ON(P)) tl_loop = (uint32_t)now_ticks();
-        // ---------------- ring messages: per in-ring its head (bell or slot), then its loaded slots, in order
-        for (uint64_t gs = __ballot(rhit || mtake); gs; gs &= gs - 1) {
+        // ---------------- loaded ring messages: per in-ring, in order from its head
+        for (uint64_t gs = __ballot(mtake > 0u); gs; gs &= gs - 1) {
             const int g = __builtin_ctzll(gs);
-            const uint32_t hb = rdl32(rhit ? 1u : 0u, g), nm = rdl32(mtake, g), b0 = rdl32(mb, g);
+            const uint32_t nm = rdl32(mtake, g), b0 = rdl32(mb, g);
             uint32_t taken = 0;
-            for (uint32_t i = 0; i < hb + nm; i++) {  // uniform
-                const bool bell = i < hb;
-                const uint32_t at = bell ? 16u * (8u * (uint32_t)(g >> 1)) : 16u * ((b0 + i - hb) * mch);
+            for (uint32_t i = 0; i < nm; i++) {  // uniform
                 u32x4 v = {0u, 0u, 0u, 0u};
-                if ((uint32_t)lane < (bell ? kBellChunks : mch)) v = *reinterpret_cast<const u32x4*>((bell ? S.bell : S.msg) + at + 16u * (uint32_t)lane);
-                // a bell holds at most kBellChunks chunks (its header says how many); a longer message comes by slot
-                if (!take(v, g, out_head_r)) break;
+                if ((uint32_t)lane < mch) v = *reinterpret_cast<const u32x4*>(S.msg + 16u * ((b0 + i) * mch) + 16u * (uint32_t)lane);
+                if (!take(v, g, out_head_r)) {
+                    room_wait = true;
+                    HP_CNT(5, 1);
+                    break;
+                }
                 taken++;
             }
             if (lane == g) in_head_r += taken;
             if (taken) progressed = true;
+            HP_CNT(3, taken);
         }
-
+        HP_MARK(5);
         // ---------------- my own originations
         if (iar) {
             for (;;) {  // the pool's decided slots (_iar_decision_bcast :908-917)
@@ -471,8 +560,11 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 const uint32_t k = (uint32_t)__builtin_ctzll(dm);
                 const uint32_t id = (uint32_t)S.own_pid[k], dec = S.own_decision[k];
                 if (!originate(K_DEC, (uint32_t)me | (TAG_DECISION << 16) | ((dec & 0xffu) << 24), id, 23u | (k << 24), 0u,
-                               out_head_r))
+                               out_head_r)) {
+                    room_wait = true;
                     break;
+                }
+                HP_CNT(6, 1);
                 if (lane == 0) {
                     S.own_decided++;
                     if (dec) S.own_approved++;
@@ -491,8 +583,11 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 const int64_t pi = P.prop_off[lr] + (int64_t)S.own_iter;
                 const uint32_t id = (uint32_t)P.prop_pid[pi];
                 if (!originate(K_PROP, (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id,
-                               (16u + P.prop_data_len[pi]) | (k << 24), (uint32_t)pi, out_head_r))
+                               (16u + P.prop_data_len[pi]) | (k << 24), (uint32_t)pi, out_head_r)) {
+                    room_wait = true;
                     break;
+                }
+                HP_CNT(6, 1);
                 if (lane == 0) {  // proposalPool_proposal_add (:1253-1279)
                     S.own_pid[k] = (int32_t)id;
                     S.own_word[k] = 0;
@@ -504,18 +599,23 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 progressed = true;
             }
         }
-        if (lat && S.lat_own_next != 0xffffffffu && latr == S.lat_own_next &&
-            originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), S.lat_own_next, P.len, 0u, out_head_r)) {
-            if (lane == 0) {
-                tl_mark(P, S.lat_own_next, TL_ORIGIN);
-                S.originated++;
-                const uint32_t np = S.lat_pos + 1u;
-                S.lat_pos = np;
-                S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
+        if (lat && own_next != 0xffffffffu && latr == own_next) {
+            if (!originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), own_next, P.len, 0u, out_head_r)) {
+                room_wait = true;
+            } else {
+                HP_CNT(6, 1);
+                if (lane == 0) {
+                    tl_mark(P, own_next, TL_ORIGIN);
+                    S.originated++;
+                    const uint32_t np = S.lat_pos + 1u;
+                    S.lat_pos = np;
+                    S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
+                }
+                progressed = true;
             }
-            progressed = true;
         }
 
+        HP_MARK(6);
         // ---------------- bookkeeping (lane 0 decides, every lane follows)
         if (lane == 0) {
             if (progressed) {
@@ -538,6 +638,9 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             done = d;
         }
         done = __builtin_amdgcn_readfirstlane((int)done) != 0;
+        idle_prev = !progressed && !done;
+        HP_CNT(7, progressed ? 1 : 0);
+        HP_MARK(7);
         // (done: one more poll round publishes this round's counters behind its drain, then the loop ends)
     }
 #undef PEND
@@ -546,7 +649,11 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
     for (int i = lane; i < kHistBins; i += 64) P.stats[lr].hist[i] = S.hist[i];
-    if (lane < 8) { P.stats[lr].prof[lane] = 0; P.stats[lr].dbg[lane] = 0; }
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (lane == i) { P.stats[lr].prof[i] = hpc[i]; P.stats[lr].dbg[i] = hpn[i]; }
+#undef HP_MARK
+#undef HP_CNT
     if (lane == 0) {
         RankStats& st = P.stats[lr];
         st.bcast_delivered = S.bcast_delivered;
