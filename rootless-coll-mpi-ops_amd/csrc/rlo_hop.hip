@@ -41,25 +41,26 @@ constexpr bool kHopProf = true;
 constexpr bool kHopProf = false;
 #endif
 
+// Per-rank state lives in registers, not LDS: every counter, the own-proposal pool, the vote-ring tails and heads
+// and the topology's remote addresses are lane-distributed VGPRs (lane i holds entry i), read with v_readlane by a
+// wave-uniform index and written by the one lane that owns the entry.  A round's effects run on the whole wave in
+// uniform control flow (no lane-0 sections of dependent LDS read-modify-writes: DESIGN.md 4.0.2).  LDS keeps only the
+// pending-proposal table (n x pend_slots entries), the slot / vote staging of a round and the rare error / log words.
 struct HopShared {
     RankTopo t;
-    uint64_t vout_tail[kMaxIn], vout_head[kMaxIn];  // vote rings towards my parents (emit_vote)
-    // own proposals: the pool (rootless_ops.c:30, :159-165, :1251-1366), slot k named by the pseq byte
-    int32_t own_pid[kPoolMax];
-    uint32_t own_word[kPoolMax], own_state[kPoolMax], own_decision[kPoolMax];
-    uint32_t own_needed, own_rr;
-    unsigned long long own_iter;
-    int64_t own_n;
-    uint32_t lat_pos, lat_pos_n, lat_own_next, lat_seen;
     uint32_t error, error_aux;
-    unsigned long long bcast_delivered, dec_delivered, dec_approved, actions, judge_calls, originated;
-    unsigned long long own_decided, own_approved, proposals_recv, log_count, stale;
+    unsigned long long log_count;
     uint64_t pk_tail;  // (log_put's host-mode fields: this kernel runs no host mode)
     uint32_t ev_n;
     uint32_t hist[kHistBins];
-    alignas(16) uint8_t bell[kHopScratch];   // in-edge k's doorbell, chunk q at 16 (8 k + q)
     alignas(16) uint8_t msg[kHopLoads * kHopScratch];  // loaded ring messages, message m chunk q at 16 (m mch + q)
-    alignas(16) uint8_t vote[kHopScratch];   // loaded votes, one 16-B slot per lane
+    alignas(16) uint8_t vote[kHopScratch];   // loaded votes, one 16-B slot per lane; a judged proposal's copy
+};
+
+// the counters of RankStats, one per lane of a single VGPR pair (cnt_r)
+enum HopCnt : int {
+    HC_BCAST = 0, HC_DEC, HC_DEC_APPR, HC_ACTIONS, HC_JUDGE, HC_ORIG, HC_OWN_DEC, HC_OWN_APPR, HC_PROP_RECV, HC_STALE,
+    HC_ITER, HC_BUSY
 };
 
 template <bool PH>
@@ -84,18 +85,9 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         for (int i = lane; i < (int)(sizeof(RankTopo) / 4); i += 64) dst[i] = src[i];
         for (int i = lane; i < P.n * (int)P.pend_slots; i += 64) pend[i] = PendState{0, 0, 0, 0, 0, 0};
         for (int i = lane; i < kHistBins; i += 64) S.hist[i] = 0;
-        if (lane < kMaxIn) { S.vout_tail[lane] = 0; S.vout_head[lane] = 0; }
-        if (lane < kPoolMax) { S.own_pid[lane] = -1; S.own_word[lane] = 0; S.own_state[lane] = 0; S.own_decision[lane] = 0; }
         if (lane == 0) {
-            S.own_needed = 0; S.own_rr = 0; S.own_iter = 0;
-            S.own_n = iar ? (P.prop_off[lr + 1] - P.prop_off[lr]) : 0;
-            S.lat_pos = 0; S.lat_seen = 0;
-            S.lat_pos_n = lat ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
-            S.lat_own_next = S.lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
             S.error = 0; S.error_aux = 0;
-            S.bcast_delivered = S.dec_delivered = S.dec_approved = S.actions = S.judge_calls = S.originated = 0;
-            S.own_decided = S.own_approved = S.proposals_recv = S.log_count = S.stale = 0;
-            S.pk_tail = 0; S.ev_n = 0;
+            S.log_count = 0; S.pk_tail = 0; S.ev_n = 0;
         }
     }
     if constexpr (PH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the table's zeros land before any read
@@ -106,7 +98,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     const int64_t expect_dec = iar ? P.expect_dec[lr] : 0;
     const uint32_t my_mask = (iar && P.judge_kind == JUDGE_MASK) ? P.judge_mask[me] : 0u;
 
-    // topology: wave-uniform scalars + lane-distributed send list
+    // topology: wave-uniform scalars + lane-distributed lists and remote addresses
     const RankTopo& t = S.t;
     const int level = uni(t.level), last_wall = uni(t.last_wall), scc = uni(t.scc), sll = uni(t.sll);
     const int n_in = uni(t.n_in), n_in2 = 2 * n_in, nout = 2 * sll;
@@ -118,18 +110,60 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);
     const uint32_t fcap_m = P.fwd_cap - 1, vcap_m = P.vote_cap - 1, oring_bytes = P.fwd_cap * P.fwd_stride;
-    // lane-distributed ring state: lane g = in-ring g (k*2 + vc), lane oi = out-ring oi (j*2 + vc), lane j = vote
-    // ring from child j, lane k = vote ring to the parent of in-edge k; published values beside them
-    uint64_t in_head_r = 0, out_tail_r = 0, vin_head_r = 0;
+    // lane g = in-ring g (k*2 + vc), lane oi = out-ring oi (j*2 + vc), lane j = vote ring from child j, lane k = in-edge k
+    // (its sender, the vote ring to it and that ring's bell)
+    const uint32_t in_src_r = lane < n_in ? (uint32_t)t.in_src[lane] : 0u;
+    const uint32_t in_data_r = lane < n_in2 ? t.in_data[lane >> 1][lane & 1] : 0u;
+    const uint32_t vin_data_r = lane < sll ? t.vin_data[lane] : 0u;
+    const uint64_t obase_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;  // out-ring oi in the child's part
+    const uint64_t bbase_r = lane < nout ? t.out_bell[lane >> 1] : 0ull;            // the child's doorbell for the edge
+    const uint64_t otail_a = lane < nout ? t.out_tail[lane >> 1][lane & 1] : 0ull;   // counter words I publish
+    const uint64_t ihead_a = lane < n_in2 ? t.in_head[lane >> 1][lane & 1] : 0ull;
+    const uint64_t vinh_a = lane < sll ? t.vin_head[lane] : 0ull;
+    const uint64_t vtail_a = lane < n_in ? t.vout_tail[lane] : 0ull;
+    const uint64_t vring_r = lane < n_in ? t.vout_ring[lane] : 0ull;  // vote ring to the parent of in-edge k
+    const uint64_t vbell_r = lane < n_in ? t.vout_bell[lane] : 0ull;  // and its vote bell
+    // ring state and the values last published
+    uint64_t in_head_r = 0, out_tail_r = 0, vin_head_r = 0, vout_tail_r = 0, vout_hd_r = 0;
     uint64_t pub_in = 0, pub_out = 0, pub_vin = 0, pub_vout = 0;
-    // this lane's out-ring (lane oi < nout): its base in the child's part and the child's doorbell for the edge
-    const uint64_t obase_r = lane < nout ? t.out_ring[lane >> 1][lane & 1] : 0ull;
-    const uint64_t bbase_r = lane < nout ? t.out_bell[lane >> 1] : 0ull;
+    // counters (HopCnt: lane i holds counter i)
+    uint64_t cnt_r = 0;
+#define CNT_ADD(i, v) (cnt_r += (lane == (i)) ? (uint64_t)(v) : 0ull)
+    // own proposals, the pool (rootless_ops.c:30, :159-165, :1251-1366): lane k = slot k, named by the pseq byte
+    int32_t own_pid_r = -1;
+    uint32_t own_word_r = 0, own_state_r = 0, own_dec_r = 0;
+    const uint32_t own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
+    uint32_t own_rr = 0;
+    int64_t own_iter = 0;
+    const int64_t poff = iar ? P.prop_off[lr] : 0;
+    const int64_t own_n = iar ? P.prop_off[lr + 1] - poff : 0;
+    // the next own proposal, fetched while the current one is in flight (RLO_submit_proposal's arguments): stage 1 its
+    // pid / data_len / data offset, stage 2 its PBuf chunks (lane q = chunk q, q >= 1), so an origination loads nothing
+    int64_t nx_i = -1;
+    uint32_t nx_stage = 0, nx_pid = 0, nx_dl = 0, nx_doff = 0;
+    u32x4 nx_v = {0u, 0u, 0u, 0u};
+    auto prefetch_meta = [&](int64_t i) {
+        nx_stage = 0;
+        nx_i = i;
+        if (i >= own_n) return;
+        nx_pid = (uint32_t)P.prop_pid[poff + i];
+        nx_dl = P.prop_data_len[poff + i];
+        nx_doff = P.prop_data_off[poff + i];
+        nx_stage = 1;
+    };
+    // the latency program: my originations
+    uint32_t lat_pos = 0, lat_seen = 0;
+    const uint32_t lat_pos_n = lat ? P.lat_own_off[lr + 1] - P.lat_own_off[lr] : 0u;
+    uint32_t lat_own_next = lat_pos_n ? P.lat_own[P.lat_own_off[lr]] : 0xffffffffu;
+    if (iar) prefetch_meta(0);
     // MODE_TL (diagnostics build): this round's poll issued / returned, counters published, ring loop entered
     uint32_t tl_iss = 0, tl_back = 0, tl_pub = 0, tl_loop = 0;
-    uint64_t n_iter = 0, n_busy = 0, idle_since = 0;
+    uint64_t idle_since = 0;
     uint32_t idle_n = 0;
     bool done = false;
+    auto err = [&](uint32_t code, uint32_t aux) {
+        if (lane == 0) set_error(S, P, code, aux);
+    };
 
     // a message (lane q holds slot chunk q, q < nch) into out-rings `need` at their tails, and into each child's
     // doorbell for the edge when it fits one (tag bell_tag(ring sequence) | vc << 31).  The caller advances out_tail_r
@@ -152,36 +186,74 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     auto full_of = [&](uint32_t need, uint64_t out_head_r) -> bool {
         return __ballot(lane < nout && ((need >> lane) & 1u) && out_tail_r - out_head_r >= P.fwd_cap) != 0ull;
     };
+    // a pending entry, read by every lane (one LDS / HBM broadcast) as {pid, word, parent_k | needed << 16 | valid << 24,
+    // pseq}; lane 0's copy is the one used (it wrote the entry last, so program order covers its own stores)
+    auto pend_rd = [&](int origin, uint32_t pseq) -> u32x4 {
+        const u32x4 x = *reinterpret_cast<const u32x4*>(&PEND(origin, pseq));
+        return u32x4{rdl32(x.x, 0), rdl32(x.y, 0), rdl32(x.z, 0), rdl32(x.w, 0)};
+    };
+    auto pend_wr = [&](int origin, uint32_t pseq, u32x4 x) {
+        if (lane == 0) *reinterpret_cast<u32x4*>(&PEND(origin, pseq)) = x;
+    };
 
-    // one vote from child j (lane 0): _iar_vote_handler :743-812, _vote_merge :1056-1070
+    // vote up towards the parent over in-edge k (_vote_back :728-741): its vote bell {origin | pseq << 16 | vote << 24,
+    // T, pid, T} (lanes 0, 1) and the 16-B slot {origin | vote << 24, pid, pseq, me} (lanes 2, 3), T = bell_tag(vote
+    // sequence); global stores, agent scope (system scope when the world spans GPUs)
+    auto vote_up = [&](uint32_t k, int origin, int32_t pid, uint32_t pseq, int vote) {
+        const uint64_t p = rdl64(vout_tail_r, (int)k);
+        if (p - rdl64(vout_hd_r, (int)k) >= P.vote_cap) {
+            err(ERR_VOTE_RING, k);
+            return;
+        }
+        if (lane == (int)k) vout_tail_r = p + 1u;
+        const uint32_t T = bell_tag(p);
+        uint64_t addr = 0, val = 0;
+        if (lane < 2) {
+            addr = rdl64(vbell_r, (int)k) + 8u * (uint32_t)lane;
+            val = lane == 0 ? ((uint64_t)(((uint32_t)origin & 0xffffu) | ((pseq & 0xffu) << 16) | ((uint32_t)(vote & 0xff) << 24)) |
+                               ((uint64_t)T << 32))
+                            : ((uint64_t)(uint32_t)pid | ((uint64_t)T << 32));
+        } else if (lane < 4) {
+            addr = rdl64(vring_r, (int)k) + (uint64_t)(p & vcap_m) * kVoteSlot + 8u * (uint32_t)(lane - 2);
+            val = lane == 2 ? ((uint64_t)((uint32_t)origin | ((uint32_t)(vote & 0xff) << 24)) | ((uint64_t)(uint32_t)pid << 32))
+                            : ((uint64_t)(pseq & 0xffu) | ((uint64_t)(uint32_t)me << 32));
+        }
+        if (lane < 4) {
+            if (sys) __hip_atomic_store(gptr64(addr), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else __hip_atomic_store(gptr64(addr), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+
+    // one vote from child j: _iar_vote_handler :743-812, _vote_merge :1056-1070 (uniform)
     auto merge_vote = [&](int origin, int32_t pid, uint32_t pseq, int vote, uint32_t vw) {
         const uint32_t inc = 1u + (vote == 0 ? 0x10000u : 0u);
         if (origin >= P.n) {
-            set_error(S, P, ERR_BAD_SLOT, vw);
+            err(ERR_BAD_SLOT, vw);
         } else if (origin == me) {  // a vote for my own proposal (:756-783)
             const uint32_t k = pseq & (P.pend_slots - 1u);
-            if (S.own_state[k] != 1 || pid != S.own_pid[k]) {
-                set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+            if (rdl32(own_state_r, (int)k) != 1u || pid != (int32_t)rdl32((uint32_t)own_pid_r, (int)k)) {
+                err(ERR_VOTE_ORPHAN, (uint32_t)pid);
             } else {
-                const uint32_t nw = (S.own_word[k] += inc);
-                if ((nw & 0xffffu) == S.own_needed) {
-                    const int d = (nw >> 16) == 0 ? 1 : 0;
+                const uint32_t nw = rdl32(own_word_r, (int)k) + inc;
+                if (lane == (int)k) own_word_r = nw;
+                if ((nw & 0xffffu) == own_needed) {
+                    const uint32_t d = (nw >> 16) == 0 ? 1u : 0u;
                     if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
-                        S.judge_calls++;
-                        log_put<kPmHop>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                        CNT_ADD(HC_JUDGE, 1);
+                        if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
                     }
-                    S.own_decision[k] = (uint32_t)d;
-                    S.own_state[k] = 2;
+                    if (lane == (int)k) { own_dec_r = d; own_state_r = 2; }
                 }
             }
         } else {
-            PendState* ps = &PEND(origin, pseq);
-            if (ps->valid != PS_ACTIVE || ps->pid != pid) {
-                set_error(S, P, ERR_VOTE_ORPHAN, (uint32_t)pid);
+            const u32x4 pe = pend_rd(origin, pseq);
+            if ((pe.z >> 24) != PS_ACTIVE || (int32_t)pe.x != pid) {
+                err(ERR_VOTE_ORPHAN, (uint32_t)pid);
             } else {
-                const uint32_t nw = (ps->word += inc);
-                if ((nw & 0xffffu) == ps->needed)
-                    emit_vote<true>(S, P, me, ps->parent_k, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
+                const uint32_t nw = pe.y + inc;
+                pend_wr(origin, pseq, u32x4{pe.x, nw, pe.z, pe.w});
+                if ((nw & 0xffffu) == ((pe.z >> 16) & 0xffu))
+                    vote_up(pe.z & 0xffffu, origin, pid, pseq, (nw >> 16) == 0 ? 1 : 0);
             }
         }
     };
@@ -192,38 +264,39 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     auto take = [&](u32x4 v, int g, uint64_t out_head_r) -> bool {
         const uint32_t tl_take = TL_ON(P) ? (uint32_t)now_ticks() : 0u;
         const uint32_t q = (uint32_t)lane;
-        const int from = uni(t.in_src[g >> 1]);
+        const int from = (int)rdl32(in_src_r, g >> 1);
         const uint32_t w0 = rdl32(v.x, 0), id = rdl32(v.y, 0), w2 = rdl32(v.z, 0), t0 = rdl32(v.w, 0);
         const int origin = (int)(w0 & 0xffffu);
         const uint32_t tag = (w0 >> 16) & 0xffu, len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4, pseq = w2 >> 24;
         const int vote = (int)(int8_t)(w0 >> 24);
         if (((w2 >> 16) & 0xffu) != kSlotMark) {  // bytes not visible behind the published tail: a protocol violation
-            if (lane == 0) {
-                S.stale++;
-                set_error(S, P, ERR_BAD_SLOT, 0x57A1Eu);
-            }
+            CNT_ADD(HC_STALE, 1);
+            err(ERR_BAD_SLOT, 0x57A1Eu);
             return true;  // consumed, never forwarded
         }
         if (origin >= P.n || nch > mch || !(tag == TAG_BCAST || tag == TAG_DECISION || tag == TAG_PROPOSAL) ||
             (tag == TAG_BCAST && lat && id >= P.lat_rounds)) {
-            if (lane == 0) set_error(S, P, ERR_BAD_SLOT, w0);
+            err(ERR_BAD_SLOT, w0);
             return true;
         }
         int judge = 1;
+        u32x4 pe = {0u, 0u, 0u, 0u};
+        if (tag != TAG_BCAST) pe = pend_rd(origin, pseq);
         if (tag == TAG_PROPOSAL) {
-            if (PEND(origin, pseq).valid != PS_NONE) return false;  // the decision ahead of it first
+            if ((pe.z >> 24) != PS_NONE) return false;  // the decision ahead of it first
             // device judge on the PBuf data [pid][vote][data_len u64][data] at slot + 16 (:1402-1410): chunk 1's
             // word 2 is data_len, the data from chunk 2 on (LDS copy of this lane's chunk)
             uint32_t dl = rdl32(v.z, 1);
             if (dl > len - 16u) dl = len > 16u ? len - 16u : 0u;
             if (P.judge_kind == JUDGE_ISP) {
-                if (q < nch) *reinterpret_cast<u32x4*>(S.vote + 16u * q) = v;  // (scratch: votes are merged already)
+                if (q < nch) *reinterpret_cast<u32x4*>(S.vote + 16u * q) = v;  // (scratch: no vote staged now)
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 const uint8_t* d = S.vote + kHdr + 16u;
                 judge = judge_eval_f(P, me, my_mask, (int32_t)id, [&](uint32_t i) { return d[i]; }, dl);
             } else {
                 judge = judge_eval_f(P, me, my_mask, (int32_t)id, [&](uint32_t) { return (uint8_t)0; }, dl);
             }
+            judge = uni(judge);
         }
         const uint32_t kids = judge == 1 ? kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane) : 0u;
         const uint32_t need = need_of_u(kids, origin, sll, sl_r, lane);
@@ -241,24 +314,24 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         if (TL_ON(P) && tag == TAG_BCAST && lane == 0) tl_put(P, id, TLC_P2, lr, (uint32_t)now_ticks());
         if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
         if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
-            uint32_t li = ~0u, li_tn = 0;
+            CNT_ADD(HC_BCAST, 1);
+            const uint32_t tn = (uint32_t)now_ticks();  // this rank's pickup
+            uint32_t li = ~0u;
             if (lane == 0) {
-                S.bcast_delivered++;
-                li_tn = (uint32_t)now_ticks();  // this rank's pickup
-                if (P.mode & MODE_HIST) S.hist[hist_bin(li_tn - t0)]++;
-                li = log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, li_tn - t0);
+                if (P.mode & MODE_HIST) atomicAdd(&S.hist[hist_bin(tn - t0)], 1u);
+                if (P.mode & MODE_LOG) li = log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_BCAST << 8), origin, from, id, len, -1, tn - t0);
             }
-            li = rdl32(li, 0);
-            if (q < nch) {
-                acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, id, TAG_BCAST, len}) : chunk_mix(q - 1u, v);
-                if (li != ~0u && q >= 1u && 16u * q <= P.log_stride)
+            if (q < nch) acc_sum += q == 0 ? chunk_mix(0xFFFFFFFFu, u32x4{(uint32_t)origin, id, TAG_BCAST, len}) : chunk_mix(q - 1u, v);
+            if (P.mode & MODE_LOG) {
+                li = rdl32(li, 0);
+                if (li != ~0u && q >= 1u && q < nch && 16u * q <= P.log_stride)
                     st_sys16(P.log_payload + ((size_t)lr * P.log_cap + li) * P.log_stride + 16u * (q - 1u), v);
             }
             if (lat && lane == 0) {  // the round's last pickup completes it
                 // the round's one-way latency: origination -> the LAST receiver's pickup, each receiver's own pickup
                 // clock (the reference harness's t_recv, ref_harness.c mode_lat), so the completion count's round
                 // trip below is not part of it (non-returning max; lat_out is zeroed at every launch)
-                __hip_atomic_fetch_max(&P.lat_out[id], (uint64_t)(li_tn - t0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_max(&P.lat_out[id], (uint64_t)(tn - t0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t old = sys ? __hip_atomic_fetch_add(&P.lat_count[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : atomicAdd(&P.lat_count[id], 1u);
                 if (old + 1u == (uint32_t)(P.n - 1)) {
@@ -269,56 +342,44 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             }
             if (TL_ON(P) && lane == 0) tl_mark(P, id, kTlGlobal + P.n_local + (uint32_t)lr);
         } else if (tag == TAG_PROPOSAL) {  // _iar_proposal_handler :668-726
-            if (lane == 0) {
-                S.proposals_recv++;
-                if (own_has(S, P, (int32_t)id)) {
-                    set_error(S, P, ERR_PID_COLLISION, id);  // :690-692
+            CNT_ADD(HC_PROP_RECV, 1);
+            // a received proposal carrying one of my own in-flight pids (:690-692; here every slot of the pool)
+            if (__ballot((uint32_t)lane < P.pend_slots && own_state_r != 0u && own_pid_r == (int32_t)id)) {
+                err(ERR_PID_COLLISION, id);
+            } else {
+                const uint32_t k = (uint32_t)g >> 1;
+                CNT_ADD(HC_JUDGE, 1);
+                if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_JUDGE, origin, from, id, len, judge, 0);
+                if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
+                    vote_up(k, origin, (int32_t)id, pseq, 0);
                 } else {
-                    const uint32_t k = (uint32_t)g >> 1;
-                    S.judge_calls++;
-                    log_put<kPmHop>(S, P, lr, LOG_JUDGE, origin, from, id, len, judge, 0);
-                    PendState* ps = &PEND(origin, pseq);
-                    if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
-                        ps->valid = PS_NONE;
-                        emit_vote<true>(S, P, me, k, origin, (int32_t)id, pseq, 0);
-                    } else {
-                        const uint32_t nk = (uint32_t)__builtin_popcount(kids);
-                        ps->pid = (int32_t)id;
-                        ps->word = 0;
-                        ps->parent_k = (uint16_t)k;
-                        ps->needed = (uint8_t)nk;
-                        ps->pseq = pseq | ((len - 16u) << 8);
-                        ps->valid = PS_ACTIVE;
-                        if (nk == 0) emit_vote<true>(S, P, me, k, origin, (int32_t)id, pseq, 1);
-                    }
+                    const uint32_t nk = (uint32_t)__builtin_popcount(kids);
+                    pend_wr(origin, pseq, u32x4{id, 0u, k | (nk << 16) | ((uint32_t)PS_ACTIVE << 24), pseq | ((len - 16u) << 8)});
+                    if (nk == 0) vote_up(k, origin, (int32_t)id, pseq, 1);
                 }
             }
-        } else if (lane == 0) {  // decision: _iar_decision_handler :814-859
-            PendState* ps = &PEND(origin, pseq);
-            if (ps->valid == PS_ACTIVE && ps->pid == (int32_t)id) {
+        } else {  // decision: _iar_decision_handler :814-859
+            if ((pe.z >> 24) == PS_ACTIVE && (int32_t)pe.x == (int32_t)id) {
                 if (vote != 0) {
-                    S.actions++;
-                    log_put<kPmHop>(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, ps->pseq >> 8);
+                    CNT_ADD(HC_ACTIONS, 1);
+                    if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, pe.w >> 8);
                 }
-                ps->valid = PS_NONE;
+                pend_wr(origin, pseq, u32x4{pe.x, pe.y, pe.z & 0x00ffffffu, pe.w});  // valid = PS_NONE
             }
-            S.dec_delivered++;
-            if (vote != 0) S.dec_approved++;
-            log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+            CNT_ADD(HC_DEC, 1);
+            if (vote != 0) CNT_ADD(HC_DEC_APPR, 1);
+            if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
         }
         return true;
     };
 
-    // a local origination to the whole send list (:1587): header + generated chunks; false (nothing changed) when
-    // an out-ring is full
-    auto originate = [&](uint32_t kind, uint32_t w0, uint32_t id, uint32_t w2, uint32_t src, uint64_t out_head_r) -> bool {
+    // a local origination to the whole send list (:1587): header + chunks (v: lane q's chunk q >= 1, generated or
+    // prefetched); false (nothing changed) when an out-ring is full
+    auto originate = [&](uint32_t w0, uint32_t id, uint32_t w2, u32x4 v, uint64_t out_head_r) -> bool {
         const uint32_t len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4;
         const uint32_t need = need_of_u((1u << sll) - 1u, me, sll, sl_r, lane);
         if (full_of(need, out_head_r)) return false;
-        const uint32_t q = (uint32_t)lane;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (q == 0) v = u32x4{w0, id, (w2 & 0xff00ffffu) | (kSlotMark << 16), (uint32_t)now_ticks()};
-        else if (q < nch) v = gen_chunk(P, kind, me, id, len, src, (int)(int8_t)(w0 >> 24), q);
+        if (lane == 0) v = u32x4{w0, id, (w2 & 0xff00ffffu) | (kSlotMark << 16), (uint32_t)now_ticks()};
         forward(v, nch, need);
         if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
         return true;
@@ -331,19 +392,20 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     // kHopProf: clocks per section (0 poll + spin, 1 bells, 2 publish, 3 loads, 4 votes, 5 loaded messages,
     // 6 originations, 7 bookkeeping) and counts (0 rounds, 1 re-polls, 2 bell takes, 3 slot takes, 4 votes merged,
     // 5 refusals, 6 originations, 7 busy rounds)
-    uint64_t hpc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hpn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // (lane i: clocks of section i, lane 8 + i: count i -- one VGPR pair, as cnt_r)
+    uint64_t hp_r = 0;
     uint64_t hpt = kHopProf ? __builtin_amdgcn_s_memtime() : 0;
-#define HP_MARK(i)                                               \
-    do {                                                         \
-        if constexpr (kHopProf) {                                \
-            const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
-            hpc[i] += t_ - hpt;                                  \
-            hpt = t_;                                            \
-        }                                                        \
+#define HP_MARK(i)                                            \
+    do {                                                      \
+        if constexpr (kHopProf) {                             \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+            hp_r += lane == (i) ? t_ - hpt : 0ull;            \
+            hpt = t_;                                         \
+        }                                                     \
     } while (0)
-#define HP_CNT(i, v)                       \
-    do {                                   \
-        if constexpr (kHopProf) hpn[i] += (v); \
+#define HP_CNT(i, v)                                                       \
+    do {                                                                   \
+        if constexpr (kHopProf) hp_r += lane == 8 + (i) ? (uint64_t)(v) : 0ull; \
     } while (0)
     for (;;) {
         // ---------------- poll: counters, doorbells, error word, round word -- one round trip
@@ -353,7 +415,6 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         const uint32_t bk = (uint32_t)lane >> 3, bq = (uint32_t)lane & 7u;
         const bool inb = (int)bk < n_in;
         const uint32_t bo = inb ? (in_bell + bk * kBellWords) * 8u + 32u * bq : kOob;
-        const uint32_t own_next = lat ? (uint32_t)uni((int)S.lat_own_next) : 0xffffffffu;
         uint64_t in_tail_r, vin_tail_r, out_head_r, vout_head_r;
         uint32_t errf, latr;
         u32x4 ba, bb, vb;
@@ -384,18 +445,17 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                                (lane < n_in2 && in_tail_r > in_head_r && in_tail_r != snap_in) ||
                                (lane < sll && vin_tail_r > vin_head_r && vin_tail_r != snap_vin) ||
                                (room_wait && lane < nout && out_head_r != snap_out) ||
-                               (latr != snap_lat && (me == 0 || latr == own_next)) || errf != 0u;
+                               (latr != snap_lat && (me == 0 || latr == lat_own_next)) || errf != 0u;
             if (__ballot(moved)) break;
         }
         snap_in = in_tail_r; snap_vin = vin_tail_r; snap_out = out_head_r; snap_lat = latr;
-        n_iter++;
+        CNT_ADD(HC_ITER, 1);
         HP_MARK(0);
         HP_CNT(0, 1);
         // the previous round's counters (its stores have drained: the wait above covered them), taken before this
         // round's first forwards move them
-        const uint64_t out_pub = out_tail_r, in_pub = in_head_r, vin_pub = vin_head_r;
-        const uint64_t vt_pub = lane < n_in ? S.vout_tail[lane] : 0ull;
-        if (lane < n_in) S.vout_head[lane] = vout_head_r;
+        const uint64_t out_pub = out_tail_r, in_pub = in_head_r, vin_pub = vin_head_r, vt_pub = vout_tail_r;
+        vout_hd_r = vout_head_r;
         bool progressed = false;
         room_wait = false;
         const bool go = !done && __builtin_amdgcn_readfirstlane(errf) == 0;
@@ -435,22 +495,42 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         HP_MARK(1);
 
         // ---- publish what the previous round left (before this round's forwards)
-        if (lane < nout && out_pub != pub_out) { pub_out = out_pub; pub64(t.out_tail[lane >> 1][lane & 1], out_pub, sys); }
-        if (lane < n_in2 && in_pub != pub_in) { pub_in = in_pub; pub64(t.in_head[lane >> 1][lane & 1], in_pub, sys); }
-        if (lane < sll && vin_pub != pub_vin) { pub_vin = vin_pub; pub64(t.vin_head[lane], vin_pub, sys); }
-        if (lane < n_in && vt_pub != pub_vout) { pub_vout = vt_pub; pub64(t.vout_tail[lane], vt_pub, sys); }
+        if (lane < nout && out_pub != pub_out) { pub_out = out_pub; pub64(otail_a, out_pub, sys); }
+        if (lane < n_in2 && in_pub != pub_in) { pub_in = in_pub; pub64(ihead_a, in_pub, sys); }
+        if (lane < sll && vin_pub != pub_vin) { pub_vin = vin_pub; pub64(vinh_a, vin_pub, sys); }
+        if (lane < n_in && vt_pub != pub_vout) { pub_vout = vt_pub; pub64(vtail_a, vt_pub, sys); }
         if (done) break;  // (the final counters are out)
         if (!go) break;   // another rank failed: stop everyone
-        if (lat && me == 0) {  // world rank 0 observes round completions on its own clock
-            const uint32_t done_r = latr, seen = S.lat_seen;
-            if (done_r > seen) {
-                const uint64_t tn = now_ticks();
-                for (uint32_t k = seen + (uint32_t)lane; k < done_r && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
-                if (lane == 0) S.lat_seen = done_r;
-            }
+        if (lat && me == 0 && latr > lat_seen) {  // world rank 0 observes round completions on its own clock
+            const uint64_t tn = now_ticks();
+            for (uint32_t k = lat_seen + (uint32_t)lane; k < latr && k < P.lat_rounds; k += 64u) P.lat_obs[k] = tn;
+            lat_seen = latr;
         }
-
+        // the next own proposal's chunks, now that its pid / length / offset are in (stage 1 -> 2)
+        if (nx_stage == 1u) {
+            const uint32_t nch = (kHdr + 16u + nx_dl + 15u) >> 4;
+            nx_v = u32x4{0u, 0u, 0u, 0u};
+            if (lane == 1) nx_v = u32x4{nx_pid, 1u, nx_dl, 0u};  // PBuf [pid][vote=1][data_len u64] (:1369-1396)
+            if (lane >= 2 && (uint32_t)lane < nch) {
+                const __attribute__((address_space(1))) uint8_t* d =
+                    (const __attribute__((address_space(1))) uint8_t*)(P.prop_data + nx_doff);
+                uint32_t w[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const uint32_t idx = 16u * ((uint32_t)lane - 2u) + 4u * e + b;
+                        if (idx < nx_dl) x |= (uint32_t)d[idx] << (8 * b);
+                    }
+                    w[e] = x;
+                }
+                nx_v = u32x4{w[0], w[1], w[2], w[3]};
+            }
+            nx_stage = 2;
+        }
         HP_MARK(2);
+
         // ---- the messages the counters show beyond what was taken (ring g: from its head, unless the head waits),
         // and the vote slots beyond child j's vote bell
         const uint64_t ip = lane < n_in2 && !((blocked >> lane) & 1ull) && in_tail_r > in_head_r ? in_tail_r - in_head_r : 0ull;
@@ -483,7 +563,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                     const uint32_t b0 = rdl32(mb, g), n0 = rdl32(mtake, g);
                     if (m >= b0 && m < b0 + n0) {
                         const uint64_t seq = rdl64(in_head_r, g) + (m - b0);
-                        src = t.in_data[g >> 1][g & 1] + (uint32_t)(seq & fcap_m) * P.fwd_stride + 16u * qq;
+                        src = rdl32(in_data_r, g) + (uint32_t)(seq & fcap_m) * P.fwd_stride + 16u * qq;
                         any = true;
                     }
                 }
@@ -497,7 +577,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                     const uint32_t b0 = rdl32(vbase, j), n0 = rdl32(vtake, j);
                     if ((uint32_t)lane >= b0 && (uint32_t)lane < b0 + n0) {
                         const uint64_t seq = rdl64(vin_head_r, j) + rdl32(vbh, j) + ((uint32_t)lane - b0);
-                        src = t.vin_data[j] + (uint32_t)(seq & vcap_m) * kVoteSlot;
+                        src = rdl32(vin_data_r, j) + (uint32_t)(seq & vcap_m) * kVoteSlot;
                         any = true;
                     }
                 }
@@ -511,19 +591,18 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         }
         HP_MARK(3);
 
-        // ---------------- votes: child j's head from its bell, then its loaded slots, in order
+        // ---------------- votes: child j's head from its bell, then its loaded slots, in order (uniform)
         for (uint64_t js = __ballot(vbh || vtake); js; js &= js - 1) {
             const int j = __builtin_ctzll(js);
             const uint32_t hb = rdl32(vbh, j), nv = rdl32(vtake, j), b0 = rdl32(vbase, j);
-            if (lane == 0) {
-                if (hb) {  // vote bell {origin | pseq << 16 | vote << 24, pid}
-                    const uint32_t x = rdl32(vb.x, j), pid = rdl32(vb.z, j);
-                    merge_vote((int)(x & 0xffffu), (int32_t)pid, (x >> 16) & 0xffu, (int)(int8_t)(x >> 24), x);
-                }
-                for (uint32_t i = 0; i < nv; i++) {  // vote slot {origin | vote << 24, pid, pseq, voter}
-                    const u32x4 vs = *reinterpret_cast<const u32x4*>(S.vote + 16u * (b0 + i));
-                    merge_vote((int)(vs.x & 0xffffu), (int32_t)vs.y, vs.z & 0xffu, (int)(int8_t)(vs.x >> 24), vs.x);
-                }
+            if (hb) {  // vote bell {origin | pseq << 16 | vote << 24, pid}
+                const uint32_t x = rdl32(vb.x, j), pid = rdl32(vb.z, j);
+                merge_vote((int)(x & 0xffffu), (int32_t)pid, (x >> 16) & 0xffu, (int)(int8_t)(x >> 24), x);
+            }
+            for (uint32_t i = 0; i < nv; i++) {  // vote slot {origin | vote << 24, pid, pseq, voter}
+                const u32x4 vs = *reinterpret_cast<const u32x4*>(S.vote + 16u * (b0 + i));
+                const uint32_t x = uni((int)vs.x), pid = uni((int)vs.y), ps = uni((int)vs.z);
+                merge_vote((int)(x & 0xffffu), (int32_t)pid, ps & 0xffu, (int)(int8_t)(x >> 24), x);
             }
             if (lane == j) vin_head_r += hb + nv;
             progressed = true;
@@ -551,93 +630,93 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             HP_CNT(3, taken);
         }
         HP_MARK(5);
+
         // ---------------- my own originations
         if (iar) {
             for (;;) {  // the pool's decided slots (_iar_decision_bcast :908-917)
-                const uint32_t ps_ = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
-                const uint64_t dm = __ballot(ps_ == 2u);
+                const uint64_t dm = __ballot((uint32_t)lane < P.pend_slots && own_state_r == 2u);
                 if (!dm) break;
-                const uint32_t k = (uint32_t)__builtin_ctzll(dm);
-                const uint32_t id = (uint32_t)S.own_pid[k], dec = S.own_decision[k];
-                if (!originate(K_DEC, (uint32_t)me | (TAG_DECISION << 16) | ((dec & 0xffu) << 24), id, 23u | (k << 24), 0u,
+                const int k = __builtin_ctzll(dm);
+                const uint32_t id = rdl32((uint32_t)own_pid_r, k), dec = rdl32(own_dec_r, k);
+                u32x4 v = {0u, 0u, 0u, 0u};  // PBuf(pid, decision, 7, "IAR_DEC") (:908-917)
+                if (lane == 1) v = u32x4{id, dec, 7u, 0u};
+                if (lane == 2) v = u32x4{0x5F524149u, 0x00434544u, 0u, 0u};
+                if (!originate((uint32_t)me | (TAG_DECISION << 16) | ((dec & 0xffu) << 24), id, 23u | ((uint32_t)k << 24), v,
                                out_head_r)) {
                     room_wait = true;
                     break;
                 }
                 HP_CNT(6, 1);
-                if (lane == 0) {
-                    S.own_decided++;
-                    if (dec) S.own_approved++;
-                    log_put<kPmHop>(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, k);
-                    S.own_state[k] = 0;
-                    S.own_pid[k] = -1;  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
-                }
+                CNT_ADD(HC_OWN_DEC, 1);
+                if (dec) CNT_ADD(HC_OWN_APPR, 1);
+                if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, (uint32_t)k);
+                if (lane == k) { own_state_r = 0; own_pid_r = -1; }  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
                 progressed = true;
             }
             for (;;) {  // RLO_submit_proposal :876-906, up to own_pool in flight
-                const uint32_t ps2 = (uint32_t)lane < P.pend_slots ? S.own_state[lane] : 0u;
-                const uint64_t busy = __ballot(ps2 != 0u);
-                if (S.own_iter >= (unsigned long long)S.own_n || (uint32_t)__popcll(busy) >= P.own_pool) break;
-                uint32_t k = S.own_rr;
+                const uint64_t busy = __ballot((uint32_t)lane < P.pend_slots && own_state_r != 0u);
+                if (own_iter >= own_n || (uint32_t)__popcll(busy) >= P.own_pool) break;
+                uint32_t k = own_rr;
                 while ((busy >> k) & 1ull) k = (k + 1u) & (P.pend_slots - 1u);
-                const int64_t pi = P.prop_off[lr] + (int64_t)S.own_iter;
-                const uint32_t id = (uint32_t)P.prop_pid[pi];
-                if (!originate(K_PROP, (uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id,
-                               (16u + P.prop_data_len[pi]) | (k << 24), (uint32_t)pi, out_head_r)) {
+                if (nx_i != own_iter || nx_stage != 2u) {  // (not prefetched yet: fetch it now, one wait)
+                    prefetch_meta(own_iter);
+                    const uint32_t nch = (kHdr + 16u + nx_dl + 15u) >> 4;
+                    nx_v = u32x4{0u, 0u, 0u, 0u};
+                    if (lane == 1) nx_v = u32x4{nx_pid, 1u, nx_dl, 0u};
+                    else if (lane >= 2 && (uint32_t)lane < nch)
+                        nx_v = gen_chunk(P, K_PROP, me, nx_pid, 16u + nx_dl, (uint32_t)(poff + own_iter), 1, (uint32_t)lane);
+                    nx_stage = 2;
+                }
+                const uint32_t id = nx_pid;
+                if (!originate((uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id, (16u + nx_dl) | (k << 24), nx_v,
+                               out_head_r)) {
                     room_wait = true;
                     break;
                 }
                 HP_CNT(6, 1);
-                if (lane == 0) {  // proposalPool_proposal_add (:1253-1279)
-                    S.own_pid[k] = (int32_t)id;
-                    S.own_word[k] = 0;
-                    S.own_needed = (uint32_t)sll;  // votes_needed = send_list_len (:881)
-                    S.own_state[k] = 1;
-                    S.own_iter++;
-                    S.own_rr = (k + 1u) & (P.pend_slots - 1u);
-                }
+                // proposalPool_proposal_add (:1253-1279)
+                if (lane == (int)k) { own_pid_r = (int32_t)id; own_word_r = 0; own_state_r = 1; }
+                own_iter++;
+                own_rr = (k + 1u) & (P.pend_slots - 1u);
+                prefetch_meta(own_iter);  // the next one's arguments, in flight until the next round
                 progressed = true;
             }
         }
-        if (lat && own_next != 0xffffffffu && latr == own_next) {
-            if (!originate(K_LAT, (uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), own_next, P.len, 0u, out_head_r)) {
+        if (lat && lat_own_next != 0xffffffffu && latr == lat_own_next) {
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (lane >= 1 && (uint32_t)lane < ((kHdr + P.len + 15u) >> 4))
+                v = gen_chunk(P, K_LAT, me, lat_own_next, P.len, 0u, -1, (uint32_t)lane);
+            if (!originate((uint32_t)me | (TAG_BCAST << 16) | (0xffu << 24), lat_own_next, P.len, v, out_head_r)) {
                 room_wait = true;
             } else {
                 HP_CNT(6, 1);
-                if (lane == 0) {
-                    tl_mark(P, own_next, TL_ORIGIN);
-                    S.originated++;
-                    const uint32_t np = S.lat_pos + 1u;
-                    S.lat_pos = np;
-                    S.lat_own_next = np < S.lat_pos_n ? P.lat_own[P.lat_own_off[lr] + np] : 0xffffffffu;
-                }
+                if (lane == 0) tl_mark(P, lat_own_next, TL_ORIGIN);
+                CNT_ADD(HC_ORIG, 1);
+                lat_pos++;
+                lat_own_next = lat_pos < lat_pos_n ? P.lat_own[P.lat_own_off[lr] + lat_pos] : 0xffffffffu;
                 progressed = true;
             }
         }
-
         HP_MARK(6);
-        // ---------------- bookkeeping (lane 0 decides, every lane follows)
-        if (lane == 0) {
-            if (progressed) {
-                n_busy++;
-                idle_n = 0;
-            } else if ((++idle_n & 63u) == 1u) {  // the clock on the 1st and every 64th idle round only
-                const uint64_t tn = now_ticks();
-                if (idle_n == 1) idle_since = tn;
-                else if (tn - idle_since > P.timeout_ticks) set_error(S, P, ERR_TIMEOUT, 0);
-            }
-            if ((n_iter & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) set_error(S, P, ERR_TIMEOUT, 1);
-            bool d = true;
-            if (lat) d &= S.lat_pos >= S.lat_pos_n && (int64_t)S.bcast_delivered == expect_bcast;
-            if (iar) {
-                bool idle = true;
-                for (uint32_t k = 0; k < P.pend_slots; k++) idle &= S.own_state[k] == 0u;
-                d &= (int64_t)S.own_iter == S.own_n && idle && (int64_t)S.dec_delivered == expect_dec;
-            }
-            if (S.error == ERR_TIMEOUT) d = true;
-            done = d;
+
+        // ---------------- bookkeeping (uniform)
+        if (progressed) {
+            CNT_ADD(HC_BUSY, 1);
+            idle_n = 0;
+        } else if ((++idle_n & 63u) == 1u) {  // the clock on the 1st and every 64th idle round only
+            const uint64_t tn = now_ticks();
+            if (idle_n == 1) idle_since = tn;
+            else if (tn - idle_since > P.timeout_ticks) err(ERR_TIMEOUT, 0);
         }
-        done = __builtin_amdgcn_readfirstlane((int)done) != 0;
+        const uint64_t n_iter = rdl64(cnt_r, HC_ITER);
+        if ((n_iter & 1023u) == 0 && now_ticks() - t_start > P.deadline_ticks) err(ERR_TIMEOUT, 1);
+        bool d = true;
+        if (lat) d &= lat_pos >= lat_pos_n && (int64_t)rdl64(cnt_r, HC_BCAST) == expect_bcast;
+        if (iar)
+            d &= own_iter == own_n && __ballot((uint32_t)lane < P.pend_slots && own_state_r != 0u) == 0ull &&
+                 (int64_t)rdl64(cnt_r, HC_DEC) == expect_dec;
+        if (uni((int)S.error) == (int)ERR_TIMEOUT) d = true;
+        done = d;
         idle_prev = !progressed && !done;
         HP_CNT(7, progressed ? 1 : 0);
         HP_MARK(7);
@@ -651,30 +730,34 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     for (int i = lane; i < kHistBins; i += 64) P.stats[lr].hist[i] = S.hist[i];
 #pragma unroll
     for (int i = 0; i < 8; i++)
-        if (lane == i) { P.stats[lr].prof[i] = hpc[i]; P.stats[lr].dbg[i] = hpn[i]; }
+        if (lane == i) { P.stats[lr].prof[i] = hp_r; P.stats[lr].dbg[i] = rdl64(hp_r, 8 + i); }
 #undef HP_MARK
 #undef HP_CNT
+    uint64_t cv[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) cv[i] = rdl64(cnt_r, i);
     if (lane == 0) {
         RankStats& st = P.stats[lr];
-        st.bcast_delivered = S.bcast_delivered;
-        st.originated = S.originated;
-        st.dec_delivered = S.dec_delivered;
-        st.dec_approved = S.dec_approved;
-        st.actions = S.actions;
-        st.judge_calls = S.judge_calls;
-        st.own_decided = S.own_decided;
-        st.own_approved = S.own_approved;
-        st.proposals_recv = S.proposals_recv;
-        st.iterations = n_iter;
-        st.busy_iterations = n_busy;
+        st.bcast_delivered = cv[HC_BCAST];
+        st.originated = cv[HC_ORIG];
+        st.dec_delivered = cv[HC_DEC];
+        st.dec_approved = cv[HC_DEC_APPR];
+        st.actions = cv[HC_ACTIONS];
+        st.judge_calls = cv[HC_JUDGE];
+        st.own_decided = cv[HC_OWN_DEC];
+        st.own_approved = cv[HC_OWN_APPR];
+        st.proposals_recv = cv[HC_PROP_RECV];
+        st.iterations = cv[HC_ITER];
+        st.busy_iterations = cv[HC_BUSY];
         st.stalls = 0;
-        st.unmarked_slots = S.stale;
+        st.unmarked_slots = cv[HC_STALE];
         st.log_count = S.log_count;
         st.t_start = t_start;
         st.t_end = now_ticks();
         st.error = S.error;
         st.error_aux = S.error_aux;
     }
+#undef CNT_ADD
 }
 
 }  // namespace rlo

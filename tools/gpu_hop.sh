@@ -1,7 +1,7 @@
 # hop-kernel iteration: the latency / iar tests, A/B of latency + one-proposal decisions against a baseline build
 # (tools/ab_libs/<base>), the latency-round timeline of the hop kernel (diagnostics build)
 set -o pipefail
-base=${1:-r6h0}; tag=${2:-hop}
+base=${1:-r6h1}; tag=${2:-hop}
 d=gpurun_out/${RLO_OUT:-r6}
 mkdir -p $d
 timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_timeline.py -m gpu -x -v --timeout 120 --timeout-method thread > $d/tests_$tag.log 2>&1
