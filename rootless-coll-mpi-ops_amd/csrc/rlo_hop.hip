@@ -63,7 +63,9 @@ enum HopCnt : int {
     HC_ITER, HC_BUSY
 };
 
-template <bool PH>
+// SYS: the world spans GPUs (Params.sys_scope): every hand-off store and counter at system scope -- a template
+// parameter, so no store of the hop path branches on the scope at run time
+template <bool PH, bool SYS>
 __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     __shared__ HopShared S;
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     const uint32_t inbox = (uint32_t)uni((int)t.inbox_ctrl), outbox = (uint32_t)uni((int)t.outbox_ctrl);
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     const uint32_t sl_r = lane < sll ? (uint32_t)t.send_list[lane] : 0u;
-    const bool sys = P.sys_scope != 0;
+    constexpr bool sys = SYS;
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);
@@ -261,8 +263,12 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     // one ring message from in-ring g, lane q holding slot chunk q (q < nch): checks, forwards, effects.  Returns
     // false when it cannot go now (an out-ring it needs is full, or its pending entry still holds the previous
     // proposal of that pool slot): nothing changed, the ring waits
+    // kHopProf: a take's clocks -- lane 0 checks (to the forward), 1 forward, 2 effects; lane 3 takes (stats.hist[124..127])
+    uint64_t tk_r = 0;
     auto take = [&](u32x4 v, int g, uint64_t out_head_r) -> bool {
         const uint32_t tl_take = TL_ON(P) ? (uint32_t)now_ticks() : 0u;
+        const uint64_t tk0 = kHopProf ? __builtin_amdgcn_s_memtime() : 0ull;
+        uint64_t tk1 = 0, tk2 = 0;
         const uint32_t q = (uint32_t)lane;
         const int from = (int)rdl32(in_src_r, g >> 1);
         const uint32_t w0 = rdl32(v.x, 0), id = rdl32(v.y, 0), w2 = rdl32(v.z, 0), t0 = rdl32(v.w, 0);
@@ -298,6 +304,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             }
             judge = uni(judge);
         }
+        const uint64_t tka = kHopProf ? __builtin_amdgcn_s_memtime() : 0ull;
         const uint32_t kids = judge == 1 ? kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane) : 0u;
         const uint32_t need = need_of_u(kids, origin, sll, sl_r, lane);
         if (full_of(need, out_head_r)) return false;
@@ -310,7 +317,9 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             tl_put(P, id, TLC_P1, lr, (uint32_t)now_ticks());
             tl_parent(P, id, lr, from);
         }
+        if constexpr (kHopProf) tk1 = __builtin_amdgcn_s_memtime();
         forward(v, nch, need);  // before the effects, as the reference forwards before queueing the pickup (:583-589)
+        if constexpr (kHopProf) tk2 = __builtin_amdgcn_s_memtime();
         if (TL_ON(P) && tag == TAG_BCAST && lane == 0) tl_put(P, id, TLC_P2, lr, (uint32_t)now_ticks());
         if (lane < nout && ((need >> lane) & 1u)) out_tail_r++;
         if (tag == TAG_BCAST) {  // delivered to this rank's pickup queue (:583-589)
@@ -369,6 +378,10 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             CNT_ADD(HC_DEC, 1);
             if (vote != 0) CNT_ADD(HC_DEC_APPR, 1);
             if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+        }
+        if constexpr (kHopProf) {
+            const uint64_t tk3 = __builtin_amdgcn_s_memtime();
+            tk_r += lane == 0 ? tk1 - tk0 : lane == 1 ? tk2 - tk1 : lane == 2 ? tk3 - tk2 : lane == 3 ? 1ull : lane == 4 ? tka - tk0 : 0ull;
         }
         return true;
     };
@@ -728,6 +741,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     atomicAdd((unsigned long long*)&P.stats[lr].bcast_sum, acc_sum);
     for (int i = lane; i < kHistBins; i += 64) P.stats[lr].hist[i] = S.hist[i];
+    if (kHopProf && lane < 5) P.stats[lr].hist[lane < 4 ? kHistBins - 4 + lane : kHistBins - 5] = (uint32_t)min(tk_r, (uint64_t)0xffffffffu);
 #pragma unroll
     for (int i = 0; i < 8; i++)
         if (lane == i) { P.stats[lr].prof[i] = hp_r; P.stats[lr].dbg[i] = rdl64(hp_r, 8 + i); }
@@ -763,31 +777,45 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
 }  // namespace rlo
 
 // C-ABI launch shims (rlo_world.cpp): one 64-thread workgroup per local rank, the pending table in dynamic LDS
-// (dyn_lds bytes) or, with Params.pend_hbm, in HBM (the PH instantiation)
-template <bool PH>
+// (dyn_lds bytes) or, with Params.pend_hbm, in HBM (the PH instantiation); system-scope worlds run the SYS one
+template <bool PH, bool SYS>
 static hipError_t hop_grant(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_hop_kernel<PH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_hop_kernel<PH, SYS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
     }
     return hipSuccess;
 }
-
-extern "C" hipError_t rlo_launch_hop(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
-    const bool ph = p->pend_hbm != nullptr;
-    hipError_t e = ph ? hop_grant<true>(dyn_lds) : hop_grant<false>(dyn_lds);
+template <bool PH, bool SYS>
+static hipError_t hop_launch(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
+    hipError_t e = hop_grant<PH, SYS>(dyn_lds);
     if (e != hipSuccess) return e;
-    if (ph) hipLaunchKernelGGL((rlo::rlo_hop_kernel<true>), dim3(blocks), dim3(64), dyn_lds, stream, *p);
-    else hipLaunchKernelGGL((rlo::rlo_hop_kernel<false>), dim3(blocks), dim3(64), dyn_lds, stream, *p);
+    hipLaunchKernelGGL((rlo::rlo_hop_kernel<PH, SYS>), dim3(blocks), dim3(64), dyn_lds, stream, *p);
     return hipGetLastError();
 }
-
-extern "C" hipError_t rlo_occupancy_hop(int* blocks, size_t dyn_lds, int ph) {
-    hipError_t e = ph ? hop_grant<true>(dyn_lds) : hop_grant<false>(dyn_lds);
+template <bool PH, bool SYS>
+static hipError_t hop_occ(int* blocks, size_t dyn_lds) {
+    hipError_t e = hop_grant<PH, SYS>(dyn_lds);
     if (e != hipSuccess) return e;
-    return ph ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<true>, 64, dyn_lds)
-              : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<false>, 64, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<PH, SYS>, 64, dyn_lds);
+}
+
+extern "C" hipError_t rlo_launch_hop(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
+    const bool ph = p->pend_hbm != nullptr, sys = p->sys_scope != 0;
+    return ph ? (sys ? hop_launch<true, true>(p, blocks, dyn_lds, stream) : hop_launch<true, false>(p, blocks, dyn_lds, stream))
+              : (sys ? hop_launch<false, true>(p, blocks, dyn_lds, stream) : hop_launch<false, false>(p, blocks, dyn_lds, stream));
+}
+
+// the smaller of the two scope instantiations' answers (the world's scope is known only at launch)
+extern "C" hipError_t rlo_occupancy_hop(int* blocks, size_t dyn_lds, int ph) {
+    int a = 0, b = 0;
+    hipError_t e = ph ? hop_occ<true, false>(&a, dyn_lds) : hop_occ<false, false>(&a, dyn_lds);
+    if (e != hipSuccess) return e;
+    e = ph ? hop_occ<true, true>(&b, dyn_lds) : hop_occ<false, true>(&b, dyn_lds);
+    if (e != hipSuccess) return e;
+    *blocks = a < b ? a : b;
+    return hipSuccess;
 }

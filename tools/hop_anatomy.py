@@ -28,6 +28,12 @@ def show(tag, st, units, unit_name):
     print("    max rank  " + " ".join("%9.0f" % v for v in prof[np.argmax(tot)] / units))
     print("    counts    " + " ".join("%9s" % s for s in CNT))
     print("    median    " + " ".join("%9.2f" % v for v in np.median(cnt, axis=0) / units), flush=True)
+    tk = st["hist"][:, -4:].astype(np.float64)  # a take's clocks: checks, forward, effects; takes
+    ntk = np.maximum(tk[:, 3], 1)
+    pre = st["hist"][:, -5].astype(np.float64)  # of the checks: entry -> the child set's computation
+    print("    per take (median over ranks): checks %.0f (header / pending / judge %.0f) forward %.0f effects %.0f cycles"
+          " (%.1f takes per %s)" % (np.median(tk[:, 0] / ntk), np.median(pre / ntk), np.median(tk[:, 1] / ntk),
+                                    np.median(tk[:, 2] / ntk), np.median(tk[:, 3]) / units, unit_name), flush=True)
 
 
 for n in [int(x) for x in (sys.argv[1:] or ["8"])]:
