@@ -11,8 +11,8 @@
 //
 //   poll   : one round trip for every counter of the rank (in-ring tails, vote-in tails, out-ring heads, vote-out
 //            heads), its forward and vote DOORBELLS (rlo_device.hpp), the part's error word and the latency round
-//            word.  The previous round's counters are published right after it returns: its wait covered the
-//            previous round's stores (vmcnt counts loads and stores in issue order), so no separate drain
+//            word; an idle rank repeats it until a polled word moves
+//   bells  : a whole doorbell is its ring's head message: taken from the poll's registers and forwarded first
 //   load   : the ring messages and votes the counters show beyond what the bells carried, one round trip
 //   votes  : _iar_vote_handler :743-812 / _vote_merge :1056-1070, a completed merge votes up (_vote_back :728-741)
 //   rings  : per in-ring, its messages in order: _bc_forward :1104-1225 (children relative to the dynamic origin,
@@ -20,6 +20,7 @@
 //            (:583-615, :668-726, :814-859); a message whose out-rings are full waits (the ring stops there)
 //   own    : the pool's decisions (_iar_decision_bcast :908-917), then its next proposals (RLO_submit_proposal
 //            :876-906), or this rank's next latency round (RLO_bcast_gen :1581-1604)
+//   publish: one drain of the round's stores, then its counters (vmcnt counts loads and stores in issue order)
 //
 // Rings, doorbells, counters, pending tables, logs and statistics are the world's own (rlo_world.cpp builds them
 // for both kernels): parts of one world may run either kernel, and every test of these programs runs this one.
@@ -709,6 +710,17 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 lat_own_next = lat_pos < lat_pos_n ? P.lat_own[P.lat_own_off[lr] + lat_pos] : 0xffffffffu;
                 progressed = true;
             }
+        }
+        // ---------------- this round's counters, published now behind one drain of its stores -- not after the next
+        // poll: a message the bells did not carry is visible to its consumer a round earlier (C4 at 8 ranks 168 K -> 175 K
+        // decisions/s, profiles/r6_hop_eager_ab.txt); the poll's wait then covers its loads only
+        if (__ballot((lane < nout && out_tail_r != pub_out) || (lane < n_in2 && in_head_r != pub_in) ||
+                     (lane < sll && vin_head_r != pub_vin) || (lane < n_in && vout_tail_r != pub_vout))) {
+            VM_DRAIN();
+            if (lane < nout && out_tail_r != pub_out) { pub_out = out_tail_r; pub64(otail_a, out_tail_r, sys); }
+            if (lane < n_in2 && in_head_r != pub_in) { pub_in = in_head_r; pub64(ihead_a, in_head_r, sys); }
+            if (lane < sll && vin_head_r != pub_vin) { pub_vin = vin_head_r; pub64(vinh_a, vin_head_r, sys); }
+            if (lane < n_in && vout_tail_r != pub_vout) { pub_vout = vout_tail_r; pub64(vtail_a, vout_tail_r, sys); }
         }
         HP_MARK(6);
 
