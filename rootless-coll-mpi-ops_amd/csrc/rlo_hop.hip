@@ -142,16 +142,21 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     const int64_t own_n = iar ? P.prop_off[lr + 1] - poff : 0;
     // the next own proposal, fetched while the current one is in flight (RLO_submit_proposal's arguments): stage 1 its
     // pid / data_len / data offset, stage 2 its PBuf chunks (lane q = chunk q, q >= 1), so an origination loads nothing
+    // (vector loads into VGPRs, read with v_readfirstlane once landed: a scalar load would count in lgkmcnt, which
+    // every LDS wait of the round also waits for -- a memory round trip inside the next LDS access)
     int64_t nx_i = -1;
-    uint32_t nx_stage = 0, nx_pid = 0, nx_dl = 0, nx_doff = 0;
+    uint32_t nx_stage = 0, nx_pid_v = 0, nx_dl_v = 0, nx_doff_v = 0;
     u32x4 nx_v = {0u, 0u, 0u, 0u};
+    auto vld32 = [&](const void* base, uint32_t idx) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b32(mk_rsrc(const_cast<void*>(base), 0xFFFFFFFFu), 4u * idx, 0, 0);
+    };
     auto prefetch_meta = [&](int64_t i) {
         nx_stage = 0;
         nx_i = i;
         if (i >= own_n) return;
-        nx_pid = (uint32_t)P.prop_pid[poff + i];
-        nx_dl = P.prop_data_len[poff + i];
-        nx_doff = P.prop_data_off[poff + i];
+        nx_pid_v = vld32(P.prop_pid, (uint32_t)(poff + i));
+        nx_dl_v = vld32(P.prop_data_len, (uint32_t)(poff + i));
+        nx_doff_v = vld32(P.prop_data_off, (uint32_t)(poff + i));
         nx_stage = 1;
     };
     // the latency program: my originations
@@ -389,9 +394,10 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
 
     // a local origination to the whole send list (:1587): header + chunks (v: lane q's chunk q >= 1, generated or
     // prefetched); false (nothing changed) when an out-ring is full
+    const uint32_t need_all = need_of_u((1u << sll) - 1u, me, sll, sl_r, lane);  // an origination's out-rings (:1587)
     auto originate = [&](uint32_t w0, uint32_t id, uint32_t w2, u32x4 v, uint64_t out_head_r) -> bool {
         const uint32_t len = w2 & 0xffffu, nch = (kHdr + len + 15u) >> 4;
-        const uint32_t need = need_of_u((1u << sll) - 1u, me, sll, sl_r, lane);
+        const uint32_t need = need_all;
         if (full_of(need, out_head_r)) return false;
         if (lane == 0) v = u32x4{w0, id, (w2 & 0xff00ffffu) | (kSlotMark << 16), (uint32_t)now_ticks()};
         forward(v, nch, need);
@@ -466,9 +472,6 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         CNT_ADD(HC_ITER, 1);
         HP_MARK(0);
         HP_CNT(0, 1);
-        // the previous round's counters (its stores have drained: the wait above covered them), taken before this
-        // round's first forwards move them
-        const uint64_t out_pub = out_tail_r, in_pub = in_head_r, vin_pub = vin_head_r, vt_pub = vout_tail_r;
         vout_hd_r = vout_head_r;
         bool progressed = false;
         room_wait = false;
@@ -478,14 +481,19 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         // its header's chunks carries bell_tag(in-ring head) | vc << 31.  Its message is the ring's head: taken straight
         // from the bell registers (lane q <- chunk q of edge k), forwarded before this rank publishes, merges or loads
         // anything -- the reference forwards on receipt too (_bc_forward from make_progress_gen :583-589)
-        const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
-        const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
-        const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;
-        const uint64_t gm = hn <= kBellChunks ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
-        const uint64_t fh = __ballot(bq == 0u && gm && ((B0 & gm) == gm || (B1 & gm) == gm));
-        const uint64_t fv = __ballot(bq == 0u && gm && (B1 & gm) == gm);
-        const int rk = lane >> 1;
-        const bool rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
+        // (most busy rounds of the iar program find no bell: one ballot on the first halves decides whether to look
+        // closer; a latency round almost always holds one)
+        bool rhit = false;
+        if (lat || __ballot(inb && bq == 0u && (ba.y == e0 || ba.y == e1))) {
+            const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
+            const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
+            const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;
+            const uint64_t gm = hn <= kBellChunks ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
+            const uint64_t fh = __ballot(bq == 0u && gm && ((B0 & gm) == gm || (B1 & gm) == gm));
+            const uint64_t fv = __ballot(bq == 0u && gm && (B1 & gm) == gm);
+            const int rk = lane >> 1;
+            rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
+        }
         uint64_t blocked = 0;  // rings whose head cannot go this round (full out-ring, pending entry busy): they wait
         if (go) {
             if (TL_ON(P)) tl_pub = tl_loop = (uint32_t)now_ticks();
@@ -508,12 +516,8 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         }
         HP_MARK(1);
 
-        // ---- publish what the previous round left (before this round's forwards)
-        if (lane < nout && out_pub != pub_out) { pub_out = out_pub; pub64(otail_a, out_pub, sys); }
-        if (lane < n_in2 && in_pub != pub_in) { pub_in = in_pub; pub64(ihead_a, in_pub, sys); }
-        if (lane < sll && vin_pub != pub_vin) { pub_vin = vin_pub; pub64(vinh_a, vin_pub, sys); }
-        if (lane < n_in && vt_pub != pub_vout) { pub_vout = vt_pub; pub64(vtail_a, vt_pub, sys); }
-        if (done) break;  // (the final counters are out)
+        // (every counter of the previous rounds is out: each round publishes its own at its end)
+        if (done) break;
         if (!go) break;   // another rank failed: stop everyone
         if (lat && me == 0 && latr > lat_seen) {  // world rank 0 observes round completions on its own clock
             const uint64_t tn = now_ticks();
@@ -522,10 +526,16 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         }
         // the next own proposal's chunks, now that its pid / length / offset are in (stage 1 -> 2)
         if (nx_stage == 1u) {
+            const uint32_t nx_dl = (uint32_t)uni((int)nx_dl_v), nx_doff = (uint32_t)uni((int)nx_doff_v);
             const uint32_t nch = (kHdr + 16u + nx_dl + 15u) >> 4;
             nx_v = u32x4{0u, 0u, 0u, 0u};
-            if (lane == 1) nx_v = u32x4{nx_pid, 1u, nx_dl, 0u};  // PBuf [pid][vote=1][data_len u64] (:1369-1396)
-            if (lane >= 2 && (uint32_t)lane < nch) {
+            if (lane == 1) nx_v = u32x4{(uint32_t)uni((int)nx_pid_v), 1u, nx_dl, 0u};  // PBuf [pid][vote=1][data_len u64] (:1369-1396)
+            if ((nx_doff & 3u) == 0u) {
+                // dword-aligned data (the usual packing): 16-B loads, left in flight -- the bytes past data_len are
+                // masked off at the origination (the range of the resource ends at the data's end, rounded up)
+                const __amdgpu_buffer_rsrc_t rd = mk_rsrc(const_cast<uint8_t*>(P.prop_data) + nx_doff, (nx_dl + 3u) & ~3u);
+                if (lane >= 2 && (uint32_t)lane < nch) nx_v = __builtin_amdgcn_raw_buffer_load_b128(rd, 16u * ((uint32_t)lane - 2u), 0, 0);
+            } else if (lane >= 2 && (uint32_t)lane < nch) {
                 const __attribute__((address_space(1))) uint8_t* d =
                     (const __attribute__((address_space(1))) uint8_t*)(P.prop_data + nx_doff);
                 uint32_t w[4];
@@ -672,17 +682,26 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 if (own_iter >= own_n || (uint32_t)__popcll(busy) >= P.own_pool) break;
                 uint32_t k = own_rr;
                 while ((busy >> k) & 1ull) k = (k + 1u) & (P.pend_slots - 1u);
+                uint32_t id, dl;
+                u32x4 pv = {0u, 0u, 0u, 0u};
                 if (nx_i != own_iter || nx_stage != 2u) {  // (not prefetched yet: fetch it now, one wait)
-                    prefetch_meta(own_iter);
-                    const uint32_t nch = (kHdr + 16u + nx_dl + 15u) >> 4;
-                    nx_v = u32x4{0u, 0u, 0u, 0u};
-                    if (lane == 1) nx_v = u32x4{nx_pid, 1u, nx_dl, 0u};
+                    const int64_t pi = poff + own_iter;
+                    id = (uint32_t)P.prop_pid[pi];
+                    dl = P.prop_data_len[pi];
+                    const uint32_t nch = (kHdr + 16u + dl + 15u) >> 4;
+                    if (lane == 1) pv = u32x4{id, 1u, dl, 0u};
                     else if (lane >= 2 && (uint32_t)lane < nch)
-                        nx_v = gen_chunk(P, K_PROP, me, nx_pid, 16u + nx_dl, (uint32_t)(poff + own_iter), 1, (uint32_t)lane);
-                    nx_stage = 2;
+                        pv = gen_chunk(P, K_PROP, me, id, 16u + dl, (uint32_t)pi, 1, (uint32_t)lane);
+                } else {
+                    id = (uint32_t)uni((int)nx_pid_v);
+                    dl = (uint32_t)uni((int)nx_dl_v);
+                    pv = nx_v;
+                    if (lane >= 2) {  // the data's zero-padded tail (loaded whole dwords)
+                        const int b0 = (int)dl - (int)(16u * ((uint32_t)lane - 2u));
+                        pv = u32x4{mask_bytes(pv.x, b0), mask_bytes(pv.y, b0 - 4), mask_bytes(pv.z, b0 - 8), mask_bytes(pv.w, b0 - 12)};
+                    }
                 }
-                const uint32_t id = nx_pid;
-                if (!originate((uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id, (16u + nx_dl) | (k << 24), nx_v,
+                if (!originate((uint32_t)me | (TAG_PROPOSAL << 16) | (1u << 24), id, (16u + dl) | (k << 24), pv,
                                out_head_r)) {
                     room_wait = true;
                     break;
