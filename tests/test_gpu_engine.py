@@ -316,7 +316,9 @@ def test_iar_concurrent_exact_sets(rlo, n, p, ppm, pool):
 
 
 @pytest.mark.parametrize("n,ln,maxp", [(4, 64, 64), (8, 64, 64), (32, 64, 64), (256, 64, 64), (4, 112, 112),
-                                        (8, 112, 112), (32, 112, 112), (256, 112, 112), (32, 64, 4096)])
+                                        (8, 112, 112), (32, 112, 112), (256, 112, 112), (32, 64, 4096),
+                                        # messages of <= 4 chunks: the hop kernel's half-bell format (rlo_hop.hip kHalfBell)
+                                        (8, 1, 64), (16, 48, 64), (64, 17, 64)])
 def test_latency_program(rlo, n, ln, maxp):
     """The latency program (one bcast at a time: the doorbell path, fwd_small / ll_pass, carries every
     message where the world has bells) at the world sizes the bench quotes p50 for, 64 B and the bell's
