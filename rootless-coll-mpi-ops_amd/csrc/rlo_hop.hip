@@ -55,6 +55,7 @@ struct HopShared {
     uint32_t ev_n;
     uint32_t hist[kHistBins];
     alignas(16) uint8_t msg[kHopLoads * kHopScratch];  // loaded ring messages, message m chunk q at 16 (m mch + q)
+    alignas(16) uint8_t bell[kHopScratch];   // a round's forward bells, in-edge k's chunk q at 16 (8 k + q)
     alignas(16) uint8_t vote[kHopScratch];   // loaded votes, one 16-B slot per lane; a judged proposal's copy
 };
 
@@ -477,32 +478,27 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         room_wait = false;
         const bool go = !done && __builtin_amdgcn_readfirstlane(errf) == 0;
 
-        // ---------------- whole doorbells first (forward-first): in-edge k's bell is whole for (k, vc) when every half of
-        // its header's chunks carries bell_tag(in-ring head) | vc << 31.  Its message is the ring's head: taken straight
-        // from the bell registers (lane q <- chunk q of edge k), forwarded before this rank publishes, merges or loads
-        // anything -- the reference forwards on receipt too (_bc_forward from make_progress_gen :583-589)
-        // (most busy rounds of the iar program find no bell: one ballot on the first halves decides whether to look
-        // closer; a latency round almost always holds one)
-        bool rhit = false;
-        if (lat || __ballot(inb && bq == 0u && (ba.y == e0 || ba.y == e1))) {
-            const uint64_t B0 = __ballot(inb && ba.y == e0 && ba.w == e0 && bb.y == e0 && bb.w == e0);
-            const uint64_t B1 = __ballot(inb && ba.y == e1 && ba.w == e1 && bb.y == e1 && bb.w == e1);
-            const uint32_t hn = (kHdr + ((uint32_t)__shfl((int)bb.x, lane & ~7) & 0xffffu) + 15u) >> 4;
-            const uint64_t gm = hn <= kBellChunks ? (((1ull << hn) - 1ull) << (lane & ~7)) : 0ull;
-            const uint64_t fh = __ballot(bq == 0u && gm && ((B0 & gm) == gm || (B1 & gm) == gm));
-            const uint64_t fv = __ballot(bq == 0u && gm && (B1 & gm) == gm);
-            const int rk = lane >> 1;
-            rhit = lane < n_in2 && ((fh >> (8 * rk)) & 1ull) && ((uint32_t)((fv >> (8 * rk)) & 1ull) == ((uint32_t)lane & 1u));
-        }
+        // ---------------- whole doorbells first (forward-first): in-edge k's bell holds ring (k, vc)'s head when every
+        // 8-byte half of its header's chunks carries bell_tag(in-ring head) | vc << 31.  That message is taken from the
+        // bells (one 16-B LDS read per lane after one write of the round's bells), forwarded before this rank merges or
+        // loads anything -- the reference forwards on receipt too (_bc_forward from make_progress_gen :583-589)
         uint64_t blocked = 0;  // rings whose head cannot go this round (full out-ring, pending entry busy): they wait
-        if (go) {
+        // lane (k, q): its chunk's tag when all four halves agree; the header lanes (q = 0) that carry a head's tag
+        const uint32_t tg = ba.y == ba.w && ba.y == bb.y && ba.y == bb.w ? ba.y : 0u;
+        const uint64_t hc = __ballot(inb && bq == 0u && tg != 0u && (tg == e0 || tg == e1));
+        if (go && hc) {
             if (TL_ON(P)) tl_pub = tl_loop = (uint32_t)now_ticks();
-            for (uint64_t gs = __ballot(rhit); gs; gs &= gs - 1) {  // (uniform)
-                const int g = __builtin_ctzll(gs);
-                const int sl = 8 * (g >> 1) + (lane & 7);
-                u32x4 v = {(uint32_t)__shfl((int)ba.x, sl), (uint32_t)__shfl((int)ba.z, sl), (uint32_t)__shfl((int)bb.x, sl),
-                           (uint32_t)__shfl((int)bb.z, sl)};
-                if ((uint32_t)lane >= kBellChunks) v = u32x4{0u, 0u, 0u, 0u};
+            *reinterpret_cast<u32x4*>(S.bell + 16u * (uint32_t)lane) = u32x4{ba.x, ba.z, bb.x, bb.z};
+            for (uint64_t cs = hc; cs; cs &= cs - 1) {  // (uniform; in-edge order)
+                const int hl = __builtin_ctzll(cs);
+                const uint32_t th = rdl32(tg, hl);
+                const int g = 2 * (hl >> 3) + (int)(th >> 31);  // (vc 1 tags carry bit 31)
+                const uint32_t nch = (kHdr + (rdl32(bb.x, hl) & 0xffffu) + 15u) >> 4;
+                if (nch > kBellChunks) continue;
+                const uint64_t m = ((1ull << nch) - 1ull) << hl;
+                if ((__ballot(tg == th) & m) != m) continue;  // not whole yet: the counter path takes it
+                u32x4 v = {0u, 0u, 0u, 0u};
+                if ((uint32_t)lane < nch) v = *reinterpret_cast<const u32x4*>(S.bell + 16u * ((uint32_t)hl + (uint32_t)lane));
                 if (take(v, g, out_head_r)) {
                     if (lane == g) in_head_r++;
                     progressed = true;
