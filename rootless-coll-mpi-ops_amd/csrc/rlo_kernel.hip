@@ -733,6 +733,10 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
 #pragma unroll
                         for (int uu = 0; uu < kMoveDepth; uu++) {
                             const uint32_t g = g0 + (uint32_t)uu * kT + (uint32_t)tid;
+#ifdef RLO_AB_VERIFY_READ_ONLY  // A/B probe (fails verification by design): the read-back without its arithmetic
+                            if (g < ngr) acc += v[uu].x ^ v[uu].y ^ v[uu].z ^ v[uu].w;
+                            continue;
+#endif
                             if (g < ngr) {
                                 const uint32_t off = off0 + 16u * g;
                                 const int b0 = (int)len - (int)off;  // the reference's zero-padded tail
@@ -743,9 +747,11 @@ __device__ __forceinline__ void mover_run(const Params& P, SH& SS, int tid) {
                                 // message is the storm payload of (origin, bid), so a granule that is not
                                 // what the origin wrote -- a tile whose stores never became visible behind a
                                 // complete count -- is a device error, not a wrong sum
+#ifndef RLO_AB_VERIFY_NO_CMP  // A/B probe: the checksum without the per-granule comparison with the generator
                                 const u32x4 x = storm_granule((uint32_t)o, jb.bid, len, off);
                                 if (w.x != x.x || w.y != x.y || w.z != x.z || w.w != x.w)
                                     bulk_fault(P, 14, (uint32_t)(me & 0xff) << 16 | ((off >> 14) & 0xffffu));
+#endif
                             }
                         }
                     };
