@@ -170,6 +170,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     uint64_t idle_since = 0;
     uint32_t idle_n = 0;
     bool done = false;
+    const bool logon = (P.mode & MODE_LOG) != 0u;  // (uniform: no lane-0 section is entered for a log that is off)
     auto err = [&](uint32_t code, uint32_t aux) {
         if (lane == 0) set_error(S, P, code, aux);
     };
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                     const uint32_t d = (nw >> 16) == 0 ? 1u : 0u;
                     if (d) {  // final judge(NULL) (:770-775): every device judge approves NULL
                         CNT_ADD(HC_JUDGE, 1);
-                        if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
+                        if (logon && lane == 0) log_put<kPmHop>(S, P, lr, LOG_JUDGE, me, -1, (uint32_t)pid, 0, 1, 1);
                     }
                     if (lane == (int)k) { own_dec_r = d; own_state_r = 2; }
                 }
@@ -270,6 +271,18 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     // one ring message from in-ring g, lane q holding slot chunk q (q < nch): checks, forwards, effects.  Returns
     // false when it cannot go now (an out-ring it needs is full, or its pending entry still holds the previous
     // proposal of that pool slot): nothing changed, the ring waits
+    // worlds of <= 16 ranks with <= 4 in-edges (every one-proposal iar world this kernel runs): a forwarded message's
+    // out-rings by (in-edge k, origin o) in lane 16 k + o, computed once (_bc_forward :1116-1223, fwd_send_cnt :1559-1579)
+    const bool ntab = P.n <= 16 && n_in <= 4;
+    uint32_t need_t = 0;
+    if (ntab) {
+        for (int k = 0; k < n_in; k++)
+            for (int o = 0; o < P.n; o++) {
+                const uint32_t nd = need_of_u(kids_of_u(me, o, (int)rdl32(in_src_r, k), level, last_wall, scc, sll, sl_r, lane), o,
+                                              sll, sl_r, lane);
+                if (lane == 16 * k + o) need_t = nd;
+            }
+    }
     // kHopProf: a take's clocks -- lane 0 checks (to the forward), 1 forward, 2 effects; lane 3 takes (stats.hist[124..127])
     uint64_t tk_r = 0;
     auto take = [&](u32x4 v, int g, uint64_t out_head_r) -> bool {
@@ -312,8 +325,12 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             judge = uni(judge);
         }
         const uint64_t tka = kHopProf ? __builtin_amdgcn_s_memtime() : 0ull;
-        const uint32_t kids = judge == 1 ? kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane) : 0u;
-        const uint32_t need = need_of_u(kids, origin, sll, sl_r, lane);
+        // the out-rings of the message's children (one per child: 2 j + vc): from the table of (in-edge, origin) pairs
+        // where the world is small enough to have one, else computed
+        const uint32_t need = judge != 1 ? 0u
+                              : ntab ? rdl32(need_t, (int)(((uint32_t)g >> 1) * 16u + (uint32_t)origin))
+                                     : need_of_u(kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane), origin, sll,
+                                                 sl_r, lane);
         if (full_of(need, out_head_r)) return false;
         if (TL_ON(P) && tag == TAG_BCAST && lane == 0) {  // the hop's clocks (tools/round_timeline.py)
             tl_put(P, id, TLC_ARRIVE, lr, tl_take);
@@ -365,11 +382,11 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             } else {
                 const uint32_t k = (uint32_t)g >> 1;
                 CNT_ADD(HC_JUDGE, 1);
-                if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_JUDGE, origin, from, id, len, judge, 0);
+                if (logon && lane == 0) log_put<kPmHop>(S, P, lr, LOG_JUDGE, origin, from, id, len, judge, 0);
                 if (!judge) {  // declined: vote 0, not forwarded, not pending (:700-706)
                     vote_up(k, origin, (int32_t)id, pseq, 0);
                 } else {
-                    const uint32_t nk = (uint32_t)__builtin_popcount(kids);
+                    const uint32_t nk = (uint32_t)__builtin_popcount(need);  // (one out-ring per child)
                     pend_wr(origin, pseq, u32x4{id, 0u, k | (nk << 16) | ((uint32_t)PS_ACTIVE << 24), pseq | ((len - 16u) << 8)});
                     if (nk == 0) vote_up(k, origin, (int32_t)id, pseq, 1);
                 }
@@ -378,13 +395,13 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             if ((pe.z >> 24) == PS_ACTIVE && (int32_t)pe.x == (int32_t)id) {
                 if (vote != 0) {
                     CNT_ADD(HC_ACTIONS, 1);
-                    if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, pe.w >> 8);
+                    if (logon && lane == 0) log_put<kPmHop>(S, P, lr, LOG_ACTION, origin, from, id, 0, 1, pe.w >> 8);
                 }
                 pend_wr(origin, pseq, u32x4{pe.x, pe.y, pe.z & 0x00ffffffu, pe.w});  // valid = PS_NONE
             }
             CNT_ADD(HC_DEC, 1);
             if (vote != 0) CNT_ADD(HC_DEC_APPR, 1);
-            if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
+            if (logon && lane == 0) log_put<kPmHop>(S, P, lr, LOG_DELIVER | (TAG_DECISION << 8), origin, from, id, 7, vote, 0);
         }
         if constexpr (kHopProf) {
             const uint64_t tk3 = __builtin_amdgcn_s_memtime();
@@ -669,7 +686,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 HP_CNT(6, 1);
                 CNT_ADD(HC_OWN_DEC, 1);
                 if (dec) CNT_ADD(HC_OWN_APPR, 1);
-                if (lane == 0) log_put<kPmHop>(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, (uint32_t)k);
+                if (logon && lane == 0) log_put<kPmHop>(S, P, lr, LOG_RESULT, me, -1, id, 0, (int)dec, (uint32_t)k);
                 if (lane == k) { own_state_r = 0; own_pid_r = -1; }  // proposalPool_rm (:1334-1347) / RLO_proposal_reset (:1649-1673)
                 progressed = true;
             }
