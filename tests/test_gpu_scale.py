@@ -64,7 +64,9 @@ def test_four_wave_parts_plan_matches(rlo, n, payload, pend_hbm):
 
 
 @pytest.mark.parametrize("n,p,ppm,pool", [(256, 4, 201, 1), (256, 8, 201, 16), (64, 16, 50000, 4), (8, 64, 20000, 16),
-                                          (5, 48, 0, 8)])
+                                          (5, 48, 0, 8),
+                                          # one own proposal in worlds of <= 16 ranks: the hop kernel's PH instantiation
+                                          (8, 64, 20000, 1), (16, 24, 3400, 1)])
 def test_iar_exact_sets_hbm_tables(rlo, n, p, ppm, pool):
     """the PH instantiation: pending entries in HBM, exact sets per (origin, pid) vs the pool oracle"""
     import iar_sets
@@ -76,8 +78,10 @@ def test_iar_exact_sets_hbm_tables(rlo, n, p, ppm, pool):
         w.program_iar(iar_sets.props(n, p), judge=kind, seed=99, ppm=ppm, log=True, log_cap=cap, pool=pool)
         w.run()
         st = w.stats()
+        kernel = w.info_now()["last_kernel"]
         logs = {r: w.log(r, cap=cap) for r in range(n)}
     assert (st["error"] == 0).all(), (st["error"], st["error_aux"])
+    assert kernel == (1 if pool == 1 and n <= 16 else 0), kernel  # 1: the hop kernel (rlo_hop.hip)
     iar_sets.check(logs, n, p, ppm, pool)
 
 
