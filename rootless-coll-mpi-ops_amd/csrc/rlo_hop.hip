@@ -34,6 +34,7 @@ constexpr uint32_t kHopScratch = 64u * 16u;  // one batch of 16-B chunks (64 lan
 constexpr uint32_t kHopLoads = 4;            // ring-message loads per lane per round trip (256 chunks)
 constexpr uint32_t kPmHop = ~(uint32_t)MODE_HOST;  // log_put: no host-mode code here
 constexpr uint32_t kHopSpin = 64;            // re-polls of an idle rank before a whole round runs again
+constexpr uint32_t kHopNeedLds = 2048;       // (in-edge, origin) pairs of the LDS out-ring table (8 KiB)
 // the diagnostics build's section profile (tools/hop_anatomy.py): shader clocks per section of a round into
 // stats.prof[0..7] and event counts into stats.dbg[0..7]; the product kernel carries none of it
 #ifdef RLO_DIAG
@@ -56,6 +57,7 @@ struct HopShared {
     uint32_t hist[kHistBins];
     alignas(16) uint8_t msg[kHopLoads * kHopScratch];  // loaded ring messages, message m chunk q at 16 (m mch + q)
     alignas(16) uint8_t bell[kHopScratch];   // a round's forward bells, in-edge k's chunk q at 16 (8 k + q)
+    uint32_t need_lds[kHopNeedLds];          // worlds of <= kHopNeedLds (in-edge, origin) pairs: out-rings by pair
     alignas(16) uint8_t vote[kHopScratch];   // loaded votes, one 16-B slot per lane; a judged proposal's copy
 };
 
@@ -283,6 +285,18 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
                 if (lane == 16 * k + o) need_t = nd;
             }
     }
+    // larger worlds up to kHopNeedLds pairs (256 ranks x 8 in-edges): the same table in LDS, entry n k + o, each lane
+    // computing its own origins' entries (kids_of / need_of: the per-lane forms)
+    const bool ltab = !ntab && (uint32_t)P.n * (uint32_t)n_in <= kHopNeedLds;
+    if (ltab) {
+        for (int k = 0; k < n_in; k++) {
+            const int from = (int)rdl32(in_src_r, k);
+            for (int o = lane; o < P.n; o += 64)
+                S.need_lds[(uint32_t)k * (uint32_t)P.n + (uint32_t)o] =
+                    need_of(kids_of(me, o, from, level, last_wall, scc, sll, sl_r), o, sll, sl_r);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     // kHopProf: a take's clocks -- lane 0 checks (to the forward), 1 forward, 2 effects; lane 3 takes (stats.hist[124..127])
     uint64_t tk_r = 0;
     auto take = [&](u32x4 v, int g, uint64_t out_head_r) -> bool {
@@ -329,6 +343,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         // where the world is small enough to have one, else computed
         const uint32_t need = judge != 1 ? 0u
                               : ntab ? rdl32(need_t, (int)(((uint32_t)g >> 1) * 16u + (uint32_t)origin))
+                              : ltab ? (uint32_t)uni((int)S.need_lds[((uint32_t)g >> 1) * (uint32_t)P.n + (uint32_t)origin])
                                      : need_of_u(kids_of_u(me, origin, from, level, last_wall, scc, sll, sl_r, lane), origin, sll,
                                                  sl_r, lane);
         if (full_of(need, out_head_r)) return false;
