@@ -12,7 +12,8 @@
 //   poll   : one round trip for every counter of the rank (in-ring tails, vote-in tails, out-ring heads, vote-out
 //            heads), its forward and vote DOORBELLS (rlo_device.hpp), the part's error word and the latency round
 //            word; an idle rank repeats it until a polled word moves
-//   bells  : a whole doorbell is its ring's head message: taken from the poll's registers and forwarded first
+//   bells  : a whole doorbell is its ring's head message: staged in LDS, taken and forwarded first (children's
+//            out-rings from a table of (in-edge, origin) pairs built at launch)
 //   load   : the ring messages and votes the counters show beyond what the bells carried, one round trip
 //   votes  : _iar_vote_handler :743-812 / _vote_merge :1056-1070, a completed merge votes up (_vote_back :728-741)
 //   rings  : per in-ring, its messages in order: _bc_forward :1104-1225 (children relative to the dynamic origin,
