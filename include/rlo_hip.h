@@ -196,7 +196,10 @@ int rlo_program_storm(rlo_world_t* w, const rlo_storm_cfg_t* cfg);
 
 /* one bcast per round, round i from splitmix64(seed + i) % N; round i+1 starts when every
  * rank has picked up round i.  rlo_latencies() returns per-round completion ticks (10 ns):
- * origination -> last pickup, on one clock only when the world is one part.  Worlds split over
+ * origination -> last pickup, on one clock only when the world is one part.  The hop kernel
+ * (rlo_hop.hip) takes the largest of the receivers' own pickup clocks (the reference harness's
+ * t_recv); the progress kernel (bulk rounds) the clock of the rank whose pickup completed the
+ * round's delivery count, so it includes that count's round trip.  Worlds split over
  * parts (processes / GPUs, <= 8192 rounds) share the round word through part 0; there
  * rlo_round_ticks() (on the part holding world rank 0) returns the clock of world rank 0 when it
  * saw round i complete: successive differences are closed-loop round times on ONE clock. */
