@@ -647,12 +647,13 @@ def small_n_legs(rlo, local, stream, sizes=(4, 8), rounds=2000, p=512):
     keeping one proposal outstanding (approve-all judge on the device)."""
     import numpy as np
 
-    out = {}
-    for n in sizes:
+    def lat_c4(n, **kw):
         rec = {}
-        with rlo.World(n, max_payload=64, device=local) as w:
+        with rlo.World(n, max_payload=64, device=local, **kw) as w:
             w.program_latency(rounds, 64, seed=21)
-            _step(w, stream, None)
+            rc0, _ = _step(w, stream, None)
+            st = w.stats()
+            ok = rc0 == 0 and (st["error"] == 0).all() and int(st["bcast_delivered"].sum()) == rounds * (n - 1)
             lat = w.latencies_ticks().astype(np.float64) * 0.01
             rec["p50_us"] = round(percentile(lat, 50), 2)
             rec["p99_us"] = round(percentile(lat, 99), 2)
@@ -665,7 +666,15 @@ def small_n_legs(rlo, local, stream, sizes=(4, 8), rounds=2000, p=512):
             rec["decisions_per_s"] = round(n * p / dt, 1)
             rec["decisions_per_s_kernel"] = round(n * p / (ms * 1e-3), 1)
             rec["decision_us"] = round(ms * 1e3 / p, 2)  # one proposal round trip per rank, back to back
-            rec["verified"] = bool(rc == 0 and (st["error"] == 0).all() and int(st["own_decided"].sum()) == n * p)
+            rec["verified"] = bool(ok and rc == 0 and (st["error"] == 0).all() and int(st["own_decided"].sum()) == n * p)
+        return rec
+
+    out = {}
+    for n in sizes:
+        rec = lat_c4(n)
+        # the same programs in a world created with RLO_PART_ONE_XCD: cached rings, every rank-wave on one XCD
+        rec["one_xcd"] = lat_c4(n, one_xcd=True)
+        rec["verified"] &= rec["one_xcd"]["verified"]
         # the proposal pool (rootless_ops.c:30, unfinished in the reference): 16 own proposals in flight
         # per rank instead of one (:241)
         with rlo.World(n, max_payload=32, device=local, proposal_pool=16) as w:
@@ -1019,12 +1028,16 @@ def main():
         for key, rec in sw.items():
             ref = ((api_leg.get(key) or {}).get("reference_host_mpi") or {})
             r_lat, r_dec = (ref.get("lat") or {}).get("p50_us"), (ref.get("iar") or {}).get("decisions_per_s")
+            ox = rec.get("one_xcd") or {}
             c4[key] = {"device_p50_us": rec.get("p50_us"), "reference_p50_us": r_lat,
                        "device_decisions_per_s": rec.get("decisions_per_s"),
+                       "device_one_xcd_p50_us": ox.get("p50_us"), "device_one_xcd_decisions_per_s": ox.get("decisions_per_s"),
                        "device_pool16_decisions_per_s": rec.get("pool16_decisions_per_s"),
                        "reference_decisions_per_s": r_dec}
             if r_dec:
                 c4[key]["decisions_x_reference"] = round(rec["decisions_per_s"] / r_dec, 2)
+                if ox.get("decisions_per_s"):
+                    c4[key]["one_xcd_decisions_x_reference"] = round(ox["decisions_per_s"] / r_dec, 2)
                 if rec.get("pool16_decisions_per_s"):
                     c4[key]["pool16_decisions_x_reference"] = round(rec["pool16_decisions_per_s"] / r_dec, 2)
         if c4:

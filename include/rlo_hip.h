@@ -53,6 +53,8 @@ extern "C" {
                                     instead of touching memory outside the heaps); site 14: a device
                                     program's VERIFY read a granule that is not what the origin wrote
                                     (aux value = receiver rank & 0xff << 16 | 16-KiB block of the message) */
+#define RLO_DERR_XCD 9           /* a RLO_PART_ONE_XCD world's rank-waves were not all placed on one XCD
+                                    (aux = the first XCC id seen + 1 << 8 | this wave's + 1)     */
 
 /* ------------------------------------------------------------------ topology (host only) */
 /* skip-ring overlay, restated from rootless_ops.c:1416-1579; usable without a GPU */
@@ -79,7 +81,7 @@ typedef struct {
      * would crowd the small copy path's stage out of LDS: rlo_world_info_t.pend_hbm); 0 = 2.  An iar
      * program keeps up to rlo_iar_cfg_t.pool <= this many own proposals in flight per rank */
     uint32_t proposal_pool;
-    uint32_t flags;       /* RLO_PART_* (RLO_PART_PEND_HBM, RLO_PART_CHUNKED); 0 = none              */
+    uint32_t flags;       /* RLO_PART_* (PEND_HBM, CHUNKED, ONE_XCD); 0 = none                      */
 } rlo_world_cfg_t;
 
 typedef struct {
@@ -127,6 +129,11 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
 #define RLO_PART_UNCACHED 1u /* allocate the part's rings uncached (for peer GPUs writing over xGMI) */
 #define RLO_PART_PEND_HBM 4u /* the pending-proposal tables in HBM whatever the world size (the layout an 8-GPU
                                  * world takes, rehearsed at smaller N; every part must set it alike) */
+#define RLO_PART_ONE_XCD 8u  /* rlo_world_create, <= 32 ranks, no bulk: the rings cached and every rank-wave of the
+                                 * hop kernel on ONE XCD, so a hand-off store stays in that XCD's L2 and the
+                                 * consumer's load hits it (one hop 0.51 vs 1.11 us, tools/xcd_probe.hip).  Only the
+                                 * hop kernel's programs run (latency; iar with pool 1, <= 16 ranks, device judges);
+                                 * a launch that needs the progress kernel returns RLO_E_INVAL */
 #define RLO_PART_CHUNKED 2u  /* bulk messages take the multi-GPU plan (chunked scatter + all-gather) even when every
                                  * part is on one GPU: the 8-GPU path, rehearsed on one (every part must set it alike) */
 typedef struct {

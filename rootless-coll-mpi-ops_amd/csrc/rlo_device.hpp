@@ -73,6 +73,7 @@ enum Mode : uint32_t {
     MODE_TL = 32768u,     // latency program: per-round event clocks into Params.tl (RLO_FLAG_TIMELINE; no path changes)
     MODE_HOPPROF = 131072u,  // diagnostics build: shader clocks at points of a doorbell hop into stats.prof (tools/hop_prof.py)
     MODE_NOHPW = 262144u,   // diagnostics build, host mode A/B: no wave-1 host poller (wave 0 polls the host words itself)
+    MODE_XCD1 = 524288u,    // RLO_PART_ONE_XCD: the hop kernel's rank-waves on one XCD, L2-kept (plain) hand-off stores
     MODE_CORRUPT = 65536u,  // diagnostics build, test of the VERIFY check: a direct scatter zeroes one granule of one copy
     MODE_HOST = 128u,  // host-service: originations / judge verdicts come from a host command ring,
                        //   deliveries / judge requests / results go to a host pickup ring (rootless_ops.h)
@@ -99,7 +100,7 @@ enum LogKind : uint32_t { LOG_DELIVER = 1, LOG_JUDGE = 2, LOG_ACTION = 3, LOG_RE
 
 enum Err : uint32_t { ERR_NONE = 0, ERR_TIMEOUT = 1, ERR_VOTE_RING = 2, ERR_PID_COLLISION = 3, ERR_VOTE_ORPHAN = 4,
                       ERR_LOG_FULL = 5, ERR_BAD_SLOT = 6, ERR_HOST_CMD = 7,
-                      ERR_BULK = 8 };  // a bulk index / job field out of range (error_aux: site << 24 | value)
+                      ERR_BULK = 8, ERR_XCD = 9 };  // a bulk index / job field out of range (error_aux: site << 24 | value)
 
 // Slot header, 16 bytes:
 //   w0 = origin (16 b) | tag (8 b) << 16 | vote (8 b) << 24
@@ -222,6 +223,7 @@ struct Params {
     uint32_t* lat_count;          // [lat_rounds] deliveries so far
     uint64_t* lat_out;            // [lat_rounds] completion ticks
     uint32_t* lat_round;          // current round (global; part 0's control region when sharded)
+    uint32_t* xcd_word;           // MODE_XCD1: the first rank-wave's XCC id + 1 (uncached; zeroed at every launch)
     uint64_t* lat_obs;            // [lat_rounds] observer clock (world rank 0) when round i completed
     uint32_t* tl;                 // MODE_TL: [tl_rounds][kTlGlobal + kTlCols n_local] low 32 bits of the 100-MHz clock
     uint32_t tl_rounds;

@@ -69,16 +69,21 @@ enum HopCnt : int {
 };
 
 // SYS: the world spans GPUs (Params.sys_scope): every hand-off store and counter at system scope -- a template
-// parameter, so no store of the hop path branches on the scope at run time
-template <bool PH, bool SYS>
+// parameter, so no store of the hop path branches on the scope at run time.  LOC (MODE_XCD1, worlds created with
+// RLO_PART_ONE_XCD): the grid is 8 workgroups per rank and only every eighth runs a rank (workgroups 8 apart share an
+// XCD; checked at launch), the rings are in cached memory and the hand-off stores are plain, so a line stays in that
+// XCD's L2 and the consumer's sc1 load hits it (tools/xcd_probe.hip: one hop 0.51 us vs 1.11 us)
+template <bool PH, bool SYS, bool LOC>
 __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     __shared__ HopShared S;
-    const int lr = blockIdx.x, me = P.rank_begin + lr;
+    if constexpr (LOC)
+        if (blockIdx.x & 7u) return;
+    const int lr = LOC ? (int)(blockIdx.x >> 3) : (int)blockIdx.x, me = P.rank_begin + lr;
     const int lane = (int)threadIdx.x;
     PendState* pend;  // [n][pend_slots]: dynamic LDS, or (PH) this rank's table in HBM
     if constexpr (PH)
-        pend = (PendState*)(__attribute__((address_space(1))) PendState*)(P.pend_hbm + (size_t)blockIdx.x * (uint32_t)P.n * P.pend_slots);
+        pend = (PendState*)(__attribute__((address_space(1))) PendState*)(P.pend_hbm + (size_t)lr * (uint32_t)P.n * P.pend_slots);
     else
         pend = reinterpret_cast<PendState*>(dyn_lds);
 #define PEND(o, q) pend[(uint32_t)(o) * P.pend_slots + ((uint32_t)(q) & (P.pend_slots - 1u))]
@@ -113,6 +118,17 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     const uint32_t in_bell = (uint32_t)uni((int)t.in_bell), vin_bell = (uint32_t)uni((int)t.vin_bell);
     const uint32_t sl_r = lane < sll ? (uint32_t)t.send_list[lane] : 0u;
     constexpr bool sys = SYS;
+    // hand-off stores: system scope (SYS), plain (LOC), else agent scope (sc1)
+    auto st16 = [&](__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+        if constexpr (SYS) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1 | 1);
+        else if constexpr (LOC) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1);
+    };
+    auto st64 = [&](uint64_t addr, uint64_t v) {
+        if constexpr (SYS) __hip_atomic_store(gptr64(addr), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if constexpr (LOC) __hip_atomic_store(gptr64(addr), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else __hip_atomic_store(gptr64(addr), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     const __amdgpu_buffer_rsrc_t rf = mk_rsrc(P.fwd_region, P.fwd_region_bytes);
     const __amdgpu_buffer_rsrc_t rv = mk_rsrc(P.vote_region, P.vote_region_bytes);
     const __amdgpu_buffer_rsrc_t rc = mk_rsrc(P.ctrl, P.ctrl_bytes);
@@ -186,12 +202,12 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             const int oi = __builtin_ctz(m);
             const uint64_t slot = rdl64(out_tail_r, oi);
             const __amdgpu_buffer_rsrc_t ro = mk_rsrc(reinterpret_cast<void*>(rdl64(obase_r, oi)), oring_bytes);
-            if (q < nch) st_ring(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v, sys);
+            if (q < nch) st16(ro, (uint32_t)(slot & fcap_m) * P.fwd_stride + 16u * q, v);
             if (nch <= kBellChunks && q < nch) {
                 const uint32_t T = bell_tag(slot) | ((uint32_t)(oi & 1) << 31);
                 const __amdgpu_buffer_rsrc_t rb = mk_rsrc(reinterpret_cast<void*>(rdl64(bbase_r, oi)), kBellWords * 8u);
-                st_ring(rb, 32u * q, u32x4{v.x, T, v.y, T}, sys);
-                st_ring(rb, 32u * q + 16u, u32x4{v.z, T, v.w, T}, sys);
+                st16(rb, 32u * q, u32x4{v.x, T, v.y, T});
+                st16(rb, 32u * q + 16u, u32x4{v.z, T, v.w, T});
             }
         }
     };
@@ -231,10 +247,7 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
             val = lane == 2 ? ((uint64_t)((uint32_t)origin | ((uint32_t)(vote & 0xff) << 24)) | ((uint64_t)(uint32_t)pid << 32))
                             : ((uint64_t)(pseq & 0xffu) | ((uint64_t)(uint32_t)me << 32));
         }
-        if (lane < 4) {
-            if (sys) __hip_atomic_store(gptr64(addr), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            else __hip_atomic_store(gptr64(addr), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (lane < 4) st64(addr, val);
     };
 
     // one vote from child j: _iar_vote_handler :743-812, _vote_merge :1056-1070 (uniform)
@@ -461,7 +474,33 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
     do {                                                                   \
         if constexpr (kHopProf) hp_r += lane == 8 + (i) ? (uint64_t)(v) : 0ull; \
     } while (0)
-    for (;;) {
+    // RLO_PART_ONE_XCD (LOC): every rank-wave must sit on the first one's XCD (HIP does not promise the round-robin
+    // placement the grid relies on).  A rendezvous on uncached words before any hand-off -- [0] the first XCC id + 1,
+    // [1] arrivals | a misplaced wave's 1 << 16, one atomic each -- and a wave elsewhere stops the whole launch with
+    // RLO_DERR_XCD instead of handing messages through another XCD's L2
+    bool xcd_ok = true;
+    if constexpr (LOC) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const uint32_t mine = (xcc & 0xFu) + 1u;
+        uint32_t first = 0, bad = 0;
+        if (lane == 0) {
+            first = atomicCAS(P.xcd_word, 0u, mine);
+            const uint32_t off = first != 0u && first != mine ? 0x10001u : 1u;
+            atomicAdd(P.xcd_word + 1, off);
+            uint32_t v = 0;
+            for (uint32_t s = 0; s < (1u << 22); s++) {  // bounded: every rank-wave is co-resident (hop_eligible)
+                v = __hip_atomic_load(P.xcd_word + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v & 0xFFFFu) >= P.n_local) break;
+            }
+            bad = (v >> 16) != 0u || (v & 0xFFFFu) < P.n_local;
+        }
+        if (rdl32(bad, 0) != 0u) {
+            err(ERR_XCD, (rdl32(first, 0) << 8) | mine);
+            xcd_ok = false;
+        }
+    }
+    while (xcd_ok) {
         // ---------------- poll: counters, doorbells, error word, round word -- one round trip
         // (branch-free: rlo_kernel_common.hpp kOob).  After a round that did nothing the poll repeats right away, with
         // no round around it, until a polled word moves: a message landing at an idle rank waits for at most one poll
@@ -765,10 +804,10 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         if (__ballot((lane < nout && out_tail_r != pub_out) || (lane < n_in2 && in_head_r != pub_in) ||
                      (lane < sll && vin_head_r != pub_vin) || (lane < n_in && vout_tail_r != pub_vout))) {
             VM_DRAIN();
-            if (lane < nout && out_tail_r != pub_out) { pub_out = out_tail_r; pub64(otail_a, out_tail_r, sys); }
-            if (lane < n_in2 && in_head_r != pub_in) { pub_in = in_head_r; pub64(ihead_a, in_head_r, sys); }
-            if (lane < sll && vin_head_r != pub_vin) { pub_vin = vin_head_r; pub64(vinh_a, vin_head_r, sys); }
-            if (lane < n_in && vout_tail_r != pub_vout) { pub_vout = vout_tail_r; pub64(vtail_a, vout_tail_r, sys); }
+            if (lane < nout && out_tail_r != pub_out) { pub_out = out_tail_r; st64(otail_a, out_tail_r); }
+            if (lane < n_in2 && in_head_r != pub_in) { pub_in = in_head_r; st64(ihead_a, in_head_r); }
+            if (lane < sll && vin_head_r != pub_vin) { pub_vin = vin_head_r; st64(vinh_a, vin_head_r); }
+            if (lane < n_in && vout_tail_r != pub_vout) { pub_vout = vout_tail_r; st64(vtail_a, vout_tail_r); }
         }
         HP_MARK(6);
 
@@ -838,33 +877,36 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
 
 // C-ABI launch shims (rlo_world.cpp): one 64-thread workgroup per local rank, the pending table in dynamic LDS
 // (dyn_lds bytes) or, with Params.pend_hbm, in HBM (the PH instantiation); system-scope worlds run the SYS one
-template <bool PH, bool SYS>
+template <bool PH, bool SYS, bool LOC = false>
 static hipError_t hop_grant(size_t dyn_lds) {
     static size_t granted = 0;
     if (dyn_lds > granted) {
-        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_hop_kernel<PH, SYS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)dyn_lds);
+        hipError_t e = hipFuncSetAttribute((const void*)rlo::rlo_hop_kernel<PH, SYS, LOC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds);
         if (e != hipSuccess) return e;
         granted = dyn_lds;
     }
     return hipSuccess;
 }
-template <bool PH, bool SYS>
+template <bool PH, bool SYS, bool LOC = false>
 static hipError_t hop_launch(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
-    hipError_t e = hop_grant<PH, SYS>(dyn_lds);
+    hipError_t e = hop_grant<PH, SYS, LOC>(dyn_lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rlo::rlo_hop_kernel<PH, SYS>), dim3(blocks), dim3(64), dyn_lds, stream, *p);
+    hipLaunchKernelGGL((rlo::rlo_hop_kernel<PH, SYS, LOC>), dim3(LOC ? 8 * blocks : blocks), dim3(64), dyn_lds, stream, *p);
     return hipGetLastError();
 }
 template <bool PH, bool SYS>
 static hipError_t hop_occ(int* blocks, size_t dyn_lds) {
     hipError_t e = hop_grant<PH, SYS>(dyn_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<PH, SYS>, 64, dyn_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, rlo::rlo_hop_kernel<PH, SYS, false>, 64, dyn_lds);
 }
 
 extern "C" hipError_t rlo_launch_hop(const rlo::Params* p, int blocks, size_t dyn_lds, hipStream_t stream) {
     const bool ph = p->pend_hbm != nullptr, sys = p->sys_scope != 0;
+    if ((p->mode & rlo::MODE_XCD1) && (sys || !p->xcd_word)) return hipErrorInvalidValue;  // (the rendezvous word)
+    if (p->mode & rlo::MODE_XCD1)  // RLO_PART_ONE_XCD
+        return ph ? hop_launch<true, false, true>(p, blocks, dyn_lds, stream) : hop_launch<false, false, true>(p, blocks, dyn_lds, stream);
     return ph ? (sys ? hop_launch<true, true>(p, blocks, dyn_lds, stream) : hop_launch<true, false>(p, blocks, dyn_lds, stream))
               : (sys ? hop_launch<false, true>(p, blocks, dyn_lds, stream) : hop_launch<false, false>(p, blocks, dyn_lds, stream));
 }

@@ -384,6 +384,7 @@ struct rlo_world {
     DevBuf<uint32_t> d_lat_own_off, d_lat_own;
     DevBuf<int32_t> d_lat_origin, d_prop_pid;
     DevBuf<uint64_t> d_lat_out, d_lat_obs;
+    uint32_t* d_xcd = nullptr;  // RLO_PART_ONE_XCD: the placement check word (uncached)
     DevBuf<uint32_t> d_tl;  // RLO_FLAG_TIMELINE rows
     uint32_t tl_rows = 0;
     DevBuf<uint8_t> d_mask, d_prop_data, d_log_payload;
@@ -870,11 +871,15 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     w->max_payload = (std::max<uint32_t>(cfg->max_payload ? cfg->max_payload : 4096u, 16u) + 15u) & ~15u;
     if (w->max_payload > 65520u) { delete w; return RLO_E_INVAL; }  // slot header: 16-bit length (rlo_device.hpp)
     w->flags = cfg->flags;
+    // RLO_PART_ONE_XCD: one part, no bulk, <= 32 ranks (one XCD's CUs), and only hop-kernel programs (rlo_launch_ex)
+    const bool one_xcd = (cfg->flags & RLO_PART_ONE_XCD) != 0;
+    if (one_xcd && (cfg->n_parts != 1 || cfg->bulk_max || cfg->n_ranks > 32)) { delete w; return RLO_E_INVAL; }
     // rings and counters in uncached memory for every world, not only for parts on other GPUs: a
     // line of ring memory left in some XCD's L2 by an earlier kernel (the creation / reset fill) is
     // not invalidated by another XCD's write-through stores, and a consumer on that XCD read the
-    // zeros (seen as unmarked slot headers that never became visible).  RLO_CACHED_RINGS=1: A/B only
-    if (!diag_env("RLO_CACHED_RINGS")) w->flags |= RLO_PART_UNCACHED;
+    // zeros (seen as unmarked slot headers that never became visible).  A ONE_XCD world's rings are
+    // cached: every producer and consumer is on one XCD, so its L2 is the one copy.  RLO_CACHED_RINGS=1: A/B only
+    if (!diag_env("RLO_CACHED_RINGS") && !one_xcd) w->flags |= RLO_PART_UNCACHED;
     {
         const uint32_t pp = cfg->proposal_pool ? cfg->proposal_pool : 2u;
         if ((pp & (pp - 1u)) || pp > (uint32_t)rlo::kPoolMax) { delete w; return RLO_E_INVAL; }
@@ -924,6 +929,10 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
         alloc_region(w, (void**)&w->ctrl, w->L.ctrl_words[me] * 8)) {
         rlo_world_destroy(w);
         return RLO_E_HIP;
+    }
+    if (one_xcd) {
+        const hipError_t e = hipExtMallocWithFlags((void**)&w->d_xcd, 256, hipDeviceMallocUncached);
+        if (e != hipSuccess) { g_last_hip = (int)e; w->d_xcd = nullptr; rlo_world_destroy(w); return RLO_E_HIP; }
     }
     if (w->pend_hbm) {  // uncached: a launch's workgroup may sit on another XCD than the previous launch's
         const uint32_t keep = w->flags;
@@ -1192,7 +1201,7 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out) {
     pc.bulk_slots = cfg->bulk_slots;
     pc.movers = cfg->movers;
     pc.proposal_pool = cfg->proposal_pool;
-    pc.flags = cfg->flags & (RLO_PART_PEND_HBM | RLO_PART_CHUNKED);
+    pc.flags = cfg->flags & (RLO_PART_PEND_HBM | RLO_PART_CHUNKED | RLO_PART_ONE_XCD);
     rlo_world* w = nullptr;
     int rc = rlo_part_create(&pc, &w);
     if (rc) return rc;
@@ -1287,6 +1296,7 @@ int rlo_world_destroy(rlo_world_t* w) {
     w->d_lat_count.release(); w->d_lat_round.release(); w->d_lat_origin.release(); w->d_prop_pid.release();
     w->d_lat_out.release(); w->d_lat_own_off.release(); w->d_lat_own.release(); w->d_mask.release(); w->d_prop_data.release(); w->d_log_payload.release();
     w->d_isp.release(); w->d_log.release();
+    if (w->d_xcd) (void)hipFree(w->d_xcd);
     host_free(w);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
@@ -2041,6 +2051,12 @@ int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {
     if (hdiag) w->P.mode |= rlo::MODE_HDIAG;
     else w->P.mode &= ~rlo::MODE_HDIAG;
     hipError_t e;
+    if (w->d_xcd) {  // RLO_PART_ONE_XCD: the hop kernel on one XCD, or nothing
+        if (!hop_eligible(w)) return RLO_E_INVAL;
+        w->P.mode |= rlo::MODE_XCD1;
+        w->P.xcd_word = w->d_xcd;  // (every program's base_params clears Params)
+        HIPCHK(hipMemsetAsync(w->d_xcd, 0, 8, s));  // the placement rendezvous (rlo_hop.hip)
+    }
     if (hop_eligible(w)) {
         w->last_hop = true;
         e = rlo_launch_hop(&w->P, w->nl, hop_lds(w), s);

@@ -27,6 +27,7 @@ RLO_PART_BLOB_BYTES = 512
 RLO_PART_UNCACHED = 1
 RLO_PART_CHUNKED = 2
 RLO_PART_PEND_HBM = 4
+RLO_PART_ONE_XCD = 8
 RLO_PEER_OTHER_GPU, RLO_PEER_IMPORTED = 1, 2  # rlo_world_info_t.peers
 RLO_LAUNCH_NO_RESET = 1
 RLO_TRIM_IMPORTS, RLO_TRIM_FREE, RLO_TRIM_RETIRED, RLO_TRIM_EXPORTED = 1, 2, 4, 8  # rlo_pool_trim

@@ -22,17 +22,19 @@ class World:
     part of a sharded world (export() -> exchange blobs -> connect(blobs))."""
 
     def __init__(self, n, max_payload=4096, ring_slots=0, device=-1, _part=None, bulk_max=0, bulk_slots=0, movers=0,
-                 proposal_pool=0, pend_hbm=False):
+                 proposal_pool=0, pend_hbm=False, one_xcd=False):
         """bulk_max > 0: messages longer than max_payload (up to bulk_max bytes) are bulk messages --
         announced through the rings, moved by `movers` mover workgroups (0 = auto) between per-rank
         heaps of bulk_slots slots per origin (rlo_hip.h).  proposal_pool: pending entries per origin
         = the most own proposals a rank can keep in flight (power of two <= 16; 0 = 2).  pend_hbm: the
-        pending-proposal tables in HBM whatever N (the 8-GPU world's layout, rehearsed at a smaller N)."""
+        pending-proposal tables in HBM whatever N (the 8-GPU world's layout, rehearsed at a smaller N).
+        one_xcd (<= 32 ranks, no bulk): cached rings and every rank-wave of the hop kernel on one XCD, hand-offs
+        through its L2 (RLO_PART_ONE_XCD); only the hop kernel's programs run in such a world."""
         self.lib = L.load()
         h = ctypes.c_void_p()
         if _part is None:
             cfg = L.WorldCfg(n, max_payload, ring_slots, device, bulk_max, bulk_slots, movers, proposal_pool,
-                             L.RLO_PART_PEND_HBM if pend_hbm else 0)
+                             (L.RLO_PART_PEND_HBM if pend_hbm else 0) | (L.RLO_PART_ONE_XCD if one_xcd else 0))
             check(self.lib.rlo_world_create(ctypes.byref(cfg), ctypes.byref(h)), "rlo_world_create")
         else:
             n_parts, part, begin, flags = _part
