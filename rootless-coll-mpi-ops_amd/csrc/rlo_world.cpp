@@ -871,9 +871,10 @@ int rlo_part_create(const rlo_part_cfg_t* cfg, rlo_world_t** out) {
     w->max_payload = (std::max<uint32_t>(cfg->max_payload ? cfg->max_payload : 4096u, 16u) + 15u) & ~15u;
     if (w->max_payload > 65520u) { delete w; return RLO_E_INVAL; }  // slot header: 16-bit length (rlo_device.hpp)
     w->flags = cfg->flags;
-    // RLO_PART_ONE_XCD: one part, no bulk, <= 32 ranks (one XCD's CUs), and only hop-kernel programs (rlo_launch_ex)
+    // RLO_PART_ONE_XCD: one part, no bulk, <= 256 ranks (as many as one XCD's CUs hold: checked at launch), and only
+    // hop-kernel programs (rlo_launch_ex)
     const bool one_xcd = (cfg->flags & RLO_PART_ONE_XCD) != 0;
-    if (one_xcd && (cfg->n_parts != 1 || cfg->bulk_max || cfg->n_ranks > 32)) { delete w; return RLO_E_INVAL; }
+    if (one_xcd && (cfg->n_parts != 1 || cfg->bulk_max || cfg->n_ranks > 256)) { delete w; return RLO_E_INVAL; }
     // rings and counters in uncached memory for every world, not only for parts on other GPUs: a
     // line of ring memory left in some XCD's L2 by an earlier kernel (the creation / reset fill) is
     // not invalidated by another XCD's write-through stores, and a consumer on that XCD read the
@@ -1991,7 +1992,8 @@ static bool hop_eligible(rlo_world* w) {
     if (lds > 64u * 1024u) return false;
     int b = 0;
     if (rlo_occupancy_hop(&b, lds, P.pend_hbm ? 1 : 0) != hipSuccess) { (void)hipGetLastError(); return false; }
-    return b > 0 && (int64_t)b * w->cus >= (int64_t)w->nl;
+    // (RLO_PART_ONE_XCD: every rank-wave on the CUs of one XCD, an eighth of the GPU's)
+    return b > 0 && (int64_t)b * (w->d_xcd ? w->cus / 8 : w->cus) >= (int64_t)w->nl;
 }
 
 int rlo_launch_ex(rlo_world_t* w, void* stream, uint32_t flags) {

@@ -23,7 +23,8 @@ def rlo():
     return _rlo
 
 
-@pytest.mark.parametrize("n,ln,maxp", [(4, 64, 64), (8, 64, 64), (8, 112, 112), (13, 100, 112), (32, 64, 64), (8, 1, 64)])
+@pytest.mark.parametrize("n,ln,maxp", [(4, 64, 64), (8, 64, 64), (8, 112, 112), (13, 100, 112), (32, 64, 64), (8, 1, 64),
+                                        (64, 64, 64), (128, 48, 64)])
 def test_one_xcd_latency_program(rlo, n, ln, maxp):
     rounds, seed = 64, 5
     ref = orc.storm(n, seed, rounds, ln, want_parent=True)
@@ -75,7 +76,7 @@ def test_one_xcd_iar_exact_sets(rlo, n, p, ppm):
 def test_one_xcd_limits(rlo):
     """Only the hop kernel's programs run in a ONE_XCD world: a storm (the progress kernel, whose rank-workgroups
     spread over every XCD and would read the cached rings through other L2s) is refused at launch, not run; worlds
-    of more than one XCD's 32 CUs of ranks, or with bulk messages, are refused at creation"""
+    of more than 256 ranks, or with bulk messages, are refused at creation"""
     with rlo.World(8, max_payload=64, one_xcd=True) as w:
         w.program_storm(64, 64, seed=3)
         with pytest.raises(Exception):
@@ -84,6 +85,6 @@ def test_one_xcd_limits(rlo):
         w.run()
         assert (w.stats()["error"] == 0).all()
     with pytest.raises(Exception):
-        rlo.World(33, max_payload=64, one_xcd=True)
+        rlo.World(257, max_payload=64, one_xcd=True)
     with pytest.raises(Exception):
         rlo.World(8, max_payload=64, bulk_max=1 << 20, one_xcd=True)
