@@ -130,7 +130,7 @@ int rlo_world_create(const rlo_world_cfg_t* cfg, rlo_world_t** out);
 #define RLO_PART_PEND_HBM 4u /* the pending-proposal tables in HBM whatever the world size (the layout an 8-GPU
                                  * world takes, rehearsed at smaller N; every part must set it alike) */
 #define RLO_PART_ONE_XCD 8u  /* rlo_world_create, no bulk, as many ranks as one XCD's CUs hold (<= 256; checked at
-                                 * launch: 128 at 64 B): the rings cached and every rank-wave of the
+                                 * launch): the rings cached and every rank-wave of the
                                  * hop kernel on ONE XCD, so a hand-off store stays in that XCD's L2 and the
                                  * consumer's load hits it (one hop 0.51 vs 1.11 us, tools/xcd_probe.hip).  Only the
                                  * hop kernel's programs run (latency; iar with pool 1, <= 16 ranks, device judges);

@@ -95,7 +95,9 @@ __global__ __launch_bounds__(64) void rlo_hop_kernel(Params P) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&P.topo[lr]);
         uint32_t* dst = reinterpret_cast<uint32_t*>(&S.t);
         for (int i = lane; i < (int)(sizeof(RankTopo) / 4); i += 64) dst[i] = src[i];
-        for (int i = lane; i < P.n * (int)P.pend_slots; i += 64) pend[i] = PendState{0, 0, 0, 0, 0, 0};
+        // (the latency program never touches the table, and is launched without one: rlo_world.cpp hop_lds)
+        if (iar)
+            for (int i = lane; i < P.n * (int)P.pend_slots; i += 64) pend[i] = PendState{0, 0, 0, 0, 0, 0};
         for (int i = lane; i < kHistBins; i += 64) S.hist[i] = 0;
         if (lane == 0) {
             S.error = 0; S.error_aux = 0;

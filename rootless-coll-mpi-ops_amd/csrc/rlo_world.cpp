@@ -1971,6 +1971,8 @@ int rlo_reset(rlo_world_t* w, void* stream) {
 // the diagnostics modes that instrument the progress kernel's doorbell pass (phase profile, hop profile, the no-fast-path
 // A/B) keep that kernel, and so does RLO_NO_HOP (diagnostics build: A/B of the two kernels)
 static size_t hop_lds(const rlo_world* w) {
+    // the pending-proposal table (iar only: the latency program launches without it, so more rank-waves share a CU)
+    if (!(w->P.mode & rlo::MODE_IAR)) return 0;
     return w->P.pend_hbm ? 0 : (size_t)16u * (uint32_t)w->L.n * w->P.pend_slots;
 }
 static bool hop_eligible(rlo_world* w) {

@@ -28,7 +28,7 @@ class World:
         heaps of bulk_slots slots per origin (rlo_hip.h).  proposal_pool: pending entries per origin
         = the most own proposals a rank can keep in flight (power of two <= 16; 0 = 2).  pend_hbm: the
         pending-proposal tables in HBM whatever N (the 8-GPU world's layout, rehearsed at a smaller N).
-        one_xcd (no bulk, as many ranks as one XCD holds: 128 at 64 B): cached rings and every rank-wave of the hop kernel on one XCD, hand-offs
+        one_xcd (no bulk, as many ranks as one XCD holds: <= 256): cached rings and every rank-wave of the hop kernel on one XCD, hand-offs
         through its L2 (RLO_PART_ONE_XCD); only the hop kernel's programs run in such a world."""
         self.lib = L.load()
         h = ctypes.c_void_p()

@@ -24,7 +24,7 @@ def rlo():
 
 
 @pytest.mark.parametrize("n,ln,maxp", [(4, 64, 64), (8, 64, 64), (8, 112, 112), (13, 100, 112), (32, 64, 64), (8, 1, 64),
-                                        (64, 64, 64), (128, 48, 64)])
+                                        (64, 64, 64), (128, 48, 64), (256, 64, 64)])
 def test_one_xcd_latency_program(rlo, n, ln, maxp):
     rounds, seed = 64, 5
     ref = orc.storm(n, seed, rounds, ln, want_parent=True)
