@@ -1,5 +1,5 @@
 """One-proposal decisions (C4) at a small world, product library: the workload for a PMC pass over the hop kernel.
-    python tools/c4_run.py [n] [proposals per rank] [runs]"""
+    python tools/c4_run.py [n] [proposals per rank] [runs] [one_xcd]"""
 import os
 import sys
 
@@ -10,7 +10,8 @@ import rlo  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 p = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 runs = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-with rlo.World(n, max_payload=64) as w:
+one_xcd = len(sys.argv) > 4 and sys.argv[4] == "one_xcd"  # RLO_PART_ONE_XCD
+with rlo.World(n, max_payload=64, one_xcd=one_xcd) as w:
     w.program_iar([(r, it * n + r, b"0123456789abcdef") for it in range(p) for r in range(n)])
     for _ in range(runs):
         ms = w.run()

@@ -1,5 +1,5 @@
 """The latency program at a world size, product library: the workload for a rocprof pass over the hop kernel.
-    python tools/lat_run.py [n] [rounds] [runs]"""
+    python tools/lat_run.py [n] [rounds] [runs] [one_xcd]"""
 import os
 import sys
 
@@ -12,7 +12,8 @@ import rlo  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
 runs = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-with rlo.World(n, max_payload=64) as w:
+one_xcd = len(sys.argv) > 4 and sys.argv[4] == "one_xcd"  # RLO_PART_ONE_XCD
+with rlo.World(n, max_payload=64, one_xcd=one_xcd) as w:
     w.program_latency(rounds, 64, seed=21)
     for _ in range(runs):
         ms = w.run()
