@@ -26,7 +26,9 @@
 // Rings, doorbells, counters, pending tables, logs and statistics are the world's own (rlo_world.cpp builds them
 // for both kernels): parts of one world may run either kernel, and every test of these programs runs this one.
 // Memory ordering as in rlo_kernel.hip: every handed-off byte stored sc1 (system scope across GPUs) and loaded
-// sc1 behind the counter that covers it; a counter is stored after its stores drained.
+// sc1 behind the counter that covers it; a counter is stored after its stores drained.  A world created with
+// RLO_PART_ONE_XCD runs the LOC instantiation instead: every rank-wave on one XCD, cached rings, plain stores that
+// stay in that XCD's L2 (still loaded sc1, past the CU's L1), the placement checked at launch.
 #include "rlo_kernel_common.hpp"
 
 namespace rlo {
